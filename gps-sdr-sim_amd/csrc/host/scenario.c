@@ -1,0 +1,618 @@
+/*
+ * scenario.c — the host control plane: main() of gpssim.c minus the per-sample loop.
+ *
+ *   gss_scn_open  ≙ gpssim.c:1738-2152  (options → inputs → start time → ephemeris set →
+ *                                        first channel allocation → antenna pattern)
+ *   gss_scn_next  ≙ gpssim.c:2154-2188  (per-block refresh: range, code phase, gain)
+ *                 + gpssim.c:2290-2352  (30 s nav/ephemeris/allocation update, time step)
+ *                 + the carrier-phase chain the sample loop carries across blocks
+ *                   (gpssim.c:2245-2250), produced exactly by the planner below.
+ *
+ * The sample loop itself is not here: its inputs are emitted as gss_chan_blk_t rows and the
+ * GPU synthesises them (gss_synth_*).
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdarg.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include "gss_host.h"
+#include "../common/gss_phase.h"
+
+/* Receiver antenna attenuation [dB] vs boresight angle 0:5:180 deg (gpssim.c:86-91). */
+double gss_ant_pat_db[37] = {
+     0.00,  0.00,  0.22,  0.44,  0.67,  1.11,  1.56,  2.00,  2.44,  2.89,  3.56,  4.22,
+     4.89,  5.56,  6.22,  6.89,  7.56,  8.22,  8.89,  9.78, 10.67, 11.56, 12.44, 13.33,
+    14.44, 15.56, 16.67, 17.78, 18.89, 20.00, 21.33, 22.67, 24.00, 25.56, 27.33, 29.33,
+    31.56};
+
+/* ---- error reporting ---------------------------------------------------------------------- */
+static __thread char g_err[512];
+
+int gss_fail(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+const char *gss_last_error(void) { return g_err; }
+
+static double wall_now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+/* ---- scenario state ------------------------------------------------------------------------ */
+struct gss_scn {
+    gss_opts_t opt;
+    int quiet;
+    eph_t eph[K_EPH_SETS + 1][K_MAX_SAT];   /* +1: the reference reads eph[ieph+1] at ieph=12 */
+    int neph, ieph;
+    iono_t io;
+    double (*xyz)[3];
+    int numd, static_mode;
+    int n_per_blk;
+    double samp_freq, delt;
+    gtime_t g0, grx;
+    chan_t chan[K_MAX_CHAN];
+    int alloc_sat[K_MAX_SAT];
+    double ant_pat[37];
+    int iumd;                               /* next block index, 1..numd-1 (gpssim.c:2154) */
+    uint32_t *nav_rows;
+    int n_nav, cap_nav;
+    double carr[K_MAX_CHAN];                /* planner: carrier at the next block start per slot */
+    double plan_sec;
+    /* per-batch side info for the planner */
+    int batch_cap;
+    int8_t *b_slot;                         /* [b][k] slot of entry k */
+    uint8_t *b_reset;                       /* [b][k] 1 if the slot's chain restarts here */
+    double *b_init;                         /* [b][k] restart value */
+};
+
+static void msg(const gss_scn *s, const char *fmt, ...)
+{
+    if (s->quiet)
+        return;
+    va_list ap;
+    va_start(ap, fmt);
+    vfprintf(stderr, fmt, ap);
+    va_end(ap);
+}
+
+/* Append a copy of ch->dwrd to the nav table and point the channel at it. */
+static int nav_push(gss_scn *s, chan_t *ch)
+{
+    if (s->n_nav == s->cap_nav) {
+        int cap = s->cap_nav ? 2 * s->cap_nav : 256;
+        uint32_t *p = realloc(s->nav_rows, (size_t)cap * GSS_NAV_WORDS * sizeof(uint32_t));
+        if (p == NULL)
+            return gss_fail(GSS_E_NOMEM, "out of memory (nav table)");
+        s->nav_rows = p;
+        s->cap_nav = cap;
+    }
+    memcpy(s->nav_rows + (size_t)s->n_nav * GSS_NAV_WORDS, ch->dwrd, sizeof ch->dwrd);
+    ch->nav_row = s->n_nav++;
+    return 0;
+}
+
+/* allocateChannel, gpssim.c:1572-1648: (de)allocate visible satellites into free slots. */
+static int allocate_channels(gss_scn *s, const eph_t *eset, gtime_t grx, const double *xyz)
+{
+    int nsat = 0;
+    const double origin[3] = {0.0, 0.0, 0.0};
+
+    for (int sv = 0; sv < K_MAX_SAT; sv++) {
+        double azel[2];
+        if (sv_visible(&eset[sv], grx, xyz, 0.0, azel) == 1) {
+            nsat++;
+            if (s->alloc_sat[sv] != -1)
+                continue;
+            int i;
+            for (i = 0; i < K_MAX_CHAN; i++) {
+                chan_t *ch = &s->chan[i];
+                if (ch->prn != 0)
+                    continue;
+                rng_t rho;
+                ch->prn = sv + 1;
+                ch->azel[0] = azel[0];
+                ch->azel[1] = azel[1];
+                ca_generate(ch->ca, ch->prn);
+                ca_pack(ch->ca, ch->ca_bits);
+                nav_subframes(&eset[sv], &s->io, ch->sbf);
+                nav_frame(grx, ch, 1);
+                int rc = nav_push(s, ch);
+                if (rc)
+                    return rc;
+                sv_range(&rho, &eset[sv], &s->io, grx, xyz);
+                ch->rho0 = rho;
+                /* initial carrier phase from the range difference to the geocentre
+                   (gpssim.c:1615-1622, FLOAT_CARR_PHASE branch) */
+                double r_xyz = rho.range;
+                sv_range(&rho, &eset[sv], &s->io, grx, origin);
+                double r_ref = rho.range;
+                double ph = (2.0 * r_ref - r_xyz) / K_LAMBDA_L1;
+                ch->carr_phase = ph - floor(ph);
+                ch->carr_fresh = 1;
+                break;
+            }
+            if (i < K_MAX_CHAN)
+                s->alloc_sat[sv] = i;
+        } else if (s->alloc_sat[sv] >= 0) {
+            s->chan[s->alloc_sat[sv]].prn = 0;
+            s->alloc_sat[sv] = -1;
+        }
+    }
+    return nsat;
+}
+
+static void print_channels(const gss_scn *s)
+{
+    for (int i = 0; i < K_MAX_CHAN; i++) {
+        const chan_t *c = &s->chan[i];
+        if (c->prn > 0)
+            msg(s, "%02d %6.1f %5.1f %11.1f %5.1f\n", c->prn, c->azel[0] * K_R2D,
+                c->azel[1] * K_R2D, c->rho0.d, c->rho0.iono_delay);
+    }
+}
+
+int gss_scn_open(gss_scn **out, const gss_opts_t *opt)
+{
+    *out = NULL;
+    gss_scn *s = calloc(1, sizeof *s);
+    if (s == NULL)
+        return gss_fail(GSS_E_NOMEM, "out of memory");
+    s->opt = *opt;
+    s->quiet = opt->quiet;
+    int ums = opt->user_motion_size > 0 ? opt->user_motion_size : 3000;
+    int rc = GSS_E_INPUT;
+
+    /* ---- options (gpssim.c:1739-1881) ---- */
+    if (opt->nav_file == NULL || opt->nav_file[0] == 0) {
+        rc = gss_fail(GSS_E_ARG, "ERROR: GPS ephemeris file is not specified.");
+        goto fail;
+    }
+    double fs = opt->samp_freq > 0 ? opt->samp_freq : 2.6e6;
+    if (fs < 1.0e6) {
+        rc = gss_fail(GSS_E_ARG, "ERROR: Invalid sampling frequency.");
+        goto fail;
+    }
+    int fmt = opt->data_format ? opt->data_format : GSS_FMT_SC16;
+    if (fmt != GSS_FMT_SC01 && fmt != GSS_FMT_SC08 && fmt != GSS_FMT_SC16) {
+        rc = gss_fail(GSS_E_ARG, "ERROR: Invalid I/Q data format.");
+        goto fail;
+    }
+    s->opt.data_format = fmt;
+    s->io.enable = opt->iono_disable ? 0 : 1;
+    /* -c/-l select static mode; so does the absence of a motion file (gpssim.c:1860-1867) */
+    s->static_mode = opt->has_xyz || opt->has_llh || opt->motion_file == NULL ||
+                     opt->motion_file[0] == 0;
+    double duration = opt->duration >= 0.0 ? opt->duration : (double)ums / 10.0;
+    if (duration < 0.0 || (duration > ((double)ums) / 10.0 && !s->static_mode) ||
+        (duration > K_STATIC_MAX_DUR && s->static_mode)) {
+        rc = gss_fail(GSS_E_ARG, "ERROR: Invalid duration.");
+        goto fail;
+    }
+    int iduration = (int)(duration * 10.0 + 0.5);
+
+    fs = floor(fs / 10.0);
+    s->n_per_blk = (int)fs;
+    fs *= 10.0;
+    s->samp_freq = fs;
+    s->delt = 1.0 / fs;
+    if (fmt == GSS_FMT_SC01 && (s->n_per_blk % 4) != 0) {
+        /* the reference overflows its 1-bit buffer here */
+        rc = gss_fail(GSS_E_ARG, "ERROR: -b 1 needs samples per 0.1 s divisible by 4.");
+        goto fail;
+    }
+
+    /* ---- receiver position (gpssim.c:1887-1917) ---- */
+    if (!s->static_mode) {
+        s->xyz = calloc((size_t)ums, sizeof *s->xyz);
+        if (s->xyz == NULL) { rc = gss_fail(GSS_E_NOMEM, "out of memory"); goto fail; }
+        int numd = opt->nmea ? motion_read_nmea(s->xyz, ums, opt->motion_file)
+                             : motion_read_csv(s->xyz, ums, opt->motion_file);
+        if (numd == -1) {
+            rc = gss_fail(GSS_E_IO, "ERROR: Failed to open user motion / NMEA GGA file.");
+            goto fail;
+        }
+        if (numd == 0) {
+            rc = gss_fail(GSS_E_INPUT, "ERROR: Failed to read user motion / NMEA GGA data.");
+            goto fail;
+        }
+        s->numd = numd > iduration ? iduration : numd;
+    } else {
+        s->xyz = calloc(1, sizeof *s->xyz);
+        if (s->xyz == NULL) { rc = gss_fail(GSS_E_NOMEM, "out of memory"); goto fail; }
+        if (opt->has_xyz) {
+            memcpy(s->xyz[0], opt->xyz, sizeof s->xyz[0]);
+        } else if (opt->has_llh) {
+            double llh[3] = {opt->llh[0] / K_R2D, opt->llh[1] / K_R2D, opt->llh[2]};
+            llh_to_ecef(llh, s->xyz[0]);
+        }
+        /* else: the reference's default (Tokyo) never reaches llh2xyz
+           and its observed behaviour is an earth-centre receiver: xyz stays {0,0,0}. */
+        msg(s, "Using static location mode.\n");
+        s->numd = iduration;
+    }
+
+    /* ---- ephemerides (gpssim.c:1926-1948) ---- */
+    s->neph = rinex_read(s->eph, &s->io, opt->nav_file);
+    if (s->neph == 0) { rc = gss_fail(GSS_E_INPUT, "ERROR: No ephemeris available."); goto fail; }
+    if (s->neph == -1) { rc = gss_fail(GSS_E_IO, "ERROR: ephemeris file not found."); goto fail; }
+    if (opt->verbose && s->io.vflg) {
+        msg(s, "  %12.3e %12.3e %12.3e %12.3e\n", s->io.alpha0, s->io.alpha1, s->io.alpha2,
+            s->io.alpha3);
+        msg(s, "  %12.3e %12.3e %12.3e %12.3e\n", s->io.beta0, s->io.beta1, s->io.beta2,
+            s->io.beta3);
+        msg(s, "   %19.11e %19.11e  %9d %9d\n", s->io.A0, s->io.A1, s->io.tot, s->io.wnt);
+        msg(s, "%6d\n", s->io.dtls);
+    }
+
+    /* ---- scenario start time (gpssim.c:1950-2039) ---- */
+    gtime_t gmin = {0, 0}, gmax = {0, 0};
+    dtime_t tmin = {0}, tmax = {0};
+    for (int sv = 0; sv < K_MAX_SAT; sv++)
+        if (s->eph[0][sv].vflg == 1) { gmin = s->eph[0][sv].toc; tmin = s->eph[0][sv].t; break; }
+    for (int sv = 0; sv < K_MAX_SAT; sv++)
+        if (s->eph[s->neph - 1][sv].vflg == 1) {
+            gmax = s->eph[s->neph - 1][sv].toc;
+            tmax = s->eph[s->neph - 1][sv].t;
+            break;
+        }
+    dtime_t t0;
+    gtime_t g0;
+    if (opt->has_start) {
+        t0.y = opt->start[0]; t0.m = opt->start[1]; t0.d = opt->start[2];
+        t0.hh = opt->start[3]; t0.mm = opt->start[4]; t0.sec = opt->start_sec;
+        gt_from_date(&t0, &g0);
+        if (opt->time_overwrite) {
+            /* move every TOC/TOE by the offset between the scenario start (2 h aligned)
+               and the file's first TOC (gpssim.c:1980-2014) */
+            gtime_t gt;
+            gt.week = g0.week;
+            gt.sec = (double)(((int)(g0.sec)) / 7200) * 7200.0;
+            double dsec = gt_diff(gt, gmin);
+            s->io.wnt = gt.week;
+            s->io.tot = (int)gt.sec;
+            for (int sv = 0; sv < K_MAX_SAT; sv++)
+                for (int i = 0; i < s->neph; i++) {
+                    eph_t *e = &s->eph[i][sv];
+                    if (e->vflg != 1)
+                        continue;
+                    gtime_t gn = gt_add(e->toc, dsec);
+                    dtime_t tn;
+                    gt_to_date(&gn, &tn);
+                    e->toc = gn;
+                    e->t = tn;
+                    e->toe = gt_add(e->toe, dsec);
+                }
+        } else if (gt_diff(g0, gmin) < 0.0 || gt_diff(gmax, g0) < 0.0) {
+            msg(s, "ERROR: Invalid start time.\n");
+            msg(s, "tmin = %4d/%02d/%02d,%02d:%02d:%02.0f (%d:%.0f)\n", tmin.y, tmin.m, tmin.d,
+                tmin.hh, tmin.mm, tmin.sec, gmin.week, gmin.sec);
+            msg(s, "tmax = %4d/%02d/%02d,%02d:%02d:%02.0f (%d:%.0f)\n", tmax.y, tmax.m, tmax.d,
+                tmax.hh, tmax.mm, tmax.sec, gmax.week, gmax.sec);
+            rc = gss_fail(GSS_E_INPUT, "ERROR: Invalid start time.");
+            goto fail;
+        }
+    } else {
+        g0 = gmin;
+        t0 = tmin;
+    }
+    s->g0 = g0;
+    msg(s, "Start time = %4d/%02d/%02d,%02d:%02d:%02.0f (%d:%.0f)\n", t0.y, t0.m, t0.d, t0.hh,
+        t0.mm, t0.sec, g0.week, g0.sec);
+    msg(s, "Duration = %.1f [sec]\n", ((double)s->numd) / 10.0);
+
+    /* ---- current ephemeris set: first set with a TOC within ±1 h (gpssim.c:2042-2067) ---- */
+    s->ieph = -1;
+    for (int i = 0; i < s->neph && s->ieph < 0; i++)
+        for (int sv = 0; sv < K_MAX_SAT; sv++)
+            if (s->eph[i][sv].vflg == 1) {
+                double dt = gt_diff(g0, s->eph[i][sv].toc);
+                if (dt >= -K_SEC_HOUR && dt < K_SEC_HOUR) {
+                    s->ieph = i;
+                    break;
+                }
+            }
+    if (s->ieph == -1) {
+        rc = gss_fail(GSS_E_INPUT, "ERROR: No current set of ephemerides has been found.");
+        goto fail;
+    }
+
+    /* ---- channels (gpssim.c:2117-2143) ---- */
+    for (int i = 0; i < K_MAX_CHAN; i++)
+        s->chan[i].prn = 0;
+    for (int sv = 0; sv < K_MAX_SAT; sv++)
+        s->alloc_sat[sv] = -1;
+    s->grx = gt_add(g0, 0.0);
+    rc = allocate_channels(s, s->eph[s->ieph], s->grx, s->xyz[0]);
+    if (rc < 0)
+        goto fail;
+    print_channels(s);
+    for (int i = 0; i < 37; i++)
+        s->ant_pat[i] = pow(10.0, -gss_ant_pat_db[i] / 20.0);
+
+    s->grx = gt_add(s->grx, 0.1);
+    s->iumd = 1;
+    *out = s;
+    return 0;
+fail:
+    gss_scn_close(s);
+    return rc;
+}
+
+int gss_scn_info(const gss_scn *s, gss_scn_info_t *info)
+{
+    if (s == NULL || info == NULL)
+        return gss_fail(GSS_E_ARG, "null argument");
+    info->n_per_blk = s->n_per_blk;
+    info->n_blocks = s->numd > 1 ? s->numd - 1 : 0;
+    info->data_format = s->opt.data_format;
+    info->samp_freq = s->samp_freq;
+    info->delt = s->delt;
+    info->week = s->g0.week;
+    info->sec = s->g0.sec;
+    return 0;
+}
+
+/* ---- exact carrier planner ------------------------------------------------------------------
+ * One chain per channel slot; a slot's chain restarts whenever allocateChannel re-initialises
+ * its carr_phase.  Slots are independent, so the planner runs one slot per thread. */
+typedef struct {
+    gss_scn *s;
+    gss_chan_blk_t *blk;
+    const int32_t *nch;
+    int nblk, slot_lo, slot_hi;
+} plan_job;
+
+static void *plan_slots(void *arg)
+{
+    plan_job *j = arg;
+    gss_scn *s = j->s;
+    for (int slot = j->slot_lo; slot < j->slot_hi; slot++) {
+        double x = s->carr[slot];
+        for (int b = 0; b < j->nblk; b++) {
+            for (int k = 0; k < j->nch[b]; k++) {
+                size_t e = (size_t)b * GSS_MAXCH + k;
+                if (s->b_slot[e] != slot)
+                    continue;
+                if (s->b_reset[e])
+                    x = s->b_init[e];
+                j->blk[e].carr0 = x;
+                x = gss_carr_walk(x, j->blk[e].carr_step, s->n_per_blk);
+                break;
+            }
+        }
+        s->carr[slot] = x;
+    }
+    return NULL;
+}
+
+static void plan_batch(gss_scn *s, gss_chan_blk_t *blk, const int32_t *nch, int nblk, int threads)
+{
+    if (threads < 1)
+        threads = 1;
+    if (threads > K_MAX_CHAN)
+        threads = K_MAX_CHAN;
+    pthread_t tid[K_MAX_CHAN];
+    plan_job job[K_MAX_CHAN];
+    int per = (K_MAX_CHAN + threads - 1) / threads;
+    int started = 0;
+    for (int t = 0; t < threads; t++) {
+        job[t] = (plan_job){s, blk, nch, nblk, t * per, (t + 1) * per};
+        if (job[t].slot_hi > K_MAX_CHAN)
+            job[t].slot_hi = K_MAX_CHAN;
+        if (job[t].slot_lo >= job[t].slot_hi)
+            break;
+        if (threads == 1 || pthread_create(&tid[t], NULL, plan_slots, &job[t]) != 0)
+            plan_slots(&job[t]);
+        else
+            started |= 1 << t;
+        (void)0;
+    }
+    for (int t = 0; t < threads; t++)
+        if (started & (1 << t))
+            pthread_join(tid[t], NULL);
+}
+
+int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, int *n_out,
+                 int threads)
+{
+    *n_out = 0;
+    if (s == NULL || blk == NULL || nch == NULL || max_blocks <= 0)
+        return gss_fail(GSS_E_ARG, "invalid argument");
+    double t_start = wall_now();
+    if (max_blocks > s->batch_cap) {
+        free(s->b_slot); free(s->b_reset); free(s->b_init);
+        size_t n = (size_t)max_blocks * GSS_MAXCH;
+        s->b_slot = malloc(n);
+        s->b_reset = malloc(n);
+        s->b_init = malloc(n * sizeof(double));
+        if (!s->b_slot || !s->b_reset || !s->b_init)
+            return gss_fail(GSS_E_NOMEM, "out of memory");
+        s->batch_cap = max_blocks;
+    }
+
+    int nb = 0;
+    while (nb < max_blocks && s->iumd < s->numd) {
+        const double *xyz = s->static_mode ? s->xyz[0] : s->xyz[s->iumd];
+        gss_chan_blk_t *row = blk + (size_t)nb * GSS_MAXCH;
+        int k = 0;
+
+        /* ---- per-block refresh (gpssim.c:2156-2188) ---- */
+        for (int i = 0; i < K_MAX_CHAN; i++) {
+            chan_t *ch = &s->chan[i];
+            if (ch->prn <= 0)
+                continue;
+            rng_t rho;
+            sv_range(&rho, &s->eph[s->ieph][ch->prn - 1], &s->io, s->grx, xyz);
+            ch->azel[0] = rho.azel[0];
+            ch->azel[1] = rho.azel[1];
+
+            /* computeCodePhase(chan, rho, 0.1), gpssim.c:1317-1351 */
+            double rhorate = (rho.range - ch->rho0.range) / 0.1;
+            ch->f_carr = -rhorate / K_LAMBDA_L1;
+            ch->f_code = K_CODE_FREQ + ch->f_carr * K_CARR_TO_CODE;
+            double ms = ((gt_diff(ch->rho0.g, ch->g0) + 6.0) - ch->rho0.range / K_C) * 1000.0;
+            int ims = (int)ms;
+            ch->code_phase = (ms - (double)ims) * K_CA_LEN;
+            ch->iword = ims / 600;
+            ims -= ch->iword * 600;
+            ch->ibit = ims / 20;
+            ims -= ch->ibit * 20;
+            ch->icode = ims;
+            ch->rho0 = rho;
+
+            /* gain: path loss × antenna pattern, scaled 2^7 (gpssim.c:2179-2186) */
+            double path_loss = 20200000.0 / rho.d;
+            int ibs = (int)((90.0 - rho.azel[1] * K_R2D) / 5.0);
+            double ant_gain = s->ant_pat[ibs];
+            int gain = (int)(path_loss * ant_gain * 128.0);
+
+            gss_chan_blk_t *p = &row[k];
+            p->carr0 = 0.0;                        /* filled by the planner */
+            p->carr_step = ch->f_carr * s->delt;
+            p->code0 = ch->code_phase;
+            p->code_step = ch->f_code * s->delt;
+            p->icode = ch->icode;
+            p->ibit = ch->ibit;
+            p->iword = ch->iword;
+            p->gain = gain;
+            p->ca_tbl = ch->prn - 1;
+            p->nav_tbl = ch->nav_row;
+            size_t e = (size_t)nb * GSS_MAXCH + k;
+            s->b_slot[e] = (int8_t)i;
+            s->b_reset[e] = (uint8_t)ch->carr_fresh;
+            s->b_init[e] = ch->carr_phase;
+            ch->carr_fresh = 0;
+            k++;
+        }
+        for (int r = k; r < GSS_MAXCH; r++)
+            memset(&row[r], 0, sizeof row[r]);
+        nch[nb] = k;
+        nb++;
+
+        /* ---- 30 s update: nav message, ephemeris set, allocation (gpssim.c:2294-2345) ---- */
+        int igrx = (int)(s->grx.sec * 10.0 + 0.5);
+        if (igrx % 300 == 0) {
+            for (int i = 0; i < K_MAX_CHAN; i++)
+                if (s->chan[i].prn > 0) {
+                    nav_frame(s->grx, &s->chan[i], 0);
+                    int rc = nav_push(s, &s->chan[i]);
+                    if (rc)
+                        return rc;
+                }
+            /* step to the next ephemeris set when its TOC is < 1 h away; only the first valid
+               SV of that set is tested (gpssim.c:2307-2326).  New subframes reach dwrd at the
+               next 30 s update. */
+            for (int sv = 0; sv < K_MAX_SAT; sv++) {
+                if (s->eph[s->ieph + 1][sv].vflg == 1) {
+                    double dt = gt_diff(s->eph[s->ieph + 1][sv].toc, s->grx);
+                    if (dt < K_SEC_HOUR) {
+                        s->ieph++;
+                        for (int i = 0; i < K_MAX_CHAN; i++)
+                            if (s->chan[i].prn != 0)
+                                nav_subframes(&s->eph[s->ieph][s->chan[i].prn - 1], &s->io,
+                                              s->chan[i].sbf);
+                    }
+                    break;
+                }
+            }
+            int rc = allocate_channels(s, s->eph[s->ieph], s->grx, xyz);
+            if (rc < 0)
+                return rc;
+            if (s->opt.verbose) {
+                msg(s, "\n");
+                print_channels(s);
+            }
+        }
+
+        s->grx = gt_add(s->grx, 0.1);
+        msg(s, "\rTime into run = %4.1f", gt_diff(s->grx, s->g0));
+        s->iumd++;
+    }
+
+    plan_batch(s, blk, nch, nb, threads);
+    s->plan_sec += wall_now() - t_start;
+    *n_out = nb;
+    return 0;
+}
+
+int gss_scn_nav_table(const gss_scn *s, const uint32_t **rows, int *n_rows)
+{
+    if (s == NULL)
+        return gss_fail(GSS_E_ARG, "null scenario");
+    *rows = s->nav_rows;
+    *n_rows = s->n_nav;
+    return 0;
+}
+
+double gss_scn_plan_seconds(const gss_scn *s) { return s ? s->plan_sec : 0.0; }
+
+int gss_scn_close(gss_scn *s)
+{
+    if (s == NULL)
+        return 0;
+    free(s->xyz);
+    free(s->nav_rows);
+    free(s->b_slot);
+    free(s->b_reset);
+    free(s->b_init);
+    free(s);
+    return 0;
+}
+
+/* ---- small exported helpers ----------------------------------------------------------------- */
+int gss_ca_table(uint32_t *out)
+{
+    int8_t ca[K_CA_LEN];
+    for (int prn = 1; prn <= 32; prn++) {
+        ca_generate(ca, prn);
+        ca_pack(ca, out + (size_t)(prn - 1) * GSS_CA_WORDS);
+    }
+    return 0;
+}
+
+double gss_carr_advance(double carr, double step, int64_t n)
+{
+    return gss_carr_walk(carr, step, n);
+}
+
+double gss_code_advance(double code, double step, int64_t n, int32_t *icode, int32_t *ibit,
+                        int32_t *iword)
+{
+    gss_code_state c = {code, *icode, *ibit, *iword};
+    gss_code_walk(&c, step, n);
+    *icode = c.icode;
+    *ibit = c.ibit;
+    *iword = c.iword;
+    return c.ph;
+}
+
+/* Carrier tables (gpssim.c:15-83): round(250 sin(2π(k+½)/512)) on a quarter wave, except the
+   reference's entry 35 (and its mirrors) which is 105, not 106; the rest follows from
+   sin(π-x)=sin x, sin(x+π)=-sin x and cos x = sin(x+π/2). */
+int gss_lut(int32_t *sin512, int32_t *cos512)
+{
+    int32_t q[128];
+    for (int k = 0; k < 128; k++)
+        q[k] = (int32_t)lround(250.0 * sin(2.0 * 3.14159265358979323846 * (k + 0.5) / 512.0));
+    q[35] = 105;
+    for (int k = 0; k < 512; k++) {
+        int h = k & 255;
+        int32_t v = h < 128 ? q[h] : q[255 - h];
+        sin512[k] = k < 256 ? v : -v;
+    }
+    for (int k = 0; k < 512; k++)
+        cos512[k] = sin512[(k + 128) & 511];
+    return 0;
+}
+
+const char *gss_version(void) { return "gpssim_amd 0.1 (gfx950)"; }

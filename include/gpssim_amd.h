@@ -1,0 +1,185 @@
+/*
+ * gpssim_amd.h — C ABI of the MI355X-native GPS L1 C/A baseband synthesiser.
+ *
+ * The reference (TheShinning/gps-sdr-sim) has no plugin/FFI API: its hot path is inline code in
+ * main() (gpssim.c:2190-2288) operating on locals chan[MAX_CHAN], gain[], iq_buff, iq8_buff, delt,
+ * iq_buff_size and data_format (gpssim.c:1686-1716).  The seam this library exports is therefore
+ * "synthesise K consecutive 0.1 s blocks given per-block channel parameters" (SURVEY.md §8b), plus
+ * the host control plane that produces those parameters (gpssim.c:1672-2353 minus the sample loop).
+ *
+ * Two layers, one shared library (libgpssim_amd.so):
+ *   1. Device layer (gss_dev_*, gss_synth_*): the hot path.  Replaces the per-sample loop
+ *      gpssim.c:2190-2264 and the quantise/pack epilogue gpssim.c:2257-2288.  Plain pointers and
+ *      sizes only; results are stream-ordered on the caller's HIP stream.
+ *   2. Host layer (gss_scn_*): ephemeris parsing, 10 Hz range/Doppler refresh, nav message and
+ *      channel allocation, and the exact carrier-phase planner.  Replaces gpssim.c:1672-2188 and
+ *      2290-2353 (everything in main() around the sample loop).
+ *
+ * Error convention: every entry point returns 0 on success and a negative GSS_E* code on failure;
+ * gss_last_error() returns a human-readable message for the calling thread.  Nothing here calls
+ * exit(); the CLI (gps-sdr-sim) turns a failure into the reference's fprintf(stderr,…); exit(1).
+ * Threading: a gss_dev / gss_scn handle is not thread-safe; use one host thread per GPU.
+ */
+#ifndef GPSSIM_AMD_H
+#define GPSSIM_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSS_MAXCH      16    /* MAX_CHAN, gpssim.h:16 */
+#define GSS_CA_LEN     1023  /* CA_SEQ_LEN, gpssim.h:36 */
+#define GSS_CA_WORDS   32    /* 1023 chips packed 32 per uint32 (bit j%32 of word j/32) */
+#define GSS_NAV_WORDS  60    /* N_DWRD, gpssim.h:33 */
+
+/* data formats: -b 1 / 8 / 16 (SC01/SC08/SC16, gpssim.h:77-79) */
+#define GSS_FMT_SC01   1
+#define GSS_FMT_SC08   8
+#define GSS_FMT_SC16   16
+
+#define GSS_OK           0
+#define GSS_E_ARG       -1   /* invalid argument */
+#define GSS_E_HIP       -2   /* HIP runtime error */
+#define GSS_E_NOMEM     -3   /* allocation failed */
+#define GSS_E_IO        -4   /* file open/read/write failed */
+#define GSS_E_INPUT     -5   /* invalid input data (RINEX, motion file, start time …) */
+#define GSS_E_STATE     -6   /* call out of order / exhausted */
+#define GSS_E_NODEV     -7   /* no GPU / kernel image unavailable */
+#define GSS_E_RANGE     -8   /* nav-word index ran past dwrd[59] (gpssim.c:2229-2232 overflow) */
+
+/* ------------------------------------------------------------------------------------------ */
+/* Per (block, channel) parameters: everything the sample loop reads.        */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct gss_chan_blk {
+    double  carr0;      /* chan[i].carr_phase at the block's first sample [cycles], FLOAT_CARR_PHASE
+                           (gpssim.h:4).  Carried across blocks by the exact planner (gss_scn_*).   */
+    double  carr_step;  /* chan[i].f_carr * delt, re-multiplied each sample in gpssim.c:2245       */
+    double  code0;      /* chan[i].code_phase after computeCodePhase (gpssim.c:1334) [chips]       */
+    double  code_step;  /* chan[i].f_code * delt (gpssim.c:2212)                                   */
+    int32_t icode;      /* gpssim.c:1342 */
+    int32_t ibit;       /* gpssim.c:1339 */
+    int32_t iword;      /* gpssim.c:1336 */
+    int32_t gain;       /* gain[i] (gpssim.c:2186), scaled by 2^7                                 */
+    int32_t ca_tbl;     /* row of the ca_bits table (normally prn-1)                               */
+    int32_t nav_tbl;    /* row of the dwrd table (chan[i].dwrd version)                            */
+} gss_chan_blk_t;       /* 56 bytes; blocks are laid out [nblk][GSS_MAXCH], first nch[b] valid     */
+
+/* ------------------------------------------------------------------------------------------ */
+/* Device layer                                                                                */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct gss_dev gss_dev;
+
+/* Open device `ordinal` (hipSetDevice).  Fails with GSS_E_NODEV when no GPU is visible.       */
+int gss_dev_open(gss_dev **out, int ordinal);
+int gss_dev_close(gss_dev *d);
+
+/* Pre-size the checkpoint workspace for batches of up to `max_blocks` blocks of `n_per_blk`
+   samples, so that gss_synth_device() performs no allocation (graph-capturable).              */
+int gss_dev_reserve(gss_dev *d, int max_blocks, int n_per_blk);
+
+/* Bytes of output one block produces: n*4 (SC16), n*2 (SC08), n/4 (SC01; n%4==0 required,
+   see SURVEY.md Appendix A.4).  Returns 0 for an invalid format.                              */
+size_t gss_block_bytes(int n_per_blk, int fmt);
+
+/* Synthesise nblk consecutive 0.1 s blocks.  ALL pointers are device pointers:
+     blk      [nblk][GSS_MAXCH] channel parameters (first nch[b] of each row valid)
+     nch      [nblk] active channel count per block (0..16)
+     ca_bits  [n_ca][GSS_CA_WORDS] packed C/A chips (codegen, gpssim.c:132-171)
+     nav      [n_nav][GSS_NAV_WORDS] 30-bit nav words (chan[i].dwrd, gpssim.c:1467-1547)
+     out      nblk * gss_block_bytes(n_per_blk, fmt) bytes, exactly the bytes the reference
+              fwrite()s for those blocks (gpssim.c:2276/2283/2287), concatenated in block order
+     carr_end optional [nblk][GSS_MAXCH]: carrier phase after the block's last sample
+     status   optional int32[1]: set non-zero if a nav-word index ran past 59
+   stream is a hipStream_t (NULL = default stream).  Asynchronous; no host synchronisation.    */
+int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
+                     const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
+                     int nblk, int n_per_blk, int fmt, void *out, double *carr_end,
+                     int32_t *status, void *stream);
+
+/* Same, from host buffers: uploads inputs, runs, downloads `out` (and carr_end if non-NULL),
+   synchronises.  Convenience for the CLI and tests; the bench uses gss_synth_device().        */
+int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
+                   const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
+                   int nblk, int n_per_blk, int fmt, void *out, double *carr_end);
+
+/* Duration in ms of the last synthesis kernel launches on `d` measured with HIP events on the
+   launch stream (checkpoint stage, synthesis stage).  Only valid after a synchronising call.  */
+int gss_dev_last_timing(gss_dev *d, float *ckpt_ms, float *synth_ms);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Host layer: scenario driver mirroring main() (gpssim.c:1672-2353)                           */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct gss_opts {
+    const char *nav_file;       /* -e  RINEX v2 navigation file (required)                     */
+    const char *motion_file;    /* -u  user motion CSV / -g NMEA GGA (NULL: static)            */
+    int    nmea;                /* 1 if motion_file is NMEA GGA (-g)                           */
+    int    has_xyz;             /* -c given: xyz holds ECEF [m]                                */
+    double xyz[3];
+    int    has_llh;             /* -l given: llh holds lat [deg], lon [deg], height [m]        */
+    double llh[3];
+    double samp_freq;           /* -s [Hz], default 2.6e6                                      */
+    int    data_format;         /* -b 1/8/16, default 16                                       */
+    double duration;            /* -d [s]; <0 → default USER_MOTION_SIZE/10                    */
+    int    has_start;           /* -t / -T given                                               */
+    int    time_overwrite;      /* -T                                                          */
+    int    start[6];            /* y m d hh mm ss (already validated & floor()ed by caller)     */
+    double start_sec;
+    int    iono_disable;        /* -i                                                          */
+    int    verbose;             /* -v                                                          */
+    int    user_motion_size;    /* USER_MOTION_SIZE (gpssim.h:19-21), 0 → 3000                 */
+    int    quiet;               /* suppress the reference's stderr chatter (library use)       */
+} gss_opts_t;
+
+typedef struct gss_scn_info {
+    int    n_per_blk;           /* iq_buff_size = floor(fs/10) (gpssim.c:1877-1878)            */
+    int    n_blocks;            /* numd-1: blocks the run writes (gpssim.c:2154)               */
+    int    data_format;
+    double samp_freq;           /* after rounding to a multiple of 10 Hz                       */
+    double delt;                /* 1/samp_freq (gpssim.c:1881)                                 */
+    int    week;  double sec;   /* g0 (start time)                                             */
+} gss_scn_info_t;
+
+typedef struct gss_scn gss_scn;
+
+/* Parse inputs, select ephemeris set and start time, allocate the first channels.
+   On error returns GSS_E_* and *out stays NULL (message via gss_last_error()).               */
+int gss_scn_open(gss_scn **out, const gss_opts_t *opt);
+int gss_scn_info(const gss_scn *s, gss_scn_info_t *info);
+
+/* Produce parameters for the next up to `max_blocks` blocks (in run order), including the
+   exact carrier phase at each block start (planner runs on `threads` host threads).
+   blk is [max_blocks][GSS_MAXCH], nch is [max_blocks].  *n_out = blocks produced (0 at end).  */
+int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, int *n_out,
+                 int threads);
+
+/* Nav-word table rows produced so far ([n][GSS_NAV_WORDS]); valid until the next gss_scn_next. */
+int gss_scn_nav_table(const gss_scn *s, const uint32_t **rows, int *n_rows);
+
+/* Packed C/A codes for PRN 1..32 into out[32][GSS_CA_WORDS] (row prn-1).                      */
+int gss_ca_table(uint32_t *out);
+
+/* Wall time [s] the host planner spent so far (control plane + carrier chain).                */
+double gss_scn_plan_seconds(const gss_scn *s);
+
+int gss_scn_close(gss_scn *s);
+
+/* Exact carrier-chain helpers (exported for tests): advance the reference recurrence
+   carr += step; wrap into [0,1) (gpssim.c:2245-2250) by n samples, exactly.                   */
+double gss_carr_advance(double carr, double step, int64_t n);
+/* Same for the code phase with its chip/bit/word counters (gpssim.c:2212-2241).               */
+double gss_code_advance(double code, double step, int64_t n, int32_t *icode, int32_t *ibit,
+                        int32_t *iword);
+
+/* The 512-entry carrier tables the sample loop uses (gpssim.c:15-83), generated.             */
+int gss_lut(int32_t *sin512, int32_t *cos512);
+
+const char *gss_last_error(void);
+const char *gss_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPSSIM_AMD_H */
