@@ -1,0 +1,275 @@
+"""Python binding of libgpssim_amd.so (C ABI declared in include/gpssim_amd.h).
+
+The product is the C library: a host control plane (gss_scn_*) mirroring gpssim.c's main() and a
+gfx950 HIP hot path (gss_synth_*) replacing its per-sample loop (gpssim.c:2190-2288).  This module
+is plumbing for the tests and bench: ctypes prototypes, numpy views of the parameter rows, and
+thin wrappers.  There is no Python or CPU implementation of the synthesis here: when the shared
+library or a GPU is missing, the calls raise.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libgpssim_amd.so")
+CLI_PATH = os.path.join(PKG_DIR, "bin", "gps-sdr-sim")
+
+MAXCH = 16
+CA_WORDS = 32
+NAV_WORDS = 60
+FMT_SC01, FMT_SC08, FMT_SC16 = 1, 8, 16
+
+# gss_chan_blk_t (56 bytes), gpssim_amd.h
+CHAN_DTYPE = np.dtype([
+    ("carr0", "<f8"), ("carr_step", "<f8"), ("code0", "<f8"), ("code_step", "<f8"),
+    ("icode", "<i4"), ("ibit", "<i4"), ("iword", "<i4"), ("gain", "<i4"),
+    ("ca_tbl", "<i4"), ("nav_tbl", "<i4"),
+])
+assert CHAN_DTYPE.itemsize == 56
+
+
+class GssError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"gpssim_amd error {code}: {msg}")
+        self.code = code
+
+
+class _Opts(C.Structure):
+    _fields_ = [
+        ("nav_file", C.c_char_p), ("motion_file", C.c_char_p), ("nmea", C.c_int),
+        ("has_xyz", C.c_int), ("xyz", C.c_double * 3), ("has_llh", C.c_int),
+        ("llh", C.c_double * 3), ("samp_freq", C.c_double), ("data_format", C.c_int),
+        ("duration", C.c_double), ("has_start", C.c_int), ("time_overwrite", C.c_int),
+        ("start", C.c_int * 6), ("start_sec", C.c_double), ("iono_disable", C.c_int),
+        ("verbose", C.c_int), ("user_motion_size", C.c_int), ("quiet", C.c_int),
+    ]
+
+
+class _Info(C.Structure):
+    _fields_ = [("n_per_blk", C.c_int), ("n_blocks", C.c_int), ("data_format", C.c_int),
+                ("samp_freq", C.c_double), ("delt", C.c_double), ("week", C.c_int),
+                ("sec", C.c_double)]
+
+
+_lib = None
+
+# name -> (restype, argtypes); every symbol include/gpssim_amd.h declares
+_P = C.c_void_p
+_SIGS = {
+    "gss_dev_open": (C.c_int, [C.POINTER(_P), C.c_int]),
+    "gss_dev_close": (C.c_int, [_P]),
+    "gss_dev_reserve": (C.c_int, [_P, C.c_int, C.c_int]),
+    "gss_block_bytes": (C.c_size_t, [C.c_int, C.c_int]),
+    "gss_synth_device": (C.c_int, [_P, _P, _P, C.c_int, _P, C.c_int, _P, C.c_int, C.c_int,
+                                   C.c_int, C.c_int, _P, _P, _P, _P]),
+    "gss_synth_host": (C.c_int, [_P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int,
+                                 C.c_int, _P, _P]),
+    "gss_dev_timing": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_float),
+                                 C.POINTER(C.c_float)]),
+    "gss_scn_open": (C.c_int, [C.POINTER(_P), C.POINTER(_Opts)]),
+    "gss_scn_info": (C.c_int, [_P, C.POINTER(_Info)]),
+    "gss_scn_next": (C.c_int, [_P, C.c_int, _P, _P, C.POINTER(C.c_int), C.c_int]),
+    "gss_scn_nav_table": (C.c_int, [_P, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_int)]),
+    "gss_ca_table": (C.c_int, [_P]),
+    "gss_scn_plan_seconds": (C.c_double, [_P]),
+    "gss_scn_close": (C.c_int, [_P]),
+    "gss_carr_advance": (C.c_double, [C.c_double, C.c_double, C.c_int64]),
+    "gss_code_advance": (C.c_double, [C.c_double, C.c_double, C.c_int64,
+                                      C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                      C.POINTER(C.c_int32)]),
+    "gss_lut": (C.c_int, [_P, _P]),
+    "gss_last_error": (C.c_char_p, []),
+    "gss_version": (C.c_char_p, []),
+}
+EXPORTED = tuple(_SIGS)
+
+
+def lib():
+    """Load the in-tree shared library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} missing: run `make -C gps-sdr-sim_amd` "
+                          "(or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise GssError(rc, lib().gss_last_error().decode(errors="replace"))
+
+
+def _ptr(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def block_bytes(n_per_blk, fmt):
+    return int(lib().gss_block_bytes(n_per_blk, fmt))
+
+
+def ca_table():
+    out = np.zeros((32, CA_WORDS), np.uint32)
+    _check(lib().gss_ca_table(_ptr(out)))
+    return out
+
+
+def lut():
+    s = np.zeros(512, np.int32)
+    c = np.zeros(512, np.int32)
+    _check(lib().gss_lut(_ptr(s), _ptr(c)))
+    return s, c
+
+
+def carr_advance(carr, step, n):
+    return lib().gss_carr_advance(carr, step, n)
+
+
+def code_advance(code, step, n, icode, ibit, iword):
+    a, b, c = C.c_int32(icode), C.c_int32(ibit), C.c_int32(iword)
+    ph = lib().gss_code_advance(code, step, n, C.byref(a), C.byref(b), C.byref(c))
+    return ph, a.value, b.value, c.value
+
+
+class Scenario:
+    """Host control plane: gpssim.c's main() around the sample loop (gss_scn_*)."""
+
+    def __init__(self, nav_file, *, llh=None, xyz=None, motion_file=None, nmea=False,
+                 samp_freq=2.6e6, data_format=16, duration=None, start=None,
+                 time_overwrite=False, iono=True, verbose=False, quiet=True,
+                 user_motion_size=3000):
+        self._keep = []
+        o = _Opts()
+        o.nav_file = self._s(nav_file)
+        o.motion_file = self._s(motion_file) if motion_file else None
+        o.nmea = int(bool(nmea))
+        if xyz is not None:
+            o.has_xyz = 1
+            o.xyz[:] = list(map(float, xyz))
+        if llh is not None:
+            o.has_llh = 1
+            o.llh[:] = list(map(float, llh))
+        o.samp_freq = float(samp_freq)
+        o.data_format = int(data_format)
+        o.duration = -1.0 if duration is None else float(duration)
+        if start is not None:
+            o.has_start = 1
+            o.start[:] = [int(v) for v in start[:5]] + [int(start[5])]
+            o.start_sec = float(start[5])
+            o.time_overwrite = int(bool(time_overwrite))
+        o.iono_disable = 0 if iono else 1
+        o.verbose = int(bool(verbose))
+        o.user_motion_size = int(user_motion_size)
+        o.quiet = int(bool(quiet))
+        self._h = C.c_void_p()
+        _check(lib().gss_scn_open(C.byref(self._h), C.byref(o)))
+        inf = _Info()
+        _check(lib().gss_scn_info(self._h, C.byref(inf)))
+        self.n_per_blk, self.n_blocks = inf.n_per_blk, inf.n_blocks
+        self.data_format, self.samp_freq, self.delt = inf.data_format, inf.samp_freq, inf.delt
+        self.start_week, self.start_sec = inf.week, inf.sec
+
+    def _s(self, v):
+        b = str(v).encode()
+        self._keep.append(b)
+        return b
+
+    def next(self, max_blocks, threads=8):
+        """Next batch: (blk[nb, 16] CHAN_DTYPE, nch[nb] int32)."""
+        blk = np.zeros((max_blocks, MAXCH), CHAN_DTYPE)
+        nch = np.zeros(max_blocks, np.int32)
+        nb = C.c_int(0)
+        _check(lib().gss_scn_next(self._h, max_blocks, _ptr(blk), _ptr(nch), C.byref(nb),
+                                  threads))
+        return blk[: nb.value].copy(), nch[: nb.value].copy()
+
+    def all_blocks(self, batch=500, threads=8):
+        bs, ns = [], []
+        while True:
+            b, n = self.next(batch, threads)
+            if len(n) == 0:
+                break
+            bs.append(b)
+            ns.append(n)
+        if not ns:
+            return np.zeros((0, MAXCH), CHAN_DTYPE), np.zeros(0, np.int32)
+        return np.concatenate(bs), np.concatenate(ns)
+
+    def nav_table(self):
+        rows = C.POINTER(C.c_uint32)()
+        n = C.c_int(0)
+        _check(lib().gss_scn_nav_table(self._h, C.byref(rows), C.byref(n)))
+        if n.value == 0:
+            return np.zeros((1, NAV_WORDS), np.uint32)
+        return np.ctypeslib.as_array(rows, shape=(n.value, NAV_WORDS)).copy()
+
+    def plan_seconds(self):
+        return lib().gss_scn_plan_seconds(self._h)
+
+    def close(self):
+        if self._h:
+            lib().gss_scn_close(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Device:
+    """One GPU (gss_dev_*).  synth_host() moves host arrays; synth_device() takes raw device
+    pointers (e.g. torch tensors' data_ptr()) and is stream-ordered."""
+
+    def __init__(self, ordinal=0):
+        self._h = C.c_void_p()
+        _check(lib().gss_dev_open(C.byref(self._h), int(ordinal)))
+
+    def reserve(self, max_blocks, n_per_blk):
+        _check(lib().gss_dev_reserve(self._h, max_blocks, n_per_blk))
+
+    def synth_host(self, blk, nch, ca, nav, n_per_blk, fmt, want_carr_end=False):
+        blk = np.ascontiguousarray(blk, CHAN_DTYPE)
+        nch = np.ascontiguousarray(nch, np.int32)
+        ca = np.ascontiguousarray(ca, np.uint32)
+        nav = np.ascontiguousarray(nav, np.uint32)
+        nblk = len(nch)
+        out = np.empty(nblk * block_bytes(n_per_blk, fmt), np.uint8)
+        cend = np.zeros((nblk, MAXCH), np.float64) if want_carr_end else None
+        _check(lib().gss_synth_host(self._h, _ptr(blk), _ptr(nch), _ptr(ca), len(ca),
+                                    _ptr(nav), len(nav), nblk, n_per_blk, fmt, _ptr(out),
+                                    _ptr(cend)))
+        return (out, cend) if want_carr_end else out
+
+    def synth_device(self, blk_ptr, nch_ptr, nch_max, ca_ptr, n_ca, nav_ptr, n_nav, nblk,
+                     n_per_blk, fmt, out_ptr, carr_end_ptr=0, status_ptr=0, stream=0):
+        _check(lib().gss_synth_device(self._h, blk_ptr, nch_ptr, nch_max, ca_ptr, n_ca, nav_ptr,
+                                      n_nav, nblk, n_per_blk, fmt, out_ptr,
+                                      carr_end_ptr or None, status_ptr or None, stream or None))
+
+    def timing_reset(self):
+        _check(lib().gss_dev_timing(self._h, 1, None, None, None))
+
+    def timing(self):
+        """(launches, avg checkpoint-stage ms, avg synthesis-stage ms) since the last reset."""
+        n, a, b = C.c_int(), C.c_float(), C.c_float()
+        _check(lib().gss_dev_timing(self._h, 0, C.byref(n), C.byref(a), C.byref(b)))
+        return n.value, a.value, b.value
+
+    def close(self):
+        if self._h:
+            lib().gss_dev_close(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

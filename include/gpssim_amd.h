@@ -87,6 +87,8 @@ size_t gss_block_bytes(int n_per_blk, int fmt);
 /* Synthesise nblk consecutive 0.1 s blocks.  ALL pointers are device pointers:
      blk      [nblk][GSS_MAXCH] channel parameters (first nch[b] of each row valid)
      nch      [nblk] active channel count per block (0..16)
+     nch_max  host-side upper bound of nch[] over the batch (selects the kernel instance;
+              blocks with fewer channels are padded with silent channels)
      ca_bits  [n_ca][GSS_CA_WORDS] packed C/A chips (codegen, gpssim.c:132-171)
      nav      [n_nav][GSS_NAV_WORDS] 30-bit nav words (chan[i].dwrd, gpssim.c:1467-1547)
      out      nblk * gss_block_bytes(n_per_blk, fmt) bytes, exactly the bytes the reference
@@ -94,7 +96,7 @@ size_t gss_block_bytes(int n_per_blk, int fmt);
      carr_end optional [nblk][GSS_MAXCH]: carrier phase after the block's last sample
      status   optional int32[1]: set non-zero if a nav-word index ran past 59
    stream is a hipStream_t (NULL = default stream).  Asynchronous; no host synchronisation.    */
-int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
+int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch, int nch_max,
                      const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
                      int nblk, int n_per_blk, int fmt, void *out, double *carr_end,
                      int32_t *status, void *stream);
@@ -105,9 +107,11 @@ int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
                    const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
                    int nblk, int n_per_blk, int fmt, void *out, double *carr_end);
 
-/* Duration in ms of the last synthesis kernel launches on `d` measured with HIP events on the
-   launch stream (checkpoint stage, synthesis stage).  Only valid after a synchronising call.  */
-int gss_dev_last_timing(gss_dev *d, float *ckpt_ms, float *synth_ms);
+/* Kernel timing from HIP events recorded on the launch stream around each stage of every
+   gss_synth_device() call (ring of the last 256 calls).  reset!=0 clears the ring (no sync);
+   otherwise waits for the last call and returns the number of calls n and the average duration
+   [ms] of the checkpoint stage and of the synthesis stage over them.                          */
+int gss_dev_timing(gss_dev *d, int reset, int *n, float *ckpt_ms, float *synth_ms);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Host layer: scenario driver mirroring main() (gpssim.c:1672-2353)                           */

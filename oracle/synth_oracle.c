@@ -132,3 +132,36 @@ int oracle_synth(const gss_chan_blk_t *blk, const int32_t *nch, const uint32_t *
     return status;
 }
 
+
+/* Brute-force reference recurrences (one double step per sample, gpssim.c:2212-2250), used by
+   the tests to check the product's jump-ahead walk. */
+double oracle_carr_brute(double x, double s, int64_t n)
+{
+    for (int64_t i = 0; i < n; i++) {
+        x += s;
+        if (x >= 1.0)
+            x -= 1.0;
+        else if (x < 0.0)
+            x += 1.0;
+    }
+    return x;
+}
+
+double oracle_code_brute(double c, double s, int64_t n, int32_t *icode, int32_t *ibit,
+                         int32_t *iword)
+{
+    for (int64_t i = 0; i < n; i++) {
+        c += s;
+        if (c >= 1023) {
+            c -= 1023;
+            if (++*icode >= 20) {
+                *icode = 0;
+                if (++*ibit >= 30) {
+                    *ibit = 0;
+                    ++*iword;
+                }
+            }
+        }
+    }
+    return c;
+}

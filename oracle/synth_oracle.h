@@ -16,6 +16,9 @@ int oracle_synth(const gss_chan_blk_t *blk, const int32_t *nch, const uint32_t *
                  const uint32_t *nav, int nblk, int n_per_blk, int fmt, void *out,
                  double *carr_end);
 size_t oracle_block_bytes(int n_per_blk, int fmt);
+double oracle_carr_brute(double x, double s, int64_t n);
+double oracle_code_brute(double c, double s, int64_t n, int32_t *icode, int32_t *ibit,
+                         int32_t *iword);
 void oracle_lut(int *sin512, int *cos512);
 #ifdef __cplusplus
 }

@@ -1,0 +1,48 @@
+"""The C-ABI boundary: the library loads without a GPU and exports exactly what
+include/gpssim_amd.h declares (no compute calls here)."""
+import ctypes
+import os
+import re
+
+from conftest import REPO
+
+import gpssim_amd as G
+
+
+def declared_functions():
+    src = open(os.path.join(REPO, "include", "gpssim_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"\b(gss_[a-z0-9_]+)\s*\(", src))
+
+
+def test_header_matches_binding():
+    assert declared_functions() == set(G.EXPORTED)
+
+
+def test_library_exports_every_symbol():
+    L = ctypes.CDLL(G.LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(L, name), name
+
+
+def test_struct_layout():
+    assert G.CHAN_DTYPE.itemsize == 56
+    assert G.block_bytes(260000, 16) == 1040000
+    assert G.block_bytes(260000, 8) == 520000
+    assert G.block_bytes(260000, 1) == 65000
+    assert G.block_bytes(260002, 1) == 0          # -b 1 needs n % 4 == 0
+    assert G.block_bytes(260000, 4) == 0
+
+
+def test_no_gpu_fails_loudly():
+    # on a GPU-less host opening a device must fail with GSS_E_NODEV, never fall back
+    import subprocess
+    r = subprocess.run(["rocminfo"], capture_output=True, text=True)
+    if "gfx950" in r.stdout:
+        return
+    try:
+        G.Device(0)
+    except G.GssError as e:
+        assert e.code == -7
+    else:
+        raise AssertionError("gss_dev_open succeeded without a GPU")

@@ -1,0 +1,163 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the reference's golden
+outputs.  Bit-exact everywhere (integer/byte output of exact double recurrences).
+
+* synthetic parameter sweeps vs the scalar oracle (gpssim.c:2190-2288 restated), including the
+  edge cases the reference can reach: 0 and 16 channels, both Doppler signs, tiny Doppler,
+  round-half-even ties, large gains, ragged blocks, carrier phase 0 and just below 1;
+* real scenarios (BASELINE.json configs) vs the golden sha256 of the reference binary;
+* checkpoint-stage carrier end phases vs the host planner's next-block start phases;
+* the CLI end to end.
+"""
+import hashlib
+import math
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import CIRCLE, LOC, NAV
+
+import gpssim_amd as G
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+DELT = 1.0 / 2600000.0
+
+
+@pytest.fixture(scope="module")
+def dev():
+    d = G.Device(0)
+    yield d
+    d.close()
+
+
+@pytest.fixture(scope="module")
+def ca():
+    return G.ca_table()
+
+
+def synth_params(rng, nblk, nch_list, n_per_blk, big_gain=False, ties=False):
+    blk = np.zeros((nblk, G.MAXCH), G.CHAN_DTYPE)
+    nch = np.array(nch_list, np.int32)
+    delt = 1.0 / (n_per_blk * 10)
+    nav = rng.integers(0, 1 << 30, size=(8, 60), dtype=np.uint32)
+    for b in range(nblk):
+        for k in range(nch[b]):
+            f = rng.uniform(-5500, 5500) if k % 4 else rng.uniform(-40, 40)
+            cs = (1.023e6 + f / 1540.0) * delt
+            s = f * delt
+            if ties and k % 3 == 0:
+                u = 2.0 ** -53
+                s = math.copysign((math.floor(abs(s) / u) + 0.5) * u, s)
+            p = blk[b, k]
+            p["carr0"] = [0.0, 1.0 - 2.0 ** -53, rng.random()][k % 3] if b == 0 else rng.random()
+            p["carr_step"] = s
+            p["code0"] = rng.random() * 1023.0 if k % 5 else 1022.9999999
+            p["code_step"] = cs
+            p["icode"] = rng.integers(0, 20)
+            p["ibit"] = rng.integers(0, 30)
+            p["iword"] = rng.integers(0, 54)
+            p["gain"] = rng.integers(2000, 9000) if big_gain else rng.integers(30, 130)
+            p["ca_tbl"] = rng.integers(0, 32)
+            p["nav_tbl"] = rng.integers(0, 8)
+    return blk, nch, nav
+
+
+@pytest.mark.parametrize("fmt", [16, 8, 1])
+@pytest.mark.parametrize("case", ["mixed", "full16", "ties_biggain", "ragged"])
+def test_synthetic_vs_oracle(dev, ca, fmt, case):
+    rng = np.random.default_rng(abs(hash((fmt, case))) % (1 << 32))
+    n = 26000
+    if case == "mixed":
+        nch = [12, 0, 1, 7, 12, 3]
+        kw = {}
+    elif case == "full16":
+        nch = [16, 16, 16]
+        kw = {}
+    elif case == "ties_biggain":
+        nch = [12, 12, 5]
+        kw = dict(big_gain=True, ties=True)
+    else:
+        n = 26004 if fmt == 1 else 26003          # last segment is ragged
+        nch = [11, 4, 11]
+        kw = {}
+    blk, nchv, nav = synth_params(rng, len(nch), nch, n, **kw)
+    want, rc = oracle.synth(blk, nchv, ca, nav, n, fmt)
+    assert rc == 0
+    got = dev.synth_host(blk, nchv, ca, nav, n, fmt)
+    assert got.shape == want.shape
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:5]}"
+
+
+def test_carr_end_matches_oracle(dev, ca):
+    rng = np.random.default_rng(7)
+    blk, nch, nav = synth_params(rng, 4, [12, 9, 16, 2], 260000, ties=True)
+    want, cend_o, rc = oracle.synth(blk, nch, ca, nav, 260000, 16, want_carr_end=True)
+    got, cend_g = dev.synth_host(blk, nch, ca, nav, 260000, 16, want_carr_end=True)
+    assert np.array_equal(got, want)
+    for b in range(4):
+        assert np.array_equal(cend_g[b, :nch[b]], cend_o[b, :nch[b]])
+
+
+def run_scenario(dev, batch=300, **kw):
+    s = G.Scenario(NAV, **kw)
+    ca = G.ca_table()
+    h = hashlib.sha256()
+    blocks = []
+    bb = G.block_bytes(s.n_per_blk, s.data_format)
+    total = 0
+    while True:
+        blk, nch = s.next(batch)
+        if len(nch) == 0:
+            break
+        out = dev.synth_host(blk, nch, ca, s.nav_table(), s.n_per_blk, s.data_format)
+        h.update(out.tobytes())
+        total += out.size
+        for i in range(len(nch)):
+            blocks.append(hashlib.sha256(out[i * bb:(i + 1) * bb].tobytes()).hexdigest()[:16])
+    return h.hexdigest(), total, blocks
+
+
+@pytest.mark.parametrize("name,kw", [
+    ("static_d30_b16", dict(llh=LOC, duration=30.0, data_format=16)),
+    ("static_d30_b8", dict(llh=LOC, duration=30.0, data_format=8)),
+    ("static_d30_b1", dict(llh=LOC, duration=30.0, data_format=1)),
+    ("static_d65_b8_noiono", dict(llh=(-33.8688, 151.2093, 58), duration=65.0, data_format=8,
+                                  iono=False)),
+    ("ecef_d35_s3M_b16", dict(xyz=(-2700000.0, -4290000.0, 3860000.0), duration=35.0,
+                              samp_freq=3.0e6, data_format=16)),
+])
+def test_scenario_bit_exact(dev, golden, name, kw):
+    sha, total, blocks = run_scenario(dev, **kw)
+    g = golden[name]
+    if blocks != g["block_sha16"]:
+        first = next(i for i, (a, b) in enumerate(zip(blocks, g["block_sha16"])) if a != b)
+        raise AssertionError(f"{name}: first differing block {first}")
+    assert total == g["bytes"] and sha == g["sha256"]
+
+
+@pytest.mark.parametrize("name,kw", [
+    ("circle_b8", dict(motion_file=CIRCLE, data_format=8)),
+    ("static_d300_b16", dict(llh=LOC, duration=300.0, data_format=16)),
+    ("static_d30_s20M_b16", dict(llh=LOC, duration=30.0, samp_freq=2.0e7, data_format=16)),
+])
+def test_baseline_configs_bit_exact(dev, golden, name, kw):
+    sha, total, blocks = run_scenario(dev, batch=100, **kw)
+    g = golden[name]
+    assert blocks == g["block_sha16"]
+    assert total == g["bytes"] and sha == g["sha256"]
+
+
+def test_cli_end_to_end(golden):
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "gpssim.bin")
+        r = subprocess.run([G.CLI_PATH, "-e", NAV, "-l", ",".join(map(str, LOC)), "-d", "30",
+                            "-b", "16", "-o", out], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert "Done!" in r.stderr
+        h = hashlib.sha256(open(out, "rb").read()).hexdigest()
+    assert h == golden["static_d30_b16"]["sha256"]

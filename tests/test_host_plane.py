@@ -1,0 +1,95 @@
+"""Host control plane (gss_scn_*): block count/size, per-block parameters, error behaviour,
+and the exact carrier planner checked against the brute-force recurrence across blocks."""
+import numpy as np
+import pytest
+
+from conftest import CIRCLE, LOC, NAV
+
+import gpssim_amd as G
+import oracle
+
+
+def test_static_geometry():
+    s = G.Scenario(NAV, llh=LOC, duration=30.0)
+    assert (s.n_per_blk, s.n_blocks, s.data_format) == (260000, 299, 16)
+    assert s.samp_freq == 2600000.0 and s.delt == 1.0 / 2600000.0
+    assert (s.start_week, s.start_sec) == (1823, 518400.0)
+    blk, nch = s.all_blocks(batch=64)
+    assert len(nch) == 299 and set(nch.tolist()) == {11}
+    act = blk[0, :11]
+    assert set(act["ca_tbl"] + 1) == {1, 2, 3, 6, 9, 10, 12, 17, 20, 23, 28}
+    assert np.all((act["carr0"] >= 0) & (act["carr0"] < 1))
+    assert np.all((act["code0"] >= 0) & (act["code0"] < 1023))
+    assert np.all(act["gain"] > 0) and np.all(act["gain"] < 200)
+    assert np.all(np.abs(act["carr_step"]) < 5000 / 2.6e6)
+
+
+def test_sample_rate_rounding():
+    s = G.Scenario(NAV, llh=LOC, duration=1.0, samp_freq=2600047.0)
+    assert s.n_per_blk == 260004 and s.samp_freq == 2600040.0
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(samp_freq=5e5), "Invalid sampling frequency"),
+    (dict(data_format=4), "Invalid I/Q data format"),
+    (dict(duration=90000.0), "Invalid duration"),
+    (dict(samp_freq=2600020.0, data_format=1), "divisible by 4"),
+])
+def test_errors(kw, msg):
+    with pytest.raises(G.GssError) as e:
+        G.Scenario(NAV, llh=LOC, **kw)
+    assert msg in str(e.value)
+
+
+def test_missing_files():
+    with pytest.raises(G.GssError, match="ephemeris file not found"):
+        G.Scenario("/nonexistent.14n", llh=LOC, duration=1.0)
+    with pytest.raises(G.GssError, match="Failed to open user motion"):
+        G.Scenario(NAV, motion_file="/nonexistent.csv", duration=1.0)
+
+
+def test_start_time_out_of_range():
+    with pytest.raises(G.GssError, match="Invalid start time"):
+        G.Scenario(NAV, llh=LOC, duration=1.0, start=(2014, 12, 25, 0, 0, 0))
+
+
+def test_dynamic_block_count():
+    s = G.Scenario(NAV, motion_file=CIRCLE)
+    assert s.n_blocks == 2999
+    with pytest.raises(G.GssError, match="Invalid duration"):
+        G.Scenario(NAV, motion_file=CIRCLE, duration=301.0)
+
+
+def test_planner_chain_matches_brute_force():
+    """carr0 of block b+1 == brute-force advance of block b's carr0 by N samples, for every
+    channel that stays allocated (same PRN); crosses a 30 s re-allocation boundary."""
+    s = G.Scenario(NAV, llh=LOC, duration=31.0, samp_freq=1.0e6)
+    blk, nch = s.all_blocks(batch=100)
+    n = s.n_per_blk
+    checked = 0
+    for b in range(0, len(nch) - 1, 37):
+        for k in range(nch[b]):
+            prn = blk[b, k]["ca_tbl"]
+            nxt = [j for j in range(nch[b + 1]) if blk[b + 1, j]["ca_tbl"] == prn]
+            if not nxt:
+                continue
+            want = oracle.carr_brute(blk[b, k]["carr0"], blk[b, k]["carr_step"], n)
+            assert blk[b + 1, nxt[0]]["carr0"] == want
+            checked += 1
+    assert checked > 50
+
+
+def test_nav_table_rows():
+    s = G.Scenario(NAV, llh=LOC, duration=31.0)
+    blk, nch = s.all_blocks()
+    nav = s.nav_table()
+    assert nav.shape[1] == 60 and np.all(nav < (1 << 30))
+    # every 30 s frame gets new rows: 11 initial + 11 at t=30 s
+    assert len(nav) == 22
+    assert blk[-1, :nch[-1]]["nav_tbl"].min() >= 11
+    # TLM preamble 0x8B in every subframe's first word (bits 29..22, possibly inverted by D30*)
+    for row in nav:
+        for sf in range(6):
+            w = int(row[sf * 10])
+            pre = (w >> 22) & 0xFF
+            assert pre in (0x8B, 0x74)

@@ -1,0 +1,73 @@
+"""The oracle is pinned before it is trusted: its LUT against the reference's table, the C/A
+generator against IS-GPS-200 Table 3-Ia, and the all-CPU restatement (product host plane +
+scalar oracle loop) against the reference binary's golden outputs."""
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import CIRCLE, LOC, NAV, REPO
+
+import gpssim_amd as G
+import oracle
+
+LUT_FIX = os.path.join(REPO, "tests", "golden", "lut512.json")
+
+
+def test_lut_matches_reference_table():
+    fix = json.load(open(LUT_FIX))
+    s, c = oracle.lut()
+    assert s.tolist() == fix["sinTable512"]
+    assert c.tolist() == fix["cosTable512"]
+    ps, pc = G.lut()
+    assert ps.tolist() == fix["sinTable512"] and pc.tolist() == fix["cosTable512"]
+
+
+def _chips(row, n=10):
+    return [(int(row[i >> 5]) >> (i & 31)) & 1 for i in range(n)]
+
+
+def test_ca_known_answer():
+    # IS-GPS-200 Table 3-Ia: first 10 chips in octal (1 = chip '1')
+    ca = G.ca_table()
+    expect = {1: 0o1440, 2: 0o1620, 3: 0o1710, 4: 0o1744, 5: 0o1133, 10: 0o1504, 32: 0o1712}
+    for prn, octal in expect.items():
+        bits = _chips(ca[prn - 1])
+        assert int("".join(map(str, bits)), 2) == octal, prn
+    # balanced Gold codes: 512 ones per period
+    for prn in range(1, 33):
+        assert sum(_chips(ca[prn - 1], 1023)) == 512
+
+
+def run_cpu_restatement(args):
+    p = subprocess.run([oracle.CLI, "-e", NAV] + args + ["-o", "-"], capture_output=True,
+                       check=True)
+    return p.stdout
+
+
+def block_hashes(buf, bb):
+    return [hashlib.sha256(buf[i:i + bb]).hexdigest()[:16] for i in range(0, len(buf), bb)]
+
+
+@pytest.mark.parametrize("fmt", [16, 8, 1])
+def test_cpu_restatement_prefix_matches_reference(golden, fmt):
+    g = golden[f"static_d30_b{fmt}"]
+    out = run_cpu_restatement(["-l", ",".join(map(str, LOC)), "-d", "3", "-b", str(fmt)])
+    bb = G.block_bytes(260000, fmt)
+    assert len(out) == 29 * bb
+    assert block_hashes(out, bb) == g["block_sha16"][:29]
+    assert out[: len(g["head_hex"]) // 2].hex() == g["head_hex"]
+
+
+def test_cpu_restatement_full_30s_b1(golden):
+    out = run_cpu_restatement(["-l", ",".join(map(str, LOC)), "-d", "30", "-b", "1"])
+    assert hashlib.sha256(out).hexdigest() == golden["static_d30_b1"]["sha256"]
+
+
+def test_cpu_restatement_dynamic_prefix(golden):
+    g = golden["circle_b8"]
+    out = run_cpu_restatement(["-u", CIRCLE, "-d", "2", "-b", "8"])
+    assert block_hashes(out, 520000) == g["block_sha16"][:19]
