@@ -123,12 +123,22 @@ GSS_HD int64_t gss_jump(double v, double s, double W, double *D)
     }
     if (lim < 0) return 0;
     *D = (s > 0.0 ? (double)K : -(double)K) * u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    /* no 64-bit integer divider on the GPU: f64 quotient (lim, K < 2^53) then exact fix-up */
+    int64_t q = (int64_t)((double)lim / (double)K);
+    if (q * K > lim) q--;
+    else if ((q + 1) * K <= lim) q++;
+    return q + 1;
+#else
     return lim / K + 1;
+#endif
 }
 
 /* Advance the carrier recurrence by n steps, exactly. */
 GSS_HD double gss_carr_walk(double x, double s, int64_t n)
 {
+    if (s == 0.0)                                /* x + 0 == x: nothing moves */
+        return x;
     while (n > 0) {
         double D;
         int64_t J = gss_jump(x, s, 1.0, &D);
@@ -148,6 +158,8 @@ GSS_HD double gss_carr_walk(double x, double s, int64_t n)
 /* Advance the code recurrence (with counters) by n steps, exactly. */
 GSS_HD void gss_code_walk(gss_code_state *c, double cs, int64_t n)
 {
+    if (cs == 0.0 && c->ph < GSS_CA_SEQ_LEN_D)   /* stationary below the wrap */
+        return;
     while (n > 0) {
         double D;
         int64_t J = gss_jump(c->ph, cs, GSS_CA_SEQ_LEN_D, &D);
@@ -163,4 +175,371 @@ GSS_HD void gss_code_walk(gss_code_state *c, double cs, int64_t n)
     }
 }
 
+
+/* =========================================================================================
+ * Cycle-granular exact walk with a cycle-map cache.
+ *
+ * Between two wraps ("a cycle") the chain starts from a post-wrap value w that sits on a coarse
+ * lattice (2^-52 for the ascending carrier, 2^-43 for the code phase, 2^-53 for the descending
+ * carrier).  Every lattice the cycle passes through is at least as fine, so translating w by a
+ * multiple δ of that coarse unit translates the whole trajectory by δ — provided every step's
+ * exact sum stays in the same binade (same rounding lattice, same tie parity) and every wrap
+ * decision is unchanged.  gss_cycle_walk() walks one cycle with the jump walk and records the
+ * δ-interval for which that holds (the "margins"); later cycles whose start falls inside a cached
+ * interval are taken in O(1): w' = w + dx after L steps.  Verified against brute force in
+ * tests/test_phase_walk.py.
+ * ========================================================================================= */
+
+typedef struct gss_cyc {
+    double lo, hi;        /* valid start values (inclusive)                                     */
+    double w0, v0;        /* the walked start and its end value: end(w) = v0 + (w - w0), where
+                             w - w0 is exact (same coarse lattice) and so is the sum (the result
+                             is representable).  A stored difference v0 - w0 would round.      */
+    int64_t L;            /* steps                                                              */
+} gss_cyc;
+
+#define GSS_CC_N 16
+typedef struct gss_cyc_cache {
+    gss_cyc e[GSS_CC_N];
+    int n, next;
+    int enabled;
+} gss_cyc_cache;
+
+/* exponent of a positive normal double: v in [2^e, 2^(e+1)) */
+GSS_HD int gss_exp2i(double v)
+{
+    gss_bits64 b;
+    b.d = v;
+    return (int)((b.u >> 52) & 0x7FF) - 1023;
+}
+
+/* Margins of one exact step v -> fl(v+s) (ascending or descending), folded into [dlo, dhi]:
+   the exact sum t = v + s must stay in its binade under translation by δ (δ a multiple of
+   dunit).  An exact tie is translation-invariant only while dunit is an even multiple of the
+   result lattice (round-half-even then sees the same parity); otherwise no translation. */
+GSS_HD void gss_margin_step(double v, double s, double dunit, double *dlo, double *dhi)
+{
+    double r = v + s;
+    double bb = r - v;
+    double err = (v - (r - bb)) + (s - bb);            /* TwoSum: t = r + err exactly */
+    double ar = r < 0.0 ? -r : r, aerr = r < 0.0 ? -err : err;   /* work with |t| */
+    if (ar == 0.0) { *dlo = 0.0; *dhi = 0.0; return; }
+    int e = gss_exp2i(ar);
+    double p = gss_pow2(e);
+    if (ar == p && aerr < 0.0) { e -= 1; p = gss_pow2(e); }
+    /* an exact round-half-even tie depends on the parity of the result: not translatable */
+    double half_ulp = gss_pow2(e - 53);
+    if ((aerr == half_ulp || aerr == -half_ulp) && 4.0 * half_ulp > dunit) {
+        *dlo = 0.0;
+        *dhi = 0.0;
+        return;
+    }
+    double below = (ar - p) + aerr;                    /* |t| - 2^e  >= 0 */
+    double above = (2.0 * p - ar) - aerr;              /* 2^(e+1) - |t| > 0 */
+    /* translating v by δ moves t by δ; in |t| terms the sign flips for negative t */
+    double lo = r < 0.0 ? -above : -below, hi = r < 0.0 ? below : above;
+    if (lo > *dlo) *dlo = lo;
+    if (hi < *dhi) *dhi = hi;
+}
+
+/* Walk ascending (s > 0) from w until the first wrap at threshold W (carrier W=1, code 1023)
+   or n steps.  Returns steps taken; *x = value reached (post-wrap if *wrapped).  If margins is
+   non-NULL, accumulates the admissible translation interval [*dlo, *dhi] of w. */
+GSS_HD int64_t gss_asc_to_wrap(double *x, double s, double W, int64_t n, int *wrapped,
+                               double *dlo, double *dhi)
+{
+    double v = *x;
+    int64_t taken = 0;
+    const double dunit = gss_pow2(gss_exp2i(W) - 52);      /* lattice of post-wrap values */
+    *wrapped = 0;
+    while (taken < n) {
+        double D;
+        int64_t J = gss_jump(v, s, W, &D);
+        if (J > 0) {
+            if (J == INT64_MAX) { if (dlo) { *dlo = 0.0; *dhi = 0.0; } taken = n; break; }
+            if (J > n - taken) J = n - taken;
+            if (dlo) {
+                gss_margin_step(v, s, dunit, dlo, dhi);
+                double vl = v + (double)(J - 1) * D;
+                gss_margin_step(vl, s, dunit, dlo, dhi);
+                double top = v + (double)J * D;         /* largest non-wrap result: r + δ < W */
+                double lim = (W - top) - 2.0 * gss_pow2(gss_exp2i(W) - 52);
+                if (lim < *dhi) *dhi = lim;
+            }
+            v = v + (double)J * D;
+            taken += J;
+            if (taken == n) break;
+        }
+        if (dlo) gss_margin_step(v, s, dunit, dlo, dhi);
+        double r = v + s;
+        taken++;
+        if (r >= W) {                                    /* wrap step: r + δ >= W */
+            if (dlo) {
+                double lim = W - r;
+                if (lim > *dlo) *dlo = lim;
+            }
+            v = r - W;
+            *wrapped = 1;
+            break;
+        }
+        if (dlo) {
+            double lim = (W - r) - 2.0 * gss_pow2(gss_exp2i(W) - 52);
+            if (lim < *dhi) *dhi = lim;
+        }
+        v = r;
+    }
+    *x = v;
+    return taken;
+}
+
+/* Descending carrier (s < 0), head of a cycle: from w walk down until the first value below T
+   (T = 2^(e_s+2) > 2|s|, so no wrap can happen in the head) or n steps; margins as above.
+   Returns steps taken; *stopped = 1 if a value < T was reached. */
+GSS_HD int64_t gss_desc_head(double *x, double s, double T, int64_t n, int *stopped,
+                             double *dlo, double *dhi)
+{
+    double v = *x;
+    int64_t taken = 0;
+    *stopped = 0;
+    while (taken < n) {
+        if (v < T) { *stopped = 1; break; }
+        double D;
+        int64_t J = gss_jump(v, s, 1.0, &D);
+        if (J > 0) {
+            if (J == INT64_MAX) { if (dlo) { *dlo = 0.0; *dhi = 0.0; } taken = n; break; }
+            if (J > n - taken) J = n - taken;
+            if (dlo) {
+                gss_margin_step(v, s, gss_pow2(-53), dlo, dhi);
+                gss_margin_step(v + (double)(J - 1) * D, s, gss_pow2(-53), dlo, dhi);
+            }
+            v = v + (double)J * D;                  /* stays >= 2^e >= T */
+            taken += J;
+            if (taken == n) break;
+            continue;
+        }
+        if (dlo) gss_margin_step(v, s, gss_pow2(-53), dlo, dhi);
+        v = v + s;                                  /* v >= T > 2|s|: no wrap */
+        taken++;
+    }
+    if (taken == n && v < T) *stopped = 1;
+    *x = v;
+    return taken;
+}
+
+#define GSS_BIG 1.0e300
+
+GSS_HD const gss_cyc *gss_cc_find(const gss_cyc_cache *cc, double w, int64_t nmax)
+{
+    for (int i = 0; i < cc->n; i++)
+        if (w >= cc->e[i].lo && w <= cc->e[i].hi && cc->e[i].L <= nmax)
+            return &cc->e[i];
+    return 0;
+}
+
+GSS_HD void gss_cc_put(gss_cyc_cache *cc, double w, double dlo, double dhi, double safe,
+                       double v_end, int64_t L)
+{
+    if (!(dlo <= 0.0 && dhi >= 0.0)) return;
+    gss_cyc *e = &cc->e[cc->next];
+    e->lo = w + dlo + safe;
+    e->hi = w + dhi - safe;
+    if (e->lo > w) e->lo = w;                  /* the walked start itself is always valid */
+    if (e->hi < w) e->hi = w;
+    e->w0 = w;
+    e->v0 = v_end;
+    e->L = L;
+    cc->next = (cc->next + 1) % GSS_CC_N;
+    if (cc->n < GSS_CC_N) cc->n++;
+}
+
+/* ---- carrier iterator: exact, cycle by cycle ---------------------------------------------- */
+typedef struct gss_carr_it {
+    double x, s, T;
+    int64_t pos, left;     /* samples done / remaining */
+    int mid;               /* x is not a post-wrap value (block start) */
+    gss_cyc_cache cc;
+} gss_carr_it;
+
+GSS_HD void gss_carr_it_init(gss_carr_it *it, double x, double s, int64_t n)
+{
+    it->x = x;
+    it->s = s;
+    it->pos = 0;
+    it->left = n;
+    it->mid = 1;
+    it->cc.n = 0;
+    it->cc.next = 0;
+    it->cc.enabled = (s != 0.0);
+    double as = s < 0.0 ? -s : s;
+    it->T = as > 0.0 ? gss_pow2(gss_exp2i(as) + 2) : 0.0;
+}
+
+/* Plain (uncached) walk to the next wrap. */
+GSS_HD int gss_carr_plain_to_wrap(gss_carr_it *it)
+{
+    int wr = 0;
+    int64_t taken;
+    if (it->s > 0.0) {
+        taken = gss_asc_to_wrap(&it->x, it->s, 1.0, it->left, &wr, 0, 0);
+    } else {
+        double v = it->x;
+        taken = 0;
+        while (taken < it->left) {
+            double D;
+            int64_t J = gss_jump(v, it->s, 1.0, &D);
+            if (J > 0) {
+                if (J == INT64_MAX) { taken = it->left; break; }
+                if (J > it->left - taken) J = it->left - taken;
+                v = v + (double)J * D;
+                taken += J;
+                if (taken == it->left) break;
+            }
+            double r = v + it->s;
+            taken++;
+            if (r >= 1.0) { v = r - 1.0; wr = 1; break; }     /* reference order: >=1 first */
+            if (r < 0.0) { v = r + 1.0; wr = 1; break; }
+            v = r;
+        }
+        it->x = v;
+    }
+    it->pos += taken;
+    it->left -= taken;
+    return wr;
+}
+
+/* Advance to just after the next wrap (returns 1, x = post-wrap value, pos = its sample index)
+   or to the end of the range (returns 0, x = final value). */
+GSS_HD int gss_carr_next_wrap(gss_carr_it *it)
+{
+    if (it->left <= 0) return 0;
+    if (it->mid || !it->cc.enabled) {
+        it->mid = 0;
+        return gss_carr_plain_to_wrap(it);
+    }
+    const double safe = 4.0 * gss_pow2(-52);
+    if (it->s > 0.0) {
+        const gss_cyc *e = gss_cc_find(&it->cc, it->x, it->left);
+        if (e) {
+            it->x = e->v0 + (it->x - e->w0);
+            it->pos += e->L;
+            it->left -= e->L;
+            return 1;
+        }
+        double w = it->x, dlo = -GSS_BIG, dhi = GSS_BIG;
+        int wr = 0;
+        int64_t taken = gss_asc_to_wrap(&it->x, it->s, 1.0, it->left, &wr, &dlo, &dhi);
+        it->pos += taken;
+        it->left -= taken;
+        if (wr) gss_cc_put(&it->cc, w, dlo, dhi, safe, it->x, taken);
+        return wr;
+    }
+    /* descending: cached head down to T, then real steps to the wrap */
+    const gss_cyc *e = gss_cc_find(&it->cc, it->x, it->left);
+    if (e) {
+        it->x = e->v0 + (it->x - e->w0);
+        it->pos += e->L;
+        it->left -= e->L;
+    } else {
+        double w = it->x, dlo = -GSS_BIG, dhi = GSS_BIG;
+        int st = 0;
+        int64_t taken = gss_desc_head(&it->x, it->s, it->T, it->left, &st, &dlo, &dhi);
+        it->pos += taken;
+        it->left -= taken;
+        if (!st) return 0;
+        gss_cc_put(&it->cc, w, dlo, dhi, safe, it->x, taken);
+    }
+    while (it->left > 0) {
+        double r = it->x + it->s;
+        it->pos++;
+        it->left--;
+        if (r < 0.0) { it->x = r + 1.0; return 1; }
+        it->x = r;
+    }
+    return 0;
+}
+
+/* Exact advance of the carrier by n samples using the cycle cache. */
+GSS_HD double gss_carr_walk_cc(double x, double s, int64_t n)
+{
+    gss_carr_it it;
+    gss_carr_it_init(&it, x, s, n);
+    while (gss_carr_next_wrap(&it)) {
+    }
+    return it.x;
+}
+
+/* ---- code iterator ---------------------------------------------------------------------- */
+typedef struct gss_code_it {
+    gss_code_state c;
+    double cs;
+    int64_t pos, left;
+    int mid;
+    gss_cyc_cache cc;
+} gss_code_it;
+
+GSS_HD void gss_code_it_init(gss_code_it *it, gss_code_state c, double cs, int64_t n)
+{
+    it->c = c;
+    it->cs = cs;
+    it->pos = 0;
+    it->left = n;
+    it->mid = 1;
+    it->cc.n = 0;
+    it->cc.next = 0;
+    it->cc.enabled = (cs > 0.0);
+}
+
+GSS_HD void gss_code_count_wrap(gss_code_state *c)
+{
+    c->icode++;
+    if (c->icode >= 20) {
+        c->icode = 0;
+        c->ibit++;
+        if (c->ibit >= 30) {
+            c->ibit = 0;
+            c->iword++;
+        }
+    }
+}
+
+GSS_HD int gss_code_next_wrap(gss_code_it *it)
+{
+    if (it->left <= 0) return 0;
+    const double W = GSS_CA_SEQ_LEN_D;
+    int wr = 0;
+    if (it->mid || !it->cc.enabled) {
+        it->mid = 0;
+        int64_t taken = gss_asc_to_wrap(&it->c.ph, it->cs, W, it->left, &wr, 0, 0);
+        it->pos += taken;
+        it->left -= taken;
+        if (wr) gss_code_count_wrap(&it->c);
+        return wr;
+    }
+    const gss_cyc *e = gss_cc_find(&it->cc, it->c.ph, it->left);
+    if (e) {
+        it->c.ph = e->v0 + (it->c.ph - e->w0);
+        it->pos += e->L;
+        it->left -= e->L;
+        gss_code_count_wrap(&it->c);
+        return 1;
+    }
+    double w = it->c.ph, dlo = -GSS_BIG, dhi = GSS_BIG;
+    int64_t taken = gss_asc_to_wrap(&it->c.ph, it->cs, W, it->left, &wr, &dlo, &dhi);
+    it->pos += taken;
+    it->left -= taken;
+    if (wr) {
+        gss_cc_put(&it->cc, w, dlo, dhi, 4.0 * gss_pow2(-43), it->c.ph, taken);
+        gss_code_count_wrap(&it->c);
+    }
+    return wr;
+}
+
+GSS_HD void gss_code_walk_cc(gss_code_state *c, double cs, int64_t n)
+{
+    gss_code_it it;
+    gss_code_it_init(&it, *c, cs, n);
+    while (gss_code_next_wrap(&it)) {
+    }
+    *c = it.c;
+}
 #endif /* GSS_PHASE_H */

@@ -2,17 +2,22 @@
  * gss_synth.hip — the hot path on gfx950: GPS L1 C/A baseband synthesis of whole 0.1 s blocks.
  *
  * Replaces the reference per-sample loop (gpssim.c:2190-2264) and its quantise/pack epilogue
- * (gpssim.c:2257-2288).  Bit-exact: the two double recurrences per channel (carrier, code) are
- * evaluated with the same IEEE double additions as the reference (-ffp-contract=off; the
- * checkpoint stage jumps over provably exact lattice runs, see common/gss_phase.h).
+ * (gpssim.c:2257-2288).  Bit-exact: every channel's carrier and code phase are the reference's
+ * serial IEEE double recurrences (built with -ffp-contract=off); the only shortcuts are provably
+ * exact lattice translations (common/gss_phase.h).
  *
- * Stage A  gss_ckpt_kernel      one lane per (block, channel): walks the block's carrier and code
- *                               chains exactly, writing the state every R samples (checkpoints).
- * Stage B  gss_synth_kernel     one lane per R-sample segment of a block, all channels:
- *                               LDS tables (per-channel LUT × gain, C/A chips in both polarities,
- *                               nav words), exact recurrences, integer accumulation, (acc+64)>>7,
- *                               SC16/SC08/SC01 packing, 16-byte stores.
- * Integer/byte work only: no MFMA.
+ * Stage A  gss_anchor_kernel    one lane per (block, channel, chain) with chain ∈ {carrier, code}.
+ *                               Walks the block cycle by cycle (cycle-map cache) and records, for
+ *                               every R-sample segment, the last wrap at or before its first
+ *                               sample: an exact "anchor" state (sample index, phase[, counters]).
+ * Stage B  gss_synth_kernel     one lane per R-sample segment of a block, all channels.  Each lane
+ *                               first jump-walks every channel from its anchor to the segment
+ *                               start (≤ one cycle), then runs the per-sample recurrences:
+ *                               LUT[floor(512 carr)] × (chip ⊕ data bit) × gain accumulated over
+ *                               channels in int32, (acc+64)>>7, SC16/SC08/SC01 packing.  Output is
+ *                               staged per lane in LDS (64 B) and stored by the wave as whole 64-B
+ *                               pieces (16 lanes' pieces per store instruction).
+ * Integer/byte work on f64 phases: no MFMA.
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -21,190 +26,209 @@
 #include "gpssim_amd.h"
 #include "../common/gss_phase.h"
 
-#define SEG_R          1024   /* samples per Stage-B lane (checkpoint spacing) */
 #define SYNTH_THREADS  256
-#define CKPT_THREADS   64
+#define SYNTH_WAVES    (SYNTH_THREADS / 64)
+#define ANCHOR_THREADS 64
+#define CHUNK_BYTES    64                /* output bytes per lane per staged chunk */
+#define LUT_N          768               /* 512 + 256: index ti + 256*neg needs no wrap */
 
-/* ---------------------------------------------------------------------------------------- */
-/* Carrier LUT (gpssim.c:15-83): quarter wave round(250 sin(2π(k+½)/512)), entry 35 = 105.   */
-/* Generated on the host once (gss_lut) and passed as a kernel argument table.               */
-/* ---------------------------------------------------------------------------------------- */
 struct lut_arg { int16_t sin512[512]; int16_t cos512[512]; };
 
+/* per (block, channel) block-uniform values, prepared by Stage A */
+struct chan_uni {
+    double S;            /* 512 * carr_step (state Y = 512 carr; scaling by 2^9 is exact)     */
+    double CS;           /* code_step                                                       */
+    int32_t gain;
+    uint32_t pad[3];
+};
+
 /* ======================================================================================== */
-/* Stage A: checkpoints                                                                     */
+/* Stage A: anchors                                                                         */
 /* ======================================================================================== */
-__global__ __launch_bounds__(CKPT_THREADS) void gss_ckpt_kernel(
-    const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch, int nblk,
-    int n_per_blk, int nseg, int nchp, double *__restrict__ ck_carr,
-    double *__restrict__ ck_code, uint32_t *__restrict__ ck_ctr, double2 *__restrict__ steps,
-    double *__restrict__ carr_end)
+__global__ __launch_bounds__(ANCHOR_THREADS) void gss_anchor_kernel(
+    const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch, int nblk, int nchp,
+    int n_per_blk, int nseg, int seg_r, int32_t *__restrict__ anc_cn, double *__restrict__ anc_cx,
+    int32_t *__restrict__ anc_kn, double *__restrict__ anc_kx, uint32_t *__restrict__ anc_kc,
+    chan_uni *__restrict__ uni, double *__restrict__ carr_end)
 {
-    int gid = blockIdx.x * CKPT_THREADS + threadIdx.x;
-    int b = gid / GSS_MAXCH, k = gid % GSS_MAXCH;
-    if (b >= nblk || k >= nchp)
+    int gid = blockIdx.x * ANCHOR_THREADS + threadIdx.x;
+    int chain = gid & 1, k = (gid >> 1) & (GSS_MAXCH - 1), b = gid >> 5;
+    if (b >= nblk)
         return;
-    size_t row = ((size_t)b * GSS_MAXCH + k) * (size_t)nseg;
-    if (k >= nch[b]) {                       /* padding channel: constant, never wraps */
-        steps[(size_t)b * GSS_MAXCH + k] = make_double2(0.0, 0.0);
-        for (int s = 0; s < nseg; s++) {
-            ck_carr[row + s] = 0.0;
-            ck_code[row + s] = 0.0;
-            ck_ctr[row + s] = 0u;
+    size_t bk = (size_t)b * GSS_MAXCH + k;
+    size_t row = bk * (size_t)nseg;
+    if (k >= nch[b]) {
+        if (k >= nchp)
+            return;
+        /* silent padding channel of the launch's kernel instance: zero gain, no motion, and
+           well-defined anchors so Stage B can initialise every channel unconditionally */
+        if (chain == 0) {
+            chan_uni u = {0.0, 0.0, 0, {0u, 0u, 0u}};
+            uni[bk] = u;
+            for (int sgi = 0; sgi < nseg; sgi++) {
+                anc_cn[row + sgi] = 0;
+                anc_cx[row + sgi] = 0.0;
+            }
+        } else {
+            for (int sgi = 0; sgi < nseg; sgi++) {
+                anc_kn[row + sgi] = 0;
+                anc_kx[row + sgi] = 0.0;
+                anc_kc[row + sgi] = 0u;
+            }
         }
         return;
     }
-    const gss_chan_blk_t p = blk[(size_t)b * GSS_MAXCH + k];
-    /* Stage B keeps the carrier as Y = 512*carr: fl(Y + 512 s) == 512 fl(carr + s) exactly */
-    steps[(size_t)b * GSS_MAXCH + k] = make_double2(p.carr_step * 512.0, p.code_step);
-    double x = p.carr0;
-    gss_code_state c;
-    c.ph = p.code0;
-    c.icode = p.icode;
-    c.ibit = p.ibit;
-    c.iword = p.iword;
-    for (int s = 0; s < nseg; s++) {
-        ck_carr[row + s] = x;
-        ck_code[row + s] = c.ph;
-        ck_ctr[row + s] = (uint32_t)c.icode | ((uint32_t)c.ibit << 8) | ((uint32_t)c.iword << 16);
-        int len = n_per_blk - s * SEG_R;
-        if (len > SEG_R) len = SEG_R;
-        x = gss_carr_walk(x, p.carr_step, len);
-        gss_code_walk(&c, p.code_step, len);
+    const gss_chan_blk_t p = blk[bk];
+    if (chain == 0) {
+        chan_uni u;
+        u.S = p.carr_step * 512.0;
+        u.CS = p.code_step;
+        u.gain = p.gain;
+        u.pad[0] = u.pad[1] = u.pad[2] = 0u;
+        uni[bk] = u;
+
+        gss_carr_it it;
+        gss_carr_it_init(&it, p.carr0, p.carr_step, n_per_blk);
+        int seg = 0;
+        int32_t an = 0;
+        double ax = p.carr0;
+        for (;;) {
+            int wr = gss_carr_next_wrap(&it);
+            int64_t nw = wr ? it.pos : (int64_t)n_per_blk;
+            while (seg < nseg && (int64_t)seg * seg_r < nw) {
+                anc_cn[row + seg] = an;
+                anc_cx[row + seg] = ax;
+                seg++;
+            }
+            if (!wr || (seg >= nseg && !carr_end))
+                break;
+            an = (int32_t)it.pos;
+            ax = it.x;
+        }
+        if (carr_end)
+            carr_end[bk] = it.x;
+    } else {
+        gss_code_state c;
+        c.ph = p.code0;
+        c.icode = p.icode;
+        c.ibit = p.ibit;
+        c.iword = p.iword;
+        gss_code_it it;
+        gss_code_it_init(&it, c, p.code_step, n_per_blk);
+        int seg = 0;
+        int32_t an = 0;
+        gss_code_state ac = c;
+        for (;;) {
+            int wr = gss_code_next_wrap(&it);
+            int64_t nw = wr ? it.pos : (int64_t)n_per_blk;
+            while (seg < nseg && (int64_t)seg * seg_r < nw) {
+                anc_kn[row + seg] = an;
+                anc_kx[row + seg] = ac.ph;
+                anc_kc[row + seg] = (uint32_t)ac.icode | ((uint32_t)ac.ibit << 8) |
+                                    ((uint32_t)ac.iword << 16);
+                seg++;
+            }
+            if (!wr || seg >= nseg)
+                break;
+            an = (int32_t)it.pos;
+            ac = it.c;
+        }
     }
-    if (carr_end)
-        carr_end[(size_t)b * GSS_MAXCH + k] = x;
 }
 
 /* ======================================================================================== */
 /* Stage B: synthesis                                                                       */
 /* ======================================================================================== */
 template <int FMT> struct fmt_traits;
-template <> struct fmt_traits<16> { static constexpr int SPV = 4; };   /* samples per 16 B */
-template <> struct fmt_traits<8>  { static constexpr int SPV = 8; };
-template <> struct fmt_traits<1>  { static constexpr int SPV = 64; };
+template <> struct fmt_traits<16> { static constexpr int SPC = 16;  };  /* samples per chunk */
+template <> struct fmt_traits<8>  { static constexpr int SPC = 32;  };
+template <> struct fmt_traits<1>  { static constexpr int SPC = 256; };
 
 __device__ __forceinline__ uint32_t hi32(double v) { return (uint32_t)__double2hiint(v); }
+__device__ __forceinline__ double with_hi(uint32_t hi) { return __hiloint2double((int)hi, 0); }
 
-/* (acc+64)>>7 → int16 pair, from the packed 64-bit accumulator  I + Q*2^32 */
-__device__ __forceinline__ void quantise(uint64_t acc, int &i16, int &q16)
-{
-    int32_t isum = (int32_t)(uint32_t)acc;
-    int32_t qsum = (int32_t)((int64_t)(acc - (uint64_t)(int64_t)isum) >> 32);
-    i16 = (int)(int16_t)((isum + 64) >> 7);
-    q16 = (int)(int16_t)((qsum + 64) >> 7);
-}
-
-/* One output sample: all channels' contributions, then the exact state advance.
-   Reference: gpssim.c:2195-2256 (per channel) and 2257-2259 (rounding). */
-template <int NCH>
-__device__ __forceinline__ void one_sample(double *Y, double *C, uint32_t *ctr, uint32_t *cab,
-                                           const uint64_t *s_lut, const uint32_t *s_ca,
-                                           const uint32_t *s_nav, const double2 *ustep,
-                                           int &bad, int &i16, int &q16)
-{
-    uint64_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < NCH; k++) {
-        /* LUT[floor(512 carr)] × chip sign × data sign × gain (gpssim.c:2200-2209); the sign
-           flips the LUT index by half a cycle: LUT[(i+256)%512] == -LUT[i]. */
-        int ci = (int)C[k];
-        uint32_t cw = *(const uint32_t *)((const uint8_t *)(s_ca + k * 2 * GSS_CA_WORDS) +
-                                          cab[k] + ((ci >> 5) << 2));
-        uint32_t neg = (cw >> (ci & 31)) & 1u;
-        int ti = (int)Y[k];
-        acc += s_lut[k * 512 + ((ti + (int)(neg << 8)) & 511)];
-
-        /* carrier advance + wrap (gpssim.c:2245-2250) in Y = 512*carr units.  The test is on
-           the value, like the reference: hi32(Y) >= hi32(512.0) holds exactly when Y >= 512
-           or Y < 0 (sign bit); then Y -= 512 or Y += 512. */
-        Y[k] = Y[k] + ustep[k].x;
-        if (hi32(Y[k]) >= 0x40800000u)
-            Y[k] = Y[k] + (Y[k] < 0.0 ? 512.0 : -512.0);
-
-        /* code advance + chip/bit/word counters (gpssim.c:2212-2237) */
-        C[k] = C[k] + ustep[k].y;
-        if (C[k] >= 1023.0) {
-            C[k] -= 1023.0;
-            uint32_t c = ctr[k];
-            int icode = (int)(c & 0xFF) + 1, ibit = (c >> 8) & 0xFF, iword = c >> 16;
-            if (icode >= 20) {
-                icode = 0;
-                if (++ibit >= 30) { ibit = 0; iword++; }
-                if (iword > 59) { bad = 1; iword = 59; }
-                cab[k] = ((s_nav[k * 64 + iword] >> (29 - ibit)) & 1u) * (GSS_CA_WORDS * 4);
-            }
-            ctr[k] = (uint32_t)icode | ((uint32_t)ibit << 8) | ((uint32_t)iword << 16);
-        }
-    }
-    quantise(acc, i16, q16);
-}
-
-/* Place one quantised sample into the 16-byte output vector (gpssim.c:2266-2287). */
-template <int FMT>
-__device__ __forceinline__ void pack_sample(uint32_t *word, int sidx, int i16, int q16)
-{
-    if (FMT == 16) {
-        word[sidx] = (uint32_t)(uint16_t)i16 | ((uint32_t)(uint16_t)q16 << 16);
-    } else if (FMT == 8) {                     /* iq_buff >> 4 → signed char */
-        uint32_t pair = (uint32_t)(uint8_t)(int8_t)(i16 >> 4) |
-                        ((uint32_t)(uint8_t)(int8_t)(q16 >> 4) << 8);
-        word[sidx >> 1] |= pair << (16 * (sidx & 1));
-    } else {                                   /* byte = {I0 Q0 I1 Q1 I2 Q2 I3 Q3}, MSB first */
-        int byte = sidx >> 2, pos = 7 - 2 * (sidx & 3);
-        uint32_t bits = ((uint32_t)(i16 > 0) << pos) | ((uint32_t)(q16 > 0) << (pos - 1));
-        word[byte >> 2] |= bits << (8 * (byte & 3));
-    }
-}
-
-/* 16 output bytes: one dwordx4 store when the address allows it (block bases are multiples of
-   the block size, which need not be a multiple of 16, e.g. -b 1 blocks of 65000 B). */
-__device__ __forceinline__ void store16(uint8_t *p, const uint32_t *w)
+/* 16 bytes to global memory: one dwordx4 store when aligned (block bases are multiples of the
+   block size, e.g. 65000 B at -b 1, so not always). */
+__device__ __forceinline__ void store16(uint8_t *p, uint4 v)
 {
     uintptr_t a = (uintptr_t)p;
     if ((a & 15) == 0) {
-        *(uint4 *)p = make_uint4(w[0], w[1], w[2], w[3]);
+        *(uint4 *)p = v;
     } else if ((a & 3) == 0) {
-        for (int i = 0; i < 4; i++)
-            ((uint32_t *)p)[i] = w[i];
+        ((uint32_t *)p)[0] = v.x; ((uint32_t *)p)[1] = v.y;
+        ((uint32_t *)p)[2] = v.z; ((uint32_t *)p)[3] = v.w;
     } else {
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
         for (int i = 0; i < 16; i++)
             p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
     }
 }
 
+/* Lane start state, walked from the anchors.  Out of line on purpose: inlined twelve times into
+   the unrolled channel loop these walks would dominate the register allocation of the whole
+   kernel; as calls they run once per lane per channel and cost nothing in the sample loop. */
+struct lane_start { double Y, C; uint32_t st; int bad; };
+
+__device__ __noinline__ lane_start lane_start_walk(double ax, int an, double cstep, double kx,
+                                                   int kn, uint32_t kc, double kstep, int n0,
+                                                   const uint32_t *nav_row)
+{
+    lane_start r;
+    r.Y = gss_carr_walk(ax, cstep, n0 - an) * 512.0;
+    gss_code_state c;
+    c.ph = kx;
+    c.icode = kc & 0xFF;
+    c.ibit = (kc >> 8) & 0xFF;
+    c.iword = kc >> 16;
+    gss_code_walk(&c, kstep, n0 - kn);
+    r.C = c.ph;
+    int iw = c.iword;
+    r.bad = 0;
+    if (iw > 59) { r.bad = 1; iw = 59; }
+    uint32_t pol = (nav_row[iw] >> (29 - c.ibit)) & 1u;
+    r.st = (uint32_t)c.icode | ((uint32_t)c.ibit << 8) | ((uint32_t)iw << 16) | (pol << 24);
+    return r;
+}
+
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int NCH, int FMT>
-__global__ __launch_bounds__(SYNTH_THREADS, 2) void gss_synth_kernel(
+__global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch,
     const uint32_t *__restrict__ ca_bits, const uint32_t *__restrict__ nav,
-    const double *__restrict__ ck_carr, const double *__restrict__ ck_code,
-    const uint32_t *__restrict__ ck_ctr, const double2 *__restrict__ steps, lut_arg lut,
-    int n_per_blk, int nseg, int wg_per_blk, uint8_t *__restrict__ out, size_t block_bytes,
-    int32_t *__restrict__ status)
+    const int32_t *__restrict__ anc_cn, const double *__restrict__ anc_cx,
+    const int32_t *__restrict__ anc_kn, const double *__restrict__ anc_kx,
+    const uint32_t *__restrict__ anc_kc, const chan_uni *__restrict__ uni, lut_arg lut,
+    int n_per_blk, int nseg, int seg_r, int wg_per_blk, uint8_t *__restrict__ out,
+    size_t block_bytes, int32_t *__restrict__ status)
 {
-    constexpr int SPV = fmt_traits<FMT>::SPV;
-    __shared__ uint64_t s_lut[NCH][512];          /* (cos*gain) + (sin*gain)<<32            */
-    __shared__ uint32_t s_ca[NCH][2][GSS_CA_WORDS]; /* [pol]: neg-sign bit per chip           */
+    constexpr int SPC = fmt_traits<FMT>::SPC;
+    constexpr int BPS4 = FMT == 16 ? 16 : FMT == 8 ? 8 : 1;      /* 4 x bytes per sample */
+    __shared__ int2 s_lut[LUT_N];                         /* (cos, sin) of index mod 512  */
+    __shared__ uint32_t s_ca[NCH][2][GSS_CA_WORDS];       /* [pol]: 1 = negative sign      */
     __shared__ uint32_t s_nav[NCH][64];
+    __shared__ uint32_t s_stage[SYNTH_WAVES][64 * CHUNK_BYTES / 4];
 
     const int b = blockIdx.x / wg_per_blk;
     const int w = blockIdx.x % wg_per_blk;
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
     const int nc = nch[b];
     const gss_chan_blk_t *prow = blk + (size_t)b * GSS_MAXCH;
 
     /* ---- LDS tables for this block ---- */
-    for (int i = tid; i < NCH * 512; i += SYNTH_THREADS) {
-        int k = i >> 9, j = i & 511;
-        int32_t g = k < nc ? prow[k].gain : 0;
-        int64_t I = (int64_t)lut.cos512[j] * g, Q = (int64_t)lut.sin512[j] * g;
-        s_lut[k][j] = (uint64_t)I + ((uint64_t)Q << 32);
-    }
+    for (int i = tid; i < LUT_N; i += SYNTH_THREADS)
+        s_lut[i] = make_int2(lut.cos512[i & 511], lut.sin512[i & 511]);
     for (int i = tid; i < NCH * GSS_CA_WORDS; i += SYNTH_THREADS) {
         int k = i / GSS_CA_WORDS, j = i % GSS_CA_WORDS;
         uint32_t v = k < nc ? ca_bits[(size_t)prow[k].ca_tbl * GSS_CA_WORDS + j] : 0u;
-        /* sign = dataBit*codeCA is negative iff chip != data bit:
-           pol 0 (data bit 0): neg = chip;  pol 1 (data bit 1): neg = !chip */
+        /* sign = dataBit*codeCA < 0 iff chip != data bit: pol 0 (bit 0): neg = chip,
+           pol 1 (bit 1): neg = !chip */
         s_ca[k][0][j] = v;
         s_ca[k][1][j] = ~v;
     }
@@ -214,60 +238,162 @@ __global__ __launch_bounds__(SYNTH_THREADS, 2) void gss_synth_kernel(
                           ? nav[(size_t)prow[k].nav_tbl * GSS_NAV_WORDS + j] : 0u;
     }
     __syncthreads();
-    const double2 *ustep = steps + (size_t)b * GSS_MAXCH;   /* block-uniform: scalar loads */
 
     const int seg = w * SYNTH_THREADS + tid;
-    if (seg >= nseg)
-        return;
-    int len = n_per_blk - seg * SEG_R;
-    if (len > SEG_R) len = SEG_R;
+    const bool active = seg < nseg;
+    const int n0 = seg * seg_r;
+    int len = active ? n_per_blk - n0 : 0;
+    if (len > seg_r) len = seg_r;
+    const int segc = active ? seg : nseg - 1;           /* inactive lanes: any valid anchor */
+    const int n0c = segc * seg_r;
+    const chan_uni *u = uni + (size_t)b * GSS_MAXCH;     /* block-uniform: scalar loads */
 
-    /* ---- per-lane channel state from the checkpoints ---- */
+    /* ---- exact per-lane start state: walk each channel from its anchor.  Unconditional
+       for every channel of the instance (padding channels have zero anchors and zero steps):
+       a conditional, partially-assigned state array costs the allocator ~4x the registers. */
     double Y[NCH], C[NCH];
-    uint32_t ctr[NCH], cab[NCH];
+    uint32_t st[NCH];             /* icode | ibit<<8 | iword<<16 | pol<<24 */
     int bad = 0;
 #pragma unroll
     for (int k = 0; k < NCH; k++) {
-        size_t r = ((size_t)b * GSS_MAXCH + k) * (size_t)nseg + seg;
-        Y[k] = ck_carr[r] * 512.0;
-        C[k] = ck_code[r];
-        ctr[k] = ck_ctr[r];
-        int ibit = (ctr[k] >> 8) & 0xFF, iword = ctr[k] >> 16;
-        if (iword > 59) { bad = 1; iword = 59; }
-        uint32_t d = (s_nav[k][iword] >> (29 - ibit)) & 1u;
-        cab[k] = d * (GSS_CA_WORDS * 4);              /* byte offset of the polarity table */
+        size_t r = ((size_t)b * GSS_MAXCH + k) * (size_t)nseg + segc;
+        lane_start ls = lane_start_walk(anc_cx[r], anc_cn[r], u[k].S * (1.0 / 512.0),
+                                        anc_kx[r], anc_kn[r], anc_kc[r], u[k].CS, n0c,
+                                        &s_nav[k][0]);
+        Y[k] = ls.Y;
+        C[k] = ls.C;
+        st[k] = ls.st;
+        bad |= ls.bad;
     }
 
-    uint8_t *dst = out + (size_t)b * block_bytes;
-    size_t byte0 = FMT == 16 ? (size_t)seg * SEG_R * 4 : FMT == 8 ? (size_t)seg * SEG_R * 2
-                                                       : (size_t)seg * SEG_R / 4;
-    uint8_t *vdst = dst + byte0;
-    const int nfull = len / SPV;
+    uint8_t *dst = out + (size_t)b * block_bytes + (size_t)n0 * BPS4 / 4;
+    uint32_t *stg = s_stage[wave];
+    uint32_t *mine = stg + lane * (CHUNK_BYTES / 4);
+    const int nchunk = len / SPC;
+    int wave_chunks = nchunk;                 /* all lanes join every staged store round */
+    for (int off = 32; off > 0; off >>= 1)
+        wave_chunks = max(wave_chunks, __shfl_xor(wave_chunks, off));
 
-    for (int v = 0; v < nfull; v++) {
-        uint32_t word[4] = {0u, 0u, 0u, 0u};
+    for (int ch = 0; ch <= wave_chunks; ch++) {
+        const bool full = ch < nchunk;
+        const int nsamp = full ? SPC : (ch == nchunk ? len - nchunk * SPC : 0);
+        uint32_t bits = 0;
+#pragma unroll 1
+        for (int sidx = 0; sidx < nsamp; sidx++) {
+            int acc_i = 0, acc_q = 0;
+            uint32_t wrapped = 0;            /* bit k: channel k's code phase reached 1023 */
+            /* channels in groups of 4: issue the group's chip-word reads, then its LUT reads,
+               then consume — keeps LDS latency overlapped without holding all 16 in flight */
 #pragma unroll
-        for (int sidx = 0; sidx < SPV; sidx++) {
-            int i16, q16;
-            one_sample<NCH>(Y, C, ctr, cab, &s_lut[0][0], &s_ca[0][0][0], &s_nav[0][0], ustep,
-                            bad, i16, q16);
-            pack_sample<FMT>(word, sidx, i16, q16);
+            for (int k0 = 0; k0 < NCH; k0 += 4) {
+                constexpr int GW = 4;
+                int ci[GW], ti[GW];
+                uint32_t cw[GW];
+                int2 e[GW];
+#pragma unroll
+                for (int j = 0; j < GW; j++) {
+                    if (k0 + j < NCH) {
+                        const int k = k0 + j;
+                        ci[j] = (int)C[k];
+                        ti[j] = (int)Y[k];
+                        cw[j] = s_ca[k][st[k] >> 24][ci[j] >> 5];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < GW; j++) {
+                    if (k0 + j < NCH) {
+                        /* LUT[floor(512 carr)] × chip sign × data sign (gpssim.c:2200-2209);
+                           a negative sign is half a carrier cycle: LUT[i+256] = -LUT[i] */
+                        uint32_t neg = (cw[j] >> (ci[j] & 31)) & 1u;
+                        e[j] = s_lut[(ti[j] & 511) + (int)(neg << 8)];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < GW; j++) {
+                    if (k0 + j < NCH) {
+                        const int k = k0 + j;
+                        int g = u[k].gain;
+                        acc_i += __mul24(e[j].x, g);
+                        acc_q += __mul24(e[j].y, g);
+
+                        /* carrier advance + wrap (gpssim.c:2245-2250), Y = 512 carr.  Same test
+                           as the reference, on the value: hi32(Y) >= hi32(512.0) holds exactly
+                           when Y >= 512 or Y < 0; then Y -= A with A = +512 for Y >= 0 and -512
+                           for Y < 0, hi32(A) = (sign of Y) | hi32(512.0). */
+                        double y = Y[k] + u[k].S;
+                        uint32_t hy = hi32(y);
+                        uint32_t ahi = (hy & 0x80000000u) | 0x40800000u;
+                        Y[k] = y - with_hi(hy >= 0x40800000u ? ahi : 0u);
+
+                        /* code advance (gpssim.c:2212); the wrap test on hi32 is C >= 1023.0 */
+                        C[k] = C[k] + u[k].CS;
+                        wrapped |= (hi32(C[k]) >= 0x408FF800u ? 1u : 0u) << k;
+                    }
+                }
+            }
+            /* rare: some channel's code phase wrapped (once per ~2600 samples per channel) */
+            if (__builtin_expect(__any(wrapped != 0), 0)) {
+#pragma unroll
+                for (int k = 0; k < NCH; k++) {
+                    if (wrapped & (1u << k)) {       /* gpssim.c:2214-2237 */
+                        C[k] -= 1023.0;
+                        uint32_t c = st[k];
+                        int icode = (int)(c & 0xFF) + 1, ibit = (c >> 8) & 0xFF,
+                            iword = (c >> 16) & 0xFF;
+                        uint32_t p2 = c >> 24;
+                        if (icode >= 20) {
+                            icode = 0;
+                            if (++ibit >= 30) { ibit = 0; iword++; }
+                            if (iword > 59) { bad = 1; iword = 59; }
+                            p2 = (s_nav[k][iword] >> (29 - ibit)) & 1u;
+                        }
+                        st[k] = (uint32_t)icode | ((uint32_t)ibit << 8) |
+                                ((uint32_t)iword << 16) | (p2 << 24);
+                    }
+                }
+            }
+            /* gpssim.c:2257-2263: (acc+64)>>7 (arithmetic), then (short) */
+            int i16 = (int)(int16_t)((acc_i + 64) >> 7);
+            int q16 = (int)(int16_t)((acc_q + 64) >> 7);
+            if (FMT == 16) {
+                mine[sidx] = (uint32_t)(uint16_t)i16 | ((uint32_t)(uint16_t)q16 << 16);
+            } else if (FMT == 8) {                    /* iq_buff >> 4 → signed char */
+                ((uint16_t *)mine)[sidx] = (uint16_t)((uint32_t)(uint8_t)(int8_t)(i16 >> 4) |
+                                           ((uint32_t)(uint8_t)(int8_t)(q16 >> 4) << 8));
+            } else {                                  /* {I0 Q0 I1 Q1 ...} MSB first */
+                bits = (bits << 2) | ((uint32_t)(i16 > 0) << 1) | (uint32_t)(q16 > 0);
+                if ((sidx & 15) == 15 || sidx == nsamp - 1) {
+                    int nb = (sidx & 15) + 1;         /* samples in this word (16 unless tail) */
+                    bits <<= 2 * (16 - nb);
+                    mine[sidx >> 4] = __builtin_bswap32(bits);
+                    bits = 0;
+                }
+            }
         }
-        store16(vdst + 16 * v, word);
-    }
-    const int remain = len - nfull * SPV;           /* ragged tail of the block's last segment */
-    if (remain > 0) {
-        uint32_t word[4] = {0u, 0u, 0u, 0u};
-        for (int sidx = 0; sidx < remain; sidx++) {
-            int i16, q16;
-            one_sample<NCH>(Y, C, ctr, cab, &s_lut[0][0], &s_ca[0][0][0], &s_nav[0][0], ustep,
-                            bad, i16, q16);
-            pack_sample<FMT>(word, sidx, i16, q16);
+        const bool any_full = __any(full);
+        if (any_full) {
+            /* the wave stores 16 lanes' 64-B pieces per instruction: lane j stores piece j%4
+               of source lane 16 i + j/4 */
+            wave_sync_lds();
+            for (int i = 0; i < 4; i++) {
+                int src = 16 * i + (lane >> 2), piece = lane & 3;
+                int src_full = __shfl(full ? 1 : 0, src);
+                if (src_full) {
+                    uint8_t *sdst = dst + (ptrdiff_t)(src - lane) * ((ptrdiff_t)seg_r * BPS4 / 4) +
+                                    (size_t)ch * CHUNK_BYTES + piece * 16;
+                    const uint32_t *sp = stg + src * (CHUNK_BYTES / 4) + piece * 4;
+                    store16(sdst, make_uint4(sp[0], sp[1], sp[2], sp[3]));
+                }
+            }
+            wave_sync_lds();
         }
-        int nbytes = FMT == 16 ? remain * 4 : FMT == 8 ? remain * 2 : remain / 4;
-        uint8_t *bp = vdst + 16 * nfull;
-        for (int i = 0; i < nbytes; i++)
-            bp[i] = (uint8_t)(word[i >> 2] >> (8 * (i & 3)));
+        if (!full && nsamp > 0) {                     /* ragged tail: this lane's own bytes */
+            int nbytes = nsamp * BPS4 / 4;
+            uint8_t *bp = dst + (size_t)ch * CHUNK_BYTES;
+            const uint8_t *sp = (const uint8_t *)mine;
+            for (int i = 0; i < nbytes; i++)
+                bp[i] = sp[i];
+        }
     }
     if (bad && status)
         atomicOr(status, 1);
@@ -278,16 +404,17 @@ __global__ __launch_bounds__(SYNTH_THREADS, 2) void gss_synth_kernel(
 /* ======================================================================================== */
 struct gss_dev {
     int ordinal;
-    double *ck_carr = nullptr, *ck_code = nullptr;
-    uint32_t *ck_ctr = nullptr;
-    size_t ck_cap = 0;                   /* entries */
-    double2 *steps = nullptr;
-    size_t steps_cap = 0;                /* blocks */
+    int seg_r = 1024;                    /* samples per Stage-B lane (env GSS_SEG_R)   */
+    int32_t *anc_cn = nullptr, *anc_kn = nullptr;   /* anchors [blocks][16][nseg]   */
+    double *anc_cx = nullptr, *anc_kx = nullptr;
+    uint32_t *anc_kc = nullptr;
+    size_t anc_cap = 0;
+    chan_uni *uni = nullptr;
+    size_t uni_cap = 0;
     static constexpr int RING = 256;
     hipEvent_t ev[RING][3];
-    int n_ev = 0;                        /* launches recorded since the last reset */
+    int n_ev = 0;
     lut_arg lut;
-    /* host-call staging */
     void *h_in = nullptr; size_t h_in_cap = 0;
     void *d_out = nullptr; size_t d_out_cap = 0;
     double *d_cend = nullptr; size_t d_cend_cap = 0;
@@ -326,9 +453,12 @@ extern "C" int gss_dev_open(gss_dev **out, int ordinal)
     HIP_TRY(hipSetDevice(ordinal));
     gss_dev *d = new gss_dev();
     d->ordinal = ordinal;
-    for (int r = 0; r < gss_dev::RING; r++)
-        for (int i = 0; i < 3; i++)
-            HIP_TRY(hipEventCreate(&d->ev[r][i]));
+    const char *r = getenv("GSS_SEG_R");
+    if (r && atoi(r) >= 256 && atoi(r) % 256 == 0)
+        d->seg_r = atoi(r);
+    for (int i = 0; i < gss_dev::RING; i++)
+        for (int j = 0; j < 3; j++)
+            HIP_TRY(hipEventCreate(&d->ev[i][j]));
     int32_t s[512], c[512];
     gss_lut(s, c);
     for (int i = 0; i < 512; i++) {
@@ -344,46 +474,54 @@ extern "C" int gss_dev_close(gss_dev *d)
 {
     if (!d) return 0;
     (void)hipSetDevice(d->ordinal);
-    void *bufs[] = {d->ck_carr, d->ck_code, d->ck_ctr, d->steps, d->h_in, d->d_out, d->d_cend,
-                    d->d_status};
+    void *bufs[] = {d->anc_cn, d->anc_kn, d->anc_cx, d->anc_kx, d->anc_kc, d->uni,
+                    d->h_in, d->d_out, d->d_cend, d->d_status};
     for (void *p : bufs)
         (void)hipFree(p);
-    for (int r = 0; r < gss_dev::RING; r++)
-        for (int i = 0; i < 3; i++)
-            (void)hipEventDestroy(d->ev[r][i]);
+    for (int i = 0; i < gss_dev::RING; i++)
+        for (int j = 0; j < 3; j++)
+            (void)hipEventDestroy(d->ev[i][j]);
     delete d;
     return 0;
 }
 
-static int nseg_of(int n) { return (n + SEG_R - 1) / SEG_R; }
+static int nseg_of(int n, int r) { return (n + r - 1) / r; }
 
 extern "C" int gss_dev_reserve(gss_dev *d, int max_blocks, int n_per_blk)
 {
     if (!d || max_blocks <= 0 || n_per_blk <= 0)
         return gss_fail(GSS_E_ARG, "invalid reserve arguments");
     HIP_TRY(hipSetDevice(d->ordinal));
-    if ((size_t)max_blocks > d->steps_cap) {
-        (void)hipFree(d->steps);
-        d->steps = nullptr;
-        d->steps_cap = 0;
-        HIP_TRY(hipMalloc(&d->steps, sizeof(double2) * GSS_MAXCH * (size_t)max_blocks));
-        d->steps_cap = (size_t)max_blocks;
+    if ((size_t)max_blocks > d->uni_cap) {
+        (void)hipFree(d->uni);
+        d->uni = nullptr;
+        d->uni_cap = 0;
+        HIP_TRY(hipMalloc(&d->uni, sizeof(chan_uni) * GSS_MAXCH * (size_t)max_blocks));
+        d->uni_cap = (size_t)max_blocks;
     }
-    size_t need = (size_t)max_blocks * GSS_MAXCH * (size_t)nseg_of(n_per_blk);
-    if (need <= d->ck_cap)
+    size_t need = (size_t)max_blocks * GSS_MAXCH * (size_t)nseg_of(n_per_blk, d->seg_r);
+    if (need <= d->anc_cap)
         return 0;
-    (void)hipFree(d->ck_carr); (void)hipFree(d->ck_code); (void)hipFree(d->ck_ctr);
-    d->ck_carr = d->ck_code = nullptr; d->ck_ctr = nullptr; d->ck_cap = 0;
-    HIP_TRY(hipMalloc(&d->ck_carr, need * sizeof(double)));
-    HIP_TRY(hipMalloc(&d->ck_code, need * sizeof(double)));
-    HIP_TRY(hipMalloc(&d->ck_ctr, need * sizeof(uint32_t)));
-    d->ck_cap = need;
+    void *old[] = {d->anc_cn, d->anc_kn, d->anc_cx, d->anc_kx, d->anc_kc};
+    for (void *p : old)
+        (void)hipFree(p);
+    d->anc_cn = d->anc_kn = nullptr;
+    d->anc_cx = d->anc_kx = nullptr;
+    d->anc_kc = nullptr;
+    d->anc_cap = 0;
+    HIP_TRY(hipMalloc(&d->anc_cn, need * sizeof(int32_t)));
+    HIP_TRY(hipMalloc(&d->anc_kn, need * sizeof(int32_t)));
+    HIP_TRY(hipMalloc(&d->anc_cx, need * sizeof(double)));
+    HIP_TRY(hipMalloc(&d->anc_kx, need * sizeof(double)));
+    HIP_TRY(hipMalloc(&d->anc_kc, need * sizeof(uint32_t)));
+    d->anc_cap = need;
     return 0;
 }
 
 typedef void (*synth_fn)(const gss_chan_blk_t *, const int32_t *, const uint32_t *,
-                         const uint32_t *, const double *, const double *, const uint32_t *,
-                         const double2 *, lut_arg, int, int, int, uint8_t *, size_t, int32_t *);
+                         const uint32_t *, const int32_t *, const double *, const int32_t *,
+                         const double *, const uint32_t *, const chan_uni *, lut_arg, int, int,
+                         int, int, uint8_t *, size_t, int32_t *);
 
 template <int FMT> static synth_fn pick_nch(int nchp)
 {
@@ -406,9 +544,9 @@ static synth_fn pick_kernel(int fmt, int nchp)
 }
 
 extern "C" int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
-                                int nch_max, const uint32_t *ca_bits, int n_ca, const uint32_t *nav,
-                                int n_nav, int nblk, int n_per_blk, int fmt, void *out,
-                                double *carr_end, int32_t *status, void *stream)
+                                int nch_max, const uint32_t *ca_bits, int n_ca,
+                                const uint32_t *nav, int n_nav, int nblk, int n_per_blk, int fmt,
+                                void *out, double *carr_end, int32_t *status, void *stream)
 {
     (void)n_ca; (void)n_nav;
     if (!d || !blk || !nch || !ca_bits || !out || nblk <= 0 || n_per_blk <= 0)
@@ -420,27 +558,28 @@ extern "C" int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int
     int rc = gss_dev_reserve(d, nblk, n_per_blk);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    int nseg = nseg_of(n_per_blk);
-    int nchp = nch_max < 1 ? 1 : nch_max;         /* kernel instance; fewer channels padded */
+    const int R = d->seg_r;
+    int nseg = nseg_of(n_per_blk, R);
+    int nchp = nch_max < 1 ? 1 : nch_max;          /* kernel instance; fewer channels padded */
     if (nchp > GSS_MAXCH)
         return gss_fail(GSS_E_ARG, "nch_max %d > %d", nch_max, GSS_MAXCH);
     synth_fn fn = pick_kernel(fmt, nchp);
     if (!fn)
         return gss_fail(GSS_E_ARG, "no kernel for fmt=%d nch=%d", fmt, nchp);
 
-    int ck_blocks = (nblk * GSS_MAXCH + CKPT_THREADS - 1) / CKPT_THREADS;
     hipEvent_t *ev = d->ev[d->n_ev % gss_dev::RING];
     d->n_ev++;
+    int a_blocks = (nblk * GSS_MAXCH * 2 + ANCHOR_THREADS - 1) / ANCHOR_THREADS;
     HIP_TRY(hipEventRecord(ev[0], st));
-    hipLaunchKernelGGL(gss_ckpt_kernel, dim3(ck_blocks), dim3(CKPT_THREADS), 0, st, blk, nch,
-                       nblk, n_per_blk, nseg, nchp, d->ck_carr, d->ck_code, d->ck_ctr,
-                       d->steps, carr_end);
+    hipLaunchKernelGGL(gss_anchor_kernel, dim3(a_blocks), dim3(ANCHOR_THREADS), 0, st, blk, nch,
+                       nblk, nchp, n_per_blk, nseg, R, d->anc_cn, d->anc_cx, d->anc_kn, d->anc_kx,
+                       d->anc_kc, d->uni, carr_end);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], st));
     int wg_per_blk = (nseg + SYNTH_THREADS - 1) / SYNTH_THREADS;
-    hipLaunchKernelGGL(fn, dim3(nblk * wg_per_blk), dim3(SYNTH_THREADS), 0, st, blk, nch,
-                       ca_bits, nav, d->ck_carr, d->ck_code, d->ck_ctr, d->steps, d->lut,
-                       n_per_blk, nseg, wg_per_blk, (uint8_t *)out, bb, status);
+    hipLaunchKernelGGL(fn, dim3(nblk * wg_per_blk), dim3(SYNTH_THREADS), 0, st, blk, nch, ca_bits,
+                       nav, d->anc_cn, d->anc_cx, d->anc_kn, d->anc_kx, d->anc_kc, d->uni, d->lut,
+                       n_per_blk, nseg, R, wg_per_blk, (uint8_t *)out, bb, status);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[2], st));
     return 0;
@@ -494,6 +633,8 @@ extern "C" int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32
     size_t bb = gss_block_bytes(n_per_blk, fmt);
     if (bb == 0)
         return gss_fail(GSS_E_ARG, "invalid format %d for %d samples/block", fmt, n_per_blk);
+    if (n_per_blk > (1 << 30))
+        return gss_fail(GSS_E_ARG, "block too large");
     HIP_TRY(hipSetDevice(d->ordinal));
     int maxc = 1;
     for (int b = 0; b < nblk; b++) {
@@ -505,7 +646,9 @@ extern "C" int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32
             if (p->ca_tbl < 0 || p->ca_tbl >= n_ca || p->nav_tbl < 0 || p->nav_tbl >= n_nav ||
                 p->ibit < 0 || p->ibit >= 30 || p->icode < 0 || p->icode >= 20 || p->iword < 0 ||
                 p->iword >= GSS_NAV_WORDS || !(p->code0 >= 0.0 && p->code0 < 1023.0) ||
-                !(p->carr0 >= 0.0 && p->carr0 <= 1.0))
+                !(p->carr0 >= 0.0 && p->carr0 <= 1.0) ||
+                !(p->code_step > 0.0 && p->code_step < 1023.0) ||
+                !(p->carr_step > -1.0 && p->carr_step < 1.0))
                 return gss_fail(GSS_E_ARG, "block %d channel %d: parameter out of range", b, k);
         }
     }
@@ -546,9 +689,9 @@ extern "C" int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32
     if (carr_end)
         HIP_TRY(hipMemcpy(carr_end, d_cend, sizeof(double) * GSS_MAXCH * (size_t)nblk,
                           hipMemcpyDeviceToHost));
-    int32_t st = 0;
-    HIP_TRY(hipMemcpy(&st, d->d_status, sizeof st, hipMemcpyDeviceToHost));
-    if (st)
+    int32_t stv = 0;
+    HIP_TRY(hipMemcpy(&stv, d->d_status, sizeof stv, hipMemcpyDeviceToHost));
+    if (stv)
         return gss_fail(GSS_E_RANGE, "nav word index ran past dwrd[59]");
     return 0;
 }

@@ -386,7 +386,7 @@ static void *plan_slots(void *arg)
                 if (s->b_reset[e])
                     x = s->b_init[e];
                 j->blk[e].carr0 = x;
-                x = gss_carr_walk(x, j->blk[e].carr_step, s->n_per_blk);
+                x = gss_carr_walk_cc(x, j->blk[e].carr_step, s->n_per_blk);
                 break;
             }
         }
@@ -582,14 +582,14 @@ int gss_ca_table(uint32_t *out)
 
 double gss_carr_advance(double carr, double step, int64_t n)
 {
-    return gss_carr_walk(carr, step, n);
+    return gss_carr_walk_cc(carr, step, n);
 }
 
 double gss_code_advance(double code, double step, int64_t n, int32_t *icode, int32_t *ibit,
                         int32_t *iword)
 {
     gss_code_state c = {code, *icode, *ibit, *iword};
-    gss_code_walk(&c, step, n);
+    gss_code_walk_cc(&c, step, n);
     *icode = c.icode;
     *ibit = c.ibit;
     *iword = c.iword;

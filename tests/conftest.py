@@ -46,3 +46,31 @@ def built():
 def golden():
     with open(GOLDEN) as f:
         return json.load(f)
+
+
+_walk = None
+
+
+def walk_lib():
+    """ctypes handle on tests/helpers/walk_check.c (built on first use with gcc)."""
+    global _walk
+    if _walk is None:
+        import ctypes as C
+        src = os.path.join(REPO, "tests", "helpers", "walk_check.c")
+        so = os.path.join(REPO, "tests", "helpers", "_walk_check.so")
+        if not os.path.exists(so) or os.path.getmtime(so) < max(
+                os.path.getmtime(src),
+                os.path.getmtime(os.path.join(PKG, "csrc", "common", "gss_phase.h"))):
+            subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-o",
+                                   so, src])
+        L = C.CDLL(so)
+        D, I64, P = C.c_double, C.c_int64, C.POINTER(C.c_int32)
+        for f in ("wc_carr_plain", "wc_carr_cached"):
+            getattr(L, f).restype = D
+            getattr(L, f).argtypes = [D, D, I64]
+        L.wc_code.restype = D
+        L.wc_code.argtypes = [C.c_int, D, D, I64, P, P, P]
+        L.wc_carr_anchors.restype = C.c_int
+        L.wc_carr_anchors.argtypes = [D, D, I64, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        _walk = L
+    return _walk

@@ -1,55 +1,105 @@
-"""The exact jump-ahead walk (common/gss_phase.h) against the brute-force reference recurrences
-(one IEEE double add per sample, gpssim.c:2212-2250): bit-identical, including forced
-round-half-even ties, zero phase, both Doppler signs and tiny steps."""
+"""The exact phase arithmetic (common/gss_phase.h) against the brute-force reference recurrences
+(one IEEE double add per sample, gpssim.c:2212-2250): the plain binade walk (Stage-B lanes), the
+cycle-cached walk (Stage A and the host planner) and the anchors Stage A emits are all
+bit-identical to brute force, including forced round-half-even ties, zero phase, both Doppler
+signs, tiny and LEO-sized Dopplers, 2.6 and 20 MS/s."""
+import ctypes as C
 import math
 import random
 
+import numpy as np
 import pytest
+
+from conftest import walk_lib
 
 import gpssim_amd as G
 import oracle
-
-DELT = 1.0 / 2600000.0
 
 
 def cases(seed, n):
     rng = random.Random(seed)
     for i in range(n):
-        f = rng.uniform(-6000, 6000) if i % 5 else rng.uniform(-60, 60)
-        s = f * DELT
+        fs = 2.6e6 if i % 3 else 2.0e7
+        f = rng.uniform(-6000, 6000)
+        if i % 5 == 0:
+            f = rng.uniform(-60, 60)
+        if i % 17 == 0:
+            f = rng.uniform(-40000, 40000)
+        s = f / fs
         if i % 7 == 0:                       # tie w.r.t. the top-binade lattice 2^-53
             u = 2.0 ** -53
             s = math.copysign((math.floor(abs(s) / u) + 0.5) * u, s)
+        if i % 19 == 0:                      # exact multiple of 2^-53
+            u = 2.0 ** -53
+            s = math.copysign(math.floor(abs(s) / u) * u, s)
         x = rng.random()
         if i % 11 == 0:
             x = 0.0
         if i % 13 == 0:
             x = 1.0 - 2.0 ** -53
-        yield x, s, rng.randint(1, 300000)
+        yield x, s, rng.randint(1, int(fs / 10))
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_carrier_walk_exact(seed):
-    for x, s, n in cases(seed, 150):
-        assert G.carr_advance(x, s, n) == oracle.carr_brute(x, s, n), (x, s, n)
+def test_carrier_walks_exact(seed):
+    W = walk_lib()
+    for x, s, n in cases(seed, 120):
+        want = oracle.carr_brute(x, s, n)
+        assert W.wc_carr_plain(x, s, n) == want, ("plain", x, s, n)
+        assert W.wc_carr_cached(x, s, n) == want, ("cached", x, s, n)
+        assert G.carr_advance(x, s, n) == want
 
 
 @pytest.mark.parametrize("seed", [4, 5])
-def test_code_walk_exact(seed):
+def test_code_walks_exact(seed):
+    W = walk_lib()
     rng = random.Random(seed)
-    for i in range(150):
+    for i in range(120):
+        fs = 2.6e6 if i % 4 else 2.0e7
         f = rng.uniform(-6000, 6000)
-        cs = (1.023e6 + f / 1540.0) * DELT
+        cs = (1.023e6 + f / 1540.0) / fs
         if i % 6 == 0:                       # tie w.r.t. the [512,1024) lattice 2^-43
             u = 2.0 ** -43
             cs = (math.floor(cs / u) + 0.5) * u
         c0 = rng.random() * 1023.0 if i % 9 else 0.0
         st = (rng.randrange(20), rng.randrange(30), rng.randrange(3))
-        n = rng.randint(1, 600000)
-        assert G.code_advance(c0, cs, n, *st) == oracle.code_brute(c0, cs, n, *st), (c0, cs, n)
+        n = rng.randint(1, int(fs / 10))
+        want = oracle.code_brute(c0, cs, n, *st)
+        for cached in (0, 1):
+            a, b, d = C.c_int32(st[0]), C.c_int32(st[1]), C.c_int32(st[2])
+            ph = W.wc_code(cached, c0, cs, n, C.byref(a), C.byref(b), C.byref(d))
+            assert (ph, a.value, b.value, d.value) == want, (cached, c0, cs, n)
+        assert G.code_advance(c0, cs, n, *st) == want
+
+
+def test_anchors_are_exact_states():
+    """Every anchor Stage A emits is a state of the brute-force chain at its sample index, lies
+    at or before its segment start, and is the last wrap before it."""
+    W = walk_lib()
+    rng = random.Random(9)
+    R, N = 1024, 260000
+    nseg = (N + R - 1) // R
+    for _ in range(12):
+        s = rng.uniform(-5000, 5000) / 2.6e6
+        x0 = rng.random()
+        an = np.zeros(nseg, np.int32)
+        ax = np.zeros(nseg)
+        assert W.wc_carr_anchors(x0, s, N, R, nseg, an.ctypes.data, ax.ctypes.data) == nseg
+        x, pos = x0, 0
+        wraps = {0: x0}
+        for seg in range(nseg):
+            tgt = int(an[seg])
+            assert tgt <= seg * R
+            while pos < tgt:
+                x = oracle.carr_brute(x, s, 1)
+                pos += 1
+            assert x == ax[seg], (seg, tgt)
 
 
 def test_stationary_and_single_steps():
+    W = walk_lib()
     for x, s in [(0.25, 1e-20), (0.75, -1e-19), (0.5, 2.0 ** -55)]:
         for n in (1, 2, 3, 1000):
-            assert G.carr_advance(x, s, n) == oracle.carr_brute(x, s, n)
+            want = oracle.carr_brute(x, s, n)
+            assert W.wc_carr_plain(x, s, n) == want
+            assert W.wc_carr_cached(x, s, n) == want

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Profiling session on the GPU box (rocprofv3): kernel trace + stats, then one PMC pass per
+# counter group (never combined with other trace domains).  Outputs under gpurun_out/prof/.
+# Usage: bash tools/profile.sh [tag]   (bench args via BENCH_ARGS)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-r1}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+BA=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline}
+run() {  # name, rocprofv3 args...
+    local name=$1; shift
+    timeout -k 10 400 rocprofv3 "$@" -d $OUT/$name -o $name -f csv -- python3 bench.py $BA \
+        > $OUT/$name.log 2>&1
+    local rc=$?; echo "$name rc=$rc" >> $OUT/session.log; return $rc
+}
+run kt --kernel-trace --stats || exit $?
+run pmc_write --pmc WRITE_SIZE --kernel-trace || exit $?
+run pmc_fetch --pmc FETCH_SIZE --kernel-trace || exit $?
+run pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_WR --kernel-trace || exit $?
+run pmc_lds --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAIT_ANY GRBM_GUI_ACTIVE --kernel-trace || exit $?
+echo done >> $OUT/session.log
