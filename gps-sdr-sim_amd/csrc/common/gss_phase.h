@@ -134,6 +134,180 @@ GSS_HD int64_t gss_jump(double v, double s, double W, double *D)
 #endif
 }
 
+/* ---- the same jump in f64 only (GPU form: no 64-bit integer multiply/divide) ------------------
+ * All quantities are integers below 2^54 held in doubles, so every operation below is exact
+ * except the one division, whose floor is corrected with an exact fma residual.  Same contract
+ * as gss_jump(), but returns J capped at nmax (a double holding an integer) and *dv = ±J*K*u,
+ * the exact total displacement.  A stationary value (K == 0) returns nmax with *dv = 0. */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GSS_FREXP_EXP(v)   __builtin_amdgcn_frexp_exp(v)
+#define GSS_LDEXP(v, e)    __builtin_amdgcn_ldexp((v), (e))
+#define GSS_FLOOR(v)       __builtin_floor(v)
+#define GSS_RINT(v)        __builtin_rint(v)
+#define GSS_FMA(a, b, c)   __builtin_fma((a), (b), (c))
+#else
+#include <math.h>
+GSS_HD int gss_frexp_exp_h(double v) { int e; (void)frexp(v, &e); return e; }
+#define GSS_FREXP_EXP(v)   gss_frexp_exp_h(v)
+#define GSS_LDEXP(v, e)    ldexp((v), (e))
+#define GSS_FLOOR(v)       floor(v)
+#define GSS_RINT(v)        rint(v)                /* default rounding: nearest-even */
+#define GSS_FMA(a, b, c)   fma((a), (b), (c))
+#endif
+
+GSS_HD double gss_jumpf(double v, double s, double W, double nmax, double *dv)
+{
+    if (!(v >= 0x1p-900)) return 0.0;             /* zero, negative, tiny, NaN: real steps */
+    int ex = GSS_FREXP_EXP(v);                    /* binade [2^(ex-1), 2^ex), lattice 2^(ex-53) */
+    double m = GSS_LDEXP(v, 53 - ex);             /* v/u in [2^52, 2^53) */
+    double as = s < 0.0 ? -s : s;
+    double sig = GSS_LDEXP(as, 53 - ex);          /* |s|/u */
+    if (!(sig < 0x1p52)) return 0.0;
+    double k = GSS_FLOOR(sig);
+    double frac = sig - k;
+    double K = GSS_RINT(sig);                     /* round-half-even = fl()'s rule from even m */
+    if (frac == 0.5) {
+        double h = m * 0.5;
+        if (h != GSS_FLOOR(h)) return 0.0;        /* tie from an odd lattice point */
+    }
+    if (K == 0.0) { *dv = 0.0; return nmax; }
+    double lim;
+    if (s > 0.0) {
+        lim = ((0x1p53 - m) - k) - 1.0;           /* result stays below 2^ex */
+        if (W <= GSS_LDEXP(1.0, ex)) {            /* and below the wrap threshold */
+            double l2 = (GSS_LDEXP(W - v, 53 - ex) - K) - 1.0;
+            if (l2 < lim) lim = l2;
+        }
+    } else {
+        lim = (m - 0x1p52) - (frac > 0.0 ? k + 1.0 : k);   /* result stays >= 2^(ex-1) */
+    }
+    if (lim < 0.0) return 0.0;
+    double q = GSS_FLOOR(lim / K);                /* correctly rounded: floor is q or q+1 */
+    if (GSS_FMA(-q, K, lim) < 0.0) q -= 1.0;
+    double J = q + 1.0;
+    if (J > nmax) J = nmax;
+    double d = GSS_LDEXP(J * K, ex - 53);         /* J*K <= 2^53: exact */
+    *dv = s > 0.0 ? d : -d;
+    return J;
+}
+
+/* n steps (n an integer held in a double) of x += s with the reference's wrap at W
+   (>= W: -W, else < 0: +W; carrier W = 1, code W = 1023).  *nwrap counts wraps. */
+GSS_HD double gss_walkf(double x, double s, double W, double n, int *nwrap)
+{
+    if (s == 0.0)
+        return x;
+    while (n > 0.0) {
+        double dv;
+        double J = gss_jumpf(x, s, W, n, &dv);
+        if (J > 0.0) {
+            x = x + dv;
+            n -= J;
+            if (n == 0.0) break;
+        }
+        x = x + s;
+        n -= 1.0;
+        if (x >= W) { x -= W; (*nwrap)++; }
+        else if (x < 0.0) { x += W; (*nwrap)++; }
+    }
+    return x;
+}
+
+/* Walk from *x until just after the next wrap, at most *left steps.  Returns 1 on a wrap
+   (*x = post-wrap value), 0 when *left runs out (*x = value reached); *left is decremented by
+   the steps taken. */
+GSS_HD int gss_to_wrapf(double *x, double s, double W, double *left)
+{
+    double v = *x, n = *left;
+    int wr = 0;
+    if (s == 0.0) {
+        n = 0.0;
+    } else {
+        while (n > 0.0) {
+            double dv;
+            double J = gss_jumpf(v, s, W, n, &dv);
+            if (J > 0.0) {
+                v = v + dv;
+                n -= J;
+                if (n == 0.0) break;
+            }
+            v = v + s;
+            n -= 1.0;
+            if (v >= W) { v -= W; wr = 1; break; }
+            if (v < 0.0) { v += W; wr = 1; break; }
+        }
+    }
+    *x = v;
+    *left = n;
+    return wr;
+}
+
+/* ---- branch-free form of one walk iteration (GPU lanes: no divergent control flow) -----------
+ * One iteration = the longest exact lattice jump from v (possibly empty, gss_jumpf's rules),
+ * then one real reference step with its wrap, if steps remain.  Every lane executes the same
+ * instruction sequence; decisions are selects.  as = |s|, rs = 1/|s| (any rounding).  Returns 1
+ * if the real step wrapped. */
+GSS_HD int gss_iter_bf(double *pv, double s, double as, double rs, double W, double *pleft)
+{
+    const double v = *pv;
+    double left = *pleft;
+    const int ex = GSS_FREXP_EXP(v);
+    const int sh = 53 - ex;
+    const double m = GSS_LDEXP(v, sh);
+    const double sig = GSS_LDEXP(as, sh);
+    const double k = GSS_FLOOR(sig);
+    const double frac = sig - k;
+    const double K = GSS_RINT(sig);
+    const double h = m * 0.5;
+    const int odd_tie = (frac == 0.5) & (h != GSS_FLOOR(h));
+    double lim_a = ((0x1p53 - m) - k) - 1.0;
+    const double l2 = (GSS_LDEXP(W - v, sh) - K) - 1.0;
+    lim_a = ((W <= GSS_LDEXP(1.0, ex)) & (l2 < lim_a)) ? l2 : lim_a;
+    const double lim_d = (m - 0x1p52) - (frac > 0.0 ? k + 1.0 : k);
+    const double lim = s > 0.0 ? lim_a : lim_d;
+    const int live = (v >= 0x1p-900) & (sig < 0x1p52) & !odd_tie;
+    const int stat = live & (K == 0.0);                /* stationary: no step moves v */
+    const int ok = live & (K != 0.0) & (lim >= 0.0);
+    const double Ks = K != 0.0 ? K : 1.0;
+    /* q = floor(lim / K) without a division: lim/sig = lim*u/|s| is within 1/2 of lim/K when
+       K >= 2^26 (|lim/K - lim/sig| <= lim/(2 K sig), lim <= 2^52), so q0 = floor(lim*u*rs) with
+       rs = 1/|s| is off by at most one, corrected with the exact residual lim - q0*K (fma). */
+    double q;
+    if (Ks >= 0x1p26) {
+        const double q0 = GSS_FLOOR(GSS_LDEXP(lim, ex - 53) * rs);
+        const double r0 = GSS_FMA(-q0, Ks, lim);
+        q = r0 < 0.0 ? q0 - 1.0 : (r0 >= Ks ? q0 + 1.0 : q0);
+    } else {                                           /* tiny steps: exact division */
+        q = GSS_FLOOR(lim / Ks);
+        q = GSS_FMA(-q, Ks, lim) < 0.0 ? q - 1.0 : q;
+    }
+    double J = q + 1.0;
+    J = J > left ? left : J;
+    J = ok ? J : (stat ? left : 0.0);
+    const double d = GSS_LDEXP(J * K, ex - 53);       /* 0 when stationary */
+    const double v1 = v + (s > 0.0 ? d : -d);
+    left -= J;
+    const int step = left > 0.0;
+    const double r = v1 + s;
+    const int hi = r >= W, lo = r < 0.0;
+    const double r2 = hi ? r - W : (lo ? r + W : r);
+    *pv = step ? r2 : v1;
+    *pleft = step ? left - 1.0 : left;
+    return step & (hi | lo);
+}
+
+/* n steps with gss_iter_bf; returns the value, *nwrap counts wraps. */
+GSS_HD double gss_walk_bf(double x, double s, double W, double n, int *nwrap)
+{
+    const double as = s < 0.0 ? -s : s;
+    if (s == 0.0)
+        return x;
+    const double rs = 1.0 / as;
+    while (n > 0.0)
+        *nwrap += gss_iter_bf(&x, s, as, rs, W, &n);
+    return x;
+}
+
 /* Advance the carrier recurrence by n steps, exactly. */
 GSS_HD double gss_carr_walk(double x, double s, int64_t n)
 {

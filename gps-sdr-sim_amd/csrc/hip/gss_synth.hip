@@ -6,17 +6,19 @@
  * serial IEEE double recurrences (built with -ffp-contract=off); the only shortcuts are provably
  * exact lattice translations (common/gss_phase.h).
  *
- * Stage A  gss_anchor_kernel    one lane per (block, channel, chain) with chain ∈ {carrier, code}.
- *                               Walks the block cycle by cycle (cycle-map cache) and records, for
- *                               every R-sample segment, the last wrap at or before its first
- *                               sample: an exact "anchor" state (sample index, phase[, counters]).
+ * Stage A  gss_anchor_kernel    one lane per (block, channel, chain) with chain ∈ {carrier, code}
+ *                               (one chain kind per wave).  Walks the block with the branch-free
+ *                               f64 lattice walk (gss_iter_bf) and records, for every R-sample
+ *                               segment, the last wrap at or before its first sample: an exact
+ *                               "anchor" state (sample index, phase[, counters]).
  * Stage B  gss_synth_kernel     one lane per R-sample segment of a block, all channels.  Each lane
- *                               first jump-walks every channel from its anchor to the segment
- *                               start (≤ one cycle), then runs the per-sample recurrences:
- *                               LUT[floor(512 carr)] × (chip ⊕ data bit) × gain accumulated over
- *                               channels in int32, (acc+64)>>7, SC16/SC08/SC01 packing.  Output is
- *                               staged per lane in LDS (64 B) and stored by the wave as whole 64-B
- *                               pieces (16 lanes' pieces per store instruction).
+ *                               first walks every channel from its anchor to the segment start
+ *                               (≤ one cycle, no wrap), then runs the per-sample recurrences:
+ *                               carrier via v_fract_f64, chip sign from a byte table, data-bit
+ *                               sign folded into the gain, LUT[floor(512 carr)] x gain summed
+ *                               over channels with v_dot2 on packed int16, (acc+64)>>7,
+ *                               SC16/SC08/SC01 packing.  Output is staged per lane in LDS
+ *                               (128 B) and stored by the wave as whole 128-B lines.
  * Integer/byte work on f64 phases: no MFMA.
  */
 #include <hip/hip_runtime.h>
@@ -28,49 +30,42 @@
 
 #define SYNTH_THREADS  256
 #define SYNTH_WAVES    (SYNTH_THREADS / 64)
-#define ANCHOR_THREADS 64
-#define CHUNK_BYTES    64                /* output bytes per lane per staged chunk */
-#define LUT_N          768               /* 512 + 256: index ti + 256*neg needs no wrap */
+#define ANCHOR_THREADS 64                /* one wave per workgroup: a wave is one chain kind  */
+#define CHUNK_BYTES    128               /* output bytes per lane per staged chunk: a line */
+#define CHUNK_PIECES   (CHUNK_BYTES / 16)
+#define LUT_N          1024              /* index ti + 256*neg <= 767; padded to a power of 2 */
+#define CHIP_N         1024              /* chip table row: chips 0..1022 (+ pad)             */
 
 struct lut_arg { int16_t sin512[512]; int16_t cos512[512]; };
-
-/* per (block, channel) block-uniform values, prepared by Stage A */
-struct chan_uni {
-    double S;            /* 512 * carr_step (state Y = 512 carr; scaling by 2^9 is exact)     */
-    double CS;           /* code_step                                                       */
-    int32_t gain;
-    uint32_t pad[3];
-};
 
 /* ======================================================================================== */
 /* Stage A: anchors                                                                         */
 /* ======================================================================================== */
+/* One lane per (block, channel) and chain; even workgroups walk carriers, odd ones code phases,
+   so a wave never diverges on the chain kind.  Lanes walk their block with the branch-free f64
+   lattice walk (gss_iter_bf: one jump + one real step per trip) and record, for every R-sample
+   segment, the last wrap at or before the segment's first sample. */
 __global__ __launch_bounds__(ANCHOR_THREADS) void gss_anchor_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch, int nblk, int nchp,
     int n_per_blk, int nseg, int seg_r, int32_t *__restrict__ anc_cn, double *__restrict__ anc_cx,
     int32_t *__restrict__ anc_kn, double *__restrict__ anc_kx, uint32_t *__restrict__ anc_kc,
-    chan_uni *__restrict__ uni, double *__restrict__ carr_end)
+    double *__restrict__ carr_end)
 {
-    int gid = blockIdx.x * ANCHOR_THREADS + threadIdx.x;
-    int chain = gid & 1, k = (gid >> 1) & (GSS_MAXCH - 1), b = gid >> 5;
+    const int chain = blockIdx.x & 1;
+    const int pair = (blockIdx.x >> 1) * ANCHOR_THREADS + threadIdx.x;
+    const int b = pair / nchp, k = pair - b * nchp;
     if (b >= nblk)
         return;
-    size_t bk = (size_t)b * GSS_MAXCH + k;
-    size_t row = bk * (size_t)nseg;
+    const size_t bk = (size_t)b * GSS_MAXCH + k;
+    const size_t row = bk * (size_t)nseg;
     if (k >= nch[b]) {
-        if (k >= nchp)
-            return;
-        /* silent padding channel of the launch's kernel instance: zero gain, no motion, and
-           well-defined anchors so Stage B can initialise every channel unconditionally */
-        if (chain == 0) {
-            chan_uni u = {0.0, 0.0, 0, {0u, 0u, 0u}};
-            uni[bk] = u;
-            for (int sgi = 0; sgi < nseg; sgi++) {
+        /* padding channel of the kernel instance: zero anchors (Stage B gives it no motion and
+           zero gain) */
+        for (int sgi = 0; sgi < nseg; sgi++) {
+            if (chain == 0) {
                 anc_cn[row + sgi] = 0;
                 anc_cx[row + sgi] = 0.0;
-            }
-        } else {
-            for (int sgi = 0; sgi < nseg; sgi++) {
+            } else {
                 anc_kn[row + sgi] = 0;
                 anc_kx[row + sgi] = 0.0;
                 anc_kc[row + sgi] = 0u;
@@ -79,73 +74,99 @@ __global__ __launch_bounds__(ANCHOR_THREADS) void gss_anchor_kernel(
         return;
     }
     const gss_chan_blk_t p = blk[bk];
-    if (chain == 0) {
-        chan_uni u;
-        u.S = p.carr_step * 512.0;
-        u.CS = p.code_step;
-        u.gain = p.gain;
-        u.pad[0] = u.pad[1] = u.pad[2] = 0u;
-        uni[bk] = u;
-
-        gss_carr_it it;
-        gss_carr_it_init(&it, p.carr0, p.carr_step, n_per_blk);
-        int seg = 0;
-        int32_t an = 0;
-        double ax = p.carr0;
-        for (;;) {
-            int wr = gss_carr_next_wrap(&it);
-            int64_t nw = wr ? it.pos : (int64_t)n_per_blk;
-            while (seg < nseg && (int64_t)seg * seg_r < nw) {
-                anc_cn[row + seg] = an;
-                anc_cx[row + seg] = ax;
-                seg++;
+    const bool carr = chain == 0;                       /* wave-uniform */
+    const double st = carr ? p.carr_step : p.code_step;
+    const double as = st < 0.0 ? -st : st;
+    const double rs = 1.0 / as;
+    const double W = carr ? 1.0 : GSS_CA_SEQ_LEN_D;
+    const double total = (double)n_per_blk;
+    double v = carr ? p.carr0 : p.code0;
+    double left = st == 0.0 ? 0.0 : total;             /* no motion: no wraps */
+    uint32_t cnt = (uint32_t)p.icode | ((uint32_t)p.ibit << 8) | ((uint32_t)p.iword << 16);
+    uint32_t acnt = cnt;
+    double ax = v;
+    int32_t an = 0;
+    int seg = 0;
+    const bool need_end = carr && carr_end != nullptr;
+    /* Flat loop, one branch-free jump+step per trip.  A segment's anchor is final once the walk
+       has passed its first sample: it is the wrap of this trip if that wrap lands exactly on the
+       segment start, else the previous one.  At most one anchor is stored per trip (a predicated
+       store, no loop); the rare backlog of two or more segments older than a fresh wrap (long
+       cycles: Dopplers below ~2.5 kHz at 2.6 MS/s) is drained in a loop first. */
+    while (left > 0.0 && (seg < nseg || need_end)) {
+        const int wr = gss_iter_bf(&v, st, as, rs, W, &left);
+        const int32_t pos = (int32_t)(total - left);
+        if (wr && seg + 1 < nseg && (seg + 1) * seg_r < pos) {
+            for (; seg + 1 < nseg && (seg + 1) * seg_r < pos; seg++) {   /* rare backlog */
+                if (carr) {
+                    anc_cn[row + seg] = an;
+                    anc_cx[row + seg] = ax;
+                } else {
+                    anc_kn[row + seg] = an;
+                    anc_kx[row + seg] = ax;
+                    anc_kc[row + seg] = acnt;
+                }
             }
-            if (!wr || (seg >= nseg && !carr_end))
-                break;
-            an = (int32_t)it.pos;
-            ax = it.x;
         }
-        if (carr_end)
-            carr_end[bk] = it.x;
-    } else {
-        gss_code_state c;
-        c.ph = p.code0;
-        c.icode = p.icode;
-        c.ibit = p.ibit;
-        c.iword = p.iword;
-        gss_code_it it;
-        gss_code_it_init(&it, c, p.code_step, n_per_blk);
-        int seg = 0;
-        int32_t an = 0;
-        gss_code_state ac = c;
-        for (;;) {
-            int wr = gss_code_next_wrap(&it);
-            int64_t nw = wr ? it.pos : (int64_t)n_per_blk;
-            while (seg < nseg && (int64_t)seg * seg_r < nw) {
-                anc_kn[row + seg] = an;
-                anc_kx[row + seg] = ac.ph;
-                anc_kc[row + seg] = (uint32_t)ac.icode | ((uint32_t)ac.ibit << 8) |
-                                    ((uint32_t)ac.iword << 16);
-                seg++;
+        if (!carr && wr) {                              /* gpssim.c:2216-2236 */
+            uint32_t icode = (cnt & 0xFFu) + 1u, ibit = (cnt >> 8) & 0xFFu, iword = cnt >> 16;
+            const uint32_t nb = icode >= 20u;
+            icode = nb ? 0u : icode;
+            ibit += nb;
+            const uint32_t nw2 = ibit >= 30u;
+            ibit = nw2 ? 0u : ibit;
+            iword += nw2;
+            cnt = icode | (ibit << 8) | (iword << 16);
+        }
+        const bool fin = seg < nseg && seg * seg_r <= pos;
+        const bool use_new = wr && seg * seg_r >= pos;
+        if (fin) {
+            const int32_t e_n = use_new ? pos : an;
+            const double e_x = use_new ? v : ax;
+            if (carr) {
+                anc_cn[row + seg] = e_n;
+                anc_cx[row + seg] = e_x;
+            } else {
+                anc_kn[row + seg] = e_n;
+                anc_kx[row + seg] = e_x;
+                anc_kc[row + seg] = use_new ? cnt : acnt;
             }
-            if (!wr || seg >= nseg)
-                break;
-            an = (int32_t)it.pos;
-            ac = it.c;
+        }
+        seg += fin ? 1 : 0;
+        an = wr ? pos : an;
+        ax = wr ? v : ax;
+        acnt = wr ? cnt : acnt;
+    }
+    for (; seg < nseg; seg++) {                         /* segments after the last wrap */
+        if (carr) {
+            anc_cn[row + seg] = an;
+            anc_cx[row + seg] = ax;
+        } else {
+            anc_kn[row + seg] = an;
+            anc_kx[row + seg] = ax;
+            anc_kc[row + seg] = acnt;
         }
     }
+    if (need_end)
+        carr_end[bk] = v;
 }
 
 /* ======================================================================================== */
 /* Stage B: synthesis                                                                       */
 /* ======================================================================================== */
 template <int FMT> struct fmt_traits;
-template <> struct fmt_traits<16> { static constexpr int SPC = 16;  };  /* samples per chunk */
-template <> struct fmt_traits<8>  { static constexpr int SPC = 32;  };
-template <> struct fmt_traits<1>  { static constexpr int SPC = 256; };
+template <> struct fmt_traits<16> { static constexpr int SPC = CHUNK_BYTES / 4; }; /* samples/chunk */
+template <> struct fmt_traits<8>  { static constexpr int SPC = CHUNK_BYTES / 2; };
+template <> struct fmt_traits<1>  { static constexpr int SPC = CHUNK_BYTES * 4; };
 
-__device__ __forceinline__ uint32_t hi32(double v) { return (uint32_t)__double2hiint(v); }
-__device__ __forceinline__ double with_hi(uint32_t hi) { return __hiloint2double((int)hi, 0); }
+typedef short gss_short2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c)
+{
+    /* v_dot2c_i32_i16: c + a.lo*b.lo + a.hi*b.hi (signed 16-bit halves) */
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(gss_short2, a),
+                                  __builtin_bit_cast(gss_short2, b), c, false);
+}
 
 /* 16 bytes to global memory: one dwordx4 store when aligned (block bases are multiples of the
    block size, e.g. 65000 B at -b 1, so not always). */
@@ -164,29 +185,20 @@ __device__ __forceinline__ void store16(uint8_t *p, uint4 v)
     }
 }
 
-/* Lane start state, walked from the anchors.  Out of line on purpose: inlined twelve times into
-   the unrolled channel loop these walks would dominate the register allocation of the whole
-   kernel; as calls they run once per lane per channel and cost nothing in the sample loop. */
-struct lane_start { double Y, C; uint32_t st; int bad; };
+/* Lane start state: both chains walked from their anchors (the last wrap at or before the
+   segment start, so the walk crosses no wrap; a crossing would be a bug and is reported).
+   Out of line on purpose: inlined NCH times into the unrolled channel loop the walk would
+   dominate the register allocation of the whole kernel. */
+struct lane_start { double carr, C; int bad; };
 
 __device__ __noinline__ lane_start lane_start_walk(double ax, int an, double cstep, double kx,
-                                                   int kn, uint32_t kc, double kstep, int n0,
-                                                   const uint32_t *nav_row)
+                                                   int kn, double kstep, int n0)
 {
     lane_start r;
-    r.Y = gss_carr_walk(ax, cstep, n0 - an) * 512.0;
-    gss_code_state c;
-    c.ph = kx;
-    c.icode = kc & 0xFF;
-    c.ibit = (kc >> 8) & 0xFF;
-    c.iword = kc >> 16;
-    gss_code_walk(&c, kstep, n0 - kn);
-    r.C = c.ph;
-    int iw = c.iword;
-    r.bad = 0;
-    if (iw > 59) { r.bad = 1; iw = 59; }
-    uint32_t pol = (nav_row[iw] >> (29 - c.ibit)) & 1u;
-    r.st = (uint32_t)c.icode | ((uint32_t)c.ibit << 8) | ((uint32_t)iw << 16) | (pol << 24);
+    int w1 = 0, w2 = 0;
+    r.carr = gss_walk_bf(ax, cstep, 1.0, (double)(n0 - an), &w1);
+    r.C = gss_walk_bf(kx, kstep, GSS_CA_SEQ_LEN_D, (double)(n0 - kn), &w2);
+    r.bad = (w1 | w2) ? 2 : 0;
     return r;
 }
 
@@ -197,20 +209,28 @@ __device__ __forceinline__ void wave_sync_lds()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+/* data-bit sign folded into the gain: I += (dataBit*gain) * (codeCA*cos), as packed int16 pairs
+   (g, 0) for I and (0, g) for Q against the LUT word (cos, sin) */
+__device__ __forceinline__ void signed_gain(int gain, uint32_t bit, uint32_t &gi, uint32_t &gq)
+{
+    int g = bit ? gain : -gain;
+    gi = (uint32_t)(uint16_t)(int16_t)g;
+    gq = gi << 16;
+}
+
 template <int NCH, int FMT>
 __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch,
     const uint32_t *__restrict__ ca_bits, const uint32_t *__restrict__ nav,
     const int32_t *__restrict__ anc_cn, const double *__restrict__ anc_cx,
     const int32_t *__restrict__ anc_kn, const double *__restrict__ anc_kx,
-    const uint32_t *__restrict__ anc_kc, const chan_uni *__restrict__ uni, lut_arg lut,
-    int n_per_blk, int nseg, int seg_r, int wg_per_blk, uint8_t *__restrict__ out,
-    size_t block_bytes, int32_t *__restrict__ status)
+    const uint32_t *__restrict__ anc_kc, lut_arg lut, int n_per_blk, int nseg, int seg_r,
+    int wg_per_blk, uint8_t *__restrict__ out, size_t block_bytes, int32_t *__restrict__ status)
 {
     constexpr int SPC = fmt_traits<FMT>::SPC;
     constexpr int BPS4 = FMT == 16 ? 16 : FMT == 8 ? 8 : 1;      /* 4 x bytes per sample */
-    __shared__ int2 s_lut[LUT_N];                         /* (cos, sin) of index mod 512  */
-    __shared__ uint32_t s_ca[NCH][2][GSS_CA_WORDS];       /* [pol]: 1 = negative sign      */
+    __shared__ uint32_t s_lut[LUT_N];                     /* cos | sin << 16, index mod 512  */
+    __shared__ uint8_t s_chip[NCH][CHIP_N];               /* 1 where codeCA = -1 (chip 0)    */
     __shared__ uint32_t s_nav[NCH][64];
     __shared__ uint32_t s_stage[SYNTH_WAVES][64 * CHUNK_BYTES / 4];
 
@@ -222,15 +242,21 @@ __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
     const gss_chan_blk_t *prow = blk + (size_t)b * GSS_MAXCH;
 
     /* ---- LDS tables for this block ---- */
-    for (int i = tid; i < LUT_N; i += SYNTH_THREADS)
-        s_lut[i] = make_int2(lut.cos512[i & 511], lut.sin512[i & 511]);
-    for (int i = tid; i < NCH * GSS_CA_WORDS; i += SYNTH_THREADS) {
-        int k = i / GSS_CA_WORDS, j = i % GSS_CA_WORDS;
-        uint32_t v = k < nc ? ca_bits[(size_t)prow[k].ca_tbl * GSS_CA_WORDS + j] : 0u;
-        /* sign = dataBit*codeCA < 0 iff chip != data bit: pol 0 (bit 0): neg = chip,
-           pol 1 (bit 1): neg = !chip */
-        s_ca[k][0][j] = v;
-        s_ca[k][1][j] = ~v;
+    for (int i = tid; i < LUT_N; i += SYNTH_THREADS) {
+        int j = i & 511;                                  /* LUT[i+256] = -LUT[i] (mod 512) */
+        s_lut[i] = (uint32_t)(uint16_t)lut.cos512[j] | ((uint32_t)(uint16_t)lut.sin512[j] << 16);
+    }
+    for (int i = tid; i < NCH * (CHIP_N / 4); i += SYNTH_THREADS) {
+        int k = i / (CHIP_N / 4), j4 = (i % (CHIP_N / 4)) * 4;
+        uint32_t v = 0;
+        if (k < nc) {
+            const uint32_t *cb = ca_bits + (size_t)prow[k].ca_tbl * GSS_CA_WORDS;
+            uint32_t word = cb[j4 >> 5] >> (j4 & 31);       /* 4 chips, never straddling */
+            for (int q = 0; q < 4; q++)
+                if (j4 + q < 1023)
+                    v |= (uint32_t)(((word >> q) & 1u) ^ 1u) << (8 * q);
+        }
+        ((uint32_t *)&s_chip[k][0])[j4 >> 2] = v;
     }
     for (int i = tid; i < NCH * 64; i += SYNTH_THREADS) {
         int k = i >> 6, j = i & 63;
@@ -246,115 +272,95 @@ __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
     if (len > seg_r) len = seg_r;
     const int segc = active ? seg : nseg - 1;           /* inactive lanes: any valid anchor */
     const int n0c = segc * seg_r;
-    const chan_uni *u = uni + (size_t)b * GSS_MAXCH;     /* block-uniform: scalar loads */
 
-    /* ---- exact per-lane start state: walk each channel from its anchor.  Unconditional
-       for every channel of the instance (padding channels have zero anchors and zero steps):
-       a conditional, partially-assigned state array costs the allocator ~4x the registers. */
-    double Y[NCH], C[NCH];
-    uint32_t st[NCH];             /* icode | ibit<<8 | iword<<16 | pol<<24 */
+    /* block-uniform channel steps (scalar registers); padding channels: no motion, no gain.
+       Gains are re-read (scalar loads) where a data bit changes, to spare scalar registers. */
+    double cs[NCH], ks[NCH];
+#pragma unroll
+    for (int k = 0; k < NCH; k++) {
+        const bool real = k < nc;
+        cs[k] = real ? prow[k].carr_step : 0.0;
+        ks[k] = real ? prow[k].code_step : 0.0;
+    }
+
+    /* ---- exact per-lane start state, unconditionally for every channel of the instance ---- */
+    double carr[NCH], C[NCH];
+    uint32_t st[NCH];             /* icode | ibit<<8 | iword<<16 */
+    uint32_t gi[NCH], gq[NCH];
     int bad = 0;
 #pragma unroll
     for (int k = 0; k < NCH; k++) {
         size_t r = ((size_t)b * GSS_MAXCH + k) * (size_t)nseg + segc;
-        lane_start ls = lane_start_walk(anc_cx[r], anc_cn[r], u[k].S * (1.0 / 512.0),
-                                        anc_kx[r], anc_kn[r], anc_kc[r], u[k].CS, n0c,
-                                        &s_nav[k][0]);
-        Y[k] = ls.Y;
+        lane_start ls = lane_start_walk(anc_cx[r], anc_cn[r], cs[k], anc_kx[r], anc_kn[r], ks[k],
+                                        n0c);
+        carr[k] = ls.carr;
         C[k] = ls.C;
-        st[k] = ls.st;
         bad |= ls.bad;
+        uint32_t c = anc_kc[r];
+        int ibit = (c >> 8) & 0xFF, iw = c >> 16;
+        if (iw > 59) { bad |= 1; iw = 59; c = (c & 0xFFFFu) | (59u << 16); }
+        st[k] = c;
+        signed_gain(k < nc ? prow[k].gain : 0, (s_nav[k][iw] >> (29 - ibit)) & 1u, gi[k], gq[k]);
     }
 
     uint8_t *dst = out + (size_t)b * block_bytes + (size_t)n0 * BPS4 / 4;
     uint32_t *stg = s_stage[wave];
     uint32_t *mine = stg + lane * (CHUNK_BYTES / 4);
-    const int nchunk = len / SPC;
-    int wave_chunks = nchunk;                 /* all lanes join every staged store round */
+    const int nchunk = len / SPC;                       /* full chunks of this lane */
+    int lane_chunks = (len + SPC - 1) / SPC;
     for (int off = 32; off > 0; off >>= 1)
-        wave_chunks = max(wave_chunks, __shfl_xor(wave_chunks, off));
+        lane_chunks = max(lane_chunks, __shfl_xor(lane_chunks, off));
+    /* wave-uniform trip counts (chunks and samples): lanes past their own end keep computing
+       (harmlessly, nothing is stored) so that no loop-carried state sits under divergent
+       control flow */
+    const int wave_chunks = __builtin_amdgcn_readfirstlane(lane_chunks);
 
-    for (int ch = 0; ch <= wave_chunks; ch++) {
+    for (int ch = 0; ch < wave_chunks; ch++) {
         const bool full = ch < nchunk;
         const int nsamp = full ? SPC : (ch == nchunk ? len - nchunk * SPC : 0);
         uint32_t bits = 0;
 #pragma unroll 1
-        for (int sidx = 0; sidx < nsamp; sidx++) {
-            int acc_i = 0, acc_q = 0;
-            uint32_t wrapped = 0;            /* bit k: channel k's code phase reached 1023 */
-            /* channels in groups of 4: issue the group's chip-word reads, then its LUT reads,
-               then consume — keeps LDS latency overlapped without holding all 16 in flight */
+        for (int sidx = 0; sidx < SPC; sidx++) {
+            int acc_i = 64, acc_q = 64;               /* the +64 of (acc+64)>>7 */
+            uint64_t any = 0;
+            /* channels in groups of 4: chip reads, then LUT reads, then consume */
 #pragma unroll
             for (int k0 = 0; k0 < NCH; k0 += 4) {
                 constexpr int GW = 4;
-                int ci[GW], ti[GW];
-                uint32_t cw[GW];
-                int2 e[GW];
+                int ti[GW];
+                uint32_t t[GW], e[GW];
 #pragma unroll
                 for (int j = 0; j < GW; j++) {
                     if (k0 + j < NCH) {
                         const int k = k0 + j;
-                        ci[j] = (int)C[k];
-                        ti[j] = (int)Y[k];
-                        cw[j] = s_ca[k][st[k] >> 24][ci[j] >> 5];
+                        ti[j] = (int)(carr[k] * 512.0);      /* floor: carr in [0,1) */
+                        t[j] = s_chip[k][(int)C[k]];
                     }
                 }
 #pragma unroll
-                for (int j = 0; j < GW; j++) {
-                    if (k0 + j < NCH) {
-                        /* LUT[floor(512 carr)] × chip sign × data sign (gpssim.c:2200-2209);
-                           a negative sign is half a carrier cycle: LUT[i+256] = -LUT[i] */
-                        uint32_t neg = (cw[j] >> (ci[j] & 31)) & 1u;
-                        e[j] = s_lut[(ti[j] & 511) + (int)(neg << 8)];
-                    }
-                }
+                for (int j = 0; j < GW; j++)
+                    if (k0 + j < NCH)          /* LUT[floor(512 carr)] x codeCA (gpssim.c:2200-2209) */
+                        e[j] = s_lut[ti[j] + (int)(t[j] << 8)];
 #pragma unroll
                 for (int j = 0; j < GW; j++) {
                     if (k0 + j < NCH) {
                         const int k = k0 + j;
-                        int g = u[k].gain;
-                        acc_i += __mul24(e[j].x, g);
-                        acc_q += __mul24(e[j].y, g);
-
-                        /* carrier advance + wrap (gpssim.c:2245-2250), Y = 512 carr.  Same test
-                           as the reference, on the value: hi32(Y) >= hi32(512.0) holds exactly
-                           when Y >= 512 or Y < 0; then Y -= A with A = +512 for Y >= 0 and -512
-                           for Y < 0, hi32(A) = (sign of Y) | hi32(512.0). */
-                        double y = Y[k] + u[k].S;
-                        uint32_t hy = hi32(y);
-                        uint32_t ahi = (hy & 0x80000000u) | 0x40800000u;
-                        Y[k] = y - with_hi(hy >= 0x40800000u ? ahi : 0u);
-
-                        /* code advance (gpssim.c:2212); the wrap test on hi32 is C >= 1023.0 */
-                        C[k] = C[k] + u[k].CS;
-                        wrapped |= (hi32(C[k]) >= 0x408FF800u ? 1u : 0u) << k;
+                        acc_i = dot2(e[j], gi[k], acc_i);
+                        acc_q = dot2(e[j], gq[k], acc_q);
+                        /* carrier (gpssim.c:2245-2250): carr+s is in [0,2) ascending or (-1,1)
+                           descending, where v_fract_f64 returns exactly the reference's
+                           carr-1 / carr+1 (x - floor(x), one IEEE rounding) */
+                        carr[k] = __builtin_amdgcn_fract(carr[k] + cs[k]);
+                        C[k] = C[k] + ks[k];                  /* code (gpssim.c:2212) */
+                        any |= __builtin_amdgcn_ballot_w64(C[k] >= GSS_CA_SEQ_LEN_D);
                     }
                 }
             }
-            /* rare: some channel's code phase wrapped (once per ~2600 samples per channel) */
-            if (__builtin_expect(__any(wrapped != 0), 0)) {
-#pragma unroll
-                for (int k = 0; k < NCH; k++) {
-                    if (wrapped & (1u << k)) {       /* gpssim.c:2214-2237 */
-                        C[k] -= 1023.0;
-                        uint32_t c = st[k];
-                        int icode = (int)(c & 0xFF) + 1, ibit = (c >> 8) & 0xFF,
-                            iword = (c >> 16) & 0xFF;
-                        uint32_t p2 = c >> 24;
-                        if (icode >= 20) {
-                            icode = 0;
-                            if (++ibit >= 30) { ibit = 0; iword++; }
-                            if (iword > 59) { bad = 1; iword = 59; }
-                            p2 = (s_nav[k][iword] >> (29 - ibit)) & 1u;
-                        }
-                        st[k] = (uint32_t)icode | ((uint32_t)ibit << 8) |
-                                ((uint32_t)iword << 16) | (p2 << 24);
-                    }
-                }
-            }
-            /* gpssim.c:2257-2263: (acc+64)>>7 (arithmetic), then (short) */
-            int i16 = (int)(int16_t)((acc_i + 64) >> 7);
-            int q16 = (int)(int16_t)((acc_q + 64) >> 7);
+            /* gpssim.c:2257-2263: (acc+64)>>7 (arithmetic), then (short).  Written before the
+               wrap fix-up below, unconditionally: samples past this lane's end land in staging
+               bytes that are never copied out. */
+            int i16 = (int)(int16_t)(acc_i >> 7);
+            int q16 = (int)(int16_t)(acc_q >> 7);
             if (FMT == 16) {
                 mine[sidx] = (uint32_t)(uint16_t)i16 | ((uint32_t)(uint16_t)q16 << 16);
             } else if (FMT == 8) {                    /* iq_buff >> 4 → signed char */
@@ -362,21 +368,53 @@ __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
                                            ((uint32_t)(uint8_t)(int8_t)(q16 >> 4) << 8));
             } else {                                  /* {I0 Q0 I1 Q1 ...} MSB first */
                 bits = (bits << 2) | ((uint32_t)(i16 > 0) << 1) | (uint32_t)(q16 > 0);
-                if ((sidx & 15) == 15 || sidx == nsamp - 1) {
-                    int nb = (sidx & 15) + 1;         /* samples in this word (16 unless tail) */
-                    bits <<= 2 * (16 - nb);
-                    mine[sidx >> 4] = __builtin_bswap32(bits);
+                if ((sidx & 15) == 15) {
+                    /* a tail word keeps its first nb samples and zero padding */
+                    int nb = nsamp - (sidx & ~15);
+                    uint32_t w32 = nb >= 16 ? bits : nb > 0 ? (bits >> 2 * (16 - nb)) << 2 * (16 - nb) : 0u;
+                    mine[sidx >> 4] = __builtin_bswap32(w32);
                     bits = 0;
+                }
+            }
+            /* rare: some lane's code phase wrapped (once per ~2600 samples per channel).  Per
+               channel a uniform branch, inside it selects only: no divergent control flow around
+               the loop-carried state. */
+            if (__builtin_expect(any != 0, 0)) {
+#pragma unroll
+                for (int k = 0; k < NCH; k++) {
+                    const bool wk = C[k] >= GSS_CA_SEQ_LEN_D;
+                    if (__builtin_amdgcn_ballot_w64(wk)) {    /* gpssim.c:2214-2237 */
+                        C[k] = wk ? C[k] - GSS_CA_SEQ_LEN_D : C[k];
+                        const uint32_t c = st[k];
+                        int icode = (int)(c & 0xFF) + 1, ibit = (c >> 8) & 0xFF,
+                            iword = (int)(c >> 16);
+                        const bool nbit = icode >= 20;
+                        if (nbit) {
+                            icode = 0;
+                            if (++ibit >= 30) { ibit = 0; iword++; }
+                            if (iword > 59) { bad |= (wk && sidx < nsamp) ? 1 : 0; iword = 59; }
+                        }
+                        const uint32_t c2 = (uint32_t)icode | ((uint32_t)ibit << 8) |
+                                            ((uint32_t)iword << 16);
+                        st[k] = wk ? c2 : c;
+                        if (__builtin_amdgcn_ballot_w64(wk && nbit)) {
+                            uint32_t ngi, ngq;
+                            signed_gain(prow[k].gain * (k < nc ? 1 : 0),
+                                        (s_nav[k][iword] >> (29 - ibit)) & 1u, ngi, ngq);
+                            gi[k] = (wk && nbit) ? ngi : gi[k];
+                            gq[k] = (wk && nbit) ? ngq : gq[k];
+                        }
+                    }
                 }
             }
         }
         const bool any_full = __any(full);
         if (any_full) {
-            /* the wave stores 16 lanes' 64-B pieces per instruction: lane j stores piece j%4
-               of source lane 16 i + j/4 */
+            /* the wave stores whole 128-B chunks of 8 lanes per instruction: lane j stores
+               16-B piece j%8 of source lane 8 i + j/8 */
             wave_sync_lds();
-            for (int i = 0; i < 4; i++) {
-                int src = 16 * i + (lane >> 2), piece = lane & 3;
+            for (int i = 0; i < CHUNK_PIECES; i++) {
+                int src = (64 / CHUNK_PIECES) * i + lane / CHUNK_PIECES, piece = lane % CHUNK_PIECES;
                 int src_full = __shfl(full ? 1 : 0, src);
                 if (src_full) {
                     uint8_t *sdst = dst + (ptrdiff_t)(src - lane) * ((ptrdiff_t)seg_r * BPS4 / 4) +
@@ -396,7 +434,7 @@ __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
         }
     }
     if (bad && status)
-        atomicOr(status, 1);
+        atomicOr(status, bad);
 }
 
 /* ======================================================================================== */
@@ -409,8 +447,6 @@ struct gss_dev {
     double *anc_cx = nullptr, *anc_kx = nullptr;
     uint32_t *anc_kc = nullptr;
     size_t anc_cap = 0;
-    chan_uni *uni = nullptr;
-    size_t uni_cap = 0;
     static constexpr int RING = 256;
     hipEvent_t ev[RING][3];
     int n_ev = 0;
@@ -474,7 +510,7 @@ extern "C" int gss_dev_close(gss_dev *d)
 {
     if (!d) return 0;
     (void)hipSetDevice(d->ordinal);
-    void *bufs[] = {d->anc_cn, d->anc_kn, d->anc_cx, d->anc_kx, d->anc_kc, d->uni,
+    void *bufs[] = {d->anc_cn, d->anc_kn, d->anc_cx, d->anc_kx, d->anc_kc,
                     d->h_in, d->d_out, d->d_cend, d->d_status};
     for (void *p : bufs)
         (void)hipFree(p);
@@ -492,13 +528,6 @@ extern "C" int gss_dev_reserve(gss_dev *d, int max_blocks, int n_per_blk)
     if (!d || max_blocks <= 0 || n_per_blk <= 0)
         return gss_fail(GSS_E_ARG, "invalid reserve arguments");
     HIP_TRY(hipSetDevice(d->ordinal));
-    if ((size_t)max_blocks > d->uni_cap) {
-        (void)hipFree(d->uni);
-        d->uni = nullptr;
-        d->uni_cap = 0;
-        HIP_TRY(hipMalloc(&d->uni, sizeof(chan_uni) * GSS_MAXCH * (size_t)max_blocks));
-        d->uni_cap = (size_t)max_blocks;
-    }
     size_t need = (size_t)max_blocks * GSS_MAXCH * (size_t)nseg_of(n_per_blk, d->seg_r);
     if (need <= d->anc_cap)
         return 0;
@@ -520,7 +549,7 @@ extern "C" int gss_dev_reserve(gss_dev *d, int max_blocks, int n_per_blk)
 
 typedef void (*synth_fn)(const gss_chan_blk_t *, const int32_t *, const uint32_t *,
                          const uint32_t *, const int32_t *, const double *, const int32_t *,
-                         const double *, const uint32_t *, const chan_uni *, lut_arg, int, int,
+                         const double *, const uint32_t *, lut_arg, int, int,
                          int, int, uint8_t *, size_t, int32_t *);
 
 template <int FMT> static synth_fn pick_nch(int nchp)
@@ -569,16 +598,17 @@ extern "C" int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int
 
     hipEvent_t *ev = d->ev[d->n_ev % gss_dev::RING];
     d->n_ev++;
-    int a_blocks = (nblk * GSS_MAXCH * 2 + ANCHOR_THREADS - 1) / ANCHOR_THREADS;
+    /* Stage A grid: pairs (block, channel < nchp) in waves of 64, each wave twice (chains) */
+    int a_blocks = 2 * ((nblk * nchp + ANCHOR_THREADS - 1) / ANCHOR_THREADS);
     HIP_TRY(hipEventRecord(ev[0], st));
     hipLaunchKernelGGL(gss_anchor_kernel, dim3(a_blocks), dim3(ANCHOR_THREADS), 0, st, blk, nch,
                        nblk, nchp, n_per_blk, nseg, R, d->anc_cn, d->anc_cx, d->anc_kn, d->anc_kx,
-                       d->anc_kc, d->uni, carr_end);
+                       d->anc_kc, carr_end);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], st));
     int wg_per_blk = (nseg + SYNTH_THREADS - 1) / SYNTH_THREADS;
     hipLaunchKernelGGL(fn, dim3(nblk * wg_per_blk), dim3(SYNTH_THREADS), 0, st, blk, nch, ca_bits,
-                       nav, d->anc_cn, d->anc_cx, d->anc_kn, d->anc_kx, d->anc_kc, d->uni, d->lut,
+                       nav, d->anc_cn, d->anc_cx, d->anc_kn, d->anc_kx, d->anc_kc, d->lut,
                        n_per_blk, nseg, R, wg_per_blk, (uint8_t *)out, bb, status);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[2], st));

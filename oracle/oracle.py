@@ -26,6 +26,8 @@ def lib():
         L.oracle_block_bytes.argtypes = [C.c_int, C.c_int]
         L.oracle_carr_brute.restype = C.c_double
         L.oracle_carr_brute.argtypes = [C.c_double, C.c_double, C.c_int64]
+        L.oracle_carr_trace.restype = None
+        L.oracle_carr_trace.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_code_brute.restype = C.c_double
         L.oracle_code_brute.argtypes = [C.c_double, C.c_double, C.c_int64,
                                         C.POINTER(C.c_int32), C.POINTER(C.c_int32),
@@ -56,6 +58,14 @@ def synth(blk, nch, ca, nav, n_per_blk, fmt, want_carr_end=False):
 
 def carr_brute(x, s, n):
     return lib().oracle_carr_brute(x, s, n)
+
+
+def carr_brute_trace(x, s, at):
+    """Brute-force carrier chain from x sampled at the ascending sample indices `at`."""
+    at = np.ascontiguousarray(at, np.int64)
+    out = np.zeros(len(at))
+    lib().oracle_carr_trace(x, s, at.ctypes.data, len(at), out.ctypes.data)
+    return out
 
 
 def code_brute(c, s, n, icode, ibit, iword):

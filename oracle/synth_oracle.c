@@ -147,6 +147,17 @@ double oracle_carr_brute(double x, double s, int64_t n)
     return x;
 }
 
+/* the brute-force carrier chain sampled at ascending sample indices at[0..m) */
+void oracle_carr_trace(double x, double s, const int64_t *at, int m, double *out)
+{
+    int64_t pos = 0;
+    for (int j = 0; j < m; j++) {
+        x = oracle_carr_brute(x, s, at[j] - pos);
+        pos = at[j];
+        out[j] = x;
+    }
+}
+
 double oracle_code_brute(double c, double s, int64_t n, int32_t *icode, int32_t *ibit,
                          int32_t *iword)
 {

@@ -17,6 +17,7 @@ int oracle_synth(const gss_chan_blk_t *blk, const int32_t *nch, const uint32_t *
                  double *carr_end);
 size_t oracle_block_bytes(int n_per_blk, int fmt);
 double oracle_carr_brute(double x, double s, int64_t n);
+void oracle_carr_trace(double x, double s, const int64_t *at, int m, double *out);
 double oracle_code_brute(double c, double s, int64_t n, int32_t *icode, int32_t *ibit,
                          int32_t *iword);
 void oracle_lut(int *sin512, int *cos512);

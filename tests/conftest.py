@@ -62,7 +62,7 @@ def walk_lib():
                 os.path.getmtime(src),
                 os.path.getmtime(os.path.join(PKG, "csrc", "common", "gss_phase.h"))):
             subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-o",
-                                   so, src])
+                                   so, src, "-lm"])
         L = C.CDLL(so)
         D, I64, P = C.c_double, C.c_int64, C.POINTER(C.c_int32)
         for f in ("wc_carr_plain", "wc_carr_cached"):
@@ -70,6 +70,16 @@ def walk_lib():
             getattr(L, f).argtypes = [D, D, I64]
         L.wc_code.restype = D
         L.wc_code.argtypes = [C.c_int, D, D, I64, P, P, P]
+        L.wc_carr_f.restype = D
+        L.wc_carr_f.argtypes = [D, D, I64, P]
+        L.wc_carr_bf.restype = D
+        L.wc_carr_bf.argtypes = [D, D, I64, P]
+        L.wc_code_bf.restype = D
+        L.wc_code_bf.argtypes = [D, D, I64, P, P, P]
+        L.wc_code_f.restype = D
+        L.wc_code_f.argtypes = [D, D, I64, P, P, P]
+        L.wc_carr_seg_starts_f.restype = C.c_int
+        L.wc_carr_seg_starts_f.argtypes = [D, D, I64, C.c_int, C.c_int, C.c_void_p]
         L.wc_carr_anchors.restype = C.c_int
         L.wc_carr_anchors.argtypes = [D, D, I64, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         _walk = L

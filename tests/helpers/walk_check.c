@@ -43,3 +43,75 @@ int wc_carr_anchors(double x0, double s, int64_t n, int seg_r, int nseg, int32_t
     }
     return seg;
 }
+
+/* ---- f64-only forms used by the GPU kernels (gss_jumpf / gss_walkf / gss_to_wrapf) ---- */
+double wc_carr_f(double x, double s, int64_t n, int32_t *nwrap)
+{
+    int w = 0;
+    double r = gss_walkf(x, s, 1.0, (double)n, &w);
+    *nwrap = w;
+    return r;
+}
+
+/* code chain advanced wrap by wrap, exactly as the Stage-A code lanes do */
+double wc_code_f(double c, double s, int64_t n, int32_t *ic, int32_t *ib, int32_t *iw)
+{
+    gss_code_state st = {c, *ic, *ib, *iw};
+    double left = (double)n;
+    while (left > 0.0 && gss_to_wrapf(&st.ph, s, GSS_CA_SEQ_LEN_D, &left))
+        gss_code_count_wrap(&st);
+    *ic = st.icode;
+    *ib = st.ibit;
+    *iw = st.iword;
+    return st.ph;
+}
+
+/* Stage A (carrier chain) + Stage B lane start, f64 forms: for every segment start n0 = seg*R the
+   exact carrier value, walked from the last wrap at or before n0.  Returns the number of Stage-B
+   walks that (wrongly) crossed a wrap; 0 expected. */
+int wc_carr_seg_starts_f(double x0, double s, int64_t n, int seg_r, int nseg, double *out)
+{
+    double left = (double)n, v = x0, ax = x0;
+    int64_t an = 0, pos = 0;
+    int seg = 0, bad = 0;
+    for (;;) {
+        double l0 = left;
+        int wr = gss_to_wrapf(&v, s, 1.0, &left);
+        pos += (int64_t)(l0 - left);
+        int64_t nw = wr ? pos : n;
+        while (seg < nseg && (int64_t)seg * seg_r < nw) {
+            int w = 0;
+            out[seg] = gss_walkf(ax, s, 1.0, (double)((int64_t)seg * seg_r - an), &w);
+            bad += w;
+            seg++;
+        }
+        if (!wr || seg >= nseg)
+            break;
+        an = pos;
+        ax = v;
+    }
+    return bad;
+}
+
+/* ---- branch-free lane form (gss_iter_bf / gss_walk_bf): what the GPU lanes execute ---- */
+double wc_carr_bf(double x, double s, int64_t n, int32_t *nwrap)
+{
+    int w = 0;
+    double r = gss_walk_bf(x, s, 1.0, (double)n, &w);
+    *nwrap = w;
+    return r;
+}
+
+double wc_code_bf(double c, double s, int64_t n, int32_t *ic, int32_t *ib, int32_t *iw)
+{
+    gss_code_state st = {c, *ic, *ib, *iw};
+    double left = (double)n, as = s < 0.0 ? -s : s, rs = 1.0 / as;
+    if (s != 0.0)
+        while (left > 0.0)
+            if (gss_iter_bf(&st.ph, s, as, rs, GSS_CA_SEQ_LEN_D, &left))
+                gss_code_count_wrap(&st);
+    *ic = st.icode;
+    *ib = st.ibit;
+    *iw = st.iword;
+    return st.ph;
+}

@@ -47,6 +47,9 @@ def test_carrier_walks_exact(seed):
         want = oracle.carr_brute(x, s, n)
         assert W.wc_carr_plain(x, s, n) == want, ("plain", x, s, n)
         assert W.wc_carr_cached(x, s, n) == want, ("cached", x, s, n)
+        nw = C.c_int32(0)
+        assert W.wc_carr_f(x, s, n, C.byref(nw)) == want, ("f64", x, s, n)
+        assert W.wc_carr_bf(x, s, n, C.byref(nw)) == want, ("branch-free", x, s, n)
         assert G.carr_advance(x, s, n) == want
 
 
@@ -69,6 +72,12 @@ def test_code_walks_exact(seed):
             a, b, d = C.c_int32(st[0]), C.c_int32(st[1]), C.c_int32(st[2])
             ph = W.wc_code(cached, c0, cs, n, C.byref(a), C.byref(b), C.byref(d))
             assert (ph, a.value, b.value, d.value) == want, (cached, c0, cs, n)
+        a, b, d = C.c_int32(st[0]), C.c_int32(st[1]), C.c_int32(st[2])
+        ph = W.wc_code_f(c0, cs, n, C.byref(a), C.byref(b), C.byref(d))
+        assert (ph, a.value, b.value, d.value) == want, ("f64", c0, cs, n)
+        a, b, d = C.c_int32(st[0]), C.c_int32(st[1]), C.c_int32(st[2])
+        ph = W.wc_code_bf(c0, cs, n, C.byref(a), C.byref(b), C.byref(d))
+        assert (ph, a.value, b.value, d.value) == want, ("branch-free", c0, cs, n)
         assert G.code_advance(c0, cs, n, *st) == want
 
 
@@ -96,10 +105,35 @@ def test_anchors_are_exact_states():
             assert x == ax[seg], (seg, tgt)
 
 
-def test_stationary_and_single_steps():
+@pytest.mark.parametrize("seed", [10, 11])
+def test_segment_start_states_f64(seed):
+    """GPU form of Stage A + Stage-B lane start (f64 jump walk): the carrier value at every
+    segment start equals the brute-force chain, and no lane-start walk crosses a wrap."""
     W = walk_lib()
-    for x, s in [(0.25, 1e-20), (0.75, -1e-19), (0.5, 2.0 ** -55)]:
-        for n in (1, 2, 3, 1000):
+    rng = random.Random(seed)
+    R, N = 1024, 260000
+    nseg = (N + R - 1) // R
+    for i in range(6):
+        s = rng.uniform(-5000, 5000) / 2.6e6
+        if i == 0:
+            s = (math.floor(abs(s) / 2.0 ** -53) + 0.5) * 2.0 ** -53     # tie at the wrap step
+        x0 = rng.random() if i != 1 else 0.0
+        out = np.zeros(nseg)
+        assert W.wc_carr_seg_starts_f(x0, s, N, R, nseg, out.ctypes.data) == 0
+        want = oracle.carr_brute_trace(x0, s, [seg * R for seg in range(nseg)])
+        assert np.array_equal(out, want), i
+
+
+def test_stationary_and_single_steps():
+    """Stationary values, and steps so small that K < 2^26 in the upper binades (the
+    branch-free walk's exact-division fallback)."""
+    W = walk_lib()
+    for x, s in [(0.25, 1e-20), (0.75, -1e-19), (0.5, 2.0 ** -55), (0.3, 3e-9), (0.9, -5e-9),
+                 (0.999, 7.3e-10), (1e-9, 2.5e-9)]:
+        for n in (1, 2, 3, 1000, 400000):
             want = oracle.carr_brute(x, s, n)
             assert W.wc_carr_plain(x, s, n) == want
             assert W.wc_carr_cached(x, s, n) == want
+            nw = C.c_int32(0)
+            assert W.wc_carr_f(x, s, n, C.byref(nw)) == want
+            assert W.wc_carr_bf(x, s, n, C.byref(nw)) == want
