@@ -103,27 +103,12 @@ def main():
     dev_t = torch.device("cuda", local)
 
     # ---- host control plane for this rank's window (untimed setup) ----
-    blocks_per = int(round(args.window * 10)) - 1            # 2999 for 300 s
+    from gpssim_amd.shard import plan_rank
     t_plan0 = time.perf_counter()
-    scn = G.Scenario(NAV, llh=LOC, duration=args.window * world if world > 1 else args.window,
-                     samp_freq=FS, data_format=args.fmt)
-    first = rank * blocks_per
-    done, keep_b, keep_n = 0, [], []
-    while done < first + blocks_per:
-        b, n = scn.next(min(1000, first + blocks_per - done), threads=args.threads)
-        if len(n) == 0:
-            break
-        lo = max(0, first - done)
-        if lo < len(n):
-            keep_b.append(b[lo:])
-            keep_n.append(n[lo:])
-        done += len(n)
-    blk = np.concatenate(keep_b)[:blocks_per]
-    nch = np.concatenate(keep_n)[:blocks_per]
-    nav = scn.nav_table()
+    blk, nch, nav, npb = plan_rank(NAV, rank, world, args.window, llh=LOC, samp_freq=FS,
+                                   data_format=args.fmt, threads=args.threads)
     host_plan_s = time.perf_counter() - t_plan0
-    nblk, npb = len(nch), scn.n_per_blk
-    assert nblk == blocks_per, (nblk, blocks_per)
+    nblk = len(nch)
 
     # ---- inputs resident in HBM ----
     dev = G.Device(local)

@@ -15,5 +15,6 @@ rc=$?; echo "pytest rc=$rc" >> $log; ok $rc || exit $rc
 rc=$?; echo "smoke rc=$rc" >> $log; ok $rc || exit $rc; }
 timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 5 --warmup 1} > gpurun_out/bench_$TAG.log 2>&1
 rc=$?; echo "bench rc=$rc" >> $log; ok $rc || exit $rc
+if [ -n "$CLI_RATE" ]; then bash tools/cli_rate.sh $TAG; rc=$?; echo "cli_rate rc=$rc" >> $log; ok $rc || exit $rc; fi
 if [ -n "$PROFILE" ]; then bash tools/profile.sh $TAG; rc=$?; echo "profile rc=$rc" >> $log; fi
 exit $rc
