@@ -245,55 +245,136 @@ GSS_HD int gss_to_wrapf(double *x, double s, double W, double *left)
 /* ---- branch-free form of one walk iteration (GPU lanes: no divergent control flow) -----------
  * One iteration = the longest exact lattice jump from v (possibly empty, gss_jumpf's rules),
  * then one real reference step with its wrap, if steps remain.  Every lane executes the same
- * instruction sequence; decisions are selects.  as = |s|, rs = 1/|s| (any rounding).  Returns 1
- * if the real step wrapped. */
-GSS_HD int gss_iter_bf(double *pv, double s, double as, double rs, double W, double *pleft)
+ * instruction sequence; decisions are selects.  Lane constants: as = |s|, rs = 1/|s| (any
+ * rounding), W the wrap threshold and exW = ceil(log2 W) (frexp convention: the wrap limit
+ * applies in the binade [2^(ex-1), 2^ex) iff ex >= exW; 0 for the carrier, 10 for the code).
+ * Returns 1 if the real step wrapped.
+ *
+ * Exactness of each line: every double below holds an integer < 2^54 or a lattice value, so all
+ * adds are exact; q0 is within one of floor(lim/K) for K >= 2^26 (see gss_jumpf) and the fma
+ * residual lim - q0*K is exact; v + J*K*u is the lattice point J steps on, exact via one fma. */
+GSS_HD int gss_iter_bfx(double *pv, double s, double as, double rs, double W, int exW,
+                        double *pleft, double *pJ, double *pDs)
 {
     const double v = *pv;
-    double left = *pleft;
+    const double left = *pleft;
     const int ex = GSS_FREXP_EXP(v);
     const int sh = 53 - ex;
-    const double m = GSS_LDEXP(v, sh);
-    const double sig = GSS_LDEXP(as, sh);
+    const double m = GSS_LDEXP(v, sh);                 /* v/u */
+    const double sig = GSS_LDEXP(as, sh);              /* |s|/u */
+    const double urs = GSS_LDEXP(rs, ex - 53);         /* u/|s| */
     const double k = GSS_FLOOR(sig);
+    const double K = GSS_RINT(sig);                    /* round-half-even, fl()'s rule */
     const double frac = sig - k;
-    const double K = GSS_RINT(sig);
     const double h = m * 0.5;
     const int odd_tie = (frac == 0.5) & (h != GSS_FLOOR(h));
-    double lim_a = ((0x1p53 - m) - k) - 1.0;
-    const double l2 = (GSS_LDEXP(W - v, sh) - K) - 1.0;
-    lim_a = ((W <= GSS_LDEXP(1.0, ex)) & (l2 < lim_a)) ? l2 : lim_a;
+    /* ascending: stay below 2^ex, and below W in W's binade */
+    double lim = ((0x1p53 - 1.0) - k) - m;
+    const double l2 = (GSS_LDEXP(W - v, sh) - 1.0) - K;
+    lim = ((ex >= exW) & (l2 < lim)) ? l2 : lim;
+    /* descending: stay >= 2^(ex-1) */
     const double lim_d = (m - 0x1p52) - (frac > 0.0 ? k + 1.0 : k);
-    const double lim = s > 0.0 ? lim_a : lim_d;
+    lim = s > 0.0 ? lim : lim_d;
     const int live = (v >= 0x1p-900) & (sig < 0x1p52) & !odd_tie;
     const int stat = live & (K == 0.0);                /* stationary: no step moves v */
     const int ok = live & (K != 0.0) & (lim >= 0.0);
-    const double Ks = K != 0.0 ? K : 1.0;
-    /* q = floor(lim / K) without a division: lim/sig = lim*u/|s| is within 1/2 of lim/K when
-       K >= 2^26 (|lim/K - lim/sig| <= lim/(2 K sig), lim <= 2^52), so q0 = floor(lim*u*rs) with
-       rs = 1/|s| is off by at most one, corrected with the exact residual lim - q0*K (fma). */
-    double q;
-    if (Ks >= 0x1p26) {
-        const double q0 = GSS_FLOOR(GSS_LDEXP(lim, ex - 53) * rs);
-        const double r0 = GSS_FMA(-q0, Ks, lim);
-        q = r0 < 0.0 ? q0 - 1.0 : (r0 >= Ks ? q0 + 1.0 : q0);
+    double J;
+    if (K >= 0x1p26) {
+        const double q0 = GSS_FLOOR(lim * urs);
+        const double r0 = GSS_FMA(-q0, K, lim);
+        J = r0 < 0.0 ? q0 : (r0 >= K ? q0 + 2.0 : q0 + 1.0);
     } else {                                           /* tiny steps: exact division */
-        q = GSS_FLOOR(lim / Ks);
+        const double Ks = K != 0.0 ? K : 1.0;
+        double q = GSS_FLOOR(lim / Ks);
         q = GSS_FMA(-q, Ks, lim) < 0.0 ? q - 1.0 : q;
+        J = q + 1.0;
     }
-    double J = q + 1.0;
     J = J > left ? left : J;
     J = ok ? J : (stat ? left : 0.0);
-    const double d = GSS_LDEXP(J * K, ex - 53);       /* 0 when stationary */
-    const double v1 = v + (s > 0.0 ? d : -d);
-    left -= J;
-    const int step = left > 0.0;
+    const double Ds = GSS_LDEXP(s > 0.0 ? K : -K, ex - 53);   /* signed K*u: one step's move */
+    const double v1 = GSS_FMA(J, Ds, v);
+    const double left1 = left - J;
+    *pJ = J;
+    *pDs = Ds;
+    const int step = left1 > 0.0;
     const double r = v1 + s;
     const int hi = r >= W, lo = r < 0.0;
-    const double r2 = hi ? r - W : (lo ? r + W : r);
-    *pv = step ? r2 : v1;
-    *pleft = step ? left - 1.0 : left;
+    const double rw = hi ? r - W : (lo ? r + W : r);
+    *pv = step ? rw : v1;
+    *pleft = step ? left1 - 1.0 : left1;
     return step & (hi | lo);
+}
+
+GSS_HD int gss_iter_bf(double *pv, double s, double as, double rs, double W, int exW,
+                       double *pleft)
+{
+    double J, Ds;
+    return gss_iter_bfx(pv, s, as, rs, W, exW, pleft, &J, &Ds);
+}
+
+/* exW for a wrap threshold W (>= 1): smallest ex with W <= 2^ex */
+GSS_HD int gss_exw(double W)
+{
+    int e = GSS_FREXP_EXP(W);                          /* W in [2^(e-1), 2^e) */
+    return GSS_LDEXP(1.0, e - 1) == W ? e - 1 : e;
+}
+
+/* Exact states at every segment start n0 = j*seg_r (j < nseg) of one chain, walking n_per_blk
+ * steps from v (Stage A of the GPU path; out_x[j] = phase at n0, out_c[j] = code counters
+ * icode|ibit<<8|iword<<16 at n0 when code != 0).  A trip covers positions (pb, pa]: a lattice
+ * jump of J steps from vb (state at pb + i is vb + i*Ds, exact) and one real step to pa.  At most
+ * one segment start usually falls in a trip; more (long jumps at tiny Dopplers) take a loop.
+ * Returns the final value if want_end (else the walk stops after the last segment). */
+GSS_HD double gss_seg_states(double v, double st, double W, int exW, int code, uint32_t cnt,
+                             int n_per_blk, int nseg, int seg_r, int want_end, double *out_x,
+                             uint32_t *out_c)
+{
+    const double as = st < 0.0 ? -st : st, rs = 1.0 / as;
+    const double total = (double)n_per_blk;
+    double left = st == 0.0 ? 0.0 : total;             /* no motion: no wraps */
+    int seg = 1;
+    out_x[0] = v;                                       /* n0 = 0: the block start */
+    if (code)
+        out_c[0] = cnt;
+    if (left == 0.0)
+        for (; seg < nseg; seg++) {
+            out_x[seg] = v;
+            if (code)
+                out_c[seg] = cnt;
+        }
+    while (left > 0.0 && (seg < nseg || want_end)) {
+        const double vb = v, pb = total - left;
+        double J, Ds;
+        const int wr = gss_iter_bfx(&v, st, as, rs, W, exW, &left, &J, &Ds);
+        const double pa = total - left;
+        const uint32_t cnt_b = cnt;
+        if (code & wr) {                                /* gpssim.c:2216-2236 */
+            uint32_t icode = (cnt & 0xFFu) + 1u, ibit = (cnt >> 8) & 0xFFu, iword = cnt >> 16;
+            const uint32_t nb = icode >= 20u;
+            icode = nb ? 0u : icode;
+            ibit += nb;
+            const uint32_t nw = ibit >= 30u;
+            ibit = nw ? 0u : ibit;
+            iword += nw;
+            cnt = icode | (ibit << 8) | (iword << 16);
+        }
+        if (seg + 1 < nseg && (double)((seg + 1) * seg_r) <= pa) {   /* rare: 2+ starts */
+            for (; seg + 1 < nseg && (double)((seg + 1) * seg_r) <= pa; seg++) {
+                const double n0 = (double)(seg * seg_r);
+                out_x[seg] = n0 <= pb + J ? GSS_FMA(n0 - pb, Ds, vb) : v;
+                if (code)
+                    out_c[seg] = n0 == pa ? cnt : cnt_b;
+            }
+        }
+        const double n0 = (double)(seg * seg_r);
+        if (seg < nseg && n0 <= pa) {
+            out_x[seg] = n0 <= pb + J ? GSS_FMA(n0 - pb, Ds, vb) : v;
+            if (code)
+                out_c[seg] = n0 == pa ? cnt : cnt_b;
+            seg++;
+        }
+    }
+    return v;
 }
 
 /* n steps with gss_iter_bf; returns the value, *nwrap counts wraps. */
@@ -303,8 +384,9 @@ GSS_HD double gss_walk_bf(double x, double s, double W, double n, int *nwrap)
     if (s == 0.0)
         return x;
     const double rs = 1.0 / as;
+    const int exw = gss_exw(W);
     while (n > 0.0)
-        *nwrap += gss_iter_bf(&x, s, as, rs, W, &n);
+        *nwrap += gss_iter_bf(&x, s, as, rs, W, exw, &n);
     return x;
 }
 

@@ -6,11 +6,11 @@
  * serial IEEE double recurrences (built with -ffp-contract=off); the only shortcuts are provably
  * exact lattice translations (common/gss_phase.h).
  *
- * Stage A  gss_anchor_kernel    one lane per (block, channel, chain) with chain ∈ {carrier, code}
- *                               (one chain kind per wave).  Walks the block with the branch-free
- *                               f64 lattice walk (gss_iter_bf) and records, for every R-sample
- *                               segment, the last wrap at or before its first sample: an exact
- *                               "anchor" state (sample index, phase[, counters]).
+ * Stage A  gss_anchor_kernel    one lane per (block, channel, chain), one chain kind per wave,
+ *                               walking the block with the branch-free f64 lattice walk
+ *                               (gss_iter_bf) and recording for every R-sample segment the last
+ *                               wrap at or before its first sample: an exact "anchor" state
+ *                               (sample index, phase[, counters]).
  * Stage B  gss_synth_kernel     one lane per R-sample segment of a block, all channels.  Each lane
  *                               first walks every channel from its anchor to the segment start
  *                               (≤ one cycle, no wrap), then runs the per-sample recurrences:
@@ -41,114 +41,43 @@ struct lut_arg { int16_t sin512[512]; int16_t cos512[512]; };
 /* ======================================================================================== */
 /* Stage A: anchors                                                                         */
 /* ======================================================================================== */
-/* One lane per (block, channel) and chain; even workgroups walk carriers, odd ones code phases,
-   so a wave never diverges on the chain kind.  Lanes walk their block with the branch-free f64
-   lattice walk (gss_iter_bf: one jump + one real step per trip) and record, for every R-sample
-   segment, the last wrap at or before the segment's first sample. */
+/* Stage A walks one chain per lane; even workgroups take the carrier chains of 64 consecutive
+   (block, channel) pairs, odd ones their code chains, so every wave runs one specialised code
+   path.  (Measured on MI355X, tools/ubench/anchor_ubench.hip: one chain per lane beats two
+   interleaved chains per lane, 1.43 vs 2.33 ms, because the trip is issue-heavy; staging the
+   outputs in LDS does not pay over direct stores.)  The walk itself is gss_seg_states: the exact
+   state at every segment start, interpolated on the lattice jump that crosses it. */
 __global__ __launch_bounds__(ANCHOR_THREADS) void gss_anchor_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch, int nblk, int nchp,
-    int n_per_blk, int nseg, int seg_r, int32_t *__restrict__ anc_cn, double *__restrict__ anc_cx,
-    int32_t *__restrict__ anc_kn, double *__restrict__ anc_kx, uint32_t *__restrict__ anc_kc,
-    double *__restrict__ carr_end)
+    int n_per_blk, int nseg, int nsegp, int seg_r, double *__restrict__ seg_carr,
+    double *__restrict__ seg_code, uint32_t *__restrict__ seg_cnt, double *__restrict__ carr_end)
 {
-    const int chain = blockIdx.x & 1;
+    const bool code = blockIdx.x & 1;                      /* wave-uniform */
     const int pair = (blockIdx.x >> 1) * ANCHOR_THREADS + threadIdx.x;
     const int b = pair / nchp, k = pair - b * nchp;
     if (b >= nblk)
         return;
     const size_t bk = (size_t)b * GSS_MAXCH + k;
-    const size_t row = bk * (size_t)nseg;
-    if (k >= nch[b]) {
-        /* padding channel of the kernel instance: zero anchors (Stage B gives it no motion and
-           zero gain) */
-        for (int sgi = 0; sgi < nseg; sgi++) {
-            if (chain == 0) {
-                anc_cn[row + sgi] = 0;
-                anc_cx[row + sgi] = 0.0;
-            } else {
-                anc_kn[row + sgi] = 0;
-                anc_kx[row + sgi] = 0.0;
-                anc_kc[row + sgi] = 0u;
-            }
-        }
-        return;
+    const size_t row = bk * (size_t)nsegp;
+    const bool real = k < nch[b];
+    /* padding channels of the kernel instance: no motion (Stage B gives them no gain) */
+    gss_chan_blk_t p = blk[bk];
+    if (!real) {
+        p.carr0 = p.carr_step = p.code0 = p.code_step = 0.0;
+        p.icode = p.ibit = p.iword = 0;
     }
-    const gss_chan_blk_t p = blk[bk];
-    const bool carr = chain == 0;                       /* wave-uniform */
-    const double st = carr ? p.carr_step : p.code_step;
-    const double as = st < 0.0 ? -st : st;
-    const double rs = 1.0 / as;
-    const double W = carr ? 1.0 : GSS_CA_SEQ_LEN_D;
-    const double total = (double)n_per_blk;
-    double v = carr ? p.carr0 : p.code0;
-    double left = st == 0.0 ? 0.0 : total;             /* no motion: no wraps */
-    uint32_t cnt = (uint32_t)p.icode | ((uint32_t)p.ibit << 8) | ((uint32_t)p.iword << 16);
-    uint32_t acnt = cnt;
-    double ax = v;
-    int32_t an = 0;
-    int seg = 0;
-    const bool need_end = carr && carr_end != nullptr;
-    /* Flat loop, one branch-free jump+step per trip.  A segment's anchor is final once the walk
-       has passed its first sample: it is the wrap of this trip if that wrap lands exactly on the
-       segment start, else the previous one.  At most one anchor is stored per trip (a predicated
-       store, no loop); the rare backlog of two or more segments older than a fresh wrap (long
-       cycles: Dopplers below ~2.5 kHz at 2.6 MS/s) is drained in a loop first. */
-    while (left > 0.0 && (seg < nseg || need_end)) {
-        const int wr = gss_iter_bf(&v, st, as, rs, W, &left);
-        const int32_t pos = (int32_t)(total - left);
-        if (wr && seg + 1 < nseg && (seg + 1) * seg_r < pos) {
-            for (; seg + 1 < nseg && (seg + 1) * seg_r < pos; seg++) {   /* rare backlog */
-                if (carr) {
-                    anc_cn[row + seg] = an;
-                    anc_cx[row + seg] = ax;
-                } else {
-                    anc_kn[row + seg] = an;
-                    anc_kx[row + seg] = ax;
-                    anc_kc[row + seg] = acnt;
-                }
-            }
-        }
-        if (!carr && wr) {                              /* gpssim.c:2216-2236 */
-            uint32_t icode = (cnt & 0xFFu) + 1u, ibit = (cnt >> 8) & 0xFFu, iword = cnt >> 16;
-            const uint32_t nb = icode >= 20u;
-            icode = nb ? 0u : icode;
-            ibit += nb;
-            const uint32_t nw2 = ibit >= 30u;
-            ibit = nw2 ? 0u : ibit;
-            iword += nw2;
-            cnt = icode | (ibit << 8) | (iword << 16);
-        }
-        const bool fin = seg < nseg && seg * seg_r <= pos;
-        const bool use_new = wr && seg * seg_r >= pos;
-        if (fin) {
-            const int32_t e_n = use_new ? pos : an;
-            const double e_x = use_new ? v : ax;
-            if (carr) {
-                anc_cn[row + seg] = e_n;
-                anc_cx[row + seg] = e_x;
-            } else {
-                anc_kn[row + seg] = e_n;
-                anc_kx[row + seg] = e_x;
-                anc_kc[row + seg] = use_new ? cnt : acnt;
-            }
-        }
-        seg += fin ? 1 : 0;
-        an = wr ? pos : an;
-        ax = wr ? v : ax;
-        acnt = wr ? cnt : acnt;
+    if (code) {
+        const uint32_t cnt = (uint32_t)p.icode | ((uint32_t)p.ibit << 8) |
+                             ((uint32_t)p.iword << 16);
+        gss_seg_states(p.code0, p.code_step, GSS_CA_SEQ_LEN_D, 10, 1, cnt, n_per_blk, nseg, seg_r,
+                       0, seg_code + row, seg_cnt + row);
+    } else {
+        const bool want_end = carr_end != nullptr && real;
+        const double e = gss_seg_states(p.carr0, p.carr_step, 1.0, 0, 0, 0u, n_per_blk, nseg,
+                                        seg_r, want_end, seg_carr + row, nullptr);
+        if (want_end)
+            carr_end[bk] = e;
     }
-    for (; seg < nseg; seg++) {                         /* segments after the last wrap */
-        if (carr) {
-            anc_cn[row + seg] = an;
-            anc_cx[row + seg] = ax;
-        } else {
-            anc_kn[row + seg] = an;
-            anc_kx[row + seg] = ax;
-            anc_kc[row + seg] = acnt;
-        }
-    }
-    if (need_end)
-        carr_end[bk] = v;
 }
 
 /* ======================================================================================== */
@@ -185,23 +114,6 @@ __device__ __forceinline__ void store16(uint8_t *p, uint4 v)
     }
 }
 
-/* Lane start state: both chains walked from their anchors (the last wrap at or before the
-   segment start, so the walk crosses no wrap; a crossing would be a bug and is reported).
-   Out of line on purpose: inlined NCH times into the unrolled channel loop the walk would
-   dominate the register allocation of the whole kernel. */
-struct lane_start { double carr, C; int bad; };
-
-__device__ __noinline__ lane_start lane_start_walk(double ax, int an, double cstep, double kx,
-                                                   int kn, double kstep, int n0)
-{
-    lane_start r;
-    int w1 = 0, w2 = 0;
-    r.carr = gss_walk_bf(ax, cstep, 1.0, (double)(n0 - an), &w1);
-    r.C = gss_walk_bf(kx, kstep, GSS_CA_SEQ_LEN_D, (double)(n0 - kn), &w2);
-    r.bad = (w1 | w2) ? 2 : 0;
-    return r;
-}
-
 __device__ __forceinline__ void wave_sync_lds()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -222,10 +134,9 @@ template <int NCH, int FMT>
 __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch,
     const uint32_t *__restrict__ ca_bits, const uint32_t *__restrict__ nav,
-    const int32_t *__restrict__ anc_cn, const double *__restrict__ anc_cx,
-    const int32_t *__restrict__ anc_kn, const double *__restrict__ anc_kx,
-    const uint32_t *__restrict__ anc_kc, lut_arg lut, int n_per_blk, int nseg, int seg_r,
-    int wg_per_blk, uint8_t *__restrict__ out, size_t block_bytes, int32_t *__restrict__ status)
+    const double *__restrict__ seg_carr, const double *__restrict__ seg_code,
+    const uint32_t *__restrict__ seg_cnt, lut_arg lut, int n_per_blk, int nseg, int nsegp,
+    int seg_r, int wg_per_blk, uint8_t *__restrict__ out, size_t block_bytes, int32_t *__restrict__ status)
 {
     constexpr int SPC = fmt_traits<FMT>::SPC;
     constexpr int BPS4 = FMT == 16 ? 16 : FMT == 8 ? 8 : 1;      /* 4 x bytes per sample */
@@ -283,20 +194,17 @@ __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
         ks[k] = real ? prow[k].code_step : 0.0;
     }
 
-    /* ---- exact per-lane start state, unconditionally for every channel of the instance ---- */
+    /* ---- exact per-lane start state (Stage A), every channel of the instance ---- */
     double carr[NCH], C[NCH];
     uint32_t st[NCH];             /* icode | ibit<<8 | iword<<16 */
     uint32_t gi[NCH], gq[NCH];
     int bad = 0;
 #pragma unroll
     for (int k = 0; k < NCH; k++) {
-        size_t r = ((size_t)b * GSS_MAXCH + k) * (size_t)nseg + segc;
-        lane_start ls = lane_start_walk(anc_cx[r], anc_cn[r], cs[k], anc_kx[r], anc_kn[r], ks[k],
-                                        n0c);
-        carr[k] = ls.carr;
-        C[k] = ls.C;
-        bad |= ls.bad;
-        uint32_t c = anc_kc[r];
+        const size_t r = ((size_t)b * GSS_MAXCH + k) * (size_t)nsegp + segc;
+        carr[k] = seg_carr[r];
+        C[k] = seg_code[r];
+        uint32_t c = seg_cnt[r];
         int ibit = (c >> 8) & 0xFF, iw = c >> 16;
         if (iw > 59) { bad |= 1; iw = 59; c = (c & 0xFFFFu) | (59u << 16); }
         st[k] = c;
@@ -443,10 +351,9 @@ __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
 struct gss_dev {
     int ordinal;
     int seg_r = 1024;                    /* samples per Stage-B lane (env GSS_SEG_R)   */
-    int32_t *anc_cn = nullptr, *anc_kn = nullptr;   /* anchors [blocks][16][nseg]   */
-    double *anc_cx = nullptr, *anc_kx = nullptr;
-    uint32_t *anc_kc = nullptr;
-    size_t anc_cap = 0;
+    double *seg_carr = nullptr, *seg_code = nullptr; /* segment-start states [blocks][16][nsegp] */
+    uint32_t *seg_cnt = nullptr;
+    size_t seg_cap = 0;
     static constexpr int RING = 256;
     hipEvent_t ev[RING][3];
     int n_ev = 0;
@@ -510,7 +417,7 @@ extern "C" int gss_dev_close(gss_dev *d)
 {
     if (!d) return 0;
     (void)hipSetDevice(d->ordinal);
-    void *bufs[] = {d->anc_cn, d->anc_kn, d->anc_cx, d->anc_kx, d->anc_kc,
+    void *bufs[] = {d->seg_carr, d->seg_code, d->seg_cnt,
                     d->h_in, d->d_out, d->d_cend, d->d_status};
     for (void *p : bufs)
         (void)hipFree(p);
@@ -522,35 +429,32 @@ extern "C" int gss_dev_close(gss_dev *d)
 }
 
 static int nseg_of(int n, int r) { return (n + r - 1) / r; }
+static int nsegp_of(int n, int r) { return (nseg_of(n, r) + 31) & ~31; }   /* anchor row stride */
 
 extern "C" int gss_dev_reserve(gss_dev *d, int max_blocks, int n_per_blk)
 {
     if (!d || max_blocks <= 0 || n_per_blk <= 0)
         return gss_fail(GSS_E_ARG, "invalid reserve arguments");
     HIP_TRY(hipSetDevice(d->ordinal));
-    size_t need = (size_t)max_blocks * GSS_MAXCH * (size_t)nseg_of(n_per_blk, d->seg_r);
-    if (need <= d->anc_cap)
+    size_t need = (size_t)max_blocks * GSS_MAXCH * (size_t)nsegp_of(n_per_blk, d->seg_r);
+    if (need <= d->seg_cap)
         return 0;
-    void *old[] = {d->anc_cn, d->anc_kn, d->anc_cx, d->anc_kx, d->anc_kc};
+    void *old[] = {d->seg_carr, d->seg_code, d->seg_cnt};
     for (void *p : old)
         (void)hipFree(p);
-    d->anc_cn = d->anc_kn = nullptr;
-    d->anc_cx = d->anc_kx = nullptr;
-    d->anc_kc = nullptr;
-    d->anc_cap = 0;
-    HIP_TRY(hipMalloc(&d->anc_cn, need * sizeof(int32_t)));
-    HIP_TRY(hipMalloc(&d->anc_kn, need * sizeof(int32_t)));
-    HIP_TRY(hipMalloc(&d->anc_cx, need * sizeof(double)));
-    HIP_TRY(hipMalloc(&d->anc_kx, need * sizeof(double)));
-    HIP_TRY(hipMalloc(&d->anc_kc, need * sizeof(uint32_t)));
-    d->anc_cap = need;
+    d->seg_carr = d->seg_code = nullptr;
+    d->seg_cnt = nullptr;
+    d->seg_cap = 0;
+    HIP_TRY(hipMalloc(&d->seg_carr, need * sizeof(double)));
+    HIP_TRY(hipMalloc(&d->seg_code, need * sizeof(double)));
+    HIP_TRY(hipMalloc(&d->seg_cnt, need * sizeof(uint32_t)));
+    d->seg_cap = need;
     return 0;
 }
 
 typedef void (*synth_fn)(const gss_chan_blk_t *, const int32_t *, const uint32_t *,
-                         const uint32_t *, const int32_t *, const double *, const int32_t *,
-                         const double *, const uint32_t *, lut_arg, int, int,
-                         int, int, uint8_t *, size_t, int32_t *);
+                         const uint32_t *, const double *, const double *, const uint32_t *,
+                         lut_arg, int, int, int, int, int, uint8_t *, size_t, int32_t *);
 
 template <int FMT> static synth_fn pick_nch(int nchp)
 {
@@ -588,7 +492,7 @@ extern "C" int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     const int R = d->seg_r;
-    int nseg = nseg_of(n_per_blk, R);
+    int nseg = nseg_of(n_per_blk, R), nsegp = nsegp_of(n_per_blk, R);
     int nchp = nch_max < 1 ? 1 : nch_max;          /* kernel instance; fewer channels padded */
     if (nchp > GSS_MAXCH)
         return gss_fail(GSS_E_ARG, "nch_max %d > %d", nch_max, GSS_MAXCH);
@@ -602,14 +506,14 @@ extern "C" int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int
     int a_blocks = 2 * ((nblk * nchp + ANCHOR_THREADS - 1) / ANCHOR_THREADS);
     HIP_TRY(hipEventRecord(ev[0], st));
     hipLaunchKernelGGL(gss_anchor_kernel, dim3(a_blocks), dim3(ANCHOR_THREADS), 0, st, blk, nch,
-                       nblk, nchp, n_per_blk, nseg, R, d->anc_cn, d->anc_cx, d->anc_kn, d->anc_kx,
-                       d->anc_kc, carr_end);
+                       nblk, nchp, n_per_blk, nseg, nsegp, R, d->seg_carr, d->seg_code, d->seg_cnt,
+                       carr_end);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], st));
     int wg_per_blk = (nseg + SYNTH_THREADS - 1) / SYNTH_THREADS;
     hipLaunchKernelGGL(fn, dim3(nblk * wg_per_blk), dim3(SYNTH_THREADS), 0, st, blk, nch, ca_bits,
-                       nav, d->anc_cn, d->anc_cx, d->anc_kn, d->anc_kx, d->anc_kc, d->lut,
-                       n_per_blk, nseg, R, wg_per_blk, (uint8_t *)out, bb, status);
+                       nav, d->seg_carr, d->seg_code, d->seg_cnt, d->lut,
+                       n_per_blk, nseg, nsegp, R, wg_per_blk, (uint8_t *)out, bb, status);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[2], st));
     return 0;

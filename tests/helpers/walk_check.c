@@ -108,10 +108,18 @@ double wc_code_bf(double c, double s, int64_t n, int32_t *ic, int32_t *ib, int32
     double left = (double)n, as = s < 0.0 ? -s : s, rs = 1.0 / as;
     if (s != 0.0)
         while (left > 0.0)
-            if (gss_iter_bf(&st.ph, s, as, rs, GSS_CA_SEQ_LEN_D, &left))
+            if (gss_iter_bf(&st.ph, s, as, rs, GSS_CA_SEQ_LEN_D, gss_exw(GSS_CA_SEQ_LEN_D), &left))
                 gss_code_count_wrap(&st);
     *ic = st.icode;
     *ib = st.ibit;
     *iw = st.iword;
     return st.ph;
+}
+
+/* Stage A (GPU form, gss_seg_states): exact phase (and code counters) at every segment start */
+double wc_seg_states(double v, double s, int code, uint32_t cnt, int n, int seg_r, int nseg,
+                     int want_end, double *out_x, uint32_t *out_c)
+{
+    double W = code ? GSS_CA_SEQ_LEN_D : 1.0;
+    return gss_seg_states(v, s, W, gss_exw(W), code, cnt, n, nseg, seg_r, want_end, out_x, out_c);
 }

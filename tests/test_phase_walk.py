@@ -124,6 +124,47 @@ def test_segment_start_states_f64(seed):
         assert np.array_equal(out, want), i
 
 
+@pytest.mark.parametrize("seed", [20, 21, 22])
+def test_stage_a_segment_states(seed):
+    """gss_seg_states (the GPU Stage A core): the exact carrier / code state at every segment
+    start, straight from the walk (lattice jumps interpolated exactly), equals brute force;
+    includes Dopplers so small that one trip spans many segments, forced ties, zero phase, and
+    the block-end value."""
+    W = walk_lib()
+    rng = random.Random(seed)
+    R, N = 1024, 260000
+    nseg = (N + R - 1) // R
+    at = [j * R for j in range(nseg)]
+    for i in range(8):
+        f = rng.uniform(-5000, 5000)
+        if i == 1:
+            f = rng.uniform(-0.5, 0.5)                     # jumps across many segments
+        if i == 2:
+            f = 0.0
+        s = f / 2.6e6
+        if i == 3:
+            s = (math.floor(abs(s) / 2.0 ** -53) + 0.5) * 2.0 ** -53     # tie at the wrap step
+        x0 = rng.random() if i != 4 else 0.0
+        ox = np.zeros(nseg)
+        oc = np.zeros(nseg, np.uint32)
+        end = W.wc_seg_states(x0, s, 0, 0, N, R, nseg, 1, ox.ctypes.data, oc.ctypes.data)
+        assert np.array_equal(ox, oracle.carr_brute_trace(x0, s, at)), i
+        assert end == oracle.carr_brute(x0, s, N), i
+        # code chain with counters
+        cs = (1.023e6 + f / 1540.0) / 2.6e6
+        if i == 5:
+            cs = (math.floor(cs / 2.0 ** -43) + 0.5) * 2.0 ** -43
+        c0 = rng.random() * 1023.0 if i != 6 else 0.0
+        st = (rng.randrange(20), rng.randrange(30), rng.randrange(3))
+        cnt0 = st[0] | (st[1] << 8) | (st[2] << 16)
+        W.wc_seg_states(c0, cs, 1, cnt0, N, R, nseg, 0, ox.ctypes.data, oc.ctypes.data)
+        c, (a, b, d) = c0, st
+        for j in range(nseg):
+            if j:
+                c, a, b, d = oracle.code_brute(c, cs, R, a, b, d)
+            assert ox[j] == c and oc[j] == (a | (b << 8) | (d << 16)), (i, j)
+
+
 def test_stationary_and_single_steps():
     """Stationary values, and steps so small that K < 2^26 in the upper binades (the
     branch-free walk's exact-division fallback)."""
