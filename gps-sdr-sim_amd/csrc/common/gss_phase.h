@@ -319,20 +319,109 @@ GSS_HD int gss_exw(double W)
     return GSS_LDEXP(1.0, e - 1) == W ? e - 1 : e;
 }
 
+/* ---- direction-specialised trips (fewer instructions; the GPU Stage A hot loop) --------------
+ * Same contract as gss_iter_bfx for one chain kind:
+ *   GSS_TRIP_CARR_ASC  carrier, s > 0 (W = 1: the wrap limit is the binade top of [0.5, 1))
+ *   GSS_TRIP_CARR_DESC carrier, s < 0 (wraps below 0 with carr += 1, rounded)
+ *   GSS_TRIP_CODE      code phase, s > 0, W = 1023 inside the binade [512, 1024)
+ * Scale factors come from the exponent field: with E the biased exponent of v (v in
+ * [2^(E-1023), 2^(E-1022)), lattice u = 2^(E-1075)), 1/u and u are built as doubles from E, and
+ * m = v/u = 2^52 + mantissa is v with its exponent field replaced by 1075.  The tie parity of m
+ * is the mantissa's last bit.  Requires v >= 2^-900 for a jump (smaller v: real steps only). */
+#define GSS_TRIP_CARR_ASC  0
+#define GSS_TRIP_CARR_DESC 1
+#define GSS_TRIP_CODE      2
+
+GSS_HD double gss_d_from_hi(uint32_t hi, uint32_t lo)
+{
+    gss_bits64 b;
+    b.u = ((uint64_t)hi << 32) | lo;
+    return b.d;
+}
+
+GSS_HD int gss_trip(int kind, double *pv, double s, double rs, double *pleft, double *pJ,
+                    double *pDs)
+{
+    const double v = *pv;
+    const double left = *pleft;
+    gss_bits64 vb;
+    vb.d = v;
+    const uint32_t hi = (uint32_t)(vb.u >> 32), lo = (uint32_t)vb.u;
+    const uint32_t X = hi & 0x7FF00000u;                       /* E << 20 */
+    const double P = gss_d_from_hi(0x83200000u - X, 0u);       /* 2^(1075-E) = 1/u */
+    const double Pi = gss_d_from_hi(X - 0x03400000u, 0u);      /* 2^(E-1075) = u   */
+    const double m = gss_d_from_hi((hi & 0x000FFFFFu) | 0x43300000u, lo);   /* v/u */
+    const double as = kind == GSS_TRIP_CARR_DESC ? -s : s;
+    const double sig = as * P;
+    const double k = GSS_FLOOR(sig);
+    const double K = GSS_RINT(sig);
+    const double frac = sig - k;
+    const int odd_tie = (frac == 0.5) & (int)(lo & 1u);
+    double lim;
+    if (kind == GSS_TRIP_CARR_DESC) {
+        lim = (m - 0x1p52) - (frac > 0.0 ? k + 1.0 : k);       /* stay >= 2^(ex-1) */
+    } else {
+        lim = ((0x1p53 - 1.0) - k) - m;                        /* stay < 2^ex */
+        if (kind == GSS_TRIP_CARR_ASC) {
+            /* top binade [0.5,1): a result rounding up to 1.0 would wrap: (j+1)K < 2^53 - m */
+            lim = X == (1022u << 20) ? lim - (K - k) : lim;
+        } else {
+            const double l2 = ((GSS_CA_SEQ_LEN_D - v) * P - 1.0) - K;    /* v + (j+1)Ku < 1023 */
+            lim = ((X >= (1032u << 20)) & (l2 < lim)) ? l2 : lim;
+        }
+    }
+    const int live = (v >= 0x1p-900) & (sig < 0x1p52) & !odd_tie & (lim >= 0.0);
+    double J;
+    if (K >= 0x1p26) {
+        const double q0 = GSS_FLOOR(lim * (rs * Pi));          /* lim*u/|s| */
+        const double r0 = GSS_FMA(-q0, K, lim);
+        J = (q0 + 1.0) + ((r0 >= K ? 1.0 : 0.0) + (r0 < 0.0 ? -1.0 : 0.0));
+        J = live ? (J < left ? J : left) : 0.0;
+    } else if (K == 0.0) {                                      /* stationary */
+        J = ((v >= 0x1p-900) & (sig < 0x1p52) & !odd_tie) ? left : 0.0;
+    } else {                                                    /* tiny steps: exact division */
+        double q = GSS_FLOOR(lim / K);
+        q = GSS_FMA(-q, K, lim) < 0.0 ? q - 1.0 : q;
+        J = live ? (q + 1.0 < left ? q + 1.0 : left) : 0.0;
+    }
+    const double Ds = kind == GSS_TRIP_CARR_DESC ? -(K * Pi) : K * Pi;   /* one step's move */
+    const double v1 = GSS_FMA(J, Ds, v);
+    const double left1 = left - J;
+    const double r = v1 + s;                                    /* the real step */
+    double r2;
+    int wr;
+    if (kind == GSS_TRIP_CARR_DESC) {
+        wr = r < 0.0;
+        r2 = r + (wr ? 1.0 : 0.0);                              /* carr += 1.0 (rounded) */
+    } else {
+        const double W = kind == GSS_TRIP_CODE ? GSS_CA_SEQ_LEN_D : 1.0;
+        wr = r >= W;
+        r2 = r - (wr ? W : 0.0);                                /* exact */
+    }
+    const int step = left1 > 0.0;
+    *pv = step ? r2 : v1;
+    *pleft = step ? left1 - 1.0 : 0.0;
+    *pJ = J;
+    *pDs = Ds;
+    return step & wr;
+}
+
 /* Exact states at every segment start n0 = j*seg_r (j < nseg) of one chain, walking n_per_blk
  * steps from v (Stage A of the GPU path; out_x[j] = phase at n0, out_c[j] = code counters
- * icode|ibit<<8|iword<<16 at n0 when code != 0).  A trip covers positions (pb, pa]: a lattice
+ * icode|ibit<<8|iword<<16 at n0 for the code chain).  A trip covers positions (pb, pa]: a lattice
  * jump of J steps from vb (state at pb + i is vb + i*Ds, exact) and one real step to pa.  At most
  * one segment start usually falls in a trip; more (long jumps at tiny Dopplers) take a loop.
+ * kind: GSS_TRIP_* (the carrier kind must match the sign of st; st == 0 means no motion).
  * Returns the final value if want_end (else the walk stops after the last segment). */
-GSS_HD double gss_seg_states(double v, double st, double W, int exW, int code, uint32_t cnt,
-                             int n_per_blk, int nseg, int seg_r, int want_end, double *out_x,
-                             uint32_t *out_c)
+GSS_HD double gss_seg_states(int kind, double v, double st, uint32_t cnt, int n_per_blk,
+                             int nseg, int seg_r, int want_end, double *out_x, uint32_t *out_c)
 {
-    const double as = st < 0.0 ? -st : st, rs = 1.0 / as;
-    const double total = (double)n_per_blk;
+    const int code = kind == GSS_TRIP_CODE;
+    const double rs = 1.0 / (st < 0.0 ? -st : st);
+    const double total = (double)n_per_blk, R = (double)seg_r;
     double left = st == 0.0 ? 0.0 : total;             /* no motion: no wraps */
     int seg = 1;
+    double n0 = R;                                      /* next segment start */
     out_x[0] = v;                                       /* n0 = 0: the block start */
     if (code)
         out_c[0] = cnt;
@@ -345,7 +434,7 @@ GSS_HD double gss_seg_states(double v, double st, double W, int exW, int code, u
     while (left > 0.0 && (seg < nseg || want_end)) {
         const double vb = v, pb = total - left;
         double J, Ds;
-        const int wr = gss_iter_bfx(&v, st, as, rs, W, exW, &left, &J, &Ds);
+        const int wr = gss_trip(kind, &v, st, rs, &left, &J, &Ds);
         const double pa = total - left;
         const uint32_t cnt_b = cnt;
         if (code & wr) {                                /* gpssim.c:2216-2236 */
@@ -358,20 +447,19 @@ GSS_HD double gss_seg_states(double v, double st, double W, int exW, int code, u
             iword += nw;
             cnt = icode | (ibit << 8) | (iword << 16);
         }
-        if (seg + 1 < nseg && (double)((seg + 1) * seg_r) <= pa) {   /* rare: 2+ starts */
-            for (; seg + 1 < nseg && (double)((seg + 1) * seg_r) <= pa; seg++) {
-                const double n0 = (double)(seg * seg_r);
+        if (seg + 1 < nseg && n0 + R <= pa) {           /* rare: two or more starts */
+            for (; seg + 1 < nseg && n0 + R <= pa; seg++, n0 += R) {
                 out_x[seg] = n0 <= pb + J ? GSS_FMA(n0 - pb, Ds, vb) : v;
                 if (code)
                     out_c[seg] = n0 == pa ? cnt : cnt_b;
             }
         }
-        const double n0 = (double)(seg * seg_r);
         if (seg < nseg && n0 <= pa) {
             out_x[seg] = n0 <= pb + J ? GSS_FMA(n0 - pb, Ds, vb) : v;
             if (code)
                 out_c[seg] = n0 == pa ? cnt : cnt_b;
             seg++;
+            n0 += R;
         }
     }
     return v;

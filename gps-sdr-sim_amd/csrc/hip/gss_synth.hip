@@ -6,11 +6,11 @@
  * serial IEEE double recurrences (built with -ffp-contract=off); the only shortcuts are provably
  * exact lattice translations (common/gss_phase.h).
  *
- * Stage A  gss_anchor_kernel    one lane per (block, channel, chain), one chain kind per wave,
- *                               walking the block with the branch-free f64 lattice walk
- *                               (gss_iter_bf) and recording for every R-sample segment the last
- *                               wrap at or before its first sample: an exact "anchor" state
- *                               (sample index, phase[, counters]).
+ * Stage A  gss_anchor_kernel    one lane per (block, channel, chain); waves are channel-major
+ *                               (64 consecutive blocks, one chain kind), walking the block with
+ *                               direction-specialised branch-free f64 lattice trips (gss_trip)
+ *                               and recording the exact phase (and code counters) at every
+ *                               R-sample segment start (gss_seg_states).
  * Stage B  gss_synth_kernel     one lane per R-sample segment of a block, all channels.  Each lane
  *                               first walks every channel from its anchor to the segment start
  *                               (≤ one cycle, no wrap), then runs the per-sample recurrences:
@@ -41,21 +41,24 @@ struct lut_arg { int16_t sin512[512]; int16_t cos512[512]; };
 /* ======================================================================================== */
 /* Stage A: anchors                                                                         */
 /* ======================================================================================== */
-/* Stage A walks one chain per lane; even workgroups take the carrier chains of 64 consecutive
-   (block, channel) pairs, odd ones their code chains, so every wave runs one specialised code
-   path.  (Measured on MI355X, tools/ubench/anchor_ubench.hip: one chain per lane beats two
-   interleaved chains per lane, 1.43 vs 2.33 ms, because the trip is issue-heavy; staging the
-   outputs in LDS does not pay over direct stores.)  The walk itself is gss_seg_states: the exact
-   state at every segment start, interpolated on the lattice jump that crosses it. */
+/* Stage A walks one chain per lane.  Waves are channel-major: a wave holds one chain kind of one
+   channel slot for 64 consecutive blocks, so the carrier's Doppler sign, and with it the
+   specialised trip (gss_trip: ascending / descending carrier, code), is wave-uniform except
+   across a zero crossing.  The trip is issue-bound (~9-cycle dependent f64 latency but ~50-100
+   VALU per trip, measured in tools/ubench/), so one chain per lane beats interleaving two.  The
+   walk is gss_seg_states: the exact state at every segment start, interpolated on the lattice
+   jump that crosses it. */
 __global__ __launch_bounds__(ANCHOR_THREADS) void gss_anchor_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch, int nblk, int nchp,
     int n_per_blk, int nseg, int nsegp, int seg_r, double *__restrict__ seg_carr,
     double *__restrict__ seg_code, uint32_t *__restrict__ seg_cnt, double *__restrict__ carr_end)
 {
     const bool code = blockIdx.x & 1;                      /* wave-uniform */
-    const int pair = (blockIdx.x >> 1) * ANCHOR_THREADS + threadIdx.x;
-    const int b = pair / nchp, k = pair - b * nchp;
-    if (b >= nblk)
+    const int nbw = (nblk + ANCHOR_THREADS - 1) / ANCHOR_THREADS;
+    const int wv = blockIdx.x >> 1;
+    const int k = wv / nbw;
+    const int b = (wv - k * nbw) * ANCHOR_THREADS + threadIdx.x;
+    if (k >= nchp || b >= nblk)
         return;
     const size_t bk = (size_t)b * GSS_MAXCH + k;
     const size_t row = bk * (size_t)nsegp;
@@ -69,15 +72,28 @@ __global__ __launch_bounds__(ANCHOR_THREADS) void gss_anchor_kernel(
     if (code) {
         const uint32_t cnt = (uint32_t)p.icode | ((uint32_t)p.ibit << 8) |
                              ((uint32_t)p.iword << 16);
-        gss_seg_states(p.code0, p.code_step, GSS_CA_SEQ_LEN_D, 10, 1, cnt, n_per_blk, nseg, seg_r,
-                       0, seg_code + row, seg_cnt + row);
-    } else {
-        const bool want_end = carr_end != nullptr && real;
-        const double e = gss_seg_states(p.carr0, p.carr_step, 1.0, 0, 0, 0u, n_per_blk, nseg,
-                                        seg_r, want_end, seg_carr + row, nullptr);
-        if (want_end)
-            carr_end[bk] = e;
+        gss_seg_states(GSS_TRIP_CODE, p.code0, p.code_step, cnt, n_per_blk, nseg, seg_r, 0,
+                       seg_code + row, seg_cnt + row);
+        return;
     }
+    const bool want_end = carr_end != nullptr && real;
+    const bool desc = p.carr_step < 0.0;
+    const uint64_t nd = __builtin_amdgcn_ballot_w64(desc);
+    double e;
+    if (nd == 0)                                           /* the usual case: uniform sign */
+        e = gss_seg_states(GSS_TRIP_CARR_ASC, p.carr0, p.carr_step, 0u, n_per_blk, nseg, seg_r,
+                           want_end, seg_carr + row, nullptr);
+    else if (nd == __builtin_amdgcn_ballot_w64(true))
+        e = gss_seg_states(GSS_TRIP_CARR_DESC, p.carr0, p.carr_step, 0u, n_per_blk, nseg, seg_r,
+                           want_end, seg_carr + row, nullptr);
+    else if (desc)                                         /* mixed wave: both paths, in turn */
+        e = gss_seg_states(GSS_TRIP_CARR_DESC, p.carr0, p.carr_step, 0u, n_per_blk, nseg, seg_r,
+                           want_end, seg_carr + row, nullptr);
+    else
+        e = gss_seg_states(GSS_TRIP_CARR_ASC, p.carr0, p.carr_step, 0u, n_per_blk, nseg, seg_r,
+                           want_end, seg_carr + row, nullptr);
+    if (want_end)
+        carr_end[bk] = e;
 }
 
 /* ======================================================================================== */
@@ -502,8 +518,8 @@ extern "C" int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int
 
     hipEvent_t *ev = d->ev[d->n_ev % gss_dev::RING];
     d->n_ev++;
-    /* Stage A grid: pairs (block, channel < nchp) in waves of 64, each wave twice (chains) */
-    int a_blocks = 2 * ((nblk * nchp + ANCHOR_THREADS - 1) / ANCHOR_THREADS);
+    /* Stage A grid: channel-major waves of 64 consecutive blocks, each twice (chain kinds) */
+    int a_blocks = 2 * nchp * ((nblk + ANCHOR_THREADS - 1) / ANCHOR_THREADS);
     HIP_TRY(hipEventRecord(ev[0], st));
     hipLaunchKernelGGL(gss_anchor_kernel, dim3(a_blocks), dim3(ANCHOR_THREADS), 0, st, blk, nch,
                        nblk, nchp, n_per_blk, nseg, nsegp, R, d->seg_carr, d->seg_code, d->seg_cnt,

@@ -80,6 +80,8 @@ def walk_lib():
         L.wc_code_f.argtypes = [D, D, I64, P, P, P]
         L.wc_carr_seg_starts_f.restype = C.c_int
         L.wc_carr_seg_starts_f.argtypes = [D, D, I64, C.c_int, C.c_int, C.c_void_p]
+        L.wc_carr_trip.restype = D
+        L.wc_carr_trip.argtypes = [D, D, I64]
         L.wc_seg_states.restype = D
         L.wc_seg_states.argtypes = [D, D, C.c_int, C.c_uint32, C.c_int, C.c_int, C.c_int,
                                     C.c_int, C.c_void_p, C.c_void_p]

@@ -120,6 +120,18 @@ double wc_code_bf(double c, double s, int64_t n, int32_t *ic, int32_t *ib, int32
 double wc_seg_states(double v, double s, int code, uint32_t cnt, int n, int seg_r, int nseg,
                      int want_end, double *out_x, uint32_t *out_c)
 {
-    double W = code ? GSS_CA_SEQ_LEN_D : 1.0;
-    return gss_seg_states(v, s, W, gss_exw(W), code, cnt, n, nseg, seg_r, want_end, out_x, out_c);
+    int kind = code ? GSS_TRIP_CODE : (s < 0.0 ? GSS_TRIP_CARR_DESC : GSS_TRIP_CARR_ASC);
+    return gss_seg_states(kind, v, s, cnt, n, nseg, seg_r, want_end, out_x, out_c);
+}
+
+/* carrier walk by specialised trips (both directions) */
+double wc_carr_trip(double x, double s, int64_t n)
+{
+    int kind = s < 0.0 ? GSS_TRIP_CARR_DESC : GSS_TRIP_CARR_ASC;
+    double left = (double)n, rs = 1.0 / (s < 0.0 ? -s : s), J, Ds;
+    if (s == 0.0)
+        return x;
+    while (left > 0.0)
+        gss_trip(kind, &x, s, rs, &left, &J, &Ds);
+    return x;
 }

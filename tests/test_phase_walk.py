@@ -50,6 +50,7 @@ def test_carrier_walks_exact(seed):
         nw = C.c_int32(0)
         assert W.wc_carr_f(x, s, n, C.byref(nw)) == want, ("f64", x, s, n)
         assert W.wc_carr_bf(x, s, n, C.byref(nw)) == want, ("branch-free", x, s, n)
+        assert W.wc_carr_trip(x, s, n) == want, ("specialised trip", x, s, n)
         assert G.carr_advance(x, s, n) == want
 
 
@@ -178,3 +179,4 @@ def test_stationary_and_single_steps():
             nw = C.c_int32(0)
             assert W.wc_carr_f(x, s, n, C.byref(nw)) == want
             assert W.wc_carr_bf(x, s, n, C.byref(nw)) == want
+            assert W.wc_carr_trip(x, s, n) == want
