@@ -79,6 +79,8 @@ def main():
     ap.add_argument("--window", type=float, default=WINDOW_S, help="seconds per GPU")
     ap.add_argument("--fmt", type=int, default=16, choices=[1, 8, 16])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ck", action="store_true",
+                    help="do not pass the planner's carrier checkpoints (GPU walks whole blocks)")
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 8))
     args = ap.parse_args()
 
@@ -105,8 +107,8 @@ def main():
     # ---- host control plane for this rank's window (untimed setup) ----
     from gpssim_amd.shard import plan_rank
     t_plan0 = time.perf_counter()
-    blk, nch, nav, npb = plan_rank(NAV, rank, world, args.window, llh=LOC, samp_freq=FS,
-                                   data_format=args.fmt, threads=args.threads)
+    blk, nch, ck, nav, npb = plan_rank(NAV, rank, world, args.window, llh=LOC, samp_freq=FS,
+                                       data_format=args.fmt, threads=args.threads)
     host_plan_s = time.perf_counter() - t_plan0
     nblk = len(nch)
 
@@ -115,6 +117,7 @@ def main():
     ca = G.ca_table()
     d_blk = torch.from_numpy(blk.view(np.uint8).reshape(-1)).to(dev_t)
     d_nch = torch.from_numpy(nch).to(dev_t)
+    d_ck = torch.from_numpy(ck).to(dev_t)        # planner carrier checkpoints (host-computed)
     d_ca = torch.from_numpy(ca.view(np.int32)).to(dev_t)
     d_nav = torch.from_numpy(nav.view(np.int32)).to(dev_t)
     bb = G.block_bytes(npb, args.fmt)
@@ -126,7 +129,7 @@ def main():
     def step():
         dev.synth_device(d_blk.data_ptr(), d_nch.data_ptr(), nch_max, d_ca.data_ptr(), len(ca),
                          d_nav.data_ptr(), len(nav), nblk, npb, args.fmt, out.data_ptr(),
-                         0, 0, stream)
+                         0, 0, stream, ck_ptr=0 if args.no_ck else d_ck.data_ptr())
 
     for _ in range(args.warmup):
         step()
@@ -172,6 +175,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic: deterministic static-receiver scenario (brdc3540.14n), no dataset",
         "config": {"workload": workload, "samples_per_gpu": samples_rank,
+                   "carrier_checkpoints": 0 if args.no_ck else 8,
                    "channels_max": nch_max, "parallelism": f"time-window shards x{world}"},
         "x_realtime": round(value / (FS / 1e6), 1),
         "stages_ms": {"checkpoint": round(ck_ms, 3), "synthesis": round(syn_ms, 3),

@@ -50,14 +50,15 @@ int main(int argc, char **argv)
     gss_chan_blk_t *blk = malloc(sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)batch);
     int32_t *nch = malloc(sizeof(int32_t) * (size_t)batch);
     unsigned char *out = malloc(bb * (size_t)batch);
-    if (!blk || !nch || !out) {
+    double *ck = malloc(sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)batch);
+    if (!blk || !nch || !out || !ck) {
         fprintf(stderr, "ERROR: Failed to allocate I/Q buffer.\n");
         return 1;
     }
     clock_t t0 = clock();
     for (;;) {
         int nb = 0;
-        if (gss_scn_next(scn, batch, blk, nch, &nb, threads)) {
+        if (gss_scn_next(scn, batch, blk, nch, ck, &nb, threads)) {
             fprintf(stderr, "\nERROR: %s\n", gss_last_error());
             return 1;
         }
@@ -66,7 +67,7 @@ int main(int argc, char **argv)
         const uint32_t *nav;
         int nnav;
         gss_scn_nav_table(scn, &nav, &nnav);
-        if (gss_synth_host(dev, blk, nch, ca, 32, nav, nnav, nb, info.n_per_blk,
+        if (gss_synth_host(dev, blk, nch, ck, ca, 32, nav, nnav, nb, info.n_per_blk,
                            info.data_format, out, NULL)) {
             fprintf(stderr, "\nERROR: %s\n", gss_last_error());
             return 1;
@@ -83,6 +84,6 @@ int main(int argc, char **argv)
     fprintf(stderr, "Process time = %.1f [sec]\n", (double)(t1 - t0) / CLOCKS_PER_SEC);
     gss_dev_close(dev);
     gss_scn_close(scn);
-    free(blk); free(nch); free(out);
+    free(blk); free(nch); free(out); free(ck);
     return 0;
 }

@@ -406,32 +406,40 @@ GSS_HD int gss_trip(int kind, double *pv, double s, double rs, double *pleft, do
     return step & wr;
 }
 
-/* Exact states at every segment start n0 = j*seg_r (j < nseg) of one chain, walking n_per_blk
- * steps from v (Stage A of the GPU path; out_x[j] = phase at n0, out_c[j] = code counters
- * icode|ibit<<8|iword<<16 at n0 for the code chain).  A trip covers positions (pb, pa]: a lattice
- * jump of J steps from vb (state at pb + i is vb + i*Ds, exact) and one real step to pa.  At most
- * one segment start usually falls in a trip; more (long jumps at tiny Dopplers) take a loop.
- * kind: GSS_TRIP_* (the carrier kind must match the sign of st; st == 0 means no motion).
- * Returns the final value if want_end (else the walk stops after the last segment). */
-GSS_HD double gss_seg_states(int kind, double v, double st, uint32_t cnt, int n_per_blk,
+/* Exact states at the segment starts n0 = j*seg_r in [pos0, pos1) of one chain (j < nseg),
+ * walking from v at position pos0 (Stage A of the GPU path: out_x[j] = phase at n0, out_c[j] =
+ * code counters icode|ibit<<8|iword<<16 at n0 for the code chain; arrays indexed by the absolute
+ * segment j).  A trip covers positions (pb, pa]: a lattice jump of J steps from vb (state at
+ * pb + i is vb + i*Ds, exact) and one real step to pa.  At most one segment start usually falls
+ * in a trip; more (long jumps at tiny Dopplers) take a loop.  kind: GSS_TRIP_* (the carrier kind
+ * must match the sign of st; st == 0 means no motion).  Returns the value at pos1 if want_end,
+ * else the value where the walk stopped (after the last segment start in range). */
+GSS_HD double gss_seg_states(int kind, double v, double st, uint32_t cnt, int pos0, int pos1,
                              int nseg, int seg_r, int want_end, double *out_x, uint32_t *out_c)
 {
     const int code = kind == GSS_TRIP_CODE;
     const double rs = 1.0 / (st < 0.0 ? -st : st);
-    const double total = (double)n_per_blk, R = (double)seg_r;
+    const double p0 = (double)pos0, total = (double)(pos1 - pos0), R = (double)seg_r;
+    int seg = (pos0 + seg_r - 1) / seg_r;               /* first segment start >= pos0 */
+    int seg_hi = (pos1 + seg_r - 1) / seg_r;            /* segment starts < pos1 */
+    if (seg_hi > nseg)
+        seg_hi = nseg;
     double left = st == 0.0 ? 0.0 : total;             /* no motion: no wraps */
-    int seg = 1;
-    double n0 = R;                                      /* next segment start */
-    out_x[0] = v;                                       /* n0 = 0: the block start */
-    if (code)
-        out_c[0] = cnt;
+    double n0 = (double)seg * R - p0;                   /* next segment start, relative */
+    if (seg < seg_hi && n0 == 0.0) {                    /* a segment starts at pos0 */
+        out_x[seg] = v;
+        if (code)
+            out_c[seg] = cnt;
+        seg++;
+        n0 += R;
+    }
     if (left == 0.0)
-        for (; seg < nseg; seg++) {
+        for (; seg < seg_hi; seg++) {
             out_x[seg] = v;
             if (code)
                 out_c[seg] = cnt;
         }
-    while (left > 0.0 && (seg < nseg || want_end)) {
+    while (left > 0.0 && (seg < seg_hi || want_end)) {
         const double vb = v, pb = total - left;
         double J, Ds;
         const int wr = gss_trip(kind, &v, st, rs, &left, &J, &Ds);
@@ -447,14 +455,14 @@ GSS_HD double gss_seg_states(int kind, double v, double st, uint32_t cnt, int n_
             iword += nw;
             cnt = icode | (ibit << 8) | (iword << 16);
         }
-        if (seg + 1 < nseg && n0 + R <= pa) {           /* rare: two or more starts */
-            for (; seg + 1 < nseg && n0 + R <= pa; seg++, n0 += R) {
+        if (seg + 1 < seg_hi && n0 + R <= pa) {         /* rare: two or more starts */
+            for (; seg + 1 < seg_hi && n0 + R <= pa; seg++, n0 += R) {
                 out_x[seg] = n0 <= pb + J ? GSS_FMA(n0 - pb, Ds, vb) : v;
                 if (code)
                     out_c[seg] = n0 == pa ? cnt : cnt_b;
             }
         }
-        if (seg < nseg && n0 <= pa) {
+        if (seg < seg_hi && n0 <= pa) {
             out_x[seg] = n0 <= pb + J ? GSS_FMA(n0 - pb, Ds, vb) : v;
             if (code)
                 out_c[seg] = n0 == pa ? cnt : cnt_b;
@@ -886,4 +894,33 @@ GSS_HD void gss_code_walk_cc(gss_code_state *c, double cs, int64_t n)
     }
     *c = it.c;
 }
+/* Carrier checkpoints the host planner records while it walks a block (the walk it must do
+ * anyway to get the next block's carr_phase): ck[j] = exact carrier at sample gss_ck_pos(j, n),
+ * j < GSS_NCK (ck[0] = x).  The GPU then walks each block's carrier as GSS_NCK independent
+ * sub-chains.  Cycle-cached wrap-by-wrap walk; each checkpoint is a plain walk of less than one
+ * cycle from the last wrap before it.  Returns the value at n (the next block's carr0). */
+#ifndef GSS_NCK
+#define GSS_NCK 8                     /* = GSS_NCK in include/gpssim_amd.h */
+#endif
+GSS_HD int gss_ck_pos(int j, int n) { return (int)(((int64_t)j * n) / GSS_NCK); }
+
+GSS_HD double gss_carr_walk_ck(double x, double s, int n, double *ck)
+{
+    gss_carr_it it;
+    gss_carr_it_init(&it, x, s, n);
+    int j = 1;
+    ck[0] = x;
+    int64_t last_pos = 0;
+    double last_x = x;
+    while (gss_carr_next_wrap(&it)) {
+        for (; j < GSS_NCK && gss_ck_pos(j, n) < it.pos; j++)
+            ck[j] = gss_carr_walk(last_x, s, gss_ck_pos(j, n) - last_pos);
+        last_pos = it.pos;
+        last_x = it.x;
+    }
+    for (; j < GSS_NCK; j++)
+        ck[j] = gss_carr_walk(last_x, s, gss_ck_pos(j, n) - last_pos);
+    return it.x;
+}
+
 #endif /* GSS_PHASE_H */

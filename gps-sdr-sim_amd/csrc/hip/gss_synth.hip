@@ -49,15 +49,31 @@ struct lut_arg { int16_t sin512[512]; int16_t cos512[512]; };
    walk is gss_seg_states: the exact state at every segment start, interpolated on the lattice
    jump that crosses it. */
 __global__ __launch_bounds__(ANCHOR_THREADS) void gss_anchor_kernel(
-    const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch, int nblk, int nchp,
-    int n_per_blk, int nseg, int nsegp, int seg_r, double *__restrict__ seg_carr,
-    double *__restrict__ seg_code, uint32_t *__restrict__ seg_cnt, double *__restrict__ carr_end)
+    const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch,
+    const double *__restrict__ carr_ck, int nblk, int nchp, int n_per_blk, int nseg, int nsegp,
+    int seg_r, double *__restrict__ seg_carr, double *__restrict__ seg_code,
+    uint32_t *__restrict__ seg_cnt, double *__restrict__ carr_end)
 {
-    const bool code = blockIdx.x & 1;                      /* wave-uniform */
+    /* wave index space: [longest chains first] code waves nchp x nbw (one lane per block) and
+       carrier waves nchp x nbwc (one lane per block sub-chain: GSS_NCK of them per block when
+       the planner's checkpoints are given, else one) */
+    const int nsub = carr_ck ? GSS_NCK : 1;
     const int nbw = (nblk + ANCHOR_THREADS - 1) / ANCHOR_THREADS;
-    const int wv = blockIdx.x >> 1;
-    const int k = wv / nbw;
-    const int b = (wv - k * nbw) * ANCHOR_THREADS + threadIdx.x;
+    const int nbwc = (nblk * nsub + ANCHOR_THREADS - 1) / ANCHOR_THREADS;
+    int wid = blockIdx.x;
+    bool code;
+    if (carr_ck) {
+        code = wid < nchp * nbw;
+        if (!code) wid -= nchp * nbw;
+    } else {
+        code = wid >= nchp * nbwc;
+        if (code) wid -= nchp * nbwc;
+    }
+    const int per = code ? nbw : nbwc;
+    const int k = wid / per;
+    const int idx = (wid - k * per) * ANCHOR_THREADS + threadIdx.x;
+    const int sub = code ? 1 : nsub;                       /* lanes per block */
+    const int b = idx / sub, j = idx - b * sub;
     if (k >= nchp || b >= nblk)
         return;
     const size_t bk = (size_t)b * GSS_MAXCH + k;
@@ -72,25 +88,28 @@ __global__ __launch_bounds__(ANCHOR_THREADS) void gss_anchor_kernel(
     if (code) {
         const uint32_t cnt = (uint32_t)p.icode | ((uint32_t)p.ibit << 8) |
                              ((uint32_t)p.iword << 16);
-        gss_seg_states(GSS_TRIP_CODE, p.code0, p.code_step, cnt, n_per_blk, nseg, seg_r, 0,
+        gss_seg_states(GSS_TRIP_CODE, p.code0, p.code_step, cnt, 0, n_per_blk, nseg, seg_r, 0,
                        seg_code + row, seg_cnt + row);
         return;
     }
-    const bool want_end = carr_end != nullptr && real;
+    const int pos0 = carr_ck ? gss_ck_pos(j, n_per_blk) : 0;
+    const int pos1 = j + 1 < nsub ? gss_ck_pos(j + 1, n_per_blk) : n_per_blk;
+    const double v0 = carr_ck && real ? carr_ck[bk * GSS_NCK + j] : p.carr0;
+    const bool want_end = carr_end != nullptr && real && j == nsub - 1;
     const bool desc = p.carr_step < 0.0;
     const uint64_t nd = __builtin_amdgcn_ballot_w64(desc);
     double e;
     if (nd == 0)                                           /* the usual case: uniform sign */
-        e = gss_seg_states(GSS_TRIP_CARR_ASC, p.carr0, p.carr_step, 0u, n_per_blk, nseg, seg_r,
+        e = gss_seg_states(GSS_TRIP_CARR_ASC, v0, p.carr_step, 0u, pos0, pos1, nseg, seg_r,
                            want_end, seg_carr + row, nullptr);
     else if (nd == __builtin_amdgcn_ballot_w64(true))
-        e = gss_seg_states(GSS_TRIP_CARR_DESC, p.carr0, p.carr_step, 0u, n_per_blk, nseg, seg_r,
+        e = gss_seg_states(GSS_TRIP_CARR_DESC, v0, p.carr_step, 0u, pos0, pos1, nseg, seg_r,
                            want_end, seg_carr + row, nullptr);
     else if (desc)                                         /* mixed wave: both paths, in turn */
-        e = gss_seg_states(GSS_TRIP_CARR_DESC, p.carr0, p.carr_step, 0u, n_per_blk, nseg, seg_r,
+        e = gss_seg_states(GSS_TRIP_CARR_DESC, v0, p.carr_step, 0u, pos0, pos1, nseg, seg_r,
                            want_end, seg_carr + row, nullptr);
     else
-        e = gss_seg_states(GSS_TRIP_CARR_ASC, p.carr0, p.carr_step, 0u, n_per_blk, nseg, seg_r,
+        e = gss_seg_states(GSS_TRIP_CARR_ASC, v0, p.carr_step, 0u, pos0, pos1, nseg, seg_r,
                            want_end, seg_carr + row, nullptr);
     if (want_end)
         carr_end[bk] = e;
@@ -493,7 +512,8 @@ static synth_fn pick_kernel(int fmt, int nchp)
 }
 
 extern "C" int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
-                                int nch_max, const uint32_t *ca_bits, int n_ca,
+                                int nch_max, const double *carr_ck, const uint32_t *ca_bits,
+                                int n_ca,
                                 const uint32_t *nav, int n_nav, int nblk, int n_per_blk, int fmt,
                                 void *out, double *carr_end, int32_t *status, void *stream)
 {
@@ -518,11 +538,13 @@ extern "C" int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int
 
     hipEvent_t *ev = d->ev[d->n_ev % gss_dev::RING];
     d->n_ev++;
-    /* Stage A grid: channel-major waves of 64 consecutive blocks, each twice (chain kinds) */
-    int a_blocks = 2 * nchp * ((nblk + ANCHOR_THREADS - 1) / ANCHOR_THREADS);
+    /* Stage A grid: channel-major waves; code chains one lane per block, carrier chains one lane
+       per block sub-chain (GSS_NCK per block with the planner's checkpoints) */
+    int a_blocks = nchp * ((nblk + ANCHOR_THREADS - 1) / ANCHOR_THREADS) +
+                   nchp * ((nblk * (carr_ck ? GSS_NCK : 1) + ANCHOR_THREADS - 1) / ANCHOR_THREADS);
     HIP_TRY(hipEventRecord(ev[0], st));
     hipLaunchKernelGGL(gss_anchor_kernel, dim3(a_blocks), dim3(ANCHOR_THREADS), 0, st, blk, nch,
-                       nblk, nchp, n_per_blk, nseg, nsegp, R, d->seg_carr, d->seg_code, d->seg_cnt,
+                       carr_ck, nblk, nchp, n_per_blk, nseg, nsegp, R, d->seg_carr, d->seg_code, d->seg_cnt,
                        carr_end);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], st));
@@ -575,7 +597,7 @@ template <class T> static int grow(T **p, size_t *cap, size_t need)
 }
 
 extern "C" int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
-                              const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
+                              const double *carr_ck, const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
                               int nblk, int n_per_blk, int fmt, void *out, double *carr_end)
 {
     if (!d || !blk || !nch || !ca_bits || !out || nblk <= 0 || n_ca <= 0)
@@ -600,14 +622,22 @@ extern "C" int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32
                 !(p->code_step > 0.0 && p->code_step < 1023.0) ||
                 !(p->carr_step > -1.0 && p->carr_step < 1.0))
                 return gss_fail(GSS_E_ARG, "block %d channel %d: parameter out of range", b, k);
+            if (carr_ck)
+                for (int j = 0; j < GSS_NCK; j++) {
+                    double c = carr_ck[((size_t)b * GSS_MAXCH + k) * GSS_NCK + j];
+                    if (!(c >= 0.0 && c <= 1.0))
+                        return gss_fail(GSS_E_ARG, "block %d channel %d: checkpoint %d out of "
+                                        "range", b, k, j);
+                }
         }
     }
     size_t sz_blk = sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)nblk;
     size_t sz_nch = sizeof(int32_t) * (size_t)nblk;
     size_t sz_ca = sizeof(uint32_t) * GSS_CA_WORDS * (size_t)n_ca;
     size_t sz_nav = sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)(n_nav > 0 ? n_nav : 1);
+    size_t sz_ck = carr_ck ? sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)nblk : 0;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    size_t tot = al(sz_blk) + al(sz_nch) + al(sz_ca) + al(sz_nav);
+    size_t tot = al(sz_blk) + al(sz_nch) + al(sz_ca) + al(sz_nav) + al(sz_ck);
     int rc = grow((uint8_t **)&d->h_in, &d->h_in_cap, tot);
     if (rc) return rc;
     uint8_t *base = (uint8_t *)d->h_in;
@@ -615,6 +645,10 @@ extern "C" int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32
     int32_t *d_nch = (int32_t *)(base + al(sz_blk));
     uint32_t *d_ca = (uint32_t *)(base + al(sz_blk) + al(sz_nch));
     uint32_t *d_nav = (uint32_t *)(base + al(sz_blk) + al(sz_nch) + al(sz_ca));
+    double *d_ck = carr_ck ? (double *)(base + al(sz_blk) + al(sz_nch) + al(sz_ca) + al(sz_nav))
+                           : nullptr;
+    if (carr_ck)
+        HIP_TRY(hipMemcpy(d_ck, carr_ck, sz_ck, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(d_blk, blk, sz_blk, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(d_nch, nch, sz_nch, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(d_ca, ca_bits, sz_ca, hipMemcpyHostToDevice));
@@ -631,7 +665,8 @@ extern "C" int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32
         d_cend = d->d_cend;
     }
     HIP_TRY(hipMemset(d->d_status, 0, sizeof(int32_t)));
-    rc = gss_synth_device(d, d_blk, d_nch, maxc, d_ca, n_ca, d_nav, n_nav, nblk, n_per_blk, fmt,
+    rc = gss_synth_device(d, d_blk, d_nch, maxc, d_ck, d_ca, n_ca, d_nav, n_nav, nblk, n_per_blk,
+                          fmt,
                           d->d_out, d_cend, d->d_status, nullptr);
     if (rc) return rc;
     HIP_TRY(hipDeviceSynchronize());

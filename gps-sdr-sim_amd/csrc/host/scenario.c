@@ -369,6 +369,7 @@ typedef struct {
     gss_scn *s;
     gss_chan_blk_t *blk;
     const int32_t *nch;
+    double *ck;
     int nblk, slot_lo, slot_hi;
 } plan_job;
 
@@ -386,7 +387,11 @@ static void *plan_slots(void *arg)
                 if (s->b_reset[e])
                     x = s->b_init[e];
                 j->blk[e].carr0 = x;
-                x = gss_carr_walk_cc(x, j->blk[e].carr_step, s->n_per_blk);
+                if (j->ck)      /* same walk, recording the sub-block checkpoints on the way */
+                    x = gss_carr_walk_ck(x, j->blk[e].carr_step, s->n_per_blk,
+                                         j->ck + e * GSS_NCK);
+                else
+                    x = gss_carr_walk_cc(x, j->blk[e].carr_step, s->n_per_blk);
                 break;
             }
         }
@@ -395,7 +400,8 @@ static void *plan_slots(void *arg)
     return NULL;
 }
 
-static void plan_batch(gss_scn *s, gss_chan_blk_t *blk, const int32_t *nch, int nblk, int threads)
+static void plan_batch(gss_scn *s, gss_chan_blk_t *blk, const int32_t *nch, double *ck, int nblk,
+                       int threads)
 {
     if (threads < 1)
         threads = 1;
@@ -406,7 +412,7 @@ static void plan_batch(gss_scn *s, gss_chan_blk_t *blk, const int32_t *nch, int 
     int per = (K_MAX_CHAN + threads - 1) / threads;
     int started = 0;
     for (int t = 0; t < threads; t++) {
-        job[t] = (plan_job){s, blk, nch, nblk, t * per, (t + 1) * per};
+        job[t] = (plan_job){s, blk, nch, ck, nblk, t * per, (t + 1) * per};
         if (job[t].slot_hi > K_MAX_CHAN)
             job[t].slot_hi = K_MAX_CHAN;
         if (job[t].slot_lo >= job[t].slot_hi)
@@ -422,8 +428,8 @@ static void plan_batch(gss_scn *s, gss_chan_blk_t *blk, const int32_t *nch, int 
             pthread_join(tid[t], NULL);
 }
 
-int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, int *n_out,
-                 int threads)
+int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, double *carr_ck,
+                 int *n_out, int threads)
 {
     *n_out = 0;
     if (s == NULL || blk == NULL || nch == NULL || max_blocks <= 0)
@@ -496,6 +502,9 @@ int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, 
         }
         for (int r = k; r < GSS_MAXCH; r++)
             memset(&row[r], 0, sizeof row[r]);
+        if (carr_ck)             /* padding rows: defined (zero) checkpoints */
+            memset(carr_ck + ((size_t)nb * GSS_MAXCH + k) * GSS_NCK, 0,
+                   sizeof(double) * GSS_NCK * (GSS_MAXCH - k));
         nch[nb] = k;
         nb++;
 
@@ -539,7 +548,7 @@ int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, 
         s->iumd++;
     }
 
-    plan_batch(s, blk, nch, nb, threads);
+    plan_batch(s, blk, nch, carr_ck, nb, threads);
     s->plan_sec += wall_now() - t_start;
     *n_out = nb;
     return 0;

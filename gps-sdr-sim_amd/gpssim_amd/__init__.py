@@ -19,6 +19,7 @@ CLI_PATH = os.path.join(PKG_DIR, "bin", "gps-sdr-sim")
 MAXCH = 16
 CA_WORDS = 32
 NAV_WORDS = 60
+NCK = 8                       # GSS_NCK: carrier checkpoints per block (gss_scn_next)
 FMT_SC01, FMT_SC08, FMT_SC16 = 1, 8, 16
 
 # gss_chan_blk_t (56 bytes), gpssim_amd.h
@@ -62,15 +63,15 @@ _SIGS = {
     "gss_dev_close": (C.c_int, [_P]),
     "gss_dev_reserve": (C.c_int, [_P, C.c_int, C.c_int]),
     "gss_block_bytes": (C.c_size_t, [C.c_int, C.c_int]),
-    "gss_synth_device": (C.c_int, [_P, _P, _P, C.c_int, _P, C.c_int, _P, C.c_int, C.c_int,
-                                   C.c_int, C.c_int, _P, _P, _P, _P]),
-    "gss_synth_host": (C.c_int, [_P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int,
+    "gss_synth_device": (C.c_int, [_P, _P, _P, C.c_int, _P, _P, C.c_int, _P, C.c_int,
+                                   C.c_int, C.c_int, C.c_int, _P, _P, _P, _P]),
+    "gss_synth_host": (C.c_int, [_P, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int,
                                  C.c_int, _P, _P]),
     "gss_dev_timing": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_float),
                                  C.POINTER(C.c_float)]),
     "gss_scn_open": (C.c_int, [C.POINTER(_P), C.POINTER(_Opts)]),
     "gss_scn_info": (C.c_int, [_P, C.POINTER(_Info)]),
-    "gss_scn_next": (C.c_int, [_P, C.c_int, _P, _P, C.POINTER(C.c_int), C.c_int]),
+    "gss_scn_next": (C.c_int, [_P, C.c_int, _P, _P, _P, C.POINTER(C.c_int), C.c_int]),
     "gss_scn_nav_table": (C.c_int, [_P, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_int)]),
     "gss_ca_table": (C.c_int, [_P]),
     "gss_scn_plan_seconds": (C.c_double, [_P]),
@@ -180,26 +181,31 @@ class Scenario:
         self._keep.append(b)
         return b
 
-    def next(self, max_blocks, threads=8):
-        """Next batch: (blk[nb, 16] CHAN_DTYPE, nch[nb] int32)."""
+    def next(self, max_blocks, threads=8, with_ck=False):
+        """Next batch: (blk[nb, 16] CHAN_DTYPE, nch[nb] int32), plus the carrier checkpoints
+        ck[nb, 16, NCK] float64 when with_ck (recorded by the planner's own carrier walk)."""
         blk = np.zeros((max_blocks, MAXCH), CHAN_DTYPE)
         nch = np.zeros(max_blocks, np.int32)
+        ck = np.zeros((max_blocks, MAXCH, NCK), np.float64) if with_ck else None
         nb = C.c_int(0)
-        _check(lib().gss_scn_next(self._h, max_blocks, _ptr(blk), _ptr(nch), C.byref(nb),
-                                  threads))
-        return blk[: nb.value].copy(), nch[: nb.value].copy()
+        _check(lib().gss_scn_next(self._h, max_blocks, _ptr(blk), _ptr(nch), _ptr(ck),
+                                  C.byref(nb), threads))
+        n = nb.value
+        if with_ck:
+            return blk[:n].copy(), nch[:n].copy(), ck[:n].copy()
+        return blk[:n].copy(), nch[:n].copy()
 
-    def all_blocks(self, batch=500, threads=8):
-        bs, ns = [], []
+    def all_blocks(self, batch=500, threads=8, with_ck=False):
+        parts = []
         while True:
-            b, n = self.next(batch, threads)
-            if len(n) == 0:
+            r = self.next(batch, threads, with_ck)
+            if len(r[1]) == 0:
                 break
-            bs.append(b)
-            ns.append(n)
-        if not ns:
-            return np.zeros((0, MAXCH), CHAN_DTYPE), np.zeros(0, np.int32)
-        return np.concatenate(bs), np.concatenate(ns)
+            parts.append(r)
+        if not parts:
+            empty = (np.zeros((0, MAXCH), CHAN_DTYPE), np.zeros(0, np.int32))
+            return empty + ((np.zeros((0, MAXCH, NCK)),) if with_ck else ())
+        return tuple(np.concatenate([p[i] for p in parts]) for i in range(len(parts[0])))
 
     def nav_table(self):
         rows = C.POINTER(C.c_uint32)()
@@ -235,22 +241,27 @@ class Device:
     def reserve(self, max_blocks, n_per_blk):
         _check(lib().gss_dev_reserve(self._h, max_blocks, n_per_blk))
 
-    def synth_host(self, blk, nch, ca, nav, n_per_blk, fmt, want_carr_end=False):
+    def synth_host(self, blk, nch, ca, nav, n_per_blk, fmt, want_carr_end=False, ck=None):
+        """ck: optional carrier checkpoints [nblk, 16, NCK] (Scenario.next(with_ck=True))."""
         blk = np.ascontiguousarray(blk, CHAN_DTYPE)
+        if ck is not None:
+            ck = np.ascontiguousarray(ck, np.float64)
+            assert ck.shape == (len(nch), MAXCH, NCK), ck.shape
         nch = np.ascontiguousarray(nch, np.int32)
         ca = np.ascontiguousarray(ca, np.uint32)
         nav = np.ascontiguousarray(nav, np.uint32)
         nblk = len(nch)
         out = np.empty(nblk * block_bytes(n_per_blk, fmt), np.uint8)
         cend = np.zeros((nblk, MAXCH), np.float64) if want_carr_end else None
-        _check(lib().gss_synth_host(self._h, _ptr(blk), _ptr(nch), _ptr(ca), len(ca),
+        _check(lib().gss_synth_host(self._h, _ptr(blk), _ptr(nch), _ptr(ck), _ptr(ca), len(ca),
                                     _ptr(nav), len(nav), nblk, n_per_blk, fmt, _ptr(out),
                                     _ptr(cend)))
         return (out, cend) if want_carr_end else out
 
     def synth_device(self, blk_ptr, nch_ptr, nch_max, ca_ptr, n_ca, nav_ptr, n_nav, nblk,
-                     n_per_blk, fmt, out_ptr, carr_end_ptr=0, status_ptr=0, stream=0):
-        _check(lib().gss_synth_device(self._h, blk_ptr, nch_ptr, nch_max, ca_ptr, n_ca, nav_ptr,
+                     n_per_blk, fmt, out_ptr, carr_end_ptr=0, status_ptr=0, stream=0, ck_ptr=0):
+        _check(lib().gss_synth_device(self._h, blk_ptr, nch_ptr, nch_max, ck_ptr or None, ca_ptr,
+                                      n_ca, nav_ptr,
                                       n_nav, nblk, n_per_blk, fmt, out_ptr,
                                       carr_end_ptr or None, status_ptr or None, stream or None))
 

@@ -29,22 +29,25 @@ def rank_range(rank, world, window_s):
 
 def plan_rank(nav_file, rank, world, window_s, *, llh, samp_freq=2.6e6, data_format=16,
               threads=8, batch=1000):
-    """Host plane for one rank: (blk[n, 16], nch[n], nav rows, n_per_blk) of its block range."""
+    """Host plane for one rank: (blk[n, 16], nch[n], ck[n, 16, NCK], nav rows, n_per_blk) of its
+    block range (ck: the planner's carrier checkpoints)."""
     first, count = rank_range(rank, world, window_s)
     scn = Scenario(nav_file, llh=llh, duration=window_s * world if world > 1 else window_s,
                    samp_freq=samp_freq, data_format=data_format)
-    done, keep_b, keep_n = 0, [], []
+    done, keep_b, keep_n, keep_c = 0, [], [], []
     while done < first + count:
-        b, n = scn.next(min(batch, first + count - done), threads=threads)
+        b, n, c = scn.next(min(batch, first + count - done), threads=threads, with_ck=True)
         if len(n) == 0:
             break
         lo = max(0, first - done)
         if lo < len(n):
             keep_b.append(b[lo:])
             keep_n.append(n[lo:])
+            keep_c.append(c[lo:])
         done += len(n)
     blk = np.concatenate(keep_b)[:count]
     nch = np.concatenate(keep_n)[:count]
+    ck = np.concatenate(keep_c)[:count]
     if len(nch) != count:
         raise RuntimeError(f"rank {rank}: planned {len(nch)} of {count} blocks")
-    return blk, nch, scn.nav_table(), scn.n_per_blk
+    return blk, nch, ck, scn.nav_table(), scn.n_per_blk

@@ -84,11 +84,18 @@ int gss_dev_reserve(gss_dev *d, int max_blocks, int n_per_blk);
    see SURVEY.md Appendix A.4).  Returns 0 for an invalid format.                              */
 size_t gss_block_bytes(int n_per_blk, int fmt);
 
+/* Carrier checkpoints per block and channel: carr_ck[b][k][j] = exact carrier phase at sample
+   (j * n_per_blk) / GSS_NCK of the block (j = 0 is carr0).  The host planner records them while
+   it walks the carrier chain anyway (gss_scn_next); with them the GPU walks each block's carrier
+   as GSS_NCK independent sub-chains.  Optional everywhere (NULL: the GPU walks whole blocks).   */
+#define GSS_NCK 8
+
 /* Synthesise nblk consecutive 0.1 s blocks.  ALL pointers are device pointers:
      blk      [nblk][GSS_MAXCH] channel parameters (first nch[b] of each row valid)
      nch      [nblk] active channel count per block (0..16)
      nch_max  host-side upper bound of nch[] over the batch (selects the kernel instance;
               blocks with fewer channels are padded with silent channels)
+     carr_ck  optional [nblk][GSS_MAXCH][GSS_NCK] carrier checkpoints (see above)
      ca_bits  [n_ca][GSS_CA_WORDS] packed C/A chips (codegen, gpssim.c:132-171)
      nav      [n_nav][GSS_NAV_WORDS] 30-bit nav words (chan[i].dwrd, gpssim.c:1467-1547)
      out      nblk * gss_block_bytes(n_per_blk, fmt) bytes, exactly the bytes the reference
@@ -97,14 +104,14 @@ size_t gss_block_bytes(int n_per_blk, int fmt);
      status   optional int32[1]: set non-zero if a nav-word index ran past 59
    stream is a hipStream_t (NULL = default stream).  Asynchronous; no host synchronisation.    */
 int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch, int nch_max,
-                     const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
+                     const double *carr_ck, const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
                      int nblk, int n_per_blk, int fmt, void *out, double *carr_end,
                      int32_t *status, void *stream);
 
 /* Same, from host buffers: uploads inputs, runs, downloads `out` (and carr_end if non-NULL),
    synchronises.  Convenience for the CLI and tests; the bench uses gss_synth_device().        */
 int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
-                   const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
+                   const double *carr_ck, const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
                    int nblk, int n_per_blk, int fmt, void *out, double *carr_end);
 
 /* Kernel timing from HIP events recorded on the launch stream around each stage of every
@@ -155,9 +162,10 @@ int gss_scn_info(const gss_scn *s, gss_scn_info_t *info);
 
 /* Produce parameters for the next up to `max_blocks` blocks (in run order), including the
    exact carrier phase at each block start (planner runs on `threads` host threads).
-   blk is [max_blocks][GSS_MAXCH], nch is [max_blocks].  *n_out = blocks produced (0 at end).  */
-int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, int *n_out,
-                 int threads);
+   blk is [max_blocks][GSS_MAXCH], nch is [max_blocks], carr_ck (optional, may be NULL) is
+   [max_blocks][GSS_MAXCH][GSS_NCK] carrier checkpoints.  *n_out = blocks produced (0 at end). */
+int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, double *carr_ck,
+                 int *n_out, int threads);
 
 /* Nav-word table rows produced so far ([n][GSS_NAV_WORDS]); valid until the next gss_scn_next. */
 int gss_scn_nav_table(const gss_scn *s, const uint32_t **rows, int *n_rows);

@@ -42,7 +42,7 @@ int main(int argc, char **argv)
     clock_t t0 = clock();
     for (;;) {
         int nb = 0;
-        rc = gss_scn_next(scn, batch, blk, nch, &nb, threads);
+        rc = gss_scn_next(scn, batch, blk, nch, NULL, &nb, threads);
         if (rc) {
             fprintf(stderr, "%s\n", gss_last_error());
             return 1;

@@ -116,13 +116,18 @@ double wc_code_bf(double c, double s, int64_t n, int32_t *ic, int32_t *ib, int32
     return st.ph;
 }
 
-/* Stage A (GPU form, gss_seg_states): exact phase (and code counters) at every segment start */
-double wc_seg_states(double v, double s, int code, uint32_t cnt, int n, int seg_r, int nseg,
-                     int want_end, double *out_x, uint32_t *out_c)
+/* Stage A (GPU form, gss_seg_states): exact phase (and code counters) at every segment start
+   in [pos0, pos1) */
+double wc_seg_states(double v, double s, int code, uint32_t cnt, int pos0, int pos1, int seg_r,
+                     int nseg, int want_end, double *out_x, uint32_t *out_c)
 {
     int kind = code ? GSS_TRIP_CODE : (s < 0.0 ? GSS_TRIP_CARR_DESC : GSS_TRIP_CARR_ASC);
-    return gss_seg_states(kind, v, s, cnt, n, nseg, seg_r, want_end, out_x, out_c);
+    return gss_seg_states(kind, v, s, cnt, pos0, pos1, nseg, seg_r, want_end, out_x, out_c);
 }
+
+/* host planner carrier checkpoints */
+double wc_carr_walk_ck(double x, double s, int n, double *ck) { return gss_carr_walk_ck(x, s, n, ck); }
+int wc_nck(void) { return GSS_NCK; }
 
 /* carrier walk by specialised trips (both directions) */
 double wc_carr_trip(double x, double s, int64_t n)

@@ -103,7 +103,8 @@ def test_carr_end_matches_oracle(dev, ca):
         assert np.array_equal(cend_g[b, :nch[b]], cend_o[b, :nch[b]])
 
 
-def run_scenario(dev, batch=300, **kw):
+def run_scenario(dev, batch=300, use_ck=True, **kw):
+    """The product path: host plane -> (planner carrier checkpoints) -> GPU, block hashes."""
     s = G.Scenario(NAV, **kw)
     ca = G.ca_table()
     h = hashlib.sha256()
@@ -111,10 +112,13 @@ def run_scenario(dev, batch=300, **kw):
     bb = G.block_bytes(s.n_per_blk, s.data_format)
     total = 0
     while True:
-        blk, nch = s.next(batch)
+        if use_ck:
+            blk, nch, ck = s.next(batch, with_ck=True)
+        else:
+            (blk, nch), ck = s.next(batch), None
         if len(nch) == 0:
             break
-        out = dev.synth_host(blk, nch, ca, s.nav_table(), s.n_per_blk, s.data_format)
+        out = dev.synth_host(blk, nch, ca, s.nav_table(), s.n_per_blk, s.data_format, ck=ck)
         h.update(out.tobytes())
         total += out.size
         for i in range(len(nch)):
@@ -137,6 +141,15 @@ def test_scenario_bit_exact(dev, golden, name, kw):
     if blocks != g["block_sha16"]:
         first = next(i for i, (a, b) in enumerate(zip(blocks, g["block_sha16"])) if a != b)
         raise AssertionError(f"{name}: first differing block {first}")
+    assert total == g["bytes"] and sha == g["sha256"]
+
+
+def test_scenario_without_checkpoints(dev, golden):
+    """Callers that pass no planner checkpoints (e.g. INTEGRATION.md's gpssim.c patch): the GPU
+    walks whole blocks and gets the same bytes."""
+    sha, total, blocks = run_scenario(dev, use_ck=False, llh=LOC, duration=30.0, data_format=16)
+    g = golden["static_d30_b16"]
+    assert blocks == g["block_sha16"]
     assert total == g["bytes"] and sha == g["sha256"]
 
 

@@ -79,6 +79,20 @@ def test_planner_chain_matches_brute_force():
     assert checked > 50
 
 
+def test_planner_checkpoints_match_brute_force():
+    """The carrier checkpoints the planner records on its walk (gss_scn_next carr_ck) are the
+    brute-force carrier at samples j*N/NCK of every block; padding rows are zero."""
+    s = G.Scenario(NAV, llh=LOC, duration=3.0)
+    blk, nch, ck = s.all_blocks(batch=10, with_ck=True)
+    n = s.n_per_blk
+    pos = [j * n // G.NCK for j in range(G.NCK)]
+    for b in range(0, len(nch), 7):
+        for k in range(nch[b]):
+            want = oracle.carr_brute_trace(blk[b, k]["carr0"], blk[b, k]["carr_step"], pos)
+            assert np.array_equal(ck[b, k], want), (b, k)
+        assert not ck[b, nch[b]:].any()
+
+
 def test_nav_table_rows():
     s = G.Scenario(NAV, llh=LOC, duration=31.0)
     blk, nch = s.all_blocks()

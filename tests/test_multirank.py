@@ -35,7 +35,7 @@ def _worker(rank, world, port, result_path):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    blk, nch, nav, npb = plan_rank(NAV, rank, world, WINDOW_S, llh=LOC, threads=2)
+    blk, nch, ck, nav, npb = plan_rank(NAV, rank, world, WINDOW_S, llh=LOC, threads=2)
     out, rc = oracle.synth(blk, nch, G.ca_table(), nav, npb, 16)
     assert rc == 0
     t = torch.from_numpy(np.ascontiguousarray(out))

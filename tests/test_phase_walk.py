@@ -148,9 +148,23 @@ def test_stage_a_segment_states(seed):
         x0 = rng.random() if i != 4 else 0.0
         ox = np.zeros(nseg)
         oc = np.zeros(nseg, np.uint32)
-        end = W.wc_seg_states(x0, s, 0, 0, N, R, nseg, 1, ox.ctypes.data, oc.ctypes.data)
-        assert np.array_equal(ox, oracle.carr_brute_trace(x0, s, at)), i
+        end = W.wc_seg_states(x0, s, 0, 0, 0, N, R, nseg, 1, ox.ctypes.data, oc.ctypes.data)
+        want = oracle.carr_brute_trace(x0, s, at)
+        assert np.array_equal(ox, want), i
         assert end == oracle.carr_brute(x0, s, N), i
+        # the same as 8 sub-chains started from the planner's checkpoints (GPU Stage A with
+        # host checkpoints): segment states and block-end value identical
+        nck = W.wc_nck()
+        ck = np.zeros(nck)
+        assert W.wc_carr_walk_ck(x0, s, N, ck.ctypes.data) == end
+        pos = [j * N // nck for j in range(nck)] + [N]
+        assert np.array_equal(ck, oracle.carr_brute_trace(x0, s, pos[:-1])), i
+        ox2 = np.full(nseg, np.nan)
+        for j in range(nck):
+            e2 = W.wc_seg_states(ck[j], s, 0, 0, pos[j], pos[j + 1], R, nseg, int(j == nck - 1),
+                                 ox2.ctypes.data, oc.ctypes.data)
+        assert np.array_equal(ox2, want), i
+        assert e2 == end, i
         # code chain with counters
         cs = (1.023e6 + f / 1540.0) / 2.6e6
         if i == 5:
@@ -158,7 +172,7 @@ def test_stage_a_segment_states(seed):
         c0 = rng.random() * 1023.0 if i != 6 else 0.0
         st = (rng.randrange(20), rng.randrange(30), rng.randrange(3))
         cnt0 = st[0] | (st[1] << 8) | (st[2] << 16)
-        W.wc_seg_states(c0, cs, 1, cnt0, N, R, nseg, 0, ox.ctypes.data, oc.ctypes.data)
+        W.wc_seg_states(c0, cs, 1, cnt0, 0, N, R, nseg, 0, ox.ctypes.data, oc.ctypes.data)
         c, (a, b, d) = c0, st
         for j in range(nseg):
             if j:

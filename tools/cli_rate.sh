@@ -7,7 +7,7 @@ TAG=${1:-s}
 mkdir -p gpurun_out
 BIN=gps-sdr-sim_amd/bin/gps-sdr-sim
 NAV=tests/golden/data/brdc3540.14n
-for d in 30 300; do
+for d in 30 300 3000; do
   t0=$(date +%s.%N)
   timeout -k 10 300 $BIN -e $NAV -l 30.286502,120.032669,100 -d $d -b 16 -o /dev/null \
       > gpurun_out/cli_${TAG}_$d.log 2>&1 || exit $?
