@@ -34,7 +34,6 @@
 #define CHUNK_BYTES    128               /* output bytes per lane per staged chunk: a line */
 #define CHUNK_PIECES   (CHUNK_BYTES / 16)
 #define LUT_N          1024              /* index ti + 256*neg <= 767; padded to a power of 2 */
-#define CHIP_N         1024              /* chip table row: chips 0..1022 (+ pad)             */
 
 struct lut_arg { int16_t sin512[512]; int16_t cos512[512]; };
 
@@ -123,13 +122,37 @@ template <> struct fmt_traits<16> { static constexpr int SPC = CHUNK_BYTES / 4; 
 template <> struct fmt_traits<8>  { static constexpr int SPC = CHUNK_BYTES / 2; };
 template <> struct fmt_traits<1>  { static constexpr int SPC = CHUNK_BYTES * 4; };
 
-typedef short gss_short2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c)
+/* floor(512 carr) and floor(C) for four channels with one v_add_f64 each: in round-toward-
+   zero mode, carr + 2^43 lands on the lattice 2^-9 of [2^43, 2^43+1) at 2^43 + floor(512 carr)/512,
+   so its low word is floor(512 carr) (carr in [0,1)); C + 2^52 has lattice 1, low word floor(C)
+   (C in [0,1024)).  The MODE switch (double rounding field, bits 3:2) and the adds sit in one asm
+   block so that no other floating-point instruction runs in the modified mode. */
+__device__ __forceinline__ void floors4(double c0, double c1, double c2, double c3, double k0,
+                                        double k1, double k2, double k3, uint32_t *ti,
+                                        uint32_t *ci)
 {
-    /* v_dot2c_i32_i16: c + a.lo*b.lo + a.hi*b.hi (signed 16-bit halves) */
-    return __builtin_amdgcn_sdot2(__builtin_bit_cast(gss_short2, a),
-                                  __builtin_bit_cast(gss_short2, b), c, false);
+    double y0, y1, y2, y3, z0, z1, z2, z3;
+    const double M9 = 0x1p43, M52 = 0x1p52;
+    asm volatile(
+        "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 3\n\t"
+        "s_nop 3\n\t"
+        "v_add_f64 %0, %8, %16\n\t"
+        "v_add_f64 %1, %9, %16\n\t"
+        "v_add_f64 %2, %10, %16\n\t"
+        "v_add_f64 %3, %11, %16\n\t"
+        "v_add_f64 %4, %12, %17\n\t"
+        "v_add_f64 %5, %13, %17\n\t"
+        "v_add_f64 %6, %14, %17\n\t"
+        "v_add_f64 %7, %15, %17\n\t"
+        "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 0\n\t"
+        "s_nop 3"
+        : "=&v"(y0), "=&v"(y1), "=&v"(y2), "=&v"(y3), "=&v"(z0), "=&v"(z1), "=&v"(z2), "=&v"(z3)
+        : "v"(c0), "v"(c1), "v"(c2), "v"(c3), "v"(k0), "v"(k1), "v"(k2), "v"(k3), "s"(M9),
+          "s"(M52));
+    ti[0] = (uint32_t)__double2loint(y0); ti[1] = (uint32_t)__double2loint(y1);
+    ti[2] = (uint32_t)__double2loint(y2); ti[3] = (uint32_t)__double2loint(y3);
+    ci[0] = (uint32_t)__double2loint(z0); ci[1] = (uint32_t)__double2loint(z1);
+    ci[2] = (uint32_t)__double2loint(z2); ci[3] = (uint32_t)__double2loint(z3);
 }
 
 /* 16 bytes to global memory: one dwordx4 store when aligned (block bases are multiples of the
@@ -156,17 +179,25 @@ __device__ __forceinline__ void wave_sync_lds()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-/* data-bit sign folded into the gain: I += (dataBit*gain) * (codeCA*cos), as packed int16 pairs
-   (g, 0) for I and (0, g) for Q against the LUT word (cos, sin) */
-__device__ __forceinline__ void signed_gain(int gain, uint32_t bit, uint32_t &gi, uint32_t &gq)
-{
-    int g = bit ? gain : -gain;
-    gi = (uint32_t)(uint16_t)(int16_t)g;
-    gq = gi << 16;
-}
+/* data-bit sign folded into the gain: I + 2^22 Q += (dataBit*gain) * (codeCA*(cos + 2^22 sin)) */
+__device__ __forceinline__ int signed_gain(int gain, uint32_t bit) { return bit ? gain : -gain; }
+
+/* Chip signs come from a per-lane 32-chip register window per channel, refreshed every P
+   samples from a bit-packed, cyclically extended chip table in LDS (CBITS_W words per channel:
+   bit j = codeCA(j mod 1023) < 0, j < 32 CBITS_W).  The window taken at extended chip index
+   `base` is rotated: bit p holds the chip j in [base, base+32) with j = p (mod 32), so the sign
+   of chip floor(C) is v_bfe_u32(win, floor(C), 1) (the offset is taken mod 32) with no
+   per-lane base.  The code phase advances <= ks_max chips per sample, so P = floor(29/ks_max)
+   samples (>= 1) never leave the window.  The lazy code wrap keeps the extended index
+   continuous: floor(C) = 1023.. reads the extension, and the wrap (C -= 1023, i.e. +1 mod 32)
+   rotates the window left by one. */
+#ifndef SYNTH_OCC
+#define SYNTH_OCC(nch) ((nch) <= 12 ? 3 : 2)   /* waves per SIMD the register budget targets */
+#endif
+#define CBITS_W 68                         /* covers extended indices < 2176 (C < 1023 + ks)  */
 
 template <int NCH, int FMT>
-__global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
+__global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(SYNTH_OCC(NCH)))) void gss_synth_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch,
     const uint32_t *__restrict__ ca_bits, const uint32_t *__restrict__ nav,
     const double *__restrict__ seg_carr, const double *__restrict__ seg_code,
@@ -174,10 +205,13 @@ __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
     int seg_r, int wg_per_blk, uint8_t *__restrict__ out, size_t block_bytes, int32_t *__restrict__ status)
 {
     constexpr int SPC = fmt_traits<FMT>::SPC;
+    constexpr int NCH4 = (NCH + 3) & ~3;
     constexpr int BPS4 = FMT == 16 ? 16 : FMT == 8 ? 8 : 1;      /* 4 x bytes per sample */
-    __shared__ uint32_t s_lut[LUT_N];                     /* cos | sin << 16, index mod 512  */
-    __shared__ uint8_t s_chip[NCH][CHIP_N];               /* 1 where codeCA = -1 (chip 0)    */
+    __shared__ int32_t s_lut[LUT_N];                      /* cos + 2^22 sin, index mod 512   */
+    __shared__ uint32_t s_cbits[NCH][CBITS_W];            /* extended chip-sign bits         */
     __shared__ uint32_t s_nav[NCH][64];
+    __shared__ uint16_t s_st[NCH][SYNTH_THREADS];         /* code counters, touched on wraps only:
+                                                             icode | ibit<<5 | iword<<10 */
     __shared__ uint32_t s_stage[SYNTH_WAVES][64 * CHUNK_BYTES / 4];
 
     const int b = blockIdx.x / wg_per_blk;
@@ -190,19 +224,20 @@ __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
     /* ---- LDS tables for this block ---- */
     for (int i = tid; i < LUT_N; i += SYNTH_THREADS) {
         int j = i & 511;                                  /* LUT[i+256] = -LUT[i] (mod 512) */
-        s_lut[i] = (uint32_t)(uint16_t)lut.cos512[j] | ((uint32_t)(uint16_t)lut.sin512[j] << 16);
+        s_lut[i] = (int32_t)lut.cos512[j] + (int32_t)lut.sin512[j] * (1 << 22);
     }
-    for (int i = tid; i < NCH * (CHIP_N / 4); i += SYNTH_THREADS) {
-        int k = i / (CHIP_N / 4), j4 = (i % (CHIP_N / 4)) * 4;
+    for (int i = tid; i < NCH * CBITS_W; i += SYNTH_THREADS) {
+        int k = i / CBITS_W, wd = i % CBITS_W;
         uint32_t v = 0;
         if (k < nc) {
             const uint32_t *cb = ca_bits + (size_t)prow[k].ca_tbl * GSS_CA_WORDS;
-            uint32_t word = cb[j4 >> 5] >> (j4 & 31);       /* 4 chips, never straddling */
-            for (int q = 0; q < 4; q++)
-                if (j4 + q < 1023)
-                    v |= (uint32_t)(((word >> q) & 1u) ^ 1u) << (8 * q);
+            int j = (32 * wd) % 1023;
+            for (int q = 0; q < 32; q++) {
+                v |= (((cb[j >> 5] >> (j & 31)) & 1u) ^ 1u) << q;
+                j = j == 1022 ? 0 : j + 1;
+            }
         }
-        ((uint32_t *)&s_chip[k][0])[j4 >> 2] = v;
+        s_cbits[k][wd] = v;
     }
     for (int i = tid; i < NCH * 64; i += SYNTH_THREADS) {
         int k = i >> 6, j = i & 63;
@@ -217,22 +252,31 @@ __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
     int len = active ? n_per_blk - n0 : 0;
     if (len > seg_r) len = seg_r;
     const int segc = active ? seg : nseg - 1;           /* inactive lanes: any valid anchor */
-    const int n0c = segc * seg_r;
 
     /* block-uniform channel steps (scalar registers); padding channels: no motion, no gain.
        Gains are re-read (scalar loads) where a data bit changes, to spare scalar registers. */
     double cs[NCH], ks[NCH];
+    double ks_max = 0.0;
+    int gsum = 0;
 #pragma unroll
     for (int k = 0; k < NCH; k++) {
         const bool real = k < nc;
         cs[k] = real ? prow[k].carr_step : 0.0;
         ks[k] = real ? prow[k].code_step : 0.0;
+        ks_max = fmax(ks_max, ks[k]);
+        const int gk = real ? prow[k].gain : 0;
+        gsum += gk < 0 ? -gk : gk;
     }
+    /* window refresh period (see CBITS_W) */
+    const int P = ks_max < 29.0 / 65536.0 ? 65536 : max(1, (int)(29.0 / ks_max));
+    /* the packed int64 accumulator needs |sum I + 64| < 2^21: 250 * sum|gain| + 64 (the
+       reference's gains are <= 129 per channel); larger gains take the int32 path */
+    const bool big = gsum > 8000;
 
     /* ---- exact per-lane start state (Stage A), every channel of the instance ---- */
     double carr[NCH], C[NCH];
-    uint32_t st[NCH];             /* icode | ibit<<8 | iword<<16 */
-    uint32_t gi[NCH], gq[NCH];
+    int g[NCH];                   /* gain with the data-bit sign */
+    uint32_t win[NCH];            /* rotated chip-sign window (see CBITS_W) */
     int bad = 0;
 #pragma unroll
     for (int k = 0; k < NCH; k++) {
@@ -242,8 +286,9 @@ __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
         uint32_t c = seg_cnt[r];
         int ibit = (c >> 8) & 0xFF, iw = c >> 16;
         if (iw > 59) { bad |= 1; iw = 59; c = (c & 0xFFFFu) | (59u << 16); }
-        st[k] = c;
-        signed_gain(k < nc ? prow[k].gain : 0, (s_nav[k][iw] >> (29 - ibit)) & 1u, gi[k], gq[k]);
+        s_st[k][tid] = (uint16_t)((c & 0x1Fu) | (((c >> 8) & 0x1Fu) << 5) | ((c >> 16) << 10));
+        g[k] = signed_gain(k < nc ? prow[k].gain : 0, (s_nav[k][iw] >> (29 - ibit)) & 1u);
+        win[k] = 0;
     }
 
     uint8_t *dst = out + (size_t)b * block_bytes + (size_t)n0 * BPS4 / 4;
@@ -257,6 +302,7 @@ __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
        (harmlessly, nothing is stored) so that no loop-carried state sits under divergent
        control flow */
     const int wave_chunks = __builtin_amdgcn_readfirstlane(lane_chunks);
+    int left = 0;                                       /* samples until the next refresh */
 
     for (int ch = 0; ch < wave_chunks; ch++) {
         const bool full = ch < nchunk;
@@ -264,44 +310,108 @@ __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
         uint32_t bits = 0;
 #pragma unroll 1
         for (int sidx = 0; sidx < SPC; sidx++) {
-            int acc_i = 64, acc_q = 64;               /* the +64 of (acc+64)>>7 */
-            uint64_t any = 0;
-            /* channels in groups of 4: chip reads, then LUT reads, then consume */
+            /* floor(512 carr) and floor(C) of the current state, four channels per mode switch */
+            uint32_t ti[NCH4], ci[NCH4];
 #pragma unroll
-            for (int k0 = 0; k0 < NCH; k0 += 4) {
-                constexpr int GW = 4;
-                int ti[GW];
-                uint32_t t[GW], e[GW];
+            for (int k0 = 0; k0 < NCH; k0 += 4)
+                floors4(carr[k0], carr[min(k0 + 1, NCH - 1)], carr[min(k0 + 2, NCH - 1)],
+                        carr[min(k0 + 3, NCH - 1)], C[k0], C[min(k0 + 1, NCH - 1)],
+                        C[min(k0 + 2, NCH - 1)], C[min(k0 + 3, NCH - 1)], &ti[k0], &ci[k0]);
+            if (left == 0) {                          /* uniform: new chip windows at floor(C) */
 #pragma unroll
-                for (int j = 0; j < GW; j++) {
-                    if (k0 + j < NCH) {
-                        const int k = k0 + j;
-                        ti[j] = (int)(carr[k] * 512.0);      /* floor: carr in [0,1) */
-                        t[j] = s_chip[k][(int)C[k]];
-                    }
+                for (int k = 0; k < NCH; k++) {
+                    const uint32_t base = ci[k];
+                    const uint32_t *row = &s_cbits[k][base >> 5];
+                    const uint32_t hi_mask = 0xFFFFFFFFu << (base & 31u);   /* v_bfi */
+                    win[k] = (row[0] & hi_mask) | (row[1] & ~hi_mask);
                 }
+                left = P;
+            }
+            left--;
+            /* chip sign (1 = codeCA -1) of every channel, before the wrap below rotates win */
+            uint32_t t[NCH];
 #pragma unroll
-                for (int j = 0; j < GW; j++)
-                    if (k0 + j < NCH)          /* LUT[floor(512 carr)] x codeCA (gpssim.c:2200-2209) */
-                        e[j] = s_lut[ti[j] + (int)(t[j] << 8)];
+            for (int k = 0; k < NCH; k++) {
+                t[k] = __builtin_amdgcn_ubfe(win[k], ci[k], 1);
+                asm volatile("" : "+v"(t[k]));   /* keep above the branch: no copies of win */
+            }
+            /* the code phase of the previous step may have reached 1023 (gpssim.c:2214): apply
+               that wrap now, before this step's add; floor(C) >= 1023 reads the table's cyclic
+               extension.  Rare (once per ~2600 samples per channel): a uniform branch per
+               channel, selects inside, so no loop-carried state sits under divergent control
+               flow. */
+            uint32_t cmax = ci[0];
 #pragma unroll
-                for (int j = 0; j < GW; j++) {
-                    if (k0 + j < NCH) {
-                        const int k = k0 + j;
-                        acc_i = dot2(e[j], gi[k], acc_i);
-                        acc_q = dot2(e[j], gq[k], acc_q);
-                        /* carrier (gpssim.c:2245-2250): carr+s is in [0,2) ascending or (-1,1)
-                           descending, where v_fract_f64 returns exactly the reference's
-                           carr-1 / carr+1 (x - floor(x), one IEEE rounding) */
-                        carr[k] = __builtin_amdgcn_fract(carr[k] + cs[k]);
-                        C[k] = C[k] + ks[k];                  /* code (gpssim.c:2212) */
-                        any |= __builtin_amdgcn_ballot_w64(C[k] >= GSS_CA_SEQ_LEN_D);
+            for (int k = 1; k < NCH; k++)
+                cmax = max(cmax, ci[k]);                      /* v_max3_u32 */
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(cmax >= 1023u) != 0, 0)) {
+#pragma unroll
+                for (int k = 0; k < NCH; k++) {
+                    const bool wk = ci[k] >= 1023u;
+                    if (__builtin_amdgcn_ballot_w64(wk)) {    /* gpssim.c:2214-2237 */
+                        C[k] = wk ? C[k] - GSS_CA_SEQ_LEN_D : C[k];
+                        win[k] = wk ? __builtin_amdgcn_alignbit(win[k], win[k], 31) : win[k];
+                        const uint32_t c = s_st[k][tid];
+                        int icode = (int)(c & 0x1F) + 1, ibit = (c >> 5) & 0x1F,
+                            iword = (int)(c >> 10);
+                        const bool nbit = icode >= 20;
+                        if (nbit) {
+                            icode = 0;
+                            if (++ibit >= 30) { ibit = 0; iword++; }
+                            if (iword > 59) { bad |= (wk && sidx < nsamp) ? 1 : 0; iword = 59; }
+                        }
+                        const uint32_t c2 = (uint32_t)icode | ((uint32_t)ibit << 5) |
+                                            ((uint32_t)iword << 10);
+                        if (wk)
+                            s_st[k][tid] = (uint16_t)c2;
+                        if (__builtin_amdgcn_ballot_w64(wk && nbit)) {
+                            const int ng = signed_gain(prow[k].gain * (k < nc ? 1 : 0),
+                                                       (s_nav[k][iword] >> (29 - ibit)) & 1u);
+                            g[k] = (wk && nbit) ? ng : g[k];
+                        }
                     }
                 }
             }
-            /* gpssim.c:2257-2263: (acc+64)>>7 (arithmetic), then (short).  Written before the
-               wrap fix-up below, unconditionally: samples past this lane's end land in staging
-               bytes that are never copied out. */
+            /* LUT[floor(512 carr)] x codeCA (gpssim.c:2200-2209) */
+            int32_t e[NCH];
+#pragma unroll
+            for (int k = 0; k < NCH; k++)
+                e[k] = s_lut[ti[k] + (t[k] << 8)];
+            int acc_i, acc_q;
+            if (__builtin_expect(!big, 1)) {
+                /* I and Q of all channels in one int64: acc = (sum I + 64) + 2^22 (sum Q + 64)
+                   (gpssim.c:2200-2210, the +64 of 2257) */
+                int64_t acc = 64 + ((int64_t)64 << 22);
+#pragma unroll
+                for (int k = 0; k < NCH; k++)
+                    acc += (int64_t)g[k] * (int64_t)e[k];          /* v_mad_i64_i32 */
+                const uint32_t alo = (uint32_t)acc;
+                acc_i = ((int)(alo << 10)) >> 10;                  /* sext22 */
+                acc_q = (int)(acc >> 22) + (int)((alo >> 21) & 1u);
+            } else {
+                /* large gains: separate (wrapping) int32 sums, as the reference's int math */
+                uint32_t ai = 64, aq = 64;
+#pragma unroll
+                for (int k = 0; k < NCH; k++) {
+                    const int cv = (int)((uint32_t)e[k] << 10) >> 10;
+                    const int sv = (e[k] - cv) >> 22;
+                    ai += (uint32_t)g[k] * (uint32_t)cv;
+                    aq += (uint32_t)g[k] * (uint32_t)sv;
+                }
+                acc_i = (int)ai;
+                acc_q = (int)aq;
+            }
+#pragma unroll
+            for (int k = 0; k < NCH; k++) {
+                /* carrier (gpssim.c:2245-2250): carr+s is in [0,2) ascending or (-1,1)
+                   descending, where v_fract_f64 returns exactly the reference's carr-1 / carr+1
+                   (x - floor(x), one IEEE rounding) */
+                carr[k] = __builtin_amdgcn_fract(carr[k] + cs[k]);
+                C[k] = C[k] + ks[k];                          /* code (gpssim.c:2212) */
+            }
+            /* gpssim.c:2257-2263: (acc+64)>>7 (arithmetic), then (short).  Written
+               unconditionally: samples past this lane's end land in staging bytes that are never
+               copied out. */
             int i16 = (int)(int16_t)(acc_i >> 7);
             int q16 = (int)(int16_t)(acc_q >> 7);
             if (FMT == 16) {
@@ -317,37 +427,6 @@ __global__ __launch_bounds__(SYNTH_THREADS) void gss_synth_kernel(
                     uint32_t w32 = nb >= 16 ? bits : nb > 0 ? (bits >> 2 * (16 - nb)) << 2 * (16 - nb) : 0u;
                     mine[sidx >> 4] = __builtin_bswap32(w32);
                     bits = 0;
-                }
-            }
-            /* rare: some lane's code phase wrapped (once per ~2600 samples per channel).  Per
-               channel a uniform branch, inside it selects only: no divergent control flow around
-               the loop-carried state. */
-            if (__builtin_expect(any != 0, 0)) {
-#pragma unroll
-                for (int k = 0; k < NCH; k++) {
-                    const bool wk = C[k] >= GSS_CA_SEQ_LEN_D;
-                    if (__builtin_amdgcn_ballot_w64(wk)) {    /* gpssim.c:2214-2237 */
-                        C[k] = wk ? C[k] - GSS_CA_SEQ_LEN_D : C[k];
-                        const uint32_t c = st[k];
-                        int icode = (int)(c & 0xFF) + 1, ibit = (c >> 8) & 0xFF,
-                            iword = (int)(c >> 16);
-                        const bool nbit = icode >= 20;
-                        if (nbit) {
-                            icode = 0;
-                            if (++ibit >= 30) { ibit = 0; iword++; }
-                            if (iword > 59) { bad |= (wk && sidx < nsamp) ? 1 : 0; iword = 59; }
-                        }
-                        const uint32_t c2 = (uint32_t)icode | ((uint32_t)ibit << 8) |
-                                            ((uint32_t)iword << 16);
-                        st[k] = wk ? c2 : c;
-                        if (__builtin_amdgcn_ballot_w64(wk && nbit)) {
-                            uint32_t ngi, ngq;
-                            signed_gain(prow[k].gain * (k < nc ? 1 : 0),
-                                        (s_nav[k][iword] >> (29 - ibit)) & 1u, ngi, ngq);
-                            gi[k] = (wk && nbit) ? ngi : gi[k];
-                            gq[k] = (wk && nbit) ? ngq : gq[k];
-                        }
-                    }
                 }
             }
         }
