@@ -473,6 +473,102 @@ GSS_HD double gss_seg_states(int kind, double v, double st, uint32_t cnt, int po
     return v;
 }
 
+/* "Some lane of the wave" on the GPU (uniform loop control); the chain itself on the host. */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GSS_ANY(c) (__builtin_amdgcn_ballot_w64(c) != 0)
+#else
+#define GSS_ANY(c) (c)
+#endif
+
+/* The code chain of gss_seg_states (GSS_TRIP_CODE, pos0 = 0, pos1 = n, no end value) without
+ * divergent branches, for the GPU Stage A where code chains are few and long and so bound by the
+ * latency of one wave's instruction stream, not by issue.  Every trip is gss_trip's K >= 2^26 form
+ * as straight-line selects (with st >= 2^-16 the lattice index K = rne(st/u) is >= 2^27 in every
+ * binade below 1024); a finished chain makes empty trips (J = 0, no step) until its wave is done.
+ * The first segment start in a trip is stored unconditionally, to row slot `dummy` (>= nseg) when
+ * there is none; a trip that crosses more starts (top-binade jumps longer than seg_r, high
+ * sample rates) takes a uniform loop.  st == 0 (padding channel): every start gets (v, cnt). */
+GSS_HD void gss_code_seg_states_bf(double v, double st, uint32_t cnt, int n, int nseg, int seg_r,
+                                   int dummy, double *out_x, uint32_t *out_c)
+{
+    const double rs = st > 0.0 ? 1.0 / st : 0.0, R = (double)seg_r, total = (double)n;
+    double left = st > 0.0 ? total : 0.0;
+    int seg = 0;
+    double n0 = 0.0;
+    if (left == 0.0) {
+        for (; seg < nseg; seg++) {
+            out_x[seg] = v;
+            out_c[seg] = cnt;
+        }
+    } else if (nseg > 0) {
+        out_x[0] = v;
+        out_c[0] = cnt;
+        seg = 1;
+        n0 = R;
+    }
+    for (;;) {
+        const double vb = v, pb = total - left;
+        const uint32_t cnt_b = cnt;
+        gss_bits64 bits;
+        bits.d = v;
+        const uint32_t hi = (uint32_t)(bits.u >> 32), lo = (uint32_t)bits.u;
+        const uint32_t X = hi & 0x7FF00000u;                       /* E << 20 */
+        const double P = gss_d_from_hi(0x83200000u - X, 0u);       /* 1/u */
+        const double Pi = gss_d_from_hi(X - 0x03400000u, 0u);      /* u   */
+        const double m = gss_d_from_hi((hi & 0x000FFFFFu) | 0x43300000u, lo);
+        const double sig = st * P;
+        const double k = GSS_FLOOR(sig);
+        const double K = GSS_RINT(sig);
+        const int odd_tie = ((sig - k) == 0.5) & (int)(lo & 1u);
+        const double lim0 = ((0x1p53 - 1.0) - k) - m;               /* stay < 2^ex */
+        const double l2 = ((GSS_CA_SEQ_LEN_D - v) * P - 1.0) - K;   /* v + (j+1)Ku < 1023 */
+        const double lim = ((X >= (1032u << 20)) & (l2 < lim0)) ? l2 : lim0;
+        const int live = (v >= 0x1p-900) & (sig < 0x1p52) & !odd_tie & (lim >= 0.0);
+        const double q0 = GSS_FLOOR(lim * (rs * Pi));
+        const double r0 = GSS_FMA(-q0, K, lim);
+        double J = (q0 + 1.0) + ((r0 >= K ? 1.0 : 0.0) + (r0 < 0.0 ? -1.0 : 0.0));
+        J = live ? (J < left ? J : left) : 0.0;
+        const double Ds = K * Pi;
+        const double v1 = GSS_FMA(J, Ds, v);
+        const double left1 = left - J;
+        const double r = v1 + st;                                   /* the real step */
+        const int wr = r >= GSS_CA_SEQ_LEN_D;
+        const double r2 = wr ? r - GSS_CA_SEQ_LEN_D : r;
+        const int step = left1 > 0.0;
+        v = step ? r2 : v1;
+        left = step ? left1 - 1.0 : 0.0;
+        {                                                           /* gpssim.c:2216-2236 */
+            uint32_t icode = (cnt & 0xFFu) + 1u, ibit = (cnt >> 8) & 0xFFu, iword = cnt >> 16;
+            const uint32_t nb = icode >= 20u;
+            icode = nb ? 0u : icode;
+            ibit += nb;
+            const uint32_t nw = ibit >= 30u;
+            ibit = nw ? 0u : ibit;
+            iword += nw;
+            cnt = (step & wr) ? (icode | (ibit << 8) | (iword << 16)) : cnt;
+        }
+        const double pa = total - left;
+        {
+            const int e1 = (seg < nseg) & (n0 <= pa);
+            const int idx = e1 ? seg : dummy;
+            out_x[idx] = n0 <= pb + J ? GSS_FMA(n0 - pb, Ds, vb) : v;
+            out_c[idx] = n0 == pa ? cnt : cnt_b;
+            seg += e1;
+            n0 += e1 ? R : 0.0;
+        }
+        if (GSS_ANY((seg < nseg) & (n0 <= pa))) {                  /* rare: more starts */
+            while ((seg < nseg) & (n0 <= pa)) {
+                out_x[seg] = n0 <= pb + J ? GSS_FMA(n0 - pb, Ds, vb) : v;
+                out_c[seg] = n0 == pa ? cnt : cnt_b;
+                seg++;
+                n0 += R;
+            }
+        }
+        if (!GSS_ANY((left > 0.0) & (seg < nseg)))
+            break;
+    }
+}
+
 /* n steps with gss_iter_bf; returns the value, *nwrap counts wraps. */
 GSS_HD double gss_walk_bf(double x, double s, double W, double n, int *nwrap)
 {

@@ -87,8 +87,15 @@ __global__ __launch_bounds__(ANCHOR_THREADS) void gss_anchor_kernel(
     if (code) {
         const uint32_t cnt = (uint32_t)p.icode | ((uint32_t)p.ibit << 8) |
                              ((uint32_t)p.iword << 16);
-        gss_seg_states(GSS_TRIP_CODE, p.code0, p.code_step, cnt, 0, n_per_blk, nseg, seg_r, 0,
-                       seg_code + row, seg_cnt + row);
+        /* code chains (one per block) are the long pole of the kernel and few: latency-bound, so
+           the branch-free walk; a code step below 2^-16 (not a GNSS sample rate) takes the
+           general walk.  Slot nseg of the row is the walk's dummy store target. */
+        if (!GSS_ANY(p.code_step != 0.0 && p.code_step < 0x1p-16))
+            gss_code_seg_states_bf(p.code0, p.code_step, cnt, n_per_blk, nseg, seg_r, nseg,
+                                   seg_code + row, seg_cnt + row);
+        else
+            gss_seg_states(GSS_TRIP_CODE, p.code0, p.code_step, cnt, 0, n_per_blk, nseg, seg_r, 0,
+                           seg_code + row, seg_cnt + row);
         return;
     }
     const int pos0 = carr_ck ? gss_ck_pos(j, n_per_blk) : 0;
@@ -543,7 +550,8 @@ extern "C" int gss_dev_close(gss_dev *d)
 }
 
 static int nseg_of(int n, int r) { return (n + r - 1) / r; }
-static int nsegp_of(int n, int r) { return (nseg_of(n, r) + 31) & ~31; }   /* anchor row stride */
+/* anchor row stride: the segment starts and one dummy slot (gss_code_seg_states_bf) */
+static int nsegp_of(int n, int r) { return (nseg_of(n, r) + 1 + 31) & ~31; }
 
 extern "C" int gss_dev_reserve(gss_dev *d, int max_blocks, int n_per_blk)
 {

@@ -85,6 +85,9 @@ def walk_lib():
         L.wc_seg_states.restype = D
         L.wc_seg_states.argtypes = [D, D, C.c_int, C.c_uint32, C.c_int, C.c_int, C.c_int,
                                     C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.wc_code_seg_bf.restype = None
+        L.wc_code_seg_bf.argtypes = [D, D, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.c_void_p, C.c_void_p]
         L.wc_carr_walk_ck.restype = D
         L.wc_carr_walk_ck.argtypes = [D, D, C.c_int, C.c_void_p]
         L.wc_carr_anchors.restype = C.c_int

@@ -125,6 +125,13 @@ double wc_seg_states(double v, double s, int code, uint32_t cnt, int pos0, int p
     return gss_seg_states(kind, v, s, cnt, pos0, pos1, nseg, seg_r, want_end, out_x, out_c);
 }
 
+/* branch-free code chain (GPU Stage A code waves) */
+void wc_code_seg_bf(double v, double s, uint32_t cnt, int n, int seg_r, int nseg, int dummy,
+                    double *out_x, uint32_t *out_c)
+{
+    gss_code_seg_states_bf(v, s, cnt, n, nseg, seg_r, dummy, out_x, out_c);
+}
+
 /* host planner carrier checkpoints */
 double wc_carr_walk_ck(double x, double s, int n, double *ck) { return gss_carr_walk_ck(x, s, n, ck); }
 int wc_nck(void) { return GSS_NCK; }

@@ -180,6 +180,44 @@ def test_stage_a_segment_states(seed):
             assert ox[j] == c and oc[j] == (a | (b << 8) | (d << 16)), (i, j)
 
 
+@pytest.mark.parametrize("seed", [30, 31])
+def test_code_chain_branch_free(seed):
+    """gss_code_seg_states_bf (the GPU Stage A code waves) equals gss_seg_states' code chain and
+    brute force at every segment start: 1, 2.6 and 20 MS/s (top-binade jumps spanning several
+    segments), forced ties on the 2^-43 lattice, zero phase, a phase just below 1023, counter
+    roll-overs, no motion; the dummy slot past nseg absorbs the trips without a start."""
+    W = walk_lib()
+    rng = random.Random(seed)
+    R = 1024
+    for i in range(9):
+        fs = [2.6e6, 2.0e7, 1.0e6][i % 3]
+        N = int(fs / 10)
+        nseg = (N + R - 1) // R
+        f = rng.uniform(-6000, 6000)
+        cs = (1.023e6 + f / 1540.0) / fs
+        if i == 4:
+            cs = (math.floor(cs / 2.0 ** -43) + 0.5) * 2.0 ** -43
+        if i == 8:
+            cs = 0.0
+        c0 = [rng.random() * 1023.0, 0.0, 1022.9999999][i % 3 if i < 6 else 0]
+        st = (rng.randrange(20), rng.randrange(30), rng.randrange(40))
+        cnt0 = st[0] | (st[1] << 8) | (st[2] << 16)
+        want_x = np.zeros(nseg)
+        want_c = np.zeros(nseg, np.uint32)
+        W.wc_seg_states(c0, cs, 1, cnt0, 0, N, R, nseg, 0, want_x.ctypes.data, want_c.ctypes.data)
+        got_x = np.full(nseg + 1, np.nan)
+        got_c = np.zeros(nseg + 1, np.uint32)
+        W.wc_code_seg_bf(c0, cs, cnt0, N, R, nseg, nseg, got_x.ctypes.data, got_c.ctypes.data)
+        assert np.array_equal(got_x[:nseg], want_x), i
+        assert np.array_equal(got_c[:nseg], want_c), i
+        if i < 3:
+            c, (a, b, d) = c0, st
+            for j in range(nseg):
+                if j:
+                    c, a, b, d = oracle.code_brute(c, cs, R, a, b, d)
+                assert got_x[j] == c and got_c[j] == (a | (b << 8) | (d << 16)), (i, j)
+
+
 def test_stationary_and_single_steps():
     """Stationary values, and steps so small that K < 2^26 in the upper binades (the
     branch-free walk's exact-division fallback)."""
