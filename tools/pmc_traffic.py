@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""profiles/pmc_traffic.json from a tools/profile.sh run: HBM bytes per launch of the synthesis
+kernel from the PMC passes (WRITE_SIZE exact, FETCH_SIZE x2 for gfx950 wide reads; both KiB,
+MI355X_MICROARCH.md §HBM), keyed by the bench workload string so that bench.py reports it as
+roofline.traffic only for the same workload.
+Usage: python tools/pmc_traffic.py gpurun_out/prof_<tag> [out.json]"""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    d = sys.argv[1]
+    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "profiles", "pmc_traffic.json")
+    summ = json.loads(subprocess.check_output([sys.executable,
+                                               os.path.join(REPO, "tools", "prof_summary.py"), d]))
+    bench = None
+    for name in ("pmc_write", "pmc_fetch", "kt"):
+        try:
+            for line in open(os.path.join(d, name + ".log")):
+                if line.startswith("{") and '"metric"' in line:
+                    bench = json.loads(line)
+        except OSError:
+            pass
+    k = next(n for n in summ if n.startswith("gss_synth_kernel"))
+    e = summ[k]
+    w, r = e["hbm_write_bytes"], e["hbm_read_bytes_corrected"]
+    alg = bench["config"]["samples_per_gpu"] * 4 if bench else None
+    res = {"workload": bench["config"]["workload"] if bench else None, "kernel": k,
+           "hbm_bytes_per_launch": round(w + r), "hbm_write_bytes_per_launch": round(w),
+           "hbm_read_bytes_per_launch": round(r), "algorithmic_bytes_per_launch": alg,
+           "kernel_avg_ns": e.get("avg_ns"), "valu_issue_frac": e.get("valu_issue_frac"),
+           "lds_busy_frac": e.get("lds_busy_frac"), "lds_conflict_frac": e.get("lds_conflict_frac"),
+           "method": "rocprofv3 --pmc WRITE_SIZE / --pmc FETCH_SIZE in separate passes "
+                     "(--kernel-trace only), KiB x1024, FETCH_SIZE x2 (gfx950 correction)",
+           "source": os.path.relpath(d, REPO)}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

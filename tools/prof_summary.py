@@ -59,6 +59,14 @@ def main():
             e["valu_insts_per_wave"] = c["SQ_INSTS_VALU"] / max(c["SQ_WAVES"], 1)
         if "GRBM_GUI_ACTIVE" in c and "avg_ns" in e:
             e["eff_clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / e["avg_ns"]
+        if "GRBM_GUI_ACTIVE" in c:
+            cyc = c["GRBM_GUI_ACTIVE"] / 8                 # per-XCD GPU cycles of the dispatch
+            if "SQ_ACTIVE_INST_VALU" in c:                 # 4 issue cycles per wave64 VALU op
+                e["valu_issue_frac"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (cyc * 1024)
+            if "SQ_LDS_IDX_ACTIVE" in c:
+                e["lds_busy_frac"] = c["SQ_LDS_IDX_ACTIVE"] / (cyc * 256)
+        if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_LDS_IDX_ACTIVE"):
+            e["lds_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
         summary[k] = e
     json.dump(summary, sys.stdout, indent=1)
     print()
