@@ -594,6 +594,11 @@ double gss_carr_advance(double carr, double step, int64_t n)
     return gss_carr_walk_cc(carr, step, n);
 }
 
+double gss_carr_advance_ck(double carr, double step, int n, double *ck)
+{
+    return gss_carr_walk_ck(carr, step, n, ck);
+}
+
 double gss_code_advance(double code, double step, int64_t n, int32_t *icode, int32_t *ibit,
                         int32_t *iword)
 {

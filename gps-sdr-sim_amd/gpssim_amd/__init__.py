@@ -77,6 +77,7 @@ _SIGS = {
     "gss_scn_plan_seconds": (C.c_double, [_P]),
     "gss_scn_close": (C.c_int, [_P]),
     "gss_carr_advance": (C.c_double, [C.c_double, C.c_double, C.c_int64]),
+    "gss_carr_advance_ck": (C.c_double, [C.c_double, C.c_double, C.c_int, C.c_void_p]),
     "gss_code_advance": (C.c_double, [C.c_double, C.c_double, C.c_int64,
                                       C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                       C.POINTER(C.c_int32)]),
@@ -130,6 +131,13 @@ def lut():
 
 def carr_advance(carr, step, n):
     return lib().gss_carr_advance(carr, step, n)
+
+
+def carr_advance_ck(carr, step, n):
+    """(phase after n samples, the NCK checkpoints of the block)"""
+    ck = np.zeros(NCK)
+    end = lib().gss_carr_advance_ck(carr, step, n, _ptr(ck))
+    return end, ck
 
 
 def code_advance(code, step, n, icode, ibit, iword):

@@ -181,6 +181,10 @@ int gss_scn_close(gss_scn *s);
 /* Exact carrier-chain helpers (exported for tests): advance the reference recurrence
    carr += step; wrap into [0,1) (gpssim.c:2245-2250) by n samples, exactly.                   */
 double gss_carr_advance(double carr, double step, int64_t n);
+/* Same over one block of n samples, also recording the GSS_NCK carrier checkpoints of the
+   block (ck[j] = phase at sample (j*n)/GSS_NCK) for gss_synth_*'s carr_ck.  Returns the phase
+   after the block, i.e. the next block's carr0.                                               */
+double gss_carr_advance_ck(double carr, double step, int n, double *ck);
 /* Same for the code phase with its chip/bit/word counters (gpssim.c:2212-2241).               */
 double gss_code_advance(double code, double step, int64_t n, int32_t *icode, int32_t *ibit,
                         int32_t *iword);

@@ -52,6 +52,11 @@ def test_carrier_walks_exact(seed):
         assert W.wc_carr_bf(x, s, n, C.byref(nw)) == want, ("branch-free", x, s, n)
         assert W.wc_carr_trip(x, s, n) == want, ("specialised trip", x, s, n)
         assert G.carr_advance(x, s, n) == want
+        if n < 1 << 31 and seed == 1:
+            end, ck = G.carr_advance_ck(x, s, n)
+            assert end == want
+            at = [j * n // G.NCK for j in range(G.NCK)]
+            assert np.array_equal(ck, oracle.carr_brute_trace(x, s, at)), ("ck", x, s, n)
 
 
 @pytest.mark.parametrize("seed", [4, 5])
