@@ -82,6 +82,11 @@ def main():
     ap.add_argument("--no-ck", action="store_true",
                     help="do not pass the planner's carrier checkpoints (GPU walks whole blocks)")
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 8))
+    ap.add_argument("--pipeline", action="store_true",
+                    help="run Stage A of batch k+1 on a second stream beside Stage B of batch k "
+                         "(gss_anchor_device/gss_render_device) instead of one gss_synth_device "
+                         "call per step; slower on MI355X today (Stage A waves displace Stage B "
+                         "workgroups), kept for measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,11 +131,47 @@ def main():
     nch_max = int(nch.max())
     stream = torch.cuda.current_stream(dev_t).cuda_stream
 
-    def step():
+    ck_ptr = 0 if args.no_ck else d_ck.data_ptr()
+
+    def step_serial():
         dev.synth_device(d_blk.data_ptr(), d_nch.data_ptr(), nch_max, d_ca.data_ptr(), len(ca),
                          d_nav.data_ptr(), len(nav), nblk, npb, args.fmt, out.data_ptr(),
-                         0, 0, stream, ck_ptr=0 if args.no_ck else d_ck.data_ptr())
+                         0, 0, stream, ck_ptr=ck_ptr)
 
+    # --pipeline: batch k is rendered (Stage B) on the main stream while Stage A of batch k+1
+    # runs on a second, higher-priority stream into the other anchor set.  Every step still runs
+    # one full Stage A and one full Stage B; events order the ping-pong sets.
+    s_b = torch.cuda.current_stream(dev_t)
+    s_a = torch.cuda.Stream(dev_t, priority=-1)
+    ev_a = [torch.cuda.Event() for _ in range(2)]
+    ev_b = [torch.cuda.Event() for _ in range(2)]
+    pipe = {"k": 0}
+
+    def anchor(k):
+        st = k % 2
+        if k >= 2:                    # set st was last read by render(k-2)
+            s_a.wait_event(ev_b[st])
+        dev.anchor_device(st, d_blk.data_ptr(), d_nch.data_ptr(), nch_max, nblk, npb,
+                          ck_ptr=ck_ptr, stream=s_a.cuda_stream)
+        ev_a[st].record(s_a)
+
+    def render(k):
+        st = k % 2
+        s_b.wait_event(ev_a[st])
+        dev.render_device(st, d_blk.data_ptr(), d_nch.data_ptr(), nch_max, d_ca.data_ptr(),
+                          len(ca), d_nav.data_ptr(), len(nav), nblk, npb, args.fmt,
+                          out.data_ptr(), stream=s_b.cuda_stream)
+        ev_b[st].record(s_b)
+
+    def step_pipelined():
+        k = pipe["k"]
+        render(k)
+        anchor(k + 1)
+        pipe["k"] = k + 1
+
+    step = step_pipelined if args.pipeline else step_serial
+    if args.pipeline:
+        anchor(0)                     # pipeline prologue (untimed)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev_t)
@@ -176,7 +217,9 @@ def main():
         "data": "synthetic: deterministic static-receiver scenario (brdc3540.14n), no dataset",
         "config": {"workload": workload, "samples_per_gpu": samples_rank,
                    "carrier_checkpoints": 0 if args.no_ck else 8,
-                   "channels_max": nch_max, "parallelism": f"time-window shards x{world}"},
+                   "channels_max": nch_max, "parallelism": f"time-window shards x{world}",
+                   "stages": "pipelined (A of batch k+1 beside B of k)" if args.pipeline
+                   else "serial (A then B, one stream)"},
         "x_realtime": round(value / (FS / 1e6), 1),
         "stages_ms": {"checkpoint": round(ck_ms, 3), "synthesis": round(syn_ms, 3),
                       "launches_timed": n_launch},

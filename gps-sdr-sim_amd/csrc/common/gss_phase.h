@@ -473,6 +473,10 @@ GSS_HD double gss_seg_states(int kind, double v, double st, uint32_t cnt, int po
     return v;
 }
 
+#ifndef GSS_CODE_MACRO
+#define GSS_CODE_MACRO 10        /* real steps right after a code wrap (gss_code_seg_states_bf) */
+#endif
+
 /* "Some lane of the wave" on the GPU (uniform loop control); the chain itself on the host. */
 #if defined(__HIP_DEVICE_COMPILE__)
 #define GSS_ANY(c) (__builtin_amdgcn_ballot_w64(c) != 0)
@@ -563,6 +567,19 @@ GSS_HD void gss_code_seg_states_bf(double v, double st, uint32_t cnt, int n, int
                 seg++;
                 n0 += R;
             }
+        }
+        {
+            /* After a wrap (v < st) the next binades are tiny: five trips cover the first ~10
+               samples.  Take GSS_CODE_MACRO real steps instead, when neither a segment start,
+               the block end nor a wrap (the steps rise monotonically) falls inside. */
+            double vm = v;
+            for (int i = 0; i < GSS_CODE_MACRO; i++)
+                vm = vm + st;
+            const int mac = (v < st) & (vm < GSS_CA_SEQ_LEN_D) &
+                            (left > (double)GSS_CODE_MACRO) &
+                            ((seg >= nseg) | (n0 > pa + (double)GSS_CODE_MACRO));
+            v = mac ? vm : v;
+            left = mac ? left - (double)GSS_CODE_MACRO : left;
         }
         if (!GSS_ANY((left > 0.0) & (seg < nseg)))
             break;

@@ -472,12 +472,14 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
 struct gss_dev {
     int ordinal;
     int seg_r = 1024;                    /* samples per Stage-B lane (env GSS_SEG_R)   */
-    double *seg_carr = nullptr, *seg_code = nullptr; /* segment-start states [blocks][16][nsegp] */
-    uint32_t *seg_cnt = nullptr;
-    size_t seg_cap = 0;
+    struct anchor_set {                  /* segment-start states [blocks][16][nsegp]     */
+        double *carr = nullptr, *code = nullptr;
+        uint32_t *cnt = nullptr;
+        size_t cap = 0;
+    } set[2];                            /* two sets: Stage A of batch k+1 beside B of k  */
     static constexpr int RING = 256;
-    hipEvent_t ev[RING][3];
-    int n_ev = 0;
+    hipEvent_t ev_a[RING][2], ev_b[RING][2];   /* start/end of each stage launch          */
+    int n_a = 0, n_b = 0;
     lut_arg lut;
     void *h_in = nullptr; size_t h_in_cap = 0;
     void *d_out = nullptr; size_t d_out_cap = 0;
@@ -521,8 +523,10 @@ extern "C" int gss_dev_open(gss_dev **out, int ordinal)
     if (r && atoi(r) >= 256 && atoi(r) % 256 == 0)
         d->seg_r = atoi(r);
     for (int i = 0; i < gss_dev::RING; i++)
-        for (int j = 0; j < 3; j++)
-            HIP_TRY(hipEventCreate(&d->ev[i][j]));
+        for (int j = 0; j < 2; j++) {
+            HIP_TRY(hipEventCreate(&d->ev_a[i][j]));
+            HIP_TRY(hipEventCreate(&d->ev_b[i][j]));
+        }
     int32_t s[512], c[512];
     gss_lut(s, c);
     for (int i = 0; i < 512; i++) {
@@ -538,13 +542,19 @@ extern "C" int gss_dev_close(gss_dev *d)
 {
     if (!d) return 0;
     (void)hipSetDevice(d->ordinal);
-    void *bufs[] = {d->seg_carr, d->seg_code, d->seg_cnt,
-                    d->h_in, d->d_out, d->d_cend, d->d_status};
+    for (auto &a : d->set) {
+        (void)hipFree(a.carr);
+        (void)hipFree(a.code);
+        (void)hipFree(a.cnt);
+    }
+    void *bufs[] = {d->h_in, d->d_out, d->d_cend, d->d_status};
     for (void *p : bufs)
         (void)hipFree(p);
     for (int i = 0; i < gss_dev::RING; i++)
-        for (int j = 0; j < 3; j++)
-            (void)hipEventDestroy(d->ev[i][j]);
+        for (int j = 0; j < 2; j++) {
+            (void)hipEventDestroy(d->ev_a[i][j]);
+            (void)hipEventDestroy(d->ev_b[i][j]);
+        }
     delete d;
     return 0;
 }
@@ -553,24 +563,34 @@ static int nseg_of(int n, int r) { return (n + r - 1) / r; }
 /* anchor row stride: the segment starts and one dummy slot (gss_code_seg_states_bf) */
 static int nsegp_of(int n, int r) { return (nseg_of(n, r) + 1 + 31) & ~31; }
 
+static int reserve_set(gss_dev *d, int set, int max_blocks, int n_per_blk)
+{
+    gss_dev::anchor_set &a = d->set[set];
+    size_t need = (size_t)max_blocks * GSS_MAXCH * (size_t)nsegp_of(n_per_blk, d->seg_r);
+    if (need <= a.cap)
+        return 0;
+    (void)hipFree(a.carr);
+    (void)hipFree(a.code);
+    (void)hipFree(a.cnt);
+    a.carr = a.code = nullptr;
+    a.cnt = nullptr;
+    a.cap = 0;
+    HIP_TRY(hipMalloc(&a.carr, need * sizeof(double)));
+    HIP_TRY(hipMalloc(&a.code, need * sizeof(double)));
+    HIP_TRY(hipMalloc(&a.cnt, need * sizeof(uint32_t)));
+    a.cap = need;
+    return 0;
+}
+
 extern "C" int gss_dev_reserve(gss_dev *d, int max_blocks, int n_per_blk)
 {
     if (!d || max_blocks <= 0 || n_per_blk <= 0)
         return gss_fail(GSS_E_ARG, "invalid reserve arguments");
     HIP_TRY(hipSetDevice(d->ordinal));
-    size_t need = (size_t)max_blocks * GSS_MAXCH * (size_t)nsegp_of(n_per_blk, d->seg_r);
-    if (need <= d->seg_cap)
-        return 0;
-    void *old[] = {d->seg_carr, d->seg_code, d->seg_cnt};
-    for (void *p : old)
-        (void)hipFree(p);
-    d->seg_carr = d->seg_code = nullptr;
-    d->seg_cnt = nullptr;
-    d->seg_cap = 0;
-    HIP_TRY(hipMalloc(&d->seg_carr, need * sizeof(double)));
-    HIP_TRY(hipMalloc(&d->seg_code, need * sizeof(double)));
-    HIP_TRY(hipMalloc(&d->seg_cnt, need * sizeof(uint32_t)));
-    d->seg_cap = need;
+    for (int set = 0; set < 2; set++) {
+        int rc = reserve_set(d, set, max_blocks, n_per_blk);
+        if (rc) return rc;
+    }
     return 0;
 }
 
@@ -598,49 +618,108 @@ static synth_fn pick_kernel(int fmt, int nchp)
     }
 }
 
+extern "C" int gss_anchor_device(gss_dev *d, int set, const gss_chan_blk_t *blk,
+                                 const int32_t *nch, int nch_max, const double *carr_ck,
+                                 int nblk, int n_per_blk, double *carr_end, void *stream)
+{
+    if (!d || !blk || !nch || nblk <= 0 || n_per_blk <= 0 || set < 0 || set > 1)
+        return gss_fail(GSS_E_ARG, "invalid anchor arguments");
+    if (nch_max > GSS_MAXCH)
+        return gss_fail(GSS_E_ARG, "nch_max %d > %d", nch_max, GSS_MAXCH);
+    HIP_TRY(hipSetDevice(d->ordinal));
+    int rc = reserve_set(d, set, nblk, n_per_blk);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const int R = d->seg_r;
+    const int nseg = nseg_of(n_per_blk, R), nsegp = nsegp_of(n_per_blk, R);
+    const int nchp = nch_max < 1 ? 1 : nch_max;
+    const gss_dev::anchor_set &a = d->set[set];
+    /* channel-major waves; code chains one lane per block (first: they are the long pole),
+       carrier chains one lane per block sub-chain (GSS_NCK per block with checkpoints) */
+    const int a_blocks = nchp * ((nblk + ANCHOR_THREADS - 1) / ANCHOR_THREADS) +
+                         nchp * ((nblk * (carr_ck ? GSS_NCK : 1) + ANCHOR_THREADS - 1) /
+                                 ANCHOR_THREADS);
+    hipEvent_t *ev = d->ev_a[d->n_a % gss_dev::RING];
+    d->n_a++;
+    HIP_TRY(hipEventRecord(ev[0], st));
+    hipLaunchKernelGGL(gss_anchor_kernel, dim3(a_blocks), dim3(ANCHOR_THREADS), 0, st, blk, nch,
+                       carr_ck, nblk, nchp, n_per_blk, nseg, nsegp, R, a.carr, a.code, a.cnt,
+                       carr_end);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev[1], st));
+    return 0;
+}
+
+extern "C" int gss_render_device(gss_dev *d, int set, const gss_chan_blk_t *blk,
+                                 const int32_t *nch, int nch_max, const uint32_t *ca_bits,
+                                 int n_ca, const uint32_t *nav, int n_nav, int nblk,
+                                 int n_per_blk, int fmt, void *out, int32_t *status, void *stream)
+{
+    (void)n_ca; (void)n_nav;
+    if (!d || !blk || !nch || !ca_bits || !out || nblk <= 0 || n_per_blk <= 0 || set < 0 ||
+        set > 1)
+        return gss_fail(GSS_E_ARG, "invalid render arguments");
+    const size_t bb = gss_block_bytes(n_per_blk, fmt);
+    if (bb == 0)
+        return gss_fail(GSS_E_ARG, "invalid format %d for %d samples/block", fmt, n_per_blk);
+    const int R = d->seg_r;
+    const int nseg = nseg_of(n_per_blk, R), nsegp = nsegp_of(n_per_blk, R);
+    const gss_dev::anchor_set &a = d->set[set];
+    if ((size_t)nblk * GSS_MAXCH * (size_t)nsegp > a.cap)
+        return gss_fail(GSS_E_STATE, "anchor set %d holds no Stage A output of this size", set);
+    const int nchp = nch_max < 1 ? 1 : nch_max;
+    if (nchp > GSS_MAXCH)
+        return gss_fail(GSS_E_ARG, "nch_max %d > %d", nch_max, GSS_MAXCH);
+    synth_fn fn = pick_kernel(fmt, nchp);
+    if (!fn)
+        return gss_fail(GSS_E_ARG, "no kernel for fmt=%d nch=%d", fmt, nchp);
+    HIP_TRY(hipSetDevice(d->ordinal));
+    hipStream_t st = (hipStream_t)stream;
+    hipEvent_t *ev = d->ev_b[d->n_b % gss_dev::RING];
+    d->n_b++;
+    const int wg_per_blk = (nseg + SYNTH_THREADS - 1) / SYNTH_THREADS;
+    HIP_TRY(hipEventRecord(ev[0], st));
+    hipLaunchKernelGGL(fn, dim3(nblk * wg_per_blk), dim3(SYNTH_THREADS), 0, st, blk, nch, ca_bits,
+                       nav, a.carr, a.code, a.cnt, d->lut, n_per_blk, nseg, nsegp, R, wg_per_blk,
+                       (uint8_t *)out, bb, status);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev[1], st));
+    return 0;
+}
+
 extern "C" int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
                                 int nch_max, const double *carr_ck, const uint32_t *ca_bits,
                                 int n_ca,
                                 const uint32_t *nav, int n_nav, int nblk, int n_per_blk, int fmt,
                                 void *out, double *carr_end, int32_t *status, void *stream)
 {
-    (void)n_ca; (void)n_nav;
     if (!d || !blk || !nch || !ca_bits || !out || nblk <= 0 || n_per_blk <= 0)
         return gss_fail(GSS_E_ARG, "invalid synth arguments");
-    size_t bb = gss_block_bytes(n_per_blk, fmt);
-    if (bb == 0)
+    if (gss_block_bytes(n_per_blk, fmt) == 0)
         return gss_fail(GSS_E_ARG, "invalid format %d for %d samples/block", fmt, n_per_blk);
-    HIP_TRY(hipSetDevice(d->ordinal));
-    int rc = gss_dev_reserve(d, nblk, n_per_blk);
+    int rc = gss_anchor_device(d, 0, blk, nch, nch_max, carr_ck, nblk, n_per_blk, carr_end,
+                               stream);
     if (rc) return rc;
-    hipStream_t st = (hipStream_t)stream;
-    const int R = d->seg_r;
-    int nseg = nseg_of(n_per_blk, R), nsegp = nsegp_of(n_per_blk, R);
-    int nchp = nch_max < 1 ? 1 : nch_max;          /* kernel instance; fewer channels padded */
-    if (nchp > GSS_MAXCH)
-        return gss_fail(GSS_E_ARG, "nch_max %d > %d", nch_max, GSS_MAXCH);
-    synth_fn fn = pick_kernel(fmt, nchp);
-    if (!fn)
-        return gss_fail(GSS_E_ARG, "no kernel for fmt=%d nch=%d", fmt, nchp);
+    return gss_render_device(d, 0, blk, nch, nch_max, ca_bits, n_ca, nav, n_nav, nblk, n_per_blk,
+                             fmt, out, status, stream);
+}
 
-    hipEvent_t *ev = d->ev[d->n_ev % gss_dev::RING];
-    d->n_ev++;
-    /* Stage A grid: channel-major waves; code chains one lane per block, carrier chains one lane
-       per block sub-chain (GSS_NCK per block with the planner's checkpoints) */
-    int a_blocks = nchp * ((nblk + ANCHOR_THREADS - 1) / ANCHOR_THREADS) +
-                   nchp * ((nblk * (carr_ck ? GSS_NCK : 1) + ANCHOR_THREADS - 1) / ANCHOR_THREADS);
-    HIP_TRY(hipEventRecord(ev[0], st));
-    hipLaunchKernelGGL(gss_anchor_kernel, dim3(a_blocks), dim3(ANCHOR_THREADS), 0, st, blk, nch,
-                       carr_ck, nblk, nchp, n_per_blk, nseg, nsegp, R, d->seg_carr, d->seg_code, d->seg_cnt,
-                       carr_end);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ev[1], st));
-    int wg_per_blk = (nseg + SYNTH_THREADS - 1) / SYNTH_THREADS;
-    hipLaunchKernelGGL(fn, dim3(nblk * wg_per_blk), dim3(SYNTH_THREADS), 0, st, blk, nch, ca_bits,
-                       nav, d->seg_carr, d->seg_code, d->seg_cnt, d->lut,
-                       n_per_blk, nseg, nsegp, R, wg_per_blk, (uint8_t *)out, bb, status);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ev[2], st));
+/* average [ms] of the last min(n, RING) launches of one stage's event ring */
+static int ring_avg(hipEvent_t (*ev)[2], int n, double *avg)
+{
+    const int cnt = n < gss_dev::RING ? n : gss_dev::RING;
+    double acc = 0.0;
+    if (cnt > 0) {
+        HIP_TRY(hipEventSynchronize(ev[(n - 1) % gss_dev::RING][1]));
+        for (int i = 0; i < cnt; i++) {
+            hipEvent_t *e = ev[(n - 1 - i) % gss_dev::RING];
+            float t = 0.f;
+            HIP_TRY(hipEventElapsedTime(&t, e[0], e[1]));
+            acc += t;
+        }
+        acc /= cnt;
+    }
+    *avg = acc;
     return 0;
 }
 
@@ -648,25 +727,15 @@ extern "C" int gss_dev_timing(gss_dev *d, int reset, int *n, float *ckpt_ms, flo
 {
     if (!d) return gss_fail(GSS_E_ARG, "null device");
     if (reset) {
-        d->n_ev = 0;
+        d->n_a = d->n_b = 0;
         return 0;
     }
-    int cnt = d->n_ev < gss_dev::RING ? d->n_ev : gss_dev::RING;
     double a = 0.0, b = 0.0;
-    if (cnt > 0) {
-        HIP_TRY(hipEventSynchronize(d->ev[(d->n_ev - 1) % gss_dev::RING][2]));
-        for (int i = 0; i < cnt; i++) {
-            hipEvent_t *e = d->ev[(d->n_ev - 1 - i) % gss_dev::RING];
-            float t0 = 0.f, t1 = 0.f;
-            HIP_TRY(hipEventElapsedTime(&t0, e[0], e[1]));
-            HIP_TRY(hipEventElapsedTime(&t1, e[1], e[2]));
-            a += t0;
-            b += t1;
-        }
-        a /= cnt;
-        b /= cnt;
-    }
-    if (n) *n = cnt;
+    int rc = ring_avg(d->ev_a, d->n_a, &a);
+    if (rc) return rc;
+    rc = ring_avg(d->ev_b, d->n_b, &b);
+    if (rc) return rc;
+    if (n) *n = d->n_b < gss_dev::RING ? d->n_b : gss_dev::RING;
     if (ckpt_ms) *ckpt_ms = (float)a;
     if (synth_ms) *synth_ms = (float)b;
     return 0;

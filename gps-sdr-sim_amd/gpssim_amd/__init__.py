@@ -63,6 +63,10 @@ _SIGS = {
     "gss_dev_close": (C.c_int, [_P]),
     "gss_dev_reserve": (C.c_int, [_P, C.c_int, C.c_int]),
     "gss_block_bytes": (C.c_size_t, [C.c_int, C.c_int]),
+    "gss_anchor_device": (C.c_int, [_P, C.c_int, _P, _P, C.c_int, _P, C.c_int, C.c_int, _P,
+                                    _P]),
+    "gss_render_device": (C.c_int, [_P, C.c_int, _P, _P, C.c_int, _P, C.c_int, _P, C.c_int,
+                                    C.c_int, C.c_int, C.c_int, _P, _P, _P]),
     "gss_synth_device": (C.c_int, [_P, _P, _P, C.c_int, _P, _P, C.c_int, _P, C.c_int,
                                    C.c_int, C.c_int, C.c_int, _P, _P, _P, _P]),
     "gss_synth_host": (C.c_int, [_P, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int,
@@ -95,6 +99,13 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise OSError(f"{LIB_PATH} missing: run `make -C gps-sdr-sim_amd` "
                           "(or __graft_entry__.build())")
+        try:
+            # A process that also uses PyTorch-ROCm must resolve libamdhip64 to torch's copy:
+            # load torch first so the library binds to the already-loaded runtime (two HIP
+            # runtimes in one process leave torch seeing no GPU).
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)
@@ -273,11 +284,24 @@ class Device:
                                       n_nav, nblk, n_per_blk, fmt, out_ptr,
                                       carr_end_ptr or None, status_ptr or None, stream or None))
 
+    def anchor_device(self, set_, blk_ptr, nch_ptr, nch_max, nblk, n_per_blk, ck_ptr=0,
+                      carr_end_ptr=0, stream=0):
+        """Stage A of a batch into anchor set set_ (0/1), asynchronous on stream."""
+        _check(lib().gss_anchor_device(self._h, set_, blk_ptr, nch_ptr, nch_max, ck_ptr or None,
+                                       nblk, n_per_blk, carr_end_ptr or None, stream or None))
+
+    def render_device(self, set_, blk_ptr, nch_ptr, nch_max, ca_ptr, n_ca, nav_ptr, n_nav, nblk,
+                      n_per_blk, fmt, out_ptr, status_ptr=0, stream=0):
+        """Stage B of a batch from anchor set set_, asynchronous on stream."""
+        _check(lib().gss_render_device(self._h, set_, blk_ptr, nch_ptr, nch_max, ca_ptr, n_ca,
+                                       nav_ptr, n_nav, nblk, n_per_blk, fmt, out_ptr,
+                                       status_ptr or None, stream or None))
+
     def timing_reset(self):
         _check(lib().gss_dev_timing(self._h, 1, None, None, None))
 
     def timing(self):
-        """(launches, avg checkpoint-stage ms, avg synthesis-stage ms) since the last reset."""
+        """(Stage B launches, avg Stage A ms, avg Stage B ms) since the last reset."""
         n, a, b = C.c_int(), C.c_float(), C.c_float()
         _check(lib().gss_dev_timing(self._h, 0, C.byref(n), C.byref(a), C.byref(b)))
         return n.value, a.value, b.value

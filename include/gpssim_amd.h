@@ -76,8 +76,8 @@ typedef struct gss_dev gss_dev;
 int gss_dev_open(gss_dev **out, int ordinal);
 int gss_dev_close(gss_dev *d);
 
-/* Pre-size the checkpoint workspace for batches of up to `max_blocks` blocks of `n_per_blk`
-   samples, so that gss_synth_device() performs no allocation (graph-capturable).              */
+/* Pre-size both anchor sets for batches of up to `max_blocks` blocks of `n_per_blk` samples,
+   so that the synthesis calls perform no allocation (graph-capturable).                       */
 int gss_dev_reserve(gss_dev *d, int max_blocks, int n_per_blk);
 
 /* Bytes of output one block produces: n*4 (SC16), n*2 (SC08), n/4 (SC01; n%4==0 required,
@@ -108,16 +108,31 @@ int gss_synth_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch, 
                      int nblk, int n_per_blk, int fmt, void *out, double *carr_end,
                      int32_t *status, void *stream);
 
+/* gss_synth_device in its two stages, for pipelining consecutive batches (Stage A of batch k+1
+   on one stream while Stage B renders batch k on another).  Stage A writes the exact state at
+   every segment start of the batch into anchor set `set` (0 or 1, device-owned buffers); Stage
+   B renders from that set.  Arguments as gss_synth_device; the caller orders the two on its
+   streams (events) and passes Stage B the same blk/nch/nch_max/nblk/n_per_blk as Stage A of
+   that set.  gss_synth_device == gss_anchor_device(set 0) then gss_render_device(set 0) on one
+   stream.                                                                                     */
+int gss_anchor_device(gss_dev *d, int set, const gss_chan_blk_t *blk, const int32_t *nch,
+                      int nch_max, const double *carr_ck, int nblk, int n_per_blk,
+                      double *carr_end, void *stream);
+int gss_render_device(gss_dev *d, int set, const gss_chan_blk_t *blk, const int32_t *nch,
+                      int nch_max, const uint32_t *ca_bits, int n_ca, const uint32_t *nav,
+                      int n_nav, int nblk, int n_per_blk, int fmt, void *out, int32_t *status,
+                      void *stream);
+
 /* Same, from host buffers: uploads inputs, runs, downloads `out` (and carr_end if non-NULL),
    synchronises.  Convenience for the CLI and tests; the bench uses gss_synth_device().        */
 int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
                    const double *carr_ck, const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
                    int nblk, int n_per_blk, int fmt, void *out, double *carr_end);
 
-/* Kernel timing from HIP events recorded on the launch stream around each stage of every
-   gss_synth_device() call (ring of the last 256 calls).  reset!=0 clears the ring (no sync);
-   otherwise waits for the last call and returns the number of calls n and the average duration
-   [ms] of the checkpoint stage and of the synthesis stage over them.                          */
+/* Kernel timing from HIP events recorded on the launch stream around every Stage A and Stage B
+   launch (gss_synth_device, gss_anchor_device, gss_render_device; rings of the last 256 of
+   each).  reset!=0 clears the rings (no sync); otherwise waits for the last launches and
+   returns the number n of Stage B launches and the average duration [ms] of each stage.      */
 int gss_dev_timing(gss_dev *d, int reset, int *n, float *ckpt_ms, float *synth_ms);
 
 /* ------------------------------------------------------------------------------------------ */

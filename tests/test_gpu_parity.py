@@ -174,3 +174,56 @@ def test_cli_end_to_end(golden):
         assert "Done!" in r.stderr
         h = hashlib.sha256(open(out, "rb").read()).hexdigest()
     assert h == golden["static_d30_b16"]["sha256"]
+
+
+def test_pipelined_stages_bit_exact(golden):
+    """The split ABI as bench.py drives it: Stage A of batch k+1 (anchor set (k+1)%2) on one
+    stream while Stage B renders batch k on another, device-resident inputs; every block equals
+    the reference's golden hash."""
+    import torch
+    dev_t = torch.device("cuda", 0)
+    s = G.Scenario(NAV, llh=LOC, duration=30.0, data_format=16)
+    batches = [s.next(100, with_ck=True) for _ in range(3)]
+    nav = s.nav_table()
+    ca = G.ca_table()
+    npb = s.n_per_blk
+    bb = G.block_bytes(npb, 16)
+    d = G.Device(0)
+    try:
+        d_ca = torch.from_numpy(ca.view(np.int32)).to(dev_t)
+        d_nav = torch.from_numpy(nav.view(np.int32)).to(dev_t)
+        ins = [(torch.from_numpy(b.view(np.uint8).reshape(-1)).to(dev_t),
+                torch.from_numpy(n).to(dev_t), torch.from_numpy(c).to(dev_t), len(n),
+                int(n.max())) for b, n, c in batches]
+        outs = [torch.empty(x[3] * bb, dtype=torch.uint8, device=dev_t) for x in ins]
+        s_a = torch.cuda.Stream(dev_t, priority=-1)
+        s_b = torch.cuda.Stream(dev_t)
+        ev_a = [torch.cuda.Event() for _ in range(2)]
+        ev_b = [torch.cuda.Event() for _ in range(2)]
+
+        def anchor(k):
+            b, n, c, nb, nm = ins[k]
+            if k >= 2:
+                s_a.wait_event(ev_b[k % 2])
+            d.anchor_device(k % 2, b.data_ptr(), n.data_ptr(), nm, nb, npb, ck_ptr=c.data_ptr(),
+                            stream=s_a.cuda_stream)
+            ev_a[k % 2].record(s_a)
+
+        anchor(0)
+        for k in range(3):
+            b, n, c, nb, nm = ins[k]
+            s_b.wait_event(ev_a[k % 2])
+            d.render_device(k % 2, b.data_ptr(), n.data_ptr(), nm, d_ca.data_ptr(), len(ca),
+                            d_nav.data_ptr(), len(nav), nb, npb, 16, outs[k].data_ptr(),
+                            stream=s_b.cuda_stream)
+            ev_b[k % 2].record(s_b)
+            if k + 1 < 3:
+                anchor(k + 1)
+        torch.cuda.synchronize(dev_t)
+        whole = b"".join(o.cpu().numpy().tobytes() for o in outs)
+    finally:
+        d.close()
+    hashes = [hashlib.sha256(whole[i * bb:(i + 1) * bb]).hexdigest()[:16]
+              for i in range(len(whole) // bb)]
+    assert hashes == golden["static_d30_b16"]["block_sha16"][:len(hashes)]
+    assert len(hashes) == 299
