@@ -406,6 +406,17 @@ GSS_HD int gss_trip(int kind, double *pv, double s, double rs, double *pleft, do
     return step & wr;
 }
 
+#ifndef GSS_CARR_MACRO
+#define GSS_CARR_MACRO 8         /* real carrier steps near a wrap (gss_seg_states) */
+#endif
+/* one reference carrier step (gpssim.c:2245-2250): on the GPU v_fract_f64 of the sum, which is
+   exactly carr-1 / carr+1 for sums in [0,2) / (-1,1) */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GSS_CARR_STEP(v, s) __builtin_amdgcn_fract((v) + (s))
+#else
+#define GSS_CARR_STEP(v, s) gss_carr_step1((v), (s))
+#endif
+
 /* Exact states at the segment starts n0 = j*seg_r in [pos0, pos1) of one chain (j < nseg),
  * walking from v at position pos0 (Stage A of the GPU path: out_x[j] = phase at n0, out_c[j] =
  * code counters icode|ibit<<8|iword<<16 at n0 for the code chain; arrays indexed by the absolute
@@ -468,6 +479,21 @@ GSS_HD double gss_seg_states(int kind, double v, double st, uint32_t cnt, int po
                 out_c[seg] = n0 == pa ? cnt : cnt_b;
             seg++;
             n0 += R;
+        }
+        if (!code) {
+            /* Carrier phases near 0 sit in tiny binades whose trips cover 1-4 samples each: right
+               after an ascending wrap (v < |s|), and in the last GSS_CARR_MACRO samples before a
+               descending wrap.  Take GSS_CARR_MACRO real steps there instead (the reference's
+               own step, wrap included), when no segment start and not the end fall inside. */
+            const double as = st < 0.0 ? -st : st;
+            double vm = v;
+            for (int i = 0; i < GSS_CARR_MACRO; i++)
+                vm = GSS_CARR_STEP(vm, st);
+            const double lo = kind == GSS_TRIP_CARR_ASC ? as : (double)GSS_CARR_MACRO * as;
+            const int mac = (v < lo) & (left > (double)GSS_CARR_MACRO) &
+                            ((seg >= seg_hi) | (n0 > pa + (double)GSS_CARR_MACRO));
+            v = mac ? vm : v;
+            left = mac ? left - (double)GSS_CARR_MACRO : left;
         }
     }
     return v;
