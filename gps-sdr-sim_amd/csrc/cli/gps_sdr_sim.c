@@ -1,18 +1,93 @@
 /*
  * gps_sdr_sim.c — the command-line program: reference option surface (-e/-u/-g/-c/-l/-t/-T/-d/
- * -o/-s/-b/-i/-v), reference stderr messages, byte-identical gpssim.bin.  The per-sample work
- * runs on the GPU (gss_synth_host); this driver only moves batches of blocks between the host
- * control plane (gss_scn_next) and the sink (fwrite to file or stdout), gpssim.c:2101-2111,
- * 2276-2287.  There is no CPU fallback: without a GPU it exits with an error.
- * Env: GSS_DEVICE (ordinal, default 0), GSS_BATCH (blocks per launch, default 100),
- *      GSS_THREADS (planner threads, default 8).
+ * -o/-s/-b/-i/-v), reference stderr messages, byte-identical gpssim.bin.  The whole block loop
+ * runs in gss_run (host planner thread, GPU stages, pinned downloads); this driver only supplies
+ * the sink (fwrite to file or stdout), gpssim.c:2101-2111, 2276-2287.  There is no CPU
+ * fallback: without a GPU it exits with an error.
+ * Multi-GPU: launched N times with RANK / WORLD_SIZE / LOCAL_RANK set (e.g. `torchrun
+ * --no-python --nproc-per-node N gps-sdr-sim ... -o FILE`), process r synthesises the contiguous
+ * block range [B r/N, B (r+1)/N) on GPU LOCAL_RANK and pwrite()s it at its byte offset of FILE
+ * (every rank ftruncate()s FILE to the run's size first, safe in any order): the same file as
+ * one process writes, with no collective.
+ * Env: GSS_DEVICE (ordinal; default LOCAL_RANK or 0), GSS_BATCH (blocks per launch, default
+ *      100), GSS_THREADS (planner threads, default 8).
  */
+#include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 #include "gpssim_amd.h"
 #include "cli_args.h"
+
+static int write_sink(void *user, const void *bytes, size_t n, int64_t first_block, int nblocks)
+{
+    (void)first_block; (void)nblocks;
+    return fwrite(bytes, 1, n, (FILE *)user) == n ? 0 : 1;
+}
+
+typedef struct { int fd; size_t block_bytes; } pwrite_ctx;
+
+static int pwrite_sink(void *user, const void *bytes, size_t n, int64_t first_block, int nblocks)
+{
+    (void)nblocks;
+    const pwrite_ctx *c = (const pwrite_ctx *)user;
+    off_t off = (off_t)first_block * (off_t)c->block_bytes;
+    const char *p = (const char *)bytes;
+    while (n > 0) {
+        ssize_t w = pwrite(c->fd, p, n, off);
+        if (w <= 0)
+            return 1;
+        p += w;
+        off += w;
+        n -= (size_t)w;
+    }
+    return 0;
+}
+
+static int env_int(const char *name, int dflt)
+{
+    const char *v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+
+/* One process of a multi-GPU run: its block range, pwrite()n at its offset of the output file. */
+static int run_rank(const gss_cli_t *cli, gss_scn *scn, const gss_scn_info_t *info, int rank,
+                    int world)
+{
+    if (!strcmp("-", cli->out_file)) {
+        fprintf(stderr, "ERROR: a multi-process run needs an output file (-o FILE).\n");
+        return 1;
+    }
+    gss_dev *dev = NULL;
+    if (gss_dev_open(&dev, env_int("GSS_DEVICE", env_int("LOCAL_RANK", 0)))) {
+        fprintf(stderr, "ERROR: %s\n", gss_last_error());
+        return 1;
+    }
+    const int64_t nb = info->n_blocks;
+    const int64_t first = nb * rank / world, last = nb * (rank + 1) / world;
+    pwrite_ctx c = {-1, gss_block_bytes(info->n_per_blk, info->data_format)};
+    c.fd = open(cli->out_file, O_WRONLY | O_CREAT, 0644);
+    if (c.fd < 0 || ftruncate(c.fd, (off_t)nb * (off_t)c.block_bytes)) {
+        fprintf(stderr, "ERROR: Failed to open output file.\n");
+        return 1;
+    }
+    if (gss_run(dev, scn, first, last - first, env_int("GSS_BATCH", 100),
+                env_int("GSS_THREADS", 8), pwrite_sink, &c)) {
+        fprintf(stderr, "\nERROR: rank %d: %s\n", rank, gss_last_error());
+        return 1;
+    }
+    if (close(c.fd)) {
+        fprintf(stderr, "ERROR: rank %d: write failed.\n", rank);
+        return 1;
+    }
+    if (rank == 0)
+        fprintf(stderr, "\nDone!\n");
+    gss_dev_close(dev);
+    gss_scn_close(scn);
+    return 0;
+}
 
 int main(int argc, char **argv)
 {
@@ -27,8 +102,16 @@ int main(int argc, char **argv)
     gss_scn_info_t info;
     gss_scn_info(scn, &info);
 
+    const int world = env_int("WORLD_SIZE", 1), rank = env_int("RANK", 0);
+    if (world < 1 || rank < 0 || rank >= world) {
+        fprintf(stderr, "ERROR: invalid RANK %d / WORLD_SIZE %d.\n", rank, world);
+        return 1;
+    }
+    if (world > 1)
+        return run_rank(&cli, scn, &info, rank, world);
+
     gss_dev *dev = NULL;
-    int ordinal = getenv("GSS_DEVICE") ? atoi(getenv("GSS_DEVICE")) : 0;
+    int ordinal = env_int("GSS_DEVICE", 0);
     if (gss_dev_open(&dev, ordinal)) {
         fprintf(stderr, "ERROR: %s\n", gss_last_error());
         return 1;
@@ -41,41 +124,15 @@ int main(int argc, char **argv)
             return 1;
         }
     }
-    int batch = getenv("GSS_BATCH") ? atoi(getenv("GSS_BATCH")) : 100;
-    int threads = getenv("GSS_THREADS") ? atoi(getenv("GSS_THREADS")) : 8;
+    int batch = env_int("GSS_BATCH", 100);
+    int threads = env_int("GSS_THREADS", 8);
     if (batch < 1) batch = 1;
-    uint32_t ca[32 * GSS_CA_WORDS];
-    gss_ca_table(ca);
-    size_t bb = gss_block_bytes(info.n_per_blk, info.data_format);
-    gss_chan_blk_t *blk = malloc(sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)batch);
-    int32_t *nch = malloc(sizeof(int32_t) * (size_t)batch);
-    unsigned char *out = malloc(bb * (size_t)batch);
-    double *ck = malloc(sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)batch);
-    if (!blk || !nch || !out || !ck) {
-        fprintf(stderr, "ERROR: Failed to allocate I/Q buffer.\n");
-        return 1;
-    }
     clock_t t0 = clock();
-    for (;;) {
-        int nb = 0;
-        if (gss_scn_next(scn, batch, blk, nch, ck, &nb, threads)) {
-            fprintf(stderr, "\nERROR: %s\n", gss_last_error());
-            return 1;
-        }
-        if (nb == 0)
-            break;
-        const uint32_t *nav;
-        int nnav;
-        gss_scn_nav_table(scn, &nav, &nnav);
-        if (gss_synth_host(dev, blk, nch, ck, ca, 32, nav, nnav, nb, info.n_per_blk,
-                           info.data_format, out, NULL)) {
-            fprintf(stderr, "\nERROR: %s\n", gss_last_error());
-            return 1;
-        }
-        if (fwrite(out, 1, bb * (size_t)nb, fp) != bb * (size_t)nb) {
-            fprintf(stderr, "\nERROR: write failed.\n");
-            return 1;
-        }
+    /* planning, upload, both kernel stages, download and fwrite overlap inside gss_run; the
+       sink sees each batch's bytes in run order (gpssim.c:2276/2283/2287) */
+    if (gss_run(dev, scn, 0, -1, batch, threads, write_sink, fp)) {
+        fprintf(stderr, "\nERROR: %s\n", gss_last_error());
+        return 1;
     }
     clock_t t1 = clock();
     fprintf(stderr, "\nDone!\n");
@@ -84,6 +141,5 @@ int main(int argc, char **argv)
     fprintf(stderr, "Process time = %.1f [sec]\n", (double)(t1 - t0) / CLOCKS_PER_SEC);
     gss_dev_close(dev);
     gss_scn_close(scn);
-    free(blk); free(nch); free(out); free(ck);
     return 0;
 }

@@ -1,0 +1,315 @@
+/*
+ * gss_run.hip — the streaming driver: whole run (or a block range of it) from the host control
+ * plane to the caller's byte sink, every stage overlapped.  Replaces the reference's block loop
+ * (gpssim.c:2154-2353: refresh, sample loop, fwrite at 2276/2283/2287, 30 s updates).
+ *
+ *   planner thread   gss_scn_next into pinned slot buffers (+ a snapshot of the nav table)
+ *   main thread      per slot: async H2D, Stage A + B (gss_synth_device), async D2H into a
+ *                    pinned output buffer; then, while the next slot is on the GPU, hands the
+ *                    previous slot's bytes to the sink in run order
+ *
+ * Slots cycle planner -> main -> sink -> planner; a slot's buffers belong to exactly one side at
+ * a time (state under a mutex).  One HIP stream, so H2D(i+1) and the kernels of i+1 queue behind
+ * D2H(i) on the device while the host runs the sink on i-1.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+#include "gpssim_amd.h"
+
+extern "C" int gss_fail(int code, const char *fmt, ...);
+
+#define RUN_TRY(x)                                                                           \
+    do {                                                                                     \
+        hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess)                                                                \
+            return gss_fail(GSS_E_HIP, "HIP error %s at %s:%d", hipGetErrorString(e_),      \
+                            __FILE__, __LINE__);                                             \
+    } while (0)
+
+namespace {
+
+constexpr int NSLOT = 3;
+constexpr size_t SLOT_OUT_MAX = (size_t)256 << 20;     /* pinned output bytes per slot */
+
+enum { FREE, PLANNED };
+
+struct Slot {
+    /* planner side (pinned host memory) */
+    gss_chan_blk_t *blk = nullptr;
+    int32_t *nch = nullptr;
+    double *ck = nullptr;
+    uint32_t *nav = nullptr;
+    int nav_cap = 0, n_nav = 0;
+    int nb = 0, nch_max = 1;
+    int64_t first = 0;               /* run index of the slot's first block */
+    int end = 0, err = 0;            /* last slot / planner error code      */
+    int state = FREE;
+    /* main side */
+    uint8_t *d_in = nullptr;
+    size_t d_in_cap = 0;
+    uint8_t *d_out = nullptr, *h_out = nullptr;
+    int32_t *d_status = nullptr, *h_status = nullptr;
+    hipEvent_t done = nullptr;
+};
+
+struct Run {
+    gss_scn *scn;
+    int batch, threads;
+    int64_t first, last;             /* [first, last) block range of the run */
+    std::mutex mu;
+    std::condition_variable cv;
+    int abort = 0;
+    Slot slot[NSLOT];
+};
+
+size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+/* Fill slot k's pinned buffers with the next batch inside [first, last); blocks before `first`
+   are planned (the carrier chain is serial) and dropped. */
+int plan_into(Run &r, Slot &sl, int64_t *cursor)
+{
+    for (;;) {
+        int64_t want = r.last - *cursor;
+        if (want <= 0) {
+            sl.nb = 0;
+            sl.end = 1;
+            return 0;
+        }
+        int ask = want < r.batch ? (int)want : r.batch;
+        if (*cursor < r.first && r.first - *cursor < ask)
+            ask = (int)(r.first - *cursor);            /* stop exactly at the range start */
+        int nb = 0;
+        int rc = gss_scn_next(r.scn, ask, sl.blk, sl.nch, sl.ck, &nb, r.threads);
+        if (rc)
+            return rc;
+        if (nb == 0) {
+            sl.nb = 0;
+            sl.end = 1;
+            return 0;
+        }
+        int64_t b0 = *cursor;
+        *cursor += nb;
+        if (b0 < r.first)
+            continue;                                  /* before the range: planned, dropped */
+        sl.first = b0;
+        sl.nb = nb;
+        int m = 1;
+        for (int i = 0; i < nb; i++)
+            m = sl.nch[i] > m ? sl.nch[i] : m;
+        sl.nch_max = m;
+        const uint32_t *rows = nullptr;
+        int n_rows = 0;
+        gss_scn_nav_table(r.scn, &rows, &n_rows);
+        if (n_rows > sl.nav_cap) {                     /* snapshot: the table grows later */
+            (void)hipHostFree(sl.nav);
+            sl.nav = nullptr;
+            sl.nav_cap = 0;
+            int cap = n_rows * 2 + 16;
+            if (hipHostMalloc((void **)&sl.nav, sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)cap,
+                              hipHostMallocDefault) != hipSuccess)
+                return gss_fail(GSS_E_NOMEM, "pinned nav table");
+            sl.nav_cap = cap;
+        }
+        if (n_rows > 0)
+            memcpy(sl.nav, rows, sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)n_rows);
+        sl.n_nav = n_rows;
+        return 0;
+    }
+}
+
+void planner(Run *r)
+{
+    int64_t cursor = 0;
+    for (int i = 0;; i++) {
+        Slot &sl = r->slot[i % NSLOT];
+        {
+            std::unique_lock<std::mutex> lk(r->mu);
+            r->cv.wait(lk, [&] { return r->abort || sl.state == FREE; });
+            if (r->abort)
+                return;
+        }
+        int rc = plan_into(*r, sl, &cursor);
+        {
+            std::lock_guard<std::mutex> lk(r->mu);
+            if (rc) {
+                sl.err = rc;
+                sl.end = 1;
+            }
+            sl.state = PLANNED;
+        }
+        r->cv.notify_all();
+        if (sl.end)
+            return;
+    }
+}
+
+int submit(gss_dev *d, Slot &sl, const uint32_t *d_ca, int n_per_blk, int fmt, size_t bb,
+           hipStream_t st)
+{
+    const size_t s_blk = sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)sl.nb;
+    const size_t s_nch = sizeof(int32_t) * (size_t)sl.nb;
+    const size_t s_ck = sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb;
+    const size_t s_nav = sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)(sl.n_nav > 0 ? sl.n_nav : 1);
+    const size_t need = al256(s_blk) + al256(s_nch) + al256(s_ck) + al256(s_nav);
+    if (need > sl.d_in_cap) {
+        RUN_TRY(hipStreamSynchronize(st));
+        (void)hipFree(sl.d_in);
+        sl.d_in = nullptr;
+        sl.d_in_cap = 0;
+        RUN_TRY(hipMalloc((void **)&sl.d_in, need));
+        sl.d_in_cap = need;
+    }
+    uint8_t *p = sl.d_in;
+    gss_chan_blk_t *d_blk = (gss_chan_blk_t *)p;
+    int32_t *d_nch = (int32_t *)(p + al256(s_blk));
+    double *d_ck = (double *)(p + al256(s_blk) + al256(s_nch));
+    uint32_t *d_nav = (uint32_t *)(p + al256(s_blk) + al256(s_nch) + al256(s_ck));
+    RUN_TRY(hipMemcpyAsync(d_blk, sl.blk, s_blk, hipMemcpyHostToDevice, st));
+    RUN_TRY(hipMemcpyAsync(d_nch, sl.nch, s_nch, hipMemcpyHostToDevice, st));
+    RUN_TRY(hipMemcpyAsync(d_ck, sl.ck, s_ck, hipMemcpyHostToDevice, st));
+    if (sl.n_nav > 0)
+        RUN_TRY(hipMemcpyAsync(d_nav, sl.nav, s_nav, hipMemcpyHostToDevice, st));
+    else
+        RUN_TRY(hipMemsetAsync(d_nav, 0, s_nav, st));
+    RUN_TRY(hipMemsetAsync(sl.d_status, 0, sizeof(int32_t), st));
+    int rc = gss_synth_device(d, d_blk, d_nch, sl.nch_max, d_ck, d_ca, 32, d_nav,
+                              sl.n_nav, sl.nb, n_per_blk, fmt, sl.d_out, nullptr, sl.d_status,
+                              st);
+    if (rc)
+        return rc;
+    RUN_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, bb * (size_t)sl.nb, hipMemcpyDeviceToHost, st));
+    RUN_TRY(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    RUN_TRY(hipEventRecord(sl.done, st));
+    return 0;
+}
+
+int drain(Run &r, Slot &sl, size_t bb, gss_sink_fn sink, void *user)
+{
+    RUN_TRY(hipEventSynchronize(sl.done));
+    if (*sl.h_status)
+        return gss_fail(GSS_E_RANGE, "nav word index ran past dwrd[59]");
+    if (sink(user, sl.h_out, bb * (size_t)sl.nb, sl.first, sl.nb))
+        return gss_fail(GSS_E_IO, "sink failed at block %lld", (long long)sl.first);
+    {
+        std::lock_guard<std::mutex> lk(r.mu);
+        sl.state = FREE;
+    }
+    r.cv.notify_all();
+    return 0;
+}
+
+int run_main(gss_dev *d, Run &r, int n_per_blk, int fmt, size_t bb, gss_sink_fn sink,
+             void *user, hipStream_t st, const uint32_t *d_ca)
+{
+    int pending = -1;                                  /* slot submitted, not yet drained */
+    for (int i = 0;; i++) {
+        Slot &sl = r.slot[i % NSLOT];
+        {
+            std::unique_lock<std::mutex> lk(r.mu);
+            r.cv.wait(lk, [&] { return sl.state == PLANNED; });
+        }
+        if (sl.end) {
+            int rc = pending >= 0 ? drain(r, r.slot[pending], bb, sink, user) : 0;
+            return sl.err ? sl.err : rc;
+        }
+        int rc = submit(d, sl, d_ca, n_per_blk, fmt, bb, st);
+        if (rc)
+            return rc;
+        if (pending >= 0) {                            /* previous slot overlaps this one */
+            rc = drain(r, r.slot[pending], bb, sink, user);
+            if (rc)
+                return rc;
+        }
+        pending = i % NSLOT;
+    }
+}
+
+}  // namespace
+
+extern "C" int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_blocks, int batch,
+                       int threads, gss_sink_fn sink, void *user)
+{
+    if (!d || !s || !sink || first_block < 0)
+        return gss_fail(GSS_E_ARG, "invalid run arguments");
+    gss_scn_info_t info;
+    int rc = gss_scn_info(s, &info);
+    if (rc) return rc;
+    const size_t bb = gss_block_bytes(info.n_per_blk, info.data_format);
+    if (bb == 0)
+        return gss_fail(GSS_E_ARG, "invalid format %d for %d samples/block", info.data_format,
+                        info.n_per_blk);
+    Run r;
+    r.scn = s;
+    r.threads = threads > 0 ? threads : 1;
+    r.batch = batch > 0 ? batch : 100;
+    if ((size_t)r.batch * bb > SLOT_OUT_MAX)
+        r.batch = (int)(SLOT_OUT_MAX / bb) > 0 ? (int)(SLOT_OUT_MAX / bb) : 1;
+    r.first = first_block;
+    r.last = n_blocks < 0 ? INT64_MAX : first_block + n_blocks;
+
+    int ordinal = 0;
+    RUN_TRY(hipGetDevice(&ordinal));
+    hipStream_t st = nullptr;
+    uint32_t *d_ca = nullptr;
+    int err = 0;
+    auto cleanup = [&]() {
+        if (st) (void)hipStreamSynchronize(st);
+        for (Slot &sl : r.slot) {
+            (void)hipHostFree(sl.blk); (void)hipHostFree(sl.nch); (void)hipHostFree(sl.ck);
+            (void)hipHostFree(sl.nav); (void)hipHostFree(sl.h_out); (void)hipHostFree(sl.h_status);
+            (void)hipFree(sl.d_in); (void)hipFree(sl.d_out); (void)hipFree(sl.d_status);
+            if (sl.done) (void)hipEventDestroy(sl.done);
+        }
+        (void)hipFree(d_ca);
+        if (st) (void)hipStreamDestroy(st);
+    };
+    /* buffers */
+    {
+        uint32_t ca[32 * GSS_CA_WORDS];
+        gss_ca_table(ca);
+        if (hipMalloc((void **)&d_ca, sizeof ca) != hipSuccess ||
+            hipMemcpy(d_ca, ca, sizeof ca, hipMemcpyHostToDevice) != hipSuccess ||
+            hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
+            err = gss_fail(GSS_E_HIP, "run setup failed");
+        const size_t nb = (size_t)r.batch;
+        for (Slot &sl : r.slot) {
+            if (err) break;
+            if (hipHostMalloc((void **)&sl.blk, sizeof(gss_chan_blk_t) * GSS_MAXCH * nb,
+                              hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void **)&sl.nch, sizeof(int32_t) * nb, hipHostMallocDefault) !=
+                    hipSuccess ||
+                hipHostMalloc((void **)&sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * nb,
+                              hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void **)&sl.h_out, bb * nb, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void **)&sl.h_status, sizeof(int32_t), hipHostMallocDefault) !=
+                    hipSuccess ||
+                hipMalloc((void **)&sl.d_out, bb * nb) != hipSuccess ||
+                hipMalloc((void **)&sl.d_status, sizeof(int32_t)) != hipSuccess ||
+                hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess)
+                err = gss_fail(GSS_E_NOMEM, "run buffers (%zu B per slot)", bb * nb);
+        }
+        if (!err)
+            err = gss_dev_reserve(d, r.batch, info.n_per_blk);
+    }
+    if (err) {
+        cleanup();
+        return err;
+    }
+    std::thread th([&r, ordinal] {
+        (void)hipSetDevice(ordinal);                   /* pinned reallocations */
+        planner(&r);
+    });
+    err = run_main(d, r, info.n_per_blk, info.data_format, bb, sink, user, st, d_ca);
+    {
+        std::lock_guard<std::mutex> lk(r.mu);
+        r.abort = 1;
+    }
+    r.cv.notify_all();
+    th.join();
+    cleanup();
+    return err;
+}

@@ -58,7 +58,10 @@ _lib = None
 
 # name -> (restype, argtypes); every symbol include/gpssim_amd.h declares
 _P = C.c_void_p
+# gss_sink_fn(user, bytes, n, first_block, nblocks)
+SINK_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int64, C.c_int)
 _SIGS = {
+    "gss_run": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.c_int, C.c_int, SINK_FN, _P]),
     "gss_dev_open": (C.c_int, [C.POINTER(_P), C.c_int]),
     "gss_dev_close": (C.c_int, [_P]),
     "gss_dev_reserve": (C.c_int, [_P, C.c_int, C.c_int]),
@@ -296,6 +299,26 @@ class Device:
         _check(lib().gss_render_device(self._h, set_, blk_ptr, nch_ptr, nch_max, ca_ptr, n_ca,
                                        nav_ptr, n_nav, nblk, n_per_blk, fmt, out_ptr,
                                        status_ptr or None, stream or None))
+
+    def run(self, scn, sink, first_block=0, n_blocks=-1, batch=100, threads=8):
+        """Stream blocks [first_block, first_block + n_blocks) of Scenario scn through gss_run;
+        sink(memoryview, first_block, nblocks) gets each batch's bytes in run order (the view
+        is valid only during the call).  An exception in sink stops the run and is re-raised."""
+        err = []
+
+        def _sink(user, ptr, n, first, nb):
+            try:
+                sink(memoryview((C.c_char * n).from_address(ptr)).cast("B"), first, nb)
+                return 0
+            except BaseException as e:          # noqa: BLE001 — re-raised below
+                err.append(e)
+                return 1
+
+        cb = SINK_FN(_sink)
+        rc = lib().gss_run(self._h, scn._h, first_block, n_blocks, batch, threads, cb, None)
+        if err:
+            raise err[0]
+        _check(rc)
 
     def timing_reset(self):
         _check(lib().gss_dev_timing(self._h, 1, None, None, None))

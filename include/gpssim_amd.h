@@ -193,6 +193,25 @@ double gss_scn_plan_seconds(const gss_scn *s);
 
 int gss_scn_close(gss_scn *s);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Streaming driver: the reference's block loop (gpssim.c:2154-2353) end to end               */
+/* ------------------------------------------------------------------------------------------ */
+/* Byte sink of gss_run: called in run order on the calling thread with the exact output bytes
+   of `nblocks` consecutive blocks starting at run block `first_block` (what the reference
+   fwrite()s for them).  Return 0 to continue, non-zero to stop the run (GSS_E_IO).            */
+typedef int (*gss_sink_fn)(void *user, const void *bytes, size_t n, int64_t first_block,
+                           int nblocks);
+
+/* Run blocks [first_block, first_block + n_blocks) of scenario s (n_blocks < 0: to the end) on
+   device d and stream their bytes to `sink`.  Planning (gss_scn_next on `threads` host
+   threads, in its own thread), upload, both kernel stages, download into pinned buffers and the
+   sink overlap; `batch` blocks per launch (capped at 256 MiB of output).  Blocks before
+   first_block are planned (the carrier chain is serial) but not synthesised: a rank of a
+   multi-GPU run passes its own range and writes at first_block * gss_block_bytes().           */
+int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_blocks, int batch,
+            int threads, gss_sink_fn sink, void *user);
+
+
 /* Exact carrier-chain helpers (exported for tests): advance the reference recurrence
    carr += step; wrap into [0,1) (gpssim.c:2245-2250) by n samples, exactly.                   */
 double gss_carr_advance(double carr, double step, int64_t n);
