@@ -29,6 +29,23 @@ TP(ldexp_f64, double d0 = u0; double d1 = u1; double d2 = u2; double d3 = u3; do
    (unsigned)(d0+d1+d2+d3+d4+d5+d6+d7))
 TP(add_u32, , asm volatile("v_add_u32 %0, %0, %8\n v_add_u32 %1, %1, %8\n v_add_u32 %2, %2, %8\n v_add_u32 %3, %3, %8\n v_add_u32 %4, %4, %8\n v_add_u32 %5, %5, %8\n v_add_u32 %6, %6, %8\n v_add_u32 %7, %7, %8" : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3), "+v"(u4), "+v"(u5), "+v"(u6), "+v"(u7) : "v"(u0));, u0+u1+u2+u3+u4+u5+u6+u7)
 
+TP(fma_f64, double d0 = u0; double d1 = u1; double d2 = u2; double d3 = u3; double d4 = u4; double d5 = u5; double d6 = u6; double d7 = u7,
+   asm volatile("v_fma_f64 %0, %0, %8, %8\n v_fma_f64 %1, %1, %8, %8\n v_fma_f64 %2, %2, %8, %8\n v_fma_f64 %3, %3, %8, %8\n v_fma_f64 %4, %4, %8, %8\n v_fma_f64 %5, %5, %8, %8\n v_fma_f64 %6, %6, %8, %8\n v_fma_f64 %7, %7, %8, %8" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7) : "v"(d0));,
+   (unsigned)(d0+d1+d2+d3+d4+d5+d6+d7))
+TP(add_f64_s, double d0 = u0; double d1 = u1; double d2 = u2; double d3 = u3; double d4 = u4; double d5 = u5; double d6 = u6; double d7 = u7; double sc = __builtin_amdgcn_readfirstlane(u0),
+   asm volatile("v_add_f64 %0, %0, %8\n v_add_f64 %1, %1, %8\n v_add_f64 %2, %2, %8\n v_add_f64 %3, %3, %8\n v_add_f64 %4, %4, %8\n v_add_f64 %5, %5, %8\n v_add_f64 %6, %6, %8\n v_add_f64 %7, %7, %8" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7) : "s"(sc));,
+   (unsigned)(d0+d1+d2+d3+d4+d5+d6+d7))
+TP(bfe_u32, , asm volatile("v_bfe_u32 %0, %0, %8, 1\n v_bfe_u32 %1, %1, %8, 1\n v_bfe_u32 %2, %2, %8, 1\n v_bfe_u32 %3, %3, %8, 1\n v_bfe_u32 %4, %4, %8, 1\n v_bfe_u32 %5, %5, %8, 1\n v_bfe_u32 %6, %6, %8, 1\n v_bfe_u32 %7, %7, %8, 1" : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3), "+v"(u4), "+v"(u5), "+v"(u6), "+v"(u7) : "v"(u0));, u0+u1+u2+u3+u4+u5+u6+u7)
+TP(lshl_add_u64, unsigned long long a0 = u0; unsigned long long a1 = u1; unsigned long long a2 = u2; unsigned long long a3 = u3; unsigned long long a4 = u4; unsigned long long a5 = u5; unsigned long long a6 = u6; unsigned long long a7 = u7,
+   asm volatile("v_lshl_add_u64 %0, %0, 0, %8\n v_lshl_add_u64 %1, %1, 0, %8\n v_lshl_add_u64 %2, %2, 0, %8\n v_lshl_add_u64 %3, %3, 0, %8\n v_lshl_add_u64 %4, %4, 0, %8\n v_lshl_add_u64 %5, %5, 0, %8\n v_lshl_add_u64 %6, %6, 0, %8\n v_lshl_add_u64 %7, %7, 0, %8" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(a0));,
+   (unsigned)(a0+a1+a2+a3+a4+a5+a6+a7))
+TP(cvt_u32_f64, double d0 = u0; unsigned e0; unsigned e1; unsigned e2; unsigned e3; unsigned e4; unsigned e5; unsigned e6; unsigned e7,
+   asm volatile("v_cvt_u32_f64 %0, %8\n v_cvt_u32_f64 %1, %8\n v_cvt_u32_f64 %2, %8\n v_cvt_u32_f64 %3, %8\n v_cvt_u32_f64 %4, %8\n v_cvt_u32_f64 %5, %8\n v_cvt_u32_f64 %6, %8\n v_cvt_u32_f64 %7, %8" : "=v"(e0), "=v"(e1), "=v"(e2), "=v"(e3), "=v"(e4), "=v"(e5), "=v"(e6), "=v"(e7) : "v"(d0)); u0 += e0+e1+e2+e3+e4+e5+e6+e7;,
+   u0)
+TP(mix_f64_int, double d0 = u0; double d1 = u1; double d2 = u2; double d3 = u3,
+   asm volatile("v_add_f64 %0, %0, %8\n v_add_u32 %4, %4, %9\n v_add_f64 %1, %1, %8\n v_add_u32 %5, %5, %9\n v_add_f64 %2, %2, %8\n v_add_u32 %6, %6, %9\n v_add_f64 %3, %3, %8\n v_add_u32 %7, %7, %9" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(u4), "+v"(u5), "+v"(u6), "+v"(u7) : "v"(d0), "v"(u0));,
+   (unsigned)(d0+d1+d2+d3)+u4+u5+u6+u7)
+
 #define RUN(name) { hipLaunchKernelGGL(t_##name, 1024, 256, 0, 0, io, cyc); hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b); \
   hipEventRecord(a); hipLaunchKernelGGL(t_##name, 1024, 256, 0, 0, io, cyc); hipEventRecord(b); hipEventSynchronize(b); float ms; hipEventElapsedTime(&ms, a, b); \
   /* 1024 WGs x 4 waves = 4096 waves = 4/SIMD; each wave issues 64*8*8 = 4096 instrs */ \
@@ -36,6 +53,6 @@ TP(add_u32, , asm volatile("v_add_u32 %0, %0, %8\n v_add_u32 %1, %1, %8\n v_add_
 int main() {
     unsigned *io; long long *cyc;
     (void)hipMalloc(&io, 256 * 4); (void)hipMalloc(&cyc, 8); (void)hipMemset(io, 1, 1024);
-    RUN(add_u32) RUN(add_f64) RUN(fract_f64) RUN(ldexp_f64) RUN(cvt_i32_f64) RUN(dot2c) RUN(mad_i64_i32)
+    RUN(add_u32) RUN(add_f64) RUN(fract_f64) RUN(ldexp_f64) RUN(cvt_i32_f64) RUN(dot2c) RUN(mad_i64_i32) RUN(fma_f64) RUN(add_f64_s) RUN(bfe_u32) RUN(lshl_add_u64) RUN(cvt_u32_f64) RUN(mix_f64_int)
     return 0;
 }
