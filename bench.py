@@ -82,6 +82,10 @@ def main():
     ap.add_argument("--no-ck", action="store_true",
                     help="do not pass the planner's carrier checkpoints (GPU walks whole blocks)")
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 8))
+    ap.add_argument("--path", choices=["lin", "walk"], default="lin",
+                    help="lin: certified integer fast path (gss_linearize + gss_synth_lin_device; "
+                         "uncertified blocks take the exact path inside the same call); walk: "
+                         "the exact walking path only (Stage A + Stage B, gss_synth_device)")
     ap.add_argument("--pipeline", action="store_true",
                     help="run Stage A of batch k+1 on a second stream beside Stage B of batch k "
                          "(gss_anchor_device/gss_render_device) instead of one gss_synth_device "
@@ -116,6 +120,14 @@ def main():
                                        data_format=args.fmt, threads=args.threads)
     host_plan_s = time.perf_counter() - t_plan0
     nblk = len(nch)
+    lin_s, n_fast = 0.0, 0
+    if args.path == "lin":
+        t_lin0 = time.perf_counter()
+        lin, fast = G.linearize(blk, nch, nav, npb, threads=args.threads)
+        lin_s = time.perf_counter() - t_lin0
+        host_plan_s += lin_s
+        n_fast = int(fast.sum())
+        fb = np.nonzero(fast == 0)[0].astype(np.int32)
 
     # ---- inputs resident in HBM ----
     dev = G.Device(local)
@@ -132,6 +144,16 @@ def main():
     stream = torch.cuda.current_stream(dev_t).cuda_stream
 
     ck_ptr = 0 if args.no_ck else d_ck.data_ptr()
+    if args.path == "lin":
+        d_lin = torch.from_numpy(lin.view(np.uint8).reshape(-1)).to(dev_t)
+        d_fast = torch.from_numpy(fast).to(dev_t)
+        d_fb = torch.from_numpy(fb if len(fb) else np.zeros(1, np.int32)).to(dev_t)
+
+    def step_lin():
+        dev.synth_lin_device(d_blk.data_ptr(), d_nch.data_ptr(), nch_max, d_lin.data_ptr(),
+                             d_fast.data_ptr(), d_fb.data_ptr(), len(fb), d_ca.data_ptr(),
+                             len(ca), d_nav.data_ptr(), len(nav), nblk, npb, args.fmt,
+                             out.data_ptr(), stream=stream, ck_ptr=ck_ptr)
 
     def step_serial():
         dev.synth_device(d_blk.data_ptr(), d_nch.data_ptr(), nch_max, d_ca.data_ptr(), len(ca),
@@ -169,7 +191,7 @@ def main():
         anchor(k + 1)
         pipe["k"] = k + 1
 
-    step = step_pipelined if args.pipeline else step_serial
+    step = step_lin if args.path == "lin" else (step_pipelined if args.pipeline else step_serial)
     if args.pipeline:
         anchor(0)                     # pipeline prologue (untimed)
     for _ in range(args.warmup):
@@ -187,17 +209,22 @@ def main():
         td.barrier()
     elapsed = time.perf_counter() - t0
     n_launch, ck_ms, syn_ms = dev.timing()
+    n_lin, lin_ms = dev.timing_lin()
     if dist:
-        t = torch.tensor([elapsed, ck_ms, syn_ms, host_plan_s], dtype=torch.float64,
+        t = torch.tensor([elapsed, ck_ms, syn_ms, host_plan_s, lin_ms], dtype=torch.float64,
                          device=dev_t)
         td.all_reduce(t, op=td.ReduceOp.MAX)
-        elapsed, ck_ms, syn_ms, host_plan_s = t.tolist()
+        elapsed, ck_ms, syn_ms, host_plan_s, lin_ms = t.tolist()
 
     samples_rank = nblk * npb
     ms_per_step = elapsed / args.steps * 1e3
     value = world * samples_rank * args.steps / elapsed / 1e6          # MS/s, whole job
-    bytes_launch = nblk * bb                                            # algorithmic bytes
-    achieved = bytes_launch / (syn_ms * 1e-3) / 1e9 if syn_ms > 0 else 0.0
+    if args.path == "lin":
+        # the dominant kernel is gss_lin_kernel; its algorithmic bytes are the certified blocks'
+        kern_ms, bytes_launch = lin_ms, n_fast * bb
+    else:
+        kern_ms, bytes_launch = syn_ms, nblk * bb                       # algorithmic bytes
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
     e2e = world * samples_rank / (host_plan_s + ms_per_step * 1e-3) / 1e6
     workload = (f"static -l {LOC[0]},{LOC[1]},{LOC[2]:g} -s 2600000 -b {args.fmt}, "
                 f"{args.window:g} s per GPU ({nblk} blocks x {npb} samples)")
@@ -216,13 +243,16 @@ def main():
         "dtype": "f64",
         "data": "synthetic: deterministic static-receiver scenario (brdc3540.14n), no dataset",
         "config": {"workload": workload, "samples_per_gpu": samples_rank,
+                   "path": args.path,
                    "carrier_checkpoints": 0 if args.no_ck else 8,
                    "channels_max": nch_max, "parallelism": f"time-window shards x{world}",
                    "stages": "pipelined (A of batch k+1 beside B of k)" if args.pipeline
                    else "serial (A then B, one stream)"},
         "x_realtime": round(value / (FS / 1e6), 1),
-        "stages_ms": {"checkpoint": round(ck_ms, 3), "synthesis": round(syn_ms, 3),
-                      "launches_timed": n_launch},
+        "stages_ms": {"fast_path": round(lin_ms, 3), "checkpoint": round(ck_ms, 3),
+                      "synthesis": round(syn_ms, 3), "launches_timed": max(n_launch, n_lin)},
+        "blocks_fast_path": n_fast if args.path == "lin" else 0, "blocks_total": nblk,
+        "host_linearize_s": round(lin_s, 3),
         "host_plan_s": round(host_plan_s, 3),
         "e2e_msps": round(e2e, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

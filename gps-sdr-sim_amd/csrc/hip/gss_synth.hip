@@ -51,8 +51,11 @@ __global__ __launch_bounds__(ANCHOR_THREADS) void gss_anchor_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch,
     const double *__restrict__ carr_ck, int nblk, int nchp, int n_per_blk, int nseg, int nsegp,
     int seg_r, double *__restrict__ seg_carr, double *__restrict__ seg_code,
-    uint32_t *__restrict__ seg_cnt, double *__restrict__ carr_end)
+    uint32_t *__restrict__ seg_cnt, double *__restrict__ carr_end,
+    const int32_t *__restrict__ blist)
 {
+    /* blist (optional): the batch's blocks this launch handles (the fast path's leftovers);
+       anchor rows are indexed by the position in the list, everything else by the block */
     /* wave index space: [longest chains first] code waves nchp x nbw (one lane per block) and
        carrier waves nchp x nbwc (one lane per block sub-chain: GSS_NCK of them per block when
        the planner's checkpoints are given, else one) */
@@ -75,9 +78,10 @@ __global__ __launch_bounds__(ANCHOR_THREADS) void gss_anchor_kernel(
     const int b = idx / sub, j = idx - b * sub;
     if (k >= nchp || b >= nblk)
         return;
-    const size_t bk = (size_t)b * GSS_MAXCH + k;
-    const size_t row = bk * (size_t)nsegp;
-    const bool real = k < nch[b];
+    const int rb = blist ? blist[b] : b;                  /* the block itself */
+    const size_t bk = (size_t)rb * GSS_MAXCH + k;
+    const size_t row = ((size_t)b * GSS_MAXCH + k) * (size_t)nsegp;
+    const bool real = k < nch[rb];
     /* padding channels of the kernel instance: no motion (Stage B gives them no gain) */
     gss_chan_blk_t p = blk[bk];
     if (!real) {
@@ -209,7 +213,8 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
     const uint32_t *__restrict__ ca_bits, const uint32_t *__restrict__ nav,
     const double *__restrict__ seg_carr, const double *__restrict__ seg_code,
     const uint32_t *__restrict__ seg_cnt, lut_arg lut, int n_per_blk, int nseg, int nsegp,
-    int seg_r, int wg_per_blk, uint8_t *__restrict__ out, size_t block_bytes, int32_t *__restrict__ status)
+    int seg_r, int wg_per_blk, uint8_t *__restrict__ out, size_t block_bytes, int32_t *__restrict__ status,
+    const int32_t *__restrict__ blist)
 {
     constexpr int SPC = fmt_traits<FMT>::SPC;
     constexpr int NCH4 = (NCH + 3) & ~3;
@@ -221,7 +226,8 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
                                                              icode | ibit<<5 | iword<<10 */
     __shared__ uint32_t s_stage[SYNTH_WAVES][64 * CHUNK_BYTES / 4];
 
-    const int b = blockIdx.x / wg_per_blk;
+    const int bc = blockIdx.x / wg_per_blk;                /* anchor row (list position)   */
+    const int b = blist ? blist[bc] : bc;                  /* the block                    */
     const int w = blockIdx.x % wg_per_blk;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -287,7 +293,7 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
     int bad = 0;
 #pragma unroll
     for (int k = 0; k < NCH; k++) {
-        const size_t r = ((size_t)b * GSS_MAXCH + k) * (size_t)nsegp + segc;
+        const size_t r = ((size_t)bc * GSS_MAXCH + k) * (size_t)nsegp + segc;
         carr[k] = seg_carr[r];
         C[k] = seg_code[r];
         uint32_t c = seg_cnt[r];
@@ -467,6 +473,222 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
 }
 
 /* ======================================================================================== */
+/* Fast path: certified integer lines (csrc/host/linearize.c)                               */
+/* ======================================================================================== */
+/* For a certified block, sample p of channel k reads LUT cell ((x0 + p xs) mod 2^64) >> 55 and
+   chip floor((z0 + p zs) / 2^50) mod 1023, with the signed gain of the schedule (gss_lin_t): no
+   floating point and no walk.  Lanes are consecutive samples: one wave step renders 64
+   consecutive samples, so the LUT reads of a wave hit a few neighbouring cells (no bank
+   conflicts) and the output leaves as one contiguous 256-B (-b 16) store per step.
+   A wave renders 64 steps (4096 samples) in chunks of LIN_CH steps.  Within a chunk the channel
+   loop is outermost: one channel's line parameters live in scalar registers at a time, its lane
+   phases X, Z (u64) are derived from the line at the chunk start, and each lane accumulates
+   LIN_CH samples (packed I/Q int64).  Chip signs: every lane's chip of two consecutive steps lies
+   in a 64-chip window starting at lane 0's chip E of the first (127 zs + 2 chips <= 64, checked by
+   gss_linearize), so one wave-uniform 64-bit window per step pair, read from the table cbw
+   (rotated: bit e mod 64 holds the sign of extended chip e, chip = e mod 1023), serves both steps
+   and a lane's sign is one 64-bit shift by its own chip index. */
+#define LIN_THREADS 256
+#define LIN_WAVES   (LIN_THREADS / 64)
+#define LIN_STEPS   64                     /* 64-sample steps per wave: 4096 samples            */
+#define LIN_CH      16                     /* steps per chunk (one accumulator each)            */
+#define CBW_X       3136                   /* windows per C/A row: chips E < 1023 + the reach of
+                                              one wave (LIN_STEPS*64 samples * 0.49) + 64       */
+
+/* per (block, channel, wave segment of 64*LIN_STEPS samples): the lines evaluated at the
+   segment start, written by gss_linseg_kernel so that the render kernel needs no 128-bit
+   arithmetic and no schedule search */
+struct lin_seg {
+    uint64_t z;                  /* (E0 << 50) | fraction: E0 = chip at the start mod 1023       */
+    uint64_t x;                  /* carrier line at the segment start (mod 2^64)                 */
+    int32_t g01;                 /* signed gain at the start (low 16) and after pos1 (high 16)   */
+    int32_t pos1;                /* sample of the first gain change in the segment, or INT32_MAX */
+    uint32_t tab;                /* row offset of the channel's C/A table in cbw (ca_tbl*CBW_X)  */
+    uint32_t pad;
+};
+
+__global__ void gss_linseg_kernel(const gss_lin_t *__restrict__ lin,
+                                  const gss_chan_blk_t *__restrict__ blk,
+                                  const int32_t *__restrict__ nch, const int32_t *__restrict__ fast,
+                                  int nblk, int nseg, lin_seg *__restrict__ seg_out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nblk * GSS_MAXCH * nseg)
+        return;
+    const int sg = i % nseg, bk = i / nseg, b = bk / GSS_MAXCH, k = bk % GSS_MAXCH;
+    if (!fast[b] || k >= nch[b])
+        return;
+    const gss_lin_t *L = lin + bk;
+    const uint64_t n0 = (uint64_t)sg * (64 * LIN_STEPS);
+    const uint64_t lo = L->z0 + n0 * L->zs;
+    const uint64_t hi = __umul64hi(n0, L->zs) + (lo < L->z0 ? 1u : 0u);
+    const uint32_t E0 = ((uint32_t)(hi << 14) | (uint32_t)(lo >> 50)) % (uint32_t)GSS_CA_LEN;
+    lin_seg r;
+    r.z = ((uint64_t)E0 << 50) | (lo & ((1ull << 50) - 1));
+    r.x = L->x0 + n0 * L->xs;
+    int q = 0;
+    while (q + 1 < GSS_NGC && L->gpos[q + 1] <= (int)n0)
+        q++;
+    const int g0 = L->gval[q];
+    const bool more = q + 1 < GSS_NGC && L->gpos[q + 1] < (int)n0 + 64 * LIN_STEPS;
+    const int g1 = more ? L->gval[q + 1] : g0;
+    r.g01 = (int32_t)(((uint32_t)g0 & 0xFFFFu) | ((uint32_t)g1 << 16));
+    r.pos1 = more ? L->gpos[q + 1] : INT32_MAX;
+    r.tab = (uint32_t)blk[bk].ca_tbl * CBW_X;
+    r.pad = 0;
+    seg_out[i] = r;
+}
+
+__global__ void gss_cbw_kernel(const uint32_t *__restrict__ ca_bits, int n_ca,
+                               uint64_t *__restrict__ cbw)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_ca * CBW_X)
+        return;
+    const int row = i / CBW_X, E = i - row * CBW_X;
+    const uint32_t *cb = ca_bits + (size_t)row * GSS_CA_WORDS;
+    uint64_t w = 0;
+    for (int q = 0; q < 64; q++) {
+        const int e = E + q, chip = e % GSS_CA_LEN;
+        const uint64_t neg = ((cb[chip >> 5] >> (chip & 31)) & 1u) ^ 1u;   /* codeCA = -1 */
+        w |= neg << (e & 63);
+    }
+    cbw[i] = w;
+}
+
+/* one channel's contribution to LIN_CH steps of the wave: X, Z lane phases at the first step,
+   Zh = bits 32..63 of lane 0's code register, the window-table row, the signed gain (per lane
+   when a data bit changes inside the chunk) */
+template <bool LANE_GAIN>
+__device__ __forceinline__ void lin_channel_chunk(int64_t (&acc)[LIN_CH], uint64_t X, uint64_t Z,
+                                                  uint32_t Zh, uint64_t xs, uint64_t zs,
+                                                  const uint64_t *__restrict__ tab, int g0,
+                                                  int g1, int pos1, int p0,
+                                                  const int32_t *__restrict__ s_lut)
+{
+    const uint64_t dX = xs << 6, dZ = zs << 6;
+    /* lane 0's chip at step pair s/2, from 32-bit truncated values: at most one chip low, which
+       the window's slack (lanes need <= 52 of its 64 chips) absorbs */
+    const uint32_t dZh = (uint32_t)((dZ << 1) >> 32);
+#pragma unroll
+    for (int s = 0; s < LIN_CH; s += 2) {
+        const uint64_t W = tab[(Zh + (uint32_t)(s / 2) * dZh) >> 18];       /* scalar */
+#pragma unroll
+        for (int ss = 0; ss < 2; ss++) {
+            const uint32_t ci = (uint32_t)(Z >> 50);
+            const uint32_t t = (uint32_t)(W >> (ci & 63));               /* bit 0: chip sign */
+            const uint32_t y = (t << 31) + (uint32_t)(X >> 32);          /* + half a cycle */
+            const int32_t e = *(const int32_t *)((const char *)s_lut + ((y >> 21) & 0x7FCu));
+            const int g = LANE_GAIN ? (p0 + (s + ss) * 64 >= pos1 ? g1 : g0) : g0;
+            acc[s + ss] += (int64_t)g * (int64_t)e;
+            X += dX;
+            Z += dZ;
+        }
+    }
+}
+
+template <int FMT, bool TAIL>
+__device__ __forceinline__ void lin_store(const int64_t (&acc)[LIN_CH], uint8_t *__restrict__ ob,
+                                          int nb0, int lane, int n_per_blk)
+{
+#pragma unroll
+    for (int s = 0; s < LIN_CH; s++) {
+        /* acc = (sum I + 64 + 2^21) + 2^22 (sum Q + 64): the 2^21 bias keeps the I field
+           non-negative, so (sum Q + 64) >> 7 is bits 29.. of acc and (sum I + 64) >> 7 is the
+           15-bit field at bit 7 with its top bit flipped (gpssim.c:2257-2263) */
+        const uint32_t lo = (uint32_t)acc[s], hi = (uint32_t)(acc[s] >> 32);
+        const int nb = nb0 + s * 64, p = nb + lane;
+        const bool in = !TAIL || p < n_per_blk;
+        if (FMT == 16) {
+            const int i16 = __builtin_amdgcn_sbfe((int)(lo ^ (1u << 21)), 7, 15);
+            const uint32_t q16 = __builtin_amdgcn_alignbit(hi, lo, 29);
+            if (in)
+                ((uint32_t *)ob)[p] = __builtin_amdgcn_perm(q16, (uint32_t)i16, 0x05040100u);
+        } else if (FMT == 8) {                            /* iq_buff >> 4 → signed char */
+            const int i8 = __builtin_amdgcn_sbfe((int)(lo ^ (1u << 21)), 11, 11);
+            const uint32_t q8 = (uint32_t)((int)hi >> 1);
+            if (in)
+                ((uint16_t *)ob)[p] =
+                    (uint16_t)__builtin_amdgcn_perm(q8, (uint32_t)i8, 0x0c0c0400u);
+        } else {                                          /* {I0 Q0 I1 Q1 ...} MSB first */
+            const int i16 = __builtin_amdgcn_sbfe((int)(lo ^ (1u << 21)), 7, 15);
+            const int q16 = (int)__builtin_amdgcn_alignbit(hi, lo, 29);
+            const uint64_t mi = __builtin_amdgcn_ballot_w64(in && i16 > 0);
+            const uint64_t mq = __builtin_amdgcn_ballot_w64(in && q16 > 0);
+            if (lane < 16 && (!TAIL || nb + 4 * lane < n_per_blk)) {
+                const uint32_t a = (uint32_t)(mi >> (4 * lane)) & 15u;
+                const uint32_t c = (uint32_t)(mq >> (4 * lane)) & 15u;
+                ob[nb / 4 + lane] = (uint8_t)(((a & 1u) << 7) | ((a & 2u) << 4) |
+                                              ((a & 4u) << 1) | ((a & 8u) >> 2) |
+                                              ((c & 1u) << 6) | ((c & 2u) << 3) | (c & 4u) |
+                                              ((c & 8u) >> 3));
+            }
+        }
+    }
+}
+
+template <int FMT>
+__global__ __launch_bounds__(LIN_THREADS) void gss_lin_kernel(
+    const gss_lin_t *__restrict__ lin, const lin_seg *__restrict__ segs,
+    const int32_t *__restrict__ nch, const int32_t *__restrict__ fast,
+    const uint64_t *__restrict__ cbw, lut_arg lut, int n_per_blk, int nseg, int wg_per_blk,
+    uint8_t *__restrict__ out, size_t block_bytes)
+{
+    __shared__ int32_t s_lut[512];                        /* cos + 2^22 sin */
+    const int b = blockIdx.x / wg_per_blk;
+    const int w = blockIdx.x - b * wg_per_blk;
+    if (!fast[b])
+        return;                                           /* the exact path renders it */
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);    /* wave-uniform: scalar */
+    for (int i = tid; i < 512; i += LIN_THREADS)
+        s_lut[i] = (int32_t)lut.cos512[i] + (int32_t)lut.sin512[i] * (1 << 22);
+    __syncthreads();
+    const int sg = w * LIN_WAVES + wave;
+    const int n0 = sg * (64 * LIN_STEPS);
+    if (n0 >= n_per_blk)
+        return;
+    const gss_lin_t *L = lin + (size_t)b * GSS_MAXCH;
+    const lin_seg *S = segs + (size_t)b * GSS_MAXCH * nseg + sg;
+    const int nc = nch[b];
+    uint8_t *ob = out + (size_t)b * block_bytes;
+
+    for (int c = 0; c < LIN_STEPS / LIN_CH; c++) {
+        const int nb0 = n0 + c * (64 * LIN_CH);           /* first sample of the chunk */
+        if (nb0 >= n_per_blk)
+            break;
+        int64_t acc[LIN_CH];
+#pragma unroll
+        for (int s = 0; s < LIN_CH; s++)
+            acc[s] = 64 + (1 << 21) + ((int64_t)64 << 22);
+        for (int k = 0; k < nc; k++) {                    /* uniform channel loop */
+            const lin_seg sk = S[(size_t)k * nseg];       /* scalar loads */
+            const uint64_t xs = L[k].xs, zs = L[k].zs;
+            const uint64_t off = (uint64_t)c * (64 * LIN_CH);
+            const uint64_t Zw = sk.z + off * zs, Xw = sk.x + off * xs;
+            const uint64_t X = Xw + (uint64_t)lane * xs;
+            const uint64_t Z = Zw + (uint64_t)lane * zs;
+            const int g0 = (int)(int16_t)(sk.g01 & 0xFFFF), g1 = sk.g01 >> 16;
+            const uint64_t *tab = cbw + sk.tab;
+            const uint32_t Zh = (uint32_t)(Zw >> 32);
+            if (__builtin_expect(sk.pos1 < nb0 + 64 * LIN_CH, 0)) {
+                if (sk.pos1 <= nb0)                       /* changed before this chunk */
+                    lin_channel_chunk<false>(acc, X, Z, Zh, xs, zs, tab, g1, 0, 0, 0, s_lut);
+                else
+                    lin_channel_chunk<true>(acc, X, Z, Zh, xs, zs, tab, g0, g1, sk.pos1,
+                                            nb0 + lane, s_lut);
+            } else {
+                lin_channel_chunk<false>(acc, X, Z, Zh, xs, zs, tab, g0, 0, 0, 0, s_lut);
+            }
+        }
+        if (nb0 + 64 * LIN_CH <= n_per_blk)
+            lin_store<FMT, false>(acc, ob, nb0, lane, n_per_blk);
+        else
+            lin_store<FMT, true>(acc, ob, nb0, lane, n_per_blk);
+    }
+}
+
+/* ======================================================================================== */
 /* C ABI                                                                                    */
 /* ======================================================================================== */
 struct gss_dev {
@@ -479,12 +701,19 @@ struct gss_dev {
     } set[2];                            /* two sets: Stage A of batch k+1 beside B of k  */
     static constexpr int RING = 256;
     hipEvent_t ev_a[RING][2], ev_b[RING][2];   /* start/end of each stage launch          */
-    int n_a = 0, n_b = 0;
+    hipEvent_t ev_l[RING][2];                  /* ... and of each fast-path launch         */
+    int n_a = 0, n_b = 0, n_l = 0;
     lut_arg lut;
     void *h_in = nullptr; size_t h_in_cap = 0;
     void *d_out = nullptr; size_t d_out_cap = 0;
     double *d_cend = nullptr; size_t d_cend_cap = 0;
+    uint64_t *d_cbw = nullptr; size_t d_cbw_cap = 0;   /* chip-sign windows (gss_cbw_kernel) */
+    void *d_seg = nullptr; size_t d_seg_cap = 0;       /* lin_seg rows (gss_linseg_kernel)   */
     int32_t *d_status = nullptr;
+    /* the exact path's leftovers of a fast-path call run on their own stream beside the fast
+       kernel (a few latency-bound blocks would otherwise serialise after it) */
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_in = nullptr, ev_fb = nullptr;
 };
 
 extern "C" int gss_fail(int code, const char *fmt, ...);
@@ -526,6 +755,7 @@ extern "C" int gss_dev_open(gss_dev **out, int ordinal)
         for (int j = 0; j < 2; j++) {
             HIP_TRY(hipEventCreate(&d->ev_a[i][j]));
             HIP_TRY(hipEventCreate(&d->ev_b[i][j]));
+            HIP_TRY(hipEventCreate(&d->ev_l[i][j]));
         }
     int32_t s[512], c[512];
     gss_lut(s, c);
@@ -534,6 +764,11 @@ extern "C" int gss_dev_open(gss_dev **out, int ordinal)
         d->lut.cos512[i] = (int16_t)c[i];
     }
     HIP_TRY(hipMalloc(&d->d_status, sizeof(int32_t)));
+    int prio_lo = 0, prio_hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    HIP_TRY(hipStreamCreateWithPriority(&d->aux, hipStreamNonBlocking, prio_hi));
+    HIP_TRY(hipEventCreateWithFlags(&d->ev_in, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&d->ev_fb, hipEventDisableTiming));
     *out = d;
     return 0;
 }
@@ -547,13 +782,17 @@ extern "C" int gss_dev_close(gss_dev *d)
         (void)hipFree(a.code);
         (void)hipFree(a.cnt);
     }
-    void *bufs[] = {d->h_in, d->d_out, d->d_cend, d->d_status};
+    if (d->aux) (void)hipStreamDestroy(d->aux);
+    if (d->ev_in) (void)hipEventDestroy(d->ev_in);
+    if (d->ev_fb) (void)hipEventDestroy(d->ev_fb);
+    void *bufs[] = {d->h_in, d->d_out, d->d_cend, d->d_cbw, d->d_seg, d->d_status};
     for (void *p : bufs)
         (void)hipFree(p);
     for (int i = 0; i < gss_dev::RING; i++)
         for (int j = 0; j < 2; j++) {
             (void)hipEventDestroy(d->ev_a[i][j]);
             (void)hipEventDestroy(d->ev_b[i][j]);
+            (void)hipEventDestroy(d->ev_l[i][j]);
         }
     delete d;
     return 0;
@@ -563,10 +802,10 @@ static int nseg_of(int n, int r) { return (n + r - 1) / r; }
 /* anchor row stride: the segment starts and one dummy slot (gss_code_seg_states_bf) */
 static int nsegp_of(int n, int r) { return (nseg_of(n, r) + 1 + 31) & ~31; }
 
-static int reserve_set(gss_dev *d, int set, int max_blocks, int n_per_blk)
+static int reserve_set(gss_dev *d, int set, int max_blocks, int n_per_blk, int R)
 {
     gss_dev::anchor_set &a = d->set[set];
-    size_t need = (size_t)max_blocks * GSS_MAXCH * (size_t)nsegp_of(n_per_blk, d->seg_r);
+    size_t need = (size_t)max_blocks * GSS_MAXCH * (size_t)nsegp_of(n_per_blk, R);
     if (need <= a.cap)
         return 0;
     (void)hipFree(a.carr);
@@ -588,7 +827,7 @@ extern "C" int gss_dev_reserve(gss_dev *d, int max_blocks, int n_per_blk)
         return gss_fail(GSS_E_ARG, "invalid reserve arguments");
     HIP_TRY(hipSetDevice(d->ordinal));
     for (int set = 0; set < 2; set++) {
-        int rc = reserve_set(d, set, max_blocks, n_per_blk);
+        int rc = reserve_set(d, set, max_blocks, n_per_blk, d->seg_r);
         if (rc) return rc;
     }
     return 0;
@@ -596,7 +835,8 @@ extern "C" int gss_dev_reserve(gss_dev *d, int max_blocks, int n_per_blk)
 
 typedef void (*synth_fn)(const gss_chan_blk_t *, const int32_t *, const uint32_t *,
                          const uint32_t *, const double *, const double *, const uint32_t *,
-                         lut_arg, int, int, int, int, int, uint8_t *, size_t, int32_t *);
+                         lut_arg, int, int, int, int, int, uint8_t *, size_t, int32_t *,
+                         const int32_t *);
 
 template <int FMT> static synth_fn pick_nch(int nchp)
 {
@@ -618,19 +858,19 @@ static synth_fn pick_kernel(int fmt, int nchp)
     }
 }
 
-extern "C" int gss_anchor_device(gss_dev *d, int set, const gss_chan_blk_t *blk,
-                                 const int32_t *nch, int nch_max, const double *carr_ck,
-                                 int nblk, int n_per_blk, double *carr_end, void *stream)
+/* Stage A over nblk blocks, or over the nblk blocks listed in blist (device) when non-null */
+static int anchor_launch(gss_dev *d, int set, const gss_chan_blk_t *blk, const int32_t *nch,
+                         int nch_max, const double *carr_ck, int nblk, int n_per_blk,
+                         double *carr_end, const int32_t *blist, int R, void *stream)
 {
     if (!d || !blk || !nch || nblk <= 0 || n_per_blk <= 0 || set < 0 || set > 1)
         return gss_fail(GSS_E_ARG, "invalid anchor arguments");
     if (nch_max > GSS_MAXCH)
         return gss_fail(GSS_E_ARG, "nch_max %d > %d", nch_max, GSS_MAXCH);
     HIP_TRY(hipSetDevice(d->ordinal));
-    int rc = reserve_set(d, set, nblk, n_per_blk);
+    int rc = reserve_set(d, set, nblk, n_per_blk, R);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    const int R = d->seg_r;
     const int nseg = nseg_of(n_per_blk, R), nsegp = nsegp_of(n_per_blk, R);
     const int nchp = nch_max < 1 ? 1 : nch_max;
     const gss_dev::anchor_set &a = d->set[set];
@@ -644,25 +884,32 @@ extern "C" int gss_anchor_device(gss_dev *d, int set, const gss_chan_blk_t *blk,
     HIP_TRY(hipEventRecord(ev[0], st));
     hipLaunchKernelGGL(gss_anchor_kernel, dim3(a_blocks), dim3(ANCHOR_THREADS), 0, st, blk, nch,
                        carr_ck, nblk, nchp, n_per_blk, nseg, nsegp, R, a.carr, a.code, a.cnt,
-                       carr_end);
+                       carr_end, blist);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], st));
     return 0;
 }
 
-extern "C" int gss_render_device(gss_dev *d, int set, const gss_chan_blk_t *blk,
-                                 const int32_t *nch, int nch_max, const uint32_t *ca_bits,
-                                 int n_ca, const uint32_t *nav, int n_nav, int nblk,
-                                 int n_per_blk, int fmt, void *out, int32_t *status, void *stream)
+extern "C" int gss_anchor_device(gss_dev *d, int set, const gss_chan_blk_t *blk,
+                                 const int32_t *nch, int nch_max, const double *carr_ck,
+                                 int nblk, int n_per_blk, double *carr_end, void *stream)
 {
-    (void)n_ca; (void)n_nav;
+    return anchor_launch(d, set, blk, nch, nch_max, carr_ck, nblk, n_per_blk, carr_end, nullptr,
+                         d->seg_r, stream);
+}
+
+/* Stage B over nblk blocks, or over the nblk blocks listed in blist (device) when non-null */
+static int render_launch(gss_dev *d, int set, const gss_chan_blk_t *blk, const int32_t *nch,
+                         int nch_max, const uint32_t *ca_bits, const uint32_t *nav, int nblk,
+                         int n_per_blk, int fmt, void *out, int32_t *status,
+                         const int32_t *blist, int R, void *stream)
+{
     if (!d || !blk || !nch || !ca_bits || !out || nblk <= 0 || n_per_blk <= 0 || set < 0 ||
         set > 1)
         return gss_fail(GSS_E_ARG, "invalid render arguments");
     const size_t bb = gss_block_bytes(n_per_blk, fmt);
     if (bb == 0)
         return gss_fail(GSS_E_ARG, "invalid format %d for %d samples/block", fmt, n_per_blk);
-    const int R = d->seg_r;
     const int nseg = nseg_of(n_per_blk, R), nsegp = nsegp_of(n_per_blk, R);
     const gss_dev::anchor_set &a = d->set[set];
     if ((size_t)nblk * GSS_MAXCH * (size_t)nsegp > a.cap)
@@ -681,9 +928,106 @@ extern "C" int gss_render_device(gss_dev *d, int set, const gss_chan_blk_t *blk,
     HIP_TRY(hipEventRecord(ev[0], st));
     hipLaunchKernelGGL(fn, dim3(nblk * wg_per_blk), dim3(SYNTH_THREADS), 0, st, blk, nch, ca_bits,
                        nav, a.carr, a.code, a.cnt, d->lut, n_per_blk, nseg, nsegp, R, wg_per_blk,
-                       (uint8_t *)out, bb, status);
+                       (uint8_t *)out, bb, status, blist);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], st));
+    return 0;
+}
+
+extern "C" int gss_render_device(gss_dev *d, int set, const gss_chan_blk_t *blk,
+                                 const int32_t *nch, int nch_max, const uint32_t *ca_bits,
+                                 int n_ca, const uint32_t *nav, int n_nav, int nblk,
+                                 int n_per_blk, int fmt, void *out, int32_t *status, void *stream)
+{
+    (void)n_ca; (void)n_nav;
+    return render_launch(d, set, blk, nch, nch_max, ca_bits, nav, nblk, n_per_blk, fmt, out,
+                         status, nullptr, d->seg_r, stream);
+}
+
+/* ---- fast path -------------------------------------------------------------------------- */
+typedef void (*lin_fn)(const gss_lin_t *, const lin_seg *, const int32_t *, const int32_t *,
+                       const uint64_t *, lut_arg, int, int, int, uint8_t *, size_t);
+
+static lin_fn pick_lin(int fmt)
+{
+    switch (fmt) {
+    case 16: return gss_lin_kernel<16>;
+    case 8: return gss_lin_kernel<8>;
+    case 1: return gss_lin_kernel<1>;
+    default: return nullptr;
+    }
+}
+
+extern "C" int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
+                                    int nch_max, const gss_lin_t *lin, const int32_t *fast,
+                                    const int32_t *fb_list, int n_fb, const double *carr_ck,
+                                    const uint32_t *ca_bits, int n_ca, const uint32_t *nav,
+                                    int n_nav, int nblk, int n_per_blk, int fmt, void *out,
+                                    int32_t *status, void *stream)
+{
+    (void)n_nav;
+    if (!d || !blk || !nch || !lin || !fast || !ca_bits || !out || nblk <= 0 || n_per_blk <= 0 ||
+        n_ca <= 0 || n_fb < 0 || n_fb > nblk || (n_fb > 0 && !fb_list))
+        return gss_fail(GSS_E_ARG, "invalid synth_lin arguments");
+    const size_t bb = gss_block_bytes(n_per_blk, fmt);
+    if (bb == 0)
+        return gss_fail(GSS_E_ARG, "invalid format %d for %d samples/block", fmt, n_per_blk);
+    const int nchp = nch_max < 1 ? 1 : nch_max;
+    if (nchp > GSS_MAXCH)
+        return gss_fail(GSS_E_ARG, "nch_max %d > %d", nch_max, GSS_MAXCH);
+    lin_fn fn = pick_lin(fmt);
+    if (!fn)
+        return gss_fail(GSS_E_ARG, "no fast kernel for fmt=%d nch=%d", fmt, nchp);
+    HIP_TRY(hipSetDevice(d->ordinal));
+    hipStream_t st = (hipStream_t)stream;
+    /* chip-sign windows of every C/A table row (32 x 1600 x 8 B; rebuilt per call: ~µs) */
+    const size_t ncbw = (size_t)n_ca * CBW_X;
+    if (ncbw * sizeof(uint64_t) > d->d_cbw_cap) {
+        (void)hipFree(d->d_cbw);
+        d->d_cbw = nullptr;
+        d->d_cbw_cap = 0;
+        HIP_TRY(hipMalloc(&d->d_cbw, ncbw * sizeof(uint64_t)));
+        d->d_cbw_cap = ncbw * sizeof(uint64_t);
+    }
+    hipLaunchKernelGGL(gss_cbw_kernel, dim3((unsigned)((ncbw + 255) / 256)), dim3(256), 0, st,
+                       ca_bits, n_ca, d->d_cbw);
+    HIP_TRY(hipGetLastError());
+    const int segs = (n_per_blk + 64 * LIN_STEPS - 1) / (64 * LIN_STEPS);
+    const int wg_per_blk = (segs + LIN_WAVES - 1) / LIN_WAVES;
+    const size_t nsegrows = (size_t)nblk * GSS_MAXCH * segs;
+    if (nsegrows * sizeof(lin_seg) > d->d_seg_cap) {
+        (void)hipFree(d->d_seg);
+        d->d_seg = nullptr;
+        d->d_seg_cap = 0;
+        HIP_TRY(hipMalloc(&d->d_seg, nsegrows * sizeof(lin_seg)));
+        d->d_seg_cap = nsegrows * sizeof(lin_seg);
+    }
+    hipLaunchKernelGGL(gss_linseg_kernel, dim3((unsigned)((nsegrows + 255) / 256)), dim3(256), 0,
+                       st, lin, blk, nch, fast, nblk, segs, (lin_seg *)d->d_seg);
+    HIP_TRY(hipGetLastError());
+    if (n_fb > 0) {          /* the exact path for the uncertified blocks, on the aux stream */
+        HIP_TRY(hipEventRecord(d->ev_in, st));
+        HIP_TRY(hipStreamWaitEvent(d->aux, d->ev_in, 0));
+        /* short Stage-B segments (256 samples): few blocks, so latency matters, not work */
+        const int R = 256;
+        int rc = anchor_launch(d, 0, blk, nch, nch_max, carr_ck, n_fb, n_per_blk, nullptr,
+                               fb_list, R, d->aux);
+        if (rc) return rc;
+        rc = render_launch(d, 0, blk, nch, nch_max, ca_bits, nav, n_fb, n_per_blk, fmt, out,
+                           status, fb_list, R, d->aux);
+        if (rc) return rc;
+        HIP_TRY(hipEventRecord(d->ev_fb, d->aux));
+    }
+    hipEvent_t *ev = d->ev_l[d->n_l % gss_dev::RING];
+    d->n_l++;
+    HIP_TRY(hipEventRecord(ev[0], st));
+    hipLaunchKernelGGL(fn, dim3((unsigned)nblk * wg_per_blk), dim3(LIN_THREADS), 0, st, lin,
+                       (const lin_seg *)d->d_seg, nch, fast, d->d_cbw, d->lut, n_per_blk, segs,
+                       wg_per_blk, (uint8_t *)out, bb);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev[1], st));
+    if (n_fb > 0)                                 /* the call completes when both are done */
+        HIP_TRY(hipStreamWaitEvent(st, d->ev_fb, 0));
     return 0;
 }
 
@@ -727,7 +1071,7 @@ extern "C" int gss_dev_timing(gss_dev *d, int reset, int *n, float *ckpt_ms, flo
 {
     if (!d) return gss_fail(GSS_E_ARG, "null device");
     if (reset) {
-        d->n_a = d->n_b = 0;
+        d->n_a = d->n_b = d->n_l = 0;
         return 0;
     }
     double a = 0.0, b = 0.0;
@@ -738,6 +1082,17 @@ extern "C" int gss_dev_timing(gss_dev *d, int reset, int *n, float *ckpt_ms, flo
     if (n) *n = d->n_b < gss_dev::RING ? d->n_b : gss_dev::RING;
     if (ckpt_ms) *ckpt_ms = (float)a;
     if (synth_ms) *synth_ms = (float)b;
+    return 0;
+}
+
+extern "C" int gss_dev_timing_lin(gss_dev *d, int *n, float *lin_ms)
+{
+    if (!d) return gss_fail(GSS_E_ARG, "null device");
+    double l = 0.0;
+    int rc = ring_avg(d->ev_l, d->n_l, &l);
+    if (rc) return rc;
+    if (n) *n = d->n_l < gss_dev::RING ? d->n_l : gss_dev::RING;
+    if (lin_ms) *lin_ms = (float)l;
     return 0;
 }
 
@@ -792,10 +1147,71 @@ extern "C" int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32
     size_t sz_ca = sizeof(uint32_t) * GSS_CA_WORDS * (size_t)n_ca;
     size_t sz_nav = sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)(n_nav > 0 ? n_nav : 1);
     size_t sz_ck = carr_ck ? sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)nblk : 0;
+    /* the certified fast path unless the caller wants carrier end phases (exact path only) */
+    const char *path = getenv("GSS_PATH");
+    const bool use_lin = carr_end == nullptr && !(path && strcmp(path, "walk") == 0);
+    size_t sz_lin = use_lin ? sizeof(gss_lin_t) * GSS_MAXCH * (size_t)nblk : 0;
+    size_t sz_fast = use_lin ? sizeof(int32_t) * 2 * (size_t)nblk : 0;   /* fast[] + list */
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    size_t tot = al(sz_blk) + al(sz_nch) + al(sz_ca) + al(sz_nav) + al(sz_ck);
+    size_t tot = al(sz_blk) + al(sz_nch) + al(sz_ca) + al(sz_nav) + al(sz_ck) + al(sz_lin) +
+                 al(sz_fast);
     int rc = grow((uint8_t **)&d->h_in, &d->h_in_cap, tot);
     if (rc) return rc;
+    if (use_lin) {
+        gss_lin_t *h_lin = (gss_lin_t *)malloc(sz_lin);
+        int32_t *h_fast = (int32_t *)malloc(sz_fast);
+        if (!h_lin || !h_fast) {
+            free(h_lin);
+            free(h_fast);
+            return gss_fail(GSS_E_NOMEM, "out of memory");
+        }
+        rc = gss_linearize(blk, nch, nblk, n_per_blk, nav, n_nav, h_lin, h_fast, 8);
+        int n_fb = 0;
+        for (int b = 0; b < nblk; b++)
+            if (!h_fast[b])
+                h_fast[nblk + n_fb++] = b;
+        uint8_t *lb = (uint8_t *)d->h_in + al(sz_blk) + al(sz_nch) + al(sz_ca) + al(sz_nav) +
+                      al(sz_ck);
+        gss_lin_t *d_lin = (gss_lin_t *)lb;
+        int32_t *d_fast = (int32_t *)(lb + al(sz_lin));
+        if (rc == 0 && hipMemcpy(d_lin, h_lin, sz_lin, hipMemcpyHostToDevice) != hipSuccess)
+            rc = gss_fail(GSS_E_HIP, "upload of the fast-path lines failed");
+        if (rc == 0 && hipMemcpy(d_fast, h_fast, sz_fast, hipMemcpyHostToDevice) != hipSuccess)
+            rc = gss_fail(GSS_E_HIP, "upload of the fast-path lines failed");
+        free(h_lin);
+        free(h_fast);
+        if (rc) return rc;
+        uint8_t *base = (uint8_t *)d->h_in;
+        gss_chan_blk_t *d_blk = (gss_chan_blk_t *)base;
+        int32_t *d_nch = (int32_t *)(base + al(sz_blk));
+        uint32_t *d_ca = (uint32_t *)(base + al(sz_blk) + al(sz_nch));
+        uint32_t *d_nav = (uint32_t *)(base + al(sz_blk) + al(sz_nch) + al(sz_ca));
+        double *d_ck = carr_ck ? (double *)(base + al(sz_blk) + al(sz_nch) + al(sz_ca) +
+                                            al(sz_nav)) : nullptr;
+        if (carr_ck)
+            HIP_TRY(hipMemcpy(d_ck, carr_ck, sz_ck, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(d_blk, blk, sz_blk, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(d_nch, nch, sz_nch, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(d_ca, ca_bits, sz_ca, hipMemcpyHostToDevice));
+        if (n_nav > 0)
+            HIP_TRY(hipMemcpy(d_nav, nav, sz_nav, hipMemcpyHostToDevice));
+        else
+            HIP_TRY(hipMemset(d_nav, 0, sz_nav));
+        rc = grow((uint8_t **)&d->d_out, &d->d_out_cap, bb * (size_t)nblk);
+        if (rc) return rc;
+        HIP_TRY(hipMemset(d->d_status, 0, sizeof(int32_t)));
+        rc = gss_synth_lin_device(d, d_blk, d_nch, maxc, d_lin, d_fast, d_fast + nblk, n_fb, d_ck,
+                                  d_ca, n_ca, d_nav, n_nav, nblk, n_per_blk, fmt, d->d_out,
+                                  d->d_status, nullptr);
+        if (rc) return rc;
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(out, d->d_out, bb * (size_t)nblk, hipMemcpyDeviceToHost));
+        int32_t stv = 0;
+        HIP_TRY(hipMemcpy(&stv, d->d_status, sizeof stv, hipMemcpyDeviceToHost));
+        if (stv)
+            return gss_fail(GSS_E_RANGE, "nav word index ran past dwrd[59]");
+        return 0;
+    }
     uint8_t *base = (uint8_t *)d->h_in;
     gss_chan_blk_t *d_blk = (gss_chan_blk_t *)base;
     int32_t *d_nch = (int32_t *)(base + al(sz_blk));

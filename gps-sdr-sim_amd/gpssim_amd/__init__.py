@@ -30,6 +30,14 @@ CHAN_DTYPE = np.dtype([
 ])
 assert CHAN_DTYPE.itemsize == 56
 
+NGC = 8                       # GSS_NGC: signed-gain schedule entries
+# gss_lin_t (96 bytes): certified integer lines of one block and channel, gpssim_amd.h
+LIN_DTYPE = np.dtype([
+    ("x0", "<u8"), ("xs", "<u8"), ("z0", "<u8"), ("zs", "<u8"),
+    ("gpos", "<i4", (NGC,)), ("gval", "<i4", (NGC,)),
+])
+assert LIN_DTYPE.itemsize == 96
+
 
 class GssError(RuntimeError):
     def __init__(self, code, msg):
@@ -74,8 +82,15 @@ _SIGS = {
                                    C.c_int, C.c_int, C.c_int, _P, _P, _P, _P]),
     "gss_synth_host": (C.c_int, [_P, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int,
                                  C.c_int, _P, _P]),
+    "gss_linearize": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_int, _P, _P, C.c_int]),
+    "gss_synth_lin_device": (C.c_int, [_P, _P, _P, C.c_int, _P, _P, _P, C.c_int, _P, _P,
+                                       C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P,
+                                       _P]),
+    "gss_minmax_mod": (None, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                              C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "gss_dev_timing": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_float),
                                  C.POINTER(C.c_float)]),
+    "gss_dev_timing_lin": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_float)]),
     "gss_scn_open": (C.c_int, [C.POINTER(_P), C.POINTER(_Opts)]),
     "gss_scn_info": (C.c_int, [_P, C.POINTER(_Info)]),
     "gss_scn_next": (C.c_int, [_P, C.c_int, _P, _P, _P, C.POINTER(C.c_int), C.c_int]),
@@ -141,6 +156,26 @@ def lut():
     c = np.zeros(512, np.int32)
     _check(lib().gss_lut(_ptr(s), _ptr(c)))
     return s, c
+
+
+def linearize(blk, nch, nav, n_per_blk, threads=8):
+    """(lin[nblk, 16] LIN_DTYPE, fast[nblk] int32): the certified integer lines of every block
+    (gss_linearize); fast[b] == 1 where the fast path renders block b exactly."""
+    blk = np.ascontiguousarray(blk, CHAN_DTYPE)
+    nch = np.ascontiguousarray(nch, np.int32)
+    nav = np.ascontiguousarray(nav, np.uint32)
+    lin = np.zeros((len(nch), MAXCH), LIN_DTYPE)
+    fast = np.zeros(len(nch), np.int32)
+    _check(lib().gss_linearize(_ptr(blk), _ptr(nch), len(nch), n_per_blk, _ptr(nav), len(nav),
+                               _ptr(lin), _ptr(fast), threads))
+    return lin, fast
+
+
+def minmax_mod(n, m, a, s):
+    """exact (min, max) of (a + p s) mod m over 0 <= p < n (the certificate's core)"""
+    mn, mx = C.c_uint64(), C.c_uint64()
+    lib().gss_minmax_mod(n, m, a, s, C.byref(mn), C.byref(mx))
+    return mn.value, mx.value
 
 
 def carr_advance(carr, step, n):
@@ -286,6 +321,22 @@ class Device:
                                       n_ca, nav_ptr,
                                       n_nav, nblk, n_per_blk, fmt, out_ptr,
                                       carr_end_ptr or None, status_ptr or None, stream or None))
+
+    def synth_lin_device(self, blk_ptr, nch_ptr, nch_max, lin_ptr, fast_ptr, fb_ptr, n_fb, ca_ptr,
+                         n_ca, nav_ptr, n_nav, nblk, n_per_blk, fmt, out_ptr, status_ptr=0,
+                         stream=0, ck_ptr=0):
+        """gss_synth_lin_device: the certified fast path for blocks with fast[b] == 1 and the
+        exact path for the n_fb blocks listed at fb_ptr; device pointers, stream-ordered."""
+        _check(lib().gss_synth_lin_device(self._h, blk_ptr, nch_ptr, nch_max, lin_ptr, fast_ptr,
+                                          fb_ptr or None, n_fb, ck_ptr or None, ca_ptr, n_ca,
+                                          nav_ptr, n_nav, nblk, n_per_blk, fmt, out_ptr,
+                                          status_ptr or None, stream or None))
+
+    def timing_lin(self):
+        """(fast-path launches, their average ms) since the last timing_reset()"""
+        n, t = C.c_int(), C.c_float()
+        _check(lib().gss_dev_timing_lin(self._h, C.byref(n), C.byref(t)))
+        return n.value, t.value
 
     def anchor_device(self, set_, blk_ptr, nch_ptr, nch_max, nblk, n_per_blk, ck_ptr=0,
                       carr_end_ptr=0, stream=0):

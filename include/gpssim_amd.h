@@ -123,8 +123,47 @@ int gss_render_device(gss_dev *d, int set, const gss_chan_blk_t *blk, const int3
                       int n_nav, int nblk, int n_per_blk, int fmt, void *out, int32_t *status,
                       void *stream);
 
+/* ---- certified linear fast path ------------------------------------------------------------
+   For most blocks each channel's exact carrier and code trajectories stay so close to a 64-bit
+   integer line that every sample's LUT cell, chip and code wrap can be read off the line.
+   gss_linearize (host) finds the lines and proves that, block by block, with exact integer
+   arithmetic; gss_synth_lin_device renders the proven blocks with integer steps only and sends
+   the rest (fast[b] == 0) through the exact walking path (Stage A + Stage B).  Same bytes.     */
+#define GSS_NGC 8                /* signed-gain schedule entries per block and channel        */
+typedef struct gss_lin {
+    uint64_t x0, xs;             /* carrier line, 2^-64 cycle: LUT cell of sample p =
+                                    ((x0 + p*xs) mod 2^64) >> 55  (= floor(512*carr_phase))    */
+    uint64_t z0, zs;             /* code line, 2^-50 chip, unwrapped: floor((z0 + p*zs) / 2^50)
+                                    = chips since the block's code wrap base; chip index is that
+                                    mod 1023 and the k-th code wrap falls where it reaches 1023k */
+    int32_t gpos[GSS_NGC];       /* gain*dataBit (gpssim.c:2186, 2234) is gval[i] for samples   */
+    int32_t gval[GSS_NGC];       /* gpos[i] <= p < gpos[i+1]; gpos[0] = 0, unused = INT32_MAX   */
+} gss_lin_t;                     /* 96 bytes, laid out [nblk][GSS_MAXCH]                       */
+
+/* Lines and proofs for nblk blocks (host arrays; nav = [n_nav][GSS_NAV_WORDS] rows as passed
+   to the synth calls).  fast[b] = 1 if every channel of block b is certified (and the block's
+   gains fit the packed accumulator), else 0.  Runs on `threads` host threads.                 */
+int gss_linearize(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
+                  const uint32_t *nav, int n_nav, gss_lin_t *lin, int32_t *fast, int threads);
+
+/* gss_synth_device over the certified fast path.  Device pointers as gss_synth_device, plus
+   lin [nblk][GSS_MAXCH] and fast [nblk] from gss_linearize, and the exact path's block list
+   fb_list [n_fb] (device; the indices b with fast[b] == 0, n_fb known on the host).  carr_ck
+   (optional) feeds the exact path's Stage A.  No carr_end output.                             */
+int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch, int nch_max,
+                         const gss_lin_t *lin, const int32_t *fast, const int32_t *fb_list,
+                         int n_fb, const double *carr_ck, const uint32_t *ca_bits, int n_ca,
+                         const uint32_t *nav, int n_nav, int nblk, int n_per_blk, int fmt,
+                         void *out, int32_t *status, void *stream);
+
+/* min and max of (a + p*s) mod m over 0 <= p < n, exactly (the certificate's core; exported for
+   tests).                                                                                      */
+void gss_minmax_mod(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint64_t *mn, uint64_t *mx);
+
 /* Same, from host buffers: uploads inputs, runs, downloads `out` (and carr_end if non-NULL),
-   synchronises.  Convenience for the CLI and tests; the bench uses gss_synth_device().        */
+   synchronises.  Convenience for the CLI and tests; the bench uses gss_synth_device().
+   Without carr_end it linearises and takes the fast path (env GSS_PATH=walk: exact path
+   only).                                                                                      */
 int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
                    const double *carr_ck, const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
                    int nblk, int n_per_blk, int fmt, void *out, double *carr_end);
@@ -134,6 +173,9 @@ int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
    each).  reset!=0 clears the rings (no sync); otherwise waits for the last launches and
    returns the number n of Stage B launches and the average duration [ms] of each stage.      */
 int gss_dev_timing(gss_dev *d, int reset, int *n, float *ckpt_ms, float *synth_ms);
+/* Same for the fast-path kernel of gss_synth_lin_device (its exact-path leftovers count as
+   Stage A / Stage B launches above); the same reset clears it.                               */
+int gss_dev_timing_lin(gss_dev *d, int *n, float *lin_ms);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Host layer: scenario driver mirroring main() (gpssim.c:1672-2353)                           */

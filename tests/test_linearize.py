@@ -1,0 +1,180 @@
+"""The certified integer linearisation (gps-sdr-sim_amd/csrc/host/linearize.c) on the CPU.
+
+* gss_minmax_mod (the certificate's core) against brute force;
+* blocks rendered from the certified lines by tests/helpers/lin_check.c (the GPU fast path's
+  arithmetic in scalar C) against the scalar oracle of the reference loop (gpssim.c:2190-2288)
+  on synthetic parameter sweeps, and against the reference's own golden block hashes on the real
+  static scenario;
+* how many blocks the proof certifies on the BASELINE scenarios (the rest take the exact path).
+"""
+import ctypes as C
+import hashlib
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import LOC, NAV, PKG, REPO
+
+import gpssim_amd as G
+import oracle
+
+HELP = os.path.join(REPO, "tests", "helpers")
+_lc = None
+
+
+def lc():
+    global _lc
+    if _lc is None:
+        src = os.path.join(HELP, "lin_check.c")
+        so = os.path.join(HELP, "_lin_check.so")
+        hdr = os.path.join(REPO, "include", "gpssim_amd.h")
+        if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(src),
+                                                                  os.path.getmtime(hdr)):
+            subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-o", so, src])
+        L = C.CDLL(so)
+        L.lc_render.restype = C.c_int
+        L.lc_render.argtypes = [C.c_void_p] * 7 + [C.c_int, C.c_int, C.c_int, C.c_void_p]
+        _lc = L
+    return _lc
+
+
+def _p(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+def render_lin(blk, nch, lin, fast, ca, n, fmt):
+    s, c = G.lut()
+    out = np.zeros(len(nch) * G.block_bytes(n, fmt), np.uint8)
+    nr = lc().lc_render(_p(np.ascontiguousarray(blk)), _p(nch), _p(lin), _p(fast), _p(ca), _p(s),
+                        _p(c), len(nch), n, fmt, _p(out))
+    return out, nr
+
+
+# ---------------------------------------------------------------------------------------------
+def brute_minmax(n, m, a, s):
+    v = [(a + p * s) % m for p in range(n)]
+    return min(v), max(v)
+
+
+def test_minmax_mod_small_vs_brute():
+    rng = np.random.default_rng(1)
+    for _ in range(3000):
+        m = int(rng.integers(1, 5000))
+        n = int(rng.integers(1, 3000))
+        a, s = int(rng.integers(0, m)), int(rng.integers(0, m))
+        assert G.minmax_mod(n, m, a, s) == brute_minmax(n, m, a, s), (n, m, a, s)
+
+
+def test_minmax_mod_edges():
+    for (n, m, a, s) in [(1, 7, 3, 5), (10, 7, 0, 0), (100, 2, 1, 1), (5, 1 << 55, 0, 1 << 54),
+                         (1000, 1 << 55, (1 << 55) - 1, 1), (300000, 1 << 50, 12345, 3),
+                         (7, 1 << 63, (1 << 63) - 5, (1 << 63) - 1)]:
+        if n <= 400000 and m < (1 << 64):
+            assert G.minmax_mod(n, m, a, s) == brute_minmax(n, m, a, s), (n, m, a, s)
+
+
+@pytest.mark.parametrize("lgm", [50, 55])
+def test_minmax_mod_pow2_vs_numpy(lgm):
+    """The certificate's actual moduli (2^50 chips, 2^55 LUT cells), long runs, vs numpy."""
+    rng = np.random.default_rng(lgm)
+    m = 1 << lgm
+    for _ in range(60):
+        n = int(rng.integers(1, 300000))
+        a = int(rng.integers(0, m, dtype=np.uint64))
+        s = int(rng.integers(0, m, dtype=np.uint64))
+        if rng.random() < 0.3:       # steps near a rational p/q of small q: long clustered runs
+            q = int(rng.integers(1, 40))
+            s = (m * int(rng.integers(0, q)) // q + int(rng.integers(-1000, 1000))) % m
+        p = np.arange(n, dtype=np.uint64)
+        v = (np.uint64(a) + p * np.uint64(s)) & np.uint64(m - 1)    # m | 2^64: wrapping is exact
+        assert G.minmax_mod(n, m, a, s) == (int(v.min()), int(v.max())), (n, a, s)
+
+
+# ---------------------------------------------------------------------------------------------
+def synth_params(rng, nblk, nch_list, n_per_blk, ties=False, tiny=False, fs=2.6e6):
+    """random blocks of n_per_blk samples at sample rate fs (realistic Doppler and code rate)"""
+    blk = np.zeros((nblk, G.MAXCH), G.CHAN_DTYPE)
+    nch = np.array(nch_list, np.int32)
+    delt = 1.0 / fs
+    nav = rng.integers(0, 1 << 30, size=(8, 60), dtype=np.uint32)
+    for b in range(nblk):
+        for k in range(nch[b]):
+            f = rng.uniform(-5500, 5500) if (k % 4 or not tiny) else rng.uniform(-40, 40)
+            s = f * delt
+            if ties and k % 3 == 0:
+                u = 2.0 ** -53
+                s = math.copysign((math.floor(abs(s) / u) + 0.5) * u, s)
+            p = blk[b, k]
+            p["carr0"] = [0.0, 1.0 - 2.0 ** -53, rng.random()][k % 3] if b == 0 else rng.random()
+            p["carr_step"] = s
+            p["code0"] = rng.random() * 1023.0 if k % 5 else 1022.9999999
+            p["code_step"] = (1.023e6 + f / 1540.0) * delt
+            p["icode"] = rng.integers(0, 20)
+            p["ibit"] = rng.integers(0, 30)
+            p["iword"] = rng.integers(0, 54)
+            p["gain"] = rng.integers(30, 130)
+            p["ca_tbl"] = rng.integers(0, 32)
+            p["nav_tbl"] = rng.integers(0, 8)
+    return blk, nch, nav
+
+
+@pytest.mark.parametrize("fmt", [16, 8, 1])
+@pytest.mark.parametrize("case", ["mixed", "ties_tiny"])
+def test_lines_render_like_oracle(fmt, case):
+    rng = np.random.default_rng(abs(hash((fmt, case))) % (1 << 32))
+    n = 26000
+    nch = [12, 0, 1, 7, 12, 3, 16, 11]
+    blk, nchv, nav = synth_params(rng, len(nch), nch, n, ties=case == "ties_tiny",
+                                  tiny=case == "ties_tiny")
+    ca = G.ca_table()
+    lin, fast = G.linearize(blk, nchv, nav, n)
+    assert fast.sum() >= len(nch) - 2, fast          # the proof rarely fails
+    want, rc = oracle.synth(blk, nchv, ca, nav, n, fmt)
+    got, nr = render_lin(blk, nchv, lin, fast, ca, n, fmt)
+    assert nr == fast.sum()
+    bb = G.block_bytes(n, fmt)
+    for b in np.nonzero(fast)[0]:
+        assert np.array_equal(got[b * bb:(b + 1) * bb], want[b * bb:(b + 1) * bb]), f"block {b}"
+
+
+def test_lines_full_blocks_like_oracle():
+    """260000-sample blocks (the BASELINE block size): the lines are proven over the whole block."""
+    rng = np.random.default_rng(5)
+    n = 260000
+    blk, nch, nav = synth_params(rng, 3, [12, 12, 9], n)
+    ca = G.ca_table()
+    lin, fast = G.linearize(blk, nch, nav, n)
+    assert fast.all(), fast
+    want, _ = oracle.synth(blk, nch, ca, nav, n, 16)
+    got, _ = render_lin(blk, nch, lin, fast, ca, n, 16)
+    assert np.array_equal(got, want)
+
+
+def test_lines_real_scenario_vs_reference_golden(golden):
+    """The static BASELINE scenario: every block the proof certifies, rendered from its lines,
+    has the reference's own block hash."""
+    s = G.Scenario(NAV, llh=LOC, duration=10.0, data_format=16)
+    blk, nch = s.next(100)
+    lin, fast = G.linearize(blk, nch, s.nav_table(), s.n_per_blk)
+    assert fast.mean() >= 0.95
+    got, _ = render_lin(blk, nch, lin, fast, G.ca_table(), s.n_per_blk, 16)
+    bb = G.block_bytes(s.n_per_blk, 16)
+    gold = golden["static_d30_b16"]["block_sha16"]
+    for i in np.nonzero(fast)[0]:
+        assert hashlib.sha256(got[i * bb:(i + 1) * bb].tobytes()).hexdigest()[:16] == gold[i], i
+
+
+@pytest.mark.parametrize("kw,min_frac", [
+    (dict(llh=LOC, duration=300.0, data_format=16), 0.99),
+    (dict(llh=LOC, duration=30.0, samp_freq=2.0e7, data_format=16), 0.8),
+])
+def test_certified_fraction(kw, min_frac):
+    s = G.Scenario(NAV, **kw)
+    blk, nch = s.all_blocks(batch=1000)
+    lin, fast = G.linearize(blk, nch, s.nav_table(), s.n_per_blk)
+    frac = fast.mean()
+    print(f"certified {fast.sum()}/{len(fast)} blocks ({frac:.4f})")
+    assert frac >= min_frac
