@@ -60,11 +60,13 @@ def cpu_baseline(seconds=60):
                       f"samples), wall {wall:.2f} s, x_realtime {msps / 2.6:.2f}"}
 
 
-def load_traffic(workload):
+def load_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` from the PMC passes (profiles/pmc_traffic.json), when
+    they were taken on this workload"""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
-        if d.get("workload") == workload:
+        if d.get("workload") == workload and str(d.get("kernel", "")).startswith(kernel):
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -79,6 +81,8 @@ def main():
     ap.add_argument("--window", type=float, default=WINDOW_S, help="seconds per GPU")
     ap.add_argument("--fmt", type=int, default=16, choices=[1, 8, 16])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-exact", action="store_true",
+                    help="lin path: skip the exact-path run on the same batch (exact_path)")
     ap.add_argument("--no-ck", action="store_true",
                     help="do not pass the planner's carrier checkpoints (GPU walks whole blocks)")
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 8))
@@ -217,6 +221,20 @@ def main():
         elapsed, ck_ms, syn_ms, host_plan_s, lin_ms = t.tolist()
 
     samples_rank = nblk * npb
+    exact = None
+    if args.path == "lin" and not dist and not args.no_exact:
+        # the same resident batch through the exact path alone (Stage A + Stage B for every
+        # block, no host-side line proofs), timed the same way
+        for _ in range(args.warmup):
+            step_serial()
+        torch.cuda.synchronize(dev_t)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step_serial()
+        torch.cuda.synchronize(dev_t)
+        el = time.perf_counter() - t1
+        exact = {"value": round(samples_rank * args.steps / el / 1e6, 2),
+                 "ms_per_step": round(el / args.steps * 1e3, 3)}
     ms_per_step = elapsed / args.steps * 1e3
     value = world * samples_rank * args.steps / elapsed / 1e6          # MS/s, whole job
     if args.path == "lin":
@@ -228,7 +246,7 @@ def main():
     e2e = world * samples_rank / (host_plan_s + ms_per_step * 1e-3) / 1e6
     workload = (f"static -l {LOC[0]},{LOC[1]},{LOC[2]:g} -s 2600000 -b {args.fmt}, "
                 f"{args.window:g} s per GPU ({nblk} blocks x {npb} samples)")
-    traffic = load_traffic(workload)
+    traffic = load_traffic(workload, "gss_lin_kernel" if args.path == "lin" else "gss_synth_kernel")
     res = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -259,6 +277,7 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic},
         "cpu_baseline": cpu,
+        "exact_path": exact,
     }
     if rank == 0:
         print(json.dumps(res), flush=True)

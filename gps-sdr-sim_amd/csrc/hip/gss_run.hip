@@ -3,8 +3,11 @@
  * plane to the caller's byte sink, every stage overlapped.  Replaces the reference's block loop
  * (gpssim.c:2154-2353: refresh, sample loop, fwrite at 2276/2283/2287, 30 s updates).
  *
- *   planner thread   gss_scn_next into pinned slot buffers (+ a snapshot of the nav table)
- *   main thread      per slot: async H2D, Stage A + B (gss_synth_device), async D2H into a
+ *   planner thread   gss_scn_next into pinned slot buffers (+ a snapshot of the nav table),
+ *                    then gss_linearize: the fast path's certified lines and patches
+ *   main thread      per slot: async H2D, gss_synth_lin_device (certified blocks on the integer
+ *                    fast path, the rest on Stage A + B; with GSS_PATH=walk gss_synth_device
+ *                    renders every block), async D2H into a
  *                    pinned output buffer; then, while the next slot is on the GPU, hands the
  *                    previous slot's bytes to the sink in run order
  *
@@ -14,6 +17,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <condition_variable>
 #include <mutex>
@@ -44,6 +48,9 @@ struct Slot {
     double *ck = nullptr;
     uint32_t *nav = nullptr;
     int nav_cap = 0, n_nav = 0;
+    gss_lin_t *lin = nullptr;        /* certified lines [nb][GSS_MAXCH] (fast path)      */
+    int32_t *fast = nullptr;         /* fast[nb], then the exact-path block list [n_fb] */
+    int n_fb = 0;
     int nb = 0, nch_max = 1;
     int64_t first = 0;               /* run index of the slot's first block */
     int end = 0, err = 0;            /* last slot / planner error code      */
@@ -58,7 +65,7 @@ struct Slot {
 
 struct Run {
     gss_scn *scn;
-    int batch, threads;
+    int batch, threads, n_per_blk, use_lin;
     int64_t first, last;             /* [first, last) block range of the run */
     std::mutex mu;
     std::condition_variable cv;
@@ -117,6 +124,17 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
         if (n_rows > 0)
             memcpy(sl.nav, rows, sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)n_rows);
         sl.n_nav = n_rows;
+        if (r.use_lin) {                               /* the proofs, on the planner thread */
+            rc = gss_linearize(sl.blk, sl.nch, nb, r.n_per_blk, sl.nav, n_rows, sl.lin, sl.fast,
+                               r.threads);
+            if (rc)
+                return rc;
+            int nf = 0;
+            for (int i = 0; i < nb; i++)
+                if (!sl.fast[i])
+                    sl.fast[nb + nf++] = i;
+            sl.n_fb = nf;
+        }
         return 0;
     }
 }
@@ -154,7 +172,10 @@ int submit(gss_dev *d, Slot &sl, const uint32_t *d_ca, int n_per_blk, int fmt, s
     const size_t s_nch = sizeof(int32_t) * (size_t)sl.nb;
     const size_t s_ck = sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb;
     const size_t s_nav = sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)(sl.n_nav > 0 ? sl.n_nav : 1);
-    const size_t need = al256(s_blk) + al256(s_nch) + al256(s_ck) + al256(s_nav);
+    const size_t s_lin = sl.lin ? sizeof(gss_lin_t) * GSS_MAXCH * (size_t)sl.nb : 0;
+    const size_t s_fast = sl.lin ? sizeof(int32_t) * 2 * (size_t)sl.nb : 0;
+    const size_t need = al256(s_blk) + al256(s_nch) + al256(s_ck) + al256(s_nav) + al256(s_lin) +
+                        al256(s_fast);
     if (need > sl.d_in_cap) {
         RUN_TRY(hipStreamSynchronize(st));
         (void)hipFree(sl.d_in);
@@ -168,6 +189,8 @@ int submit(gss_dev *d, Slot &sl, const uint32_t *d_ca, int n_per_blk, int fmt, s
     int32_t *d_nch = (int32_t *)(p + al256(s_blk));
     double *d_ck = (double *)(p + al256(s_blk) + al256(s_nch));
     uint32_t *d_nav = (uint32_t *)(p + al256(s_blk) + al256(s_nch) + al256(s_ck));
+    gss_lin_t *d_lin = (gss_lin_t *)((uint8_t *)d_nav + al256(s_nav));
+    int32_t *d_fast = (int32_t *)((uint8_t *)d_lin + al256(s_lin));
     RUN_TRY(hipMemcpyAsync(d_blk, sl.blk, s_blk, hipMemcpyHostToDevice, st));
     RUN_TRY(hipMemcpyAsync(d_nch, sl.nch, s_nch, hipMemcpyHostToDevice, st));
     RUN_TRY(hipMemcpyAsync(d_ck, sl.ck, s_ck, hipMemcpyHostToDevice, st));
@@ -176,9 +199,18 @@ int submit(gss_dev *d, Slot &sl, const uint32_t *d_ca, int n_per_blk, int fmt, s
     else
         RUN_TRY(hipMemsetAsync(d_nav, 0, s_nav, st));
     RUN_TRY(hipMemsetAsync(sl.d_status, 0, sizeof(int32_t), st));
-    int rc = gss_synth_device(d, d_blk, d_nch, sl.nch_max, d_ck, d_ca, 32, d_nav,
-                              sl.n_nav, sl.nb, n_per_blk, fmt, sl.d_out, nullptr, sl.d_status,
-                              st);
+    int rc;
+    if (sl.lin) {
+        RUN_TRY(hipMemcpyAsync(d_lin, sl.lin, s_lin, hipMemcpyHostToDevice, st));
+        RUN_TRY(hipMemcpyAsync(d_fast, sl.fast, sizeof(int32_t) * (size_t)(sl.nb + sl.n_fb),
+                               hipMemcpyHostToDevice, st));
+        rc = gss_synth_lin_device(d, d_blk, d_nch, sl.nch_max, d_lin, d_fast, d_fast + sl.nb,
+                                  sl.n_fb, d_ck, d_ca, 32, d_nav, sl.n_nav, sl.nb, n_per_blk,
+                                  fmt, sl.d_out, sl.d_status, st);
+    } else {
+        rc = gss_synth_device(d, d_blk, d_nch, sl.nch_max, d_ck, d_ca, 32, d_nav, sl.n_nav,
+                              sl.nb, n_per_blk, fmt, sl.d_out, nullptr, sl.d_status, st);
+    }
     if (rc)
         return rc;
     RUN_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, bb * (size_t)sl.nb, hipMemcpyDeviceToHost, st));
@@ -245,6 +277,11 @@ extern "C" int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_bl
     Run r;
     r.scn = s;
     r.threads = threads > 0 ? threads : 1;
+    r.n_per_blk = info.n_per_blk;
+    {
+        const char *path = getenv("GSS_PATH");        /* "walk": the exact path for every block */
+        r.use_lin = !(path && strcmp(path, "walk") == 0);
+    }
     r.batch = batch > 0 ? batch : 100;
     if ((size_t)r.batch * bb > SLOT_OUT_MAX)
         r.batch = (int)(SLOT_OUT_MAX / bb) > 0 ? (int)(SLOT_OUT_MAX / bb) : 1;
@@ -261,6 +298,7 @@ extern "C" int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_bl
         for (Slot &sl : r.slot) {
             (void)hipHostFree(sl.blk); (void)hipHostFree(sl.nch); (void)hipHostFree(sl.ck);
             (void)hipHostFree(sl.nav); (void)hipHostFree(sl.h_out); (void)hipHostFree(sl.h_status);
+            (void)hipHostFree(sl.lin); (void)hipHostFree(sl.fast);
             (void)hipFree(sl.d_in); (void)hipFree(sl.d_out); (void)hipFree(sl.d_status);
             if (sl.done) (void)hipEventDestroy(sl.done);
         }
@@ -291,6 +329,13 @@ extern "C" int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_bl
                 hipMalloc((void **)&sl.d_status, sizeof(int32_t)) != hipSuccess ||
                 hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess)
                 err = gss_fail(GSS_E_NOMEM, "run buffers (%zu B per slot)", bb * nb);
+            if (!err && r.use_lin &&
+                (hipHostMalloc((void **)&sl.lin, sizeof(gss_lin_t) * GSS_MAXCH * nb,
+                               hipHostMallocDefault) != hipSuccess ||
+                 hipHostMalloc((void **)&sl.fast, sizeof(int32_t) * 2 * nb,
+                               hipHostMallocDefault) != hipSuccess))
+                err = gss_fail(GSS_E_NOMEM, "run lines (%zu B per slot)",
+                               sizeof(gss_lin_t) * GSS_MAXCH * nb);
         }
         if (!err)
             err = gss_dev_reserve(d, r.batch, info.n_per_blk);

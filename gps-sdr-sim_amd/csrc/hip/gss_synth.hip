@@ -504,7 +504,7 @@ struct lin_seg {
     int32_t g01;                 /* signed gain at the start (low 16) and after pos1 (high 16)   */
     int32_t pos1;                /* sample of the first gain change in the segment, or INT32_MAX */
     uint32_t tab;                /* row offset of the channel's C/A table in cbw (ca_tbl*CBW_X)  */
-    uint32_t pad;
+    uint32_t npatch;             /* patched samples of the channel inside the segment            */
 };
 
 __global__ void gss_linseg_kernel(const gss_lin_t *__restrict__ lin,
@@ -535,7 +535,10 @@ __global__ void gss_linseg_kernel(const gss_lin_t *__restrict__ lin,
     r.g01 = (int32_t)(((uint32_t)g0 & 0xFFFFu) | ((uint32_t)g1 << 16));
     r.pos1 = more ? L->gpos[q + 1] : INT32_MAX;
     r.tab = (uint32_t)blk[bk].ca_tbl * CBW_X;
-    r.pad = 0;
+    int np = 0;
+    for (int j = 0; j < GSS_NPATCH; j++)
+        np += L->ppos[j] >= (int)n0 && L->ppos[j] < (int)n0 + 64 * LIN_STEPS;
+    r.npatch = (uint32_t)np;
     seg_out[i] = r;
 }
 
@@ -627,6 +630,43 @@ __device__ __forceinline__ void lin_store(const int64_t (&acc)[LIN_CH], uint8_t 
     }
 }
 
+/* The chunk holds samples where the channel's line does not give the exact LUT cell or chip
+   (gss_lin_t ppos/pval, rare): in that lane and step, replace the line's term by the exact one.
+   A patched sample is the same for every lane, so its phases are wave-uniform. */
+__device__ __forceinline__ void lin_patch_fix(int64_t (&acc)[LIN_CH], uint64_t Xw, uint64_t Zw,
+                                              uint64_t xs, uint64_t zs,
+                                              const uint64_t *__restrict__ tab,
+                                              const gss_lin_t *__restrict__ Lk, int nb0, int lane,
+                                              int g0, int g1, int pos1,
+                                              const int32_t *__restrict__ s_lut)
+{
+    for (int j = 0; j < GSS_NPATCH; j++) {
+        const int pp = Lk->ppos[j];
+        if (pp < nb0 || pp >= nb0 + 64 * LIN_CH || (j > 0 && Lk->ppos[j - 1] == pp))
+            continue;                                 /* one pass per patched sample */
+        const int q = pp - nb0;
+        const uint64_t X = Xw + (uint64_t)q * xs, Z = Zw + (uint64_t)q * zs;
+        const uint32_t E = (uint32_t)(Z >> 50);       /* the line's chip (extended index) */
+        uint32_t t = (uint32_t)(tab[E] >> (E & 63)), hx = (uint32_t)(X >> 32);
+        const uint32_t y0 = (t << 31) + hx;
+        for (int i = j; i < GSS_NPATCH && Lk->ppos[i] == pp; i++) {
+            const int v = Lk->pval[i] & 0xFFFF;
+            if (Lk->pval[i] >> 16)
+                t = (uint32_t)(tab[v] >> (v & 63));   /* the exact chip */
+            else
+                hx = (uint32_t)v << 23;               /* the exact LUT cell */
+        }
+        const uint32_t y1 = (t << 31) + hx;
+        const int32_t d = s_lut[y1 >> 23] - s_lut[y0 >> 23];
+        const int g = pp >= pos1 ? g1 : g0;
+        const int64_t add = lane == (q & 63) ? (int64_t)g * (int64_t)d : 0;
+#pragma unroll
+        for (int s = 0; s < LIN_CH; s++)
+            if (s == (q >> 6))
+                acc[s] += add;
+    }
+}
+
 template <int FMT>
 __global__ __launch_bounds__(LIN_THREADS) void gss_lin_kernel(
     const gss_lin_t *__restrict__ lin, const lin_seg *__restrict__ segs,
@@ -671,15 +711,17 @@ __global__ __launch_bounds__(LIN_THREADS) void gss_lin_kernel(
             const int g0 = (int)(int16_t)(sk.g01 & 0xFFFF), g1 = sk.g01 >> 16;
             const uint64_t *tab = cbw + sk.tab;
             const uint32_t Zh = (uint32_t)(Zw >> 32);
-            if (__builtin_expect(sk.pos1 < nb0 + 64 * LIN_CH, 0)) {
-                if (sk.pos1 <= nb0)                       /* changed before this chunk */
-                    lin_channel_chunk<false>(acc, X, Z, Zh, xs, zs, tab, g1, 0, 0, 0, s_lut);
-                else
-                    lin_channel_chunk<true>(acc, X, Z, Zh, xs, zs, tab, g0, g1, sk.pos1,
-                                            nb0 + lane, s_lut);
-            } else {
-                lin_channel_chunk<false>(acc, X, Z, Zh, xs, zs, tab, g0, 0, 0, 0, s_lut);
+            const bool chg = sk.pos1 < nb0 + 64 * LIN_CH;    /* a data bit by the chunk's end */
+            lin_channel_chunk<false>(acc, X, Z, Zh, xs, zs, tab, chg && sk.pos1 <= nb0 ? g1 : g0,
+                                     0, 0, 0, s_lut);
+            if (__builtin_expect(chg && sk.pos1 > nb0, 0)) {  /* ... inside it: add (g1-g0) e */
+                uint32_t l2 = (uint32_t)lane;
+                asm volatile("" : "+v"(l2));               /* recomputed: nothing stays live */
+                lin_channel_chunk<true>(acc, Xw + l2 * xs, Zw + l2 * zs, Zh, xs, zs, tab, 0,
+                                        g1 - g0, sk.pos1, nb0 + (int)l2, s_lut);
             }
+            if (__builtin_expect(sk.npatch != 0, 0))
+                lin_patch_fix(acc, Xw, Zw, xs, zs, tab, L + k, nb0, lane, g0, g1, sk.pos1, s_lut);
         }
         if (nb0 + 64 * LIN_CH <= n_per_blk)
             lin_store<FMT, false>(acc, ob, nb0, lane, n_per_blk);

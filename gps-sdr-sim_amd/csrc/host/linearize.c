@@ -1,30 +1,38 @@
 /*
- * linearize.c — certified integer linearisation of the sample loop's two double recurrences.
+ * linearize.c — certified integer lines for the sample loop's two double recurrences: the host
+ * side of the GPU fast path (gss_lin_kernel).
  *
  * The reference steps, per sample and channel (gpssim.c:2212-2250),
  *     code += f_code*delt  (wrap at 1023, counters icode/ibit/iword, new data bit every 20 wraps)
  *     carr += f_carr*delt  (wrap into [0,1))
- * and reads LUT[floor(512 carr)] and ca[floor(code)].  Every step is one IEEE rounding, so the
- * exact trajectory differs from the real line x0 + p*s by a deterministic, slowly varying error.
- * For one 0.1 s block this file finds a 64-bit integer line L(p) = L0 + p*S and proves, with exact
- * integer arithmetic, that floor(L(p) / B) equals floor(exact(p) / B) for every sample p of the
- * block (B = 2^55 in carrier units of 2^-64 cycle: the 512 LUT cells; B = 2^50 in code units of
- * 2^-50 chip: the chips, and so also the 1023-chip wraps).  The GPU fast path (gss_lin_kernel)
- * then needs only 64-bit integer adds per sample.
+ * and reads LUT[floor(512 carr)] and ca[floor(code)].  For one block this file takes the
+ * fixed-point lines of the block's own start values and steps,
+ *     carrier  X(p) = rnd(carr0 2^64) + p rnd(carr_step 2^64)  mod 2^64,  LUT cell X >> 55
+ *     code     Z(p) = rnd(code0 2^50) + p rnd(code_step 2^50),            chip (Z >> 50) mod 1023
+ * and proves, with exact integer arithmetic, at which samples they could select another LUT cell
+ * or chip than the reference's doubles.  Those samples are decided exactly and, where the line is
+ * wrong, patched (gss_lin_t ppos/pval).
  *
- * Proof, per chain:
- *   1. The exact chain is walked wrap by wrap (gss_phase.h cycle-cached walks, the same ones the
- *      planner uses), giving the exact unwrapped value U at p = 0, at every wrap and at p = n.
- *   2. S = round((U(n) - U(0)) / n); e(p) = U(p) - L(p) is known exactly at those points.
- *   3. Between two known points e changes by at most g per sample, g = |s*2^k - S| + (bound of
- *      one step's rounding error: 2^-53 cycle = 2^11 units for the carrier, 2^-44 chip = 2^6
- *      units for the code; the bounds used are doubled).  So |e| <= (|e_a| + |e_b| + (p_b-p_a) g)/2
- *      on [p_a, p_b]; Delta is the maximum over the block.
- *   4. min_p (L(p) mod B) >= Delta and max_p (L(p) mod B) <= B-1-Delta over p in [0, n), both
- *      computed exactly (gss_minmod: Euclid-like, O(log B)).  Then no cell boundary lies between
- *      L(p) and the exact value, for any p.
- * A channel that fails (or any other precondition below) sends its block to the exact walking
- * path (Stage A + Stage B); gss_linearize reports that per block.
+ * Proof, per chain and block of n samples:
+ *   1. Each reference step is one IEEE addition (error <= 2^-53 cycle for sums below 2, <= 2^-44
+ *      chip below 1024) plus a wrap that is exact (carr -= 1 and code -= 1023, Sterbenz) or
+ *      rounded once (carr += 1, <= 2^-54).  So the unwrapped exact value moves by the step plus
+ *      less than 2^12 units of 2^-64 cycle (2^7 units of 2^-50 chip) per sample, and the line by
+ *      the step plus at most half a unit: |line - exact| <= Delta = 2 + n (err + 1) over the
+ *      block, about 2^-34 cycle and 2^-25 chip for a 0.1 s block at 2.6 MS/s.
+ *   2. A sample can read another cell than the line only if the line lies within Delta of a cell
+ *      boundary (a multiple of B = 2^55, resp. 2^50): (line(p) + Delta) mod B < 2 Delta.  These
+ *      samples are enumerated exactly: gss_minmod computes min over p of (a + p s) mod m in
+ *      O(log m) steps (a Euclid-like reduction of the sawtooth), inside a binary search over
+ *      prefixes.  At 2.6 MS/s about one chain in sixty has one.
+ *   3. The exact value at each of them comes from the cycle-cached walks of gss_phase.h; where
+ *      the line's cell or chip is not the exact one it becomes a patch.
+ *   4. Code wraps are chip boundaries too: the k-th wrap falls where the line crosses
+ *      1023 k 2^50, one sample earlier or later only where step 3 found the exact value on the
+ *      other side.  The counters and the signed gain (gpssim.c:2186, 2219-2237) follow.
+ * A channel with more than LIN_MAXHIT ambiguous samples or GSS_NPATCH patches, or failing a
+ * precondition of the kernel (below), sends its block to the exact walking path (Stage A +
+ * Stage B); gss_linearize reports that per block.  Cost: O(log B) per chain plus the rare walks.
  */
 #include <math.h>
 #include <pthread.h>
@@ -107,122 +115,116 @@ static i128 to_fix(double x, int k, int *inexact)
     return m < 0 ? -(i128)q : (i128)q;
 }
 
-static i128 iabs128(i128 v) { return v < 0 ? -v : v; }
-
-static i128 round_div(i128 num, int64_t den)        /* den > 0, nearest */
+/* Step 2: the samples p in [1, n) where the line L0 + p S comes within delta of a cell boundary
+   (a multiple of 2^lgB).  Writes up to cap of them in ascending order to hit[]; returns their
+   number, or -1 if there are more (or delta is not small against B).  Binary search over prefix
+   minima. */
+static int ambiguous(i128 L0, i128 S, i128 delta, int lgB, int64_t n, int64_t *hit, int cap)
 {
-    i128 h = den / 2;
-    return num >= 0 ? (num + h) / den : -((-num + h) / den);
-}
-
-/* known exact points of one chain: sample index and unwrapped fixed-point value */
-typedef struct {
-    int64_t *p;
-    i128 *u;
-    int n, cap;
-} pts_t;
-
-static int pts_push(pts_t *t, int64_t p, i128 u)
-{
-    if (t->n == t->cap) {
-        int nc = t->cap ? 2 * t->cap : 64;
-        int64_t *np = realloc(t->p, sizeof(int64_t) * nc);
-        if (!np) return -1;
-        t->p = np;
-        i128 *nu = realloc(t->u, sizeof(i128) * nc);
-        if (!nu) return -1;
-        t->u = nu;
-        t->cap = nc;
-    }
-    t->p[t->n] = p;
-    t->u[t->n] = u;
-    t->n++;
-    return 0;
-}
-
-/* Steps 2-4 for a chain with known points t (first at p=0, last at p=n): slope, Delta, and the
-   certificate against cells of size 2^lgB.  step_err: bound of one step's rounding error in
-   units; s_fix: the step s in units (rounded).  Returns 1 if certified. */
-static int certify(const pts_t *t, int64_t n, i128 s_fix, i128 step_err, int lgB, i128 *L0,
-                   i128 *S, i128 *delta_out)
-{
-    const i128 u0 = t->u[0];
-    const i128 sl = round_div(t->u[t->n - 1] - u0, n);
-    const i128 g = iabs128(s_fix - sl) + 1 + step_err;
-    i128 delta = 0;
-    i128 e_prev = 0;
-    for (int i = 0; i < t->n; i++) {
-        const i128 e = t->u[i] - (u0 + (i128)t->p[i] * sl);
-        if (i > 0) {
-            const i128 b = (iabs128(e_prev) + iabs128(e) + (i128)(t->p[i] - t->p[i - 1]) * g + 1) / 2;
-            if (b > delta) delta = b;
-        }
-        e_prev = e;
-    }
-    delta += 4;                                      /* fixed-point roundings of the points */
-    *L0 = u0;
-    *S = sl;
-    *delta_out = delta;
     const u128 B = (u128)1 << lgB;
     if (delta >= (i128)(B / 4))
-        return 0;
-    /* samples 1 .. n-1 (sample 0 is L(0) = the start value rounded: the caller checks it) */
-    if (n < 2)
-        return 1;
-    const u128 st = (u128)(((sl % (i128)B) + (i128)B) % (i128)B);
-    const u128 a = ((u128)(((u0 % (i128)B) + (i128)B) % (i128)B) + st) % B;
-    const u128 mn = gss_minmod((u128)(n - 1), B, a, st);
-    const u128 mx = gss_maxmod((u128)(n - 1), B, a, st);
-    if (getenv("GSS_LIN_DEBUG"))
-        fprintf(stderr, "certify lgB=%d pts=%d delta=2^%.1f g=2^%.1f min=2^%.1f B-1-max=2^%.1f\n",
-                lgB, t->n, log2((double)delta), log2((double)g), log2((double)mn + 1),
-                log2((double)(B - 1 - mx) + 1));
-    return mn >= (u128)delta && mx + (u128)delta <= B - 1;
+        return -1;
+    const u128 st = (u128)(((S % (i128)B) + (i128)B) % (i128)B);
+    /* r(p) in [0, delta) or [B - delta, B)  <=>  (r(p) + delta) mod B < 2 delta */
+    const u128 a0 = ((u128)(((L0 % (i128)B) + (i128)B) % (i128)B) + (u128)delta) % B;
+    const u128 w = 2 * (u128)delta;
+    int nh = 0;
+    int64_t p0 = 1;
+    while (p0 < n) {
+        const u128 a = (a0 + (u128)p0 % B * st) % B;
+        const u128 m = (u128)(n - p0);
+        if (gss_minmod(m, B, a, st) >= w)
+            break;
+        u128 lo = 1, hi = m;                         /* smallest prefix length with a hit */
+        while (lo < hi) {
+            const u128 mid = (lo + hi) / 2;
+            if (gss_minmod(mid, B, a, st) < w) hi = mid; else lo = mid + 1;
+        }
+        if (nh == cap)
+            return -1;
+        hit[nh++] = p0 + (int64_t)lo - 1;
+        p0 += (int64_t)lo;
+    }
+    return nh;
 }
 
 /* ---- one block ------------------------------------------------------------------------------ */
 #define LIN_CARR_LGB 55          /* 2^55 units of 2^-64 cycle = one of the 512 LUT cells */
 #define LIN_CODE_LGB 50          /* 2^50 units of 2^-50 chip = one chip */
-#define LIN_CARR_ERR ((i128)1 << 12)
-#define LIN_CODE_ERR ((i128)1 << 7)
-
-typedef struct {
-    pts_t pc, pz;
-} lin_ws;
+#define LIN_CARR_ERR ((i128)1 << 12)    /* one step's rounding (bound), units of 2^-64 cycle */
+#define LIN_CODE_ERR ((i128)1 << 7)     /* one step's rounding (bound), units of 2^-50 chip  */
+#define LIN_MAXHIT 16            /* ambiguous samples examined per chain */
 
 static int signed_gain(int gain, const uint32_t *nav, int iword, int ibit)
 {
     return ((nav[iword] >> (29 - ibit)) & 1u) ? gain : -gain;
 }
 
-/* 1 if certified (lin filled), 0 if this channel needs the exact path, <0 on allocation error */
-static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, lin_ws *ws,
-                       gss_lin_t *lin)
+/* Record that sample pos reads cell/chip `value` instead of the line's (kind 0: LUT cell,
+   kind 1: chip).  Patches stay sorted by position; 0 when the table is full. */
+static int add_patch(gss_lin_t *lin, int64_t pos, int kind, int value)
+{
+    int j = 0;
+    while (j < GSS_NPATCH && lin->ppos[j] != INT32_MAX)
+        j++;
+    if (j == GSS_NPATCH)
+        return 0;
+    while (j > 0 && lin->ppos[j - 1] > pos) {
+        lin->ppos[j] = lin->ppos[j - 1];
+        lin->pval[j] = lin->pval[j - 1];
+        j--;
+    }
+    lin->ppos[j] = (int32_t)pos;
+    lin->pval[j] = (kind << 16) | value;
+    return 1;
+}
+
+static int find_hit(const int64_t *hit, int nh, int64_t q)
+{
+    for (int i = 0; i < nh; i++)
+        if (hit[i] == q)
+            return i;
+    return -1;
+}
+
+/* code wraps between the block start and state c, from the counters */
+static int64_t wraps_of(const gss_code_state *c, const gss_chan_blk_t *p)
+{
+    return ((int64_t)(c->iword - p->iword) * 30 + (c->ibit - p->ibit)) * 20 +
+           (c->icode - p->icode);
+}
+
+/* 1 if certified (lin filled), 0 if this channel needs the exact path */
+static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, gss_lin_t *lin)
 {
     int inexact = 0;
+    int64_t hit[LIN_MAXHIT];
+    gss_code_state at_hit[LIN_MAXHIT];
+
     /* ---- carrier (gpssim.c:2245-2250) ---- */
     const double x0 = p->carr0, s = p->carr_step;
     if (!(x0 >= 0.0 && x0 < 1.0) || !(s > -0.5 && s < 0.5))
         return 0;
-    pts_t *t = &ws->pc;
-    t->n = 0;
-    gss_carr_it it;
-    gss_carr_it_init(&it, x0, s, n);
-    int64_t w = 0;
-    if (pts_push(t, 0, to_fix(x0, 64, &inexact))) return -1;
-    while (gss_carr_next_wrap(&it)) {
-        w += s > 0.0 ? 1 : -1;
-        if (pts_push(t, it.pos, to_fix(it.x, 64, &inexact) + ((i128)w << 64))) return -1;
-    }
-    if (it.pos != n) return 0;
-    if (pts_push(t, n, to_fix(it.x, 64, &inexact) + ((i128)w << 64))) return -1;
-    i128 L0, S, dl;
-    if (!certify(t, n, to_fix(s, 64, &inexact), LIN_CARR_ERR, LIN_CARR_LGB, &L0, &S, &dl))
+    const i128 X0 = to_fix(x0, 64, &inexact), XS = to_fix(s, 64, &inexact);
+    int nh = ambiguous(X0, XS, 2 + (i128)n * (LIN_CARR_ERR + 1), LIN_CARR_LGB, n, hit,
+                       LIN_MAXHIT);
+    if (nh < 0)
         return 0;
-    if (L0 < 0 || L0 >= ((i128)1 << 64) || (int)(L0 >> LIN_CARR_LGB) != (int)floor(x0 * 512.0))
+    const int cell0 = (int)floor(x0 * 512.0);
+    if ((int)((uint64_t)X0 >> LIN_CARR_LGB) != cell0 && !add_patch(lin, 0, 0, cell0))
         return 0;                                /* sample 0: the rounded start's own cell */
-    lin->x0 = (uint64_t)L0;
-    lin->xs = (uint64_t)S;
+    double x = x0;
+    int64_t at = 0;
+    for (int i = 0; i < nh; i++) {               /* the ambiguous samples, exactly */
+        x = gss_carr_walk_cc(x, s, hit[i] - at);
+        at = hit[i];
+        const int cell = (int)floor(x * 512.0);
+        const int line = (int)((uint64_t)(X0 + (i128)hit[i] * XS) >> LIN_CARR_LGB);
+        if (cell != line && !add_patch(lin, hit[i], 0, cell))
+            return 0;
+    }
+    lin->x0 = (uint64_t)X0;
+    lin->xs = (uint64_t)XS;
 
     /* ---- code with its counters (gpssim.c:2212-2237) ---- */
     const double c0 = p->code0, cs = p->code_step;
@@ -231,53 +233,82 @@ static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, lin_
     if (p->iword < 0 || p->iword >= GSS_NAV_WORDS || p->ibit < 0 || p->ibit >= 30 ||
         p->icode < 0 || p->icode >= 20)
         return 0;
-    t = &ws->pz;
-    t->n = 0;
-    gss_code_state st0 = {c0, p->icode, p->ibit, p->iword};
-    gss_code_it ic;
-    gss_code_it_init(&ic, st0, cs, n);
-    const i128 per = (i128)GSS_CA_LEN << LIN_CODE_LGB;
-    if (pts_push(t, 0, to_fix(c0, 50, &inexact))) return -1;
+    const int64_t Z0 = (int64_t)to_fix(c0, 50, &inexact);
+    const int64_t ZS = (int64_t)to_fix(cs, 50, &inexact);
+    const int64_t per = (int64_t)GSS_CA_LEN << LIN_CODE_LGB;
+    /* the kernel reads a 64-chip window per two 64-sample steps: 127 steps + 2 chips <= 64 */
+    if (ZS <= 0 || Z0 >= per ||
+        ZS * 127 + ((int64_t)2 << LIN_CODE_LGB) > ((int64_t)64 << LIN_CODE_LGB))
+        return 0;
+    nh = ambiguous(Z0, ZS, 2 + (i128)n * (LIN_CODE_ERR + 1), LIN_CODE_LGB, n, hit, LIN_MAXHIT);
+    if (nh < 0)
+        return 0;
+    const int chip0 = (int)floor(c0);
+    if ((int)(Z0 >> LIN_CODE_LGB) != chip0 && !add_patch(lin, 0, 1, chip0))
+        return 0;                                /* sample 0: the rounded start's own chip */
+    gss_code_state st = {c0, p->icode, p->ibit, p->iword};
+    at = 0;
+    for (int i = 0; i < nh; i++) {
+        gss_code_walk_cc(&st, cs, hit[i] - at);
+        at = hit[i];
+        at_hit[i] = st;
+        const int chip = (int)floor(st.ph);
+        const int line = (int)(((Z0 + (i128)hit[i] * ZS) >> LIN_CODE_LGB) % GSS_CA_LEN);
+        if (chip != line && !add_patch(lin, hit[i], 1, chip))
+            return 0;
+    }
+    lin->z0 = (uint64_t)Z0;
+    lin->zs = (uint64_t)ZS;
+
+    /* ---- code wraps, data bits and the signed-gain schedule ---- */
     int ng = 0;
     int g = signed_gain(p->gain, nav, p->iword, p->ibit);
     lin->gpos[ng] = 0;
     lin->gval[ng++] = g;
-    int64_t nw = 0;
-    int prev_ibit = p->ibit, prev_iword = p->iword;
-    while (gss_code_next_wrap(&ic)) {
-        nw++;
-        if (pts_push(t, ic.pos, to_fix(ic.c.ph, 50, &inexact) + nw * per)) return -1;
-        if (ic.c.ibit != prev_ibit || ic.c.iword != prev_iword) {     /* a new data bit */
-            prev_ibit = ic.c.ibit;
-            prev_iword = ic.c.iword;
-            if (ic.c.iword >= GSS_NAV_WORDS)
-                return 0;                       /* dwrd[60]: the exact path reports it */
-            const int g2 = signed_gain(p->gain, nav, ic.c.iword, ic.c.ibit);
+    gss_code_state cnt = {0.0, p->icode, p->ibit, p->iword};
+    /* the line's k-th wrap is the first q with Z0 + q ZS >= k per:  q = u + (v > 0) where
+       k per - Z0 = u ZS + v, 0 <= v < ZS; k -> k + 1 adds per = Q ZS + R */
+    const int64_t Q = per / ZS, R = per % ZS;
+    int64_t u = (per - Z0) / ZS, v = (per - Z0) % ZS;
+    for (int64_t k = 1;; k++) {
+        int64_t q = u + (v > 0);
+        if (q - 1 >= n)
+            break;
+        int j = find_hit(hit, nh, q - 1);
+        if (j >= 0 && wraps_of(&at_hit[j], p) >= k)
+            q--;                                 /* the exact value wrapped one sample earlier */
+        else if ((j = find_hit(hit, nh, q)) >= 0 && wraps_of(&at_hit[j], p) < k)
+            q++;                                 /* ... or one sample later */
+        if (q >= n)
+            break;
+        const int pb = cnt.ibit, pw = cnt.iword;
+        gss_code_count_wrap(&cnt);
+        if (cnt.ibit != pb || cnt.iword != pw) {            /* a new data bit */
+            if (cnt.iword >= GSS_NAV_WORDS)
+                return 0;                        /* dwrd[60]: the exact path reports it */
+            const int g2 = signed_gain(p->gain, nav, cnt.iword, cnt.ibit);
             if (g2 != g) {
                 /* the kernel takes at most one change per 4096-sample wave segment (they are
                    >= 20 code periods = 20 ms apart in any real run) */
-                if (ng == GSS_NGC || (ng > 1 && ic.pos - lin->gpos[ng - 1] < 4096)) return 0;
-                lin->gpos[ng] = (int32_t)ic.pos;
+                if (ng == GSS_NGC || (ng > 1 && q - lin->gpos[ng - 1] < 4096))
+                    return 0;
+                lin->gpos[ng] = (int32_t)q;
                 lin->gval[ng++] = g2;
                 g = g2;
             }
         }
+        u += Q;
+        v += R;
+        if (v >= ZS) {
+            v -= ZS;
+            u++;
+        }
     }
-    if (ic.pos != n) return 0;
-    if (pts_push(t, n, to_fix(ic.c.ph, 50, &inexact) + nw * per)) return -1;
-    if (!certify(t, n, to_fix(cs, 50, &inexact), LIN_CODE_ERR, LIN_CODE_LGB, &L0, &S, &dl))
-        return 0;
-    if (L0 < 0 || (int64_t)(L0 >> LIN_CODE_LGB) != (int64_t)floor(c0))
-        return 0;                                /* sample 0: the rounded start's own chip */
-    /* the kernel reads a 64-chip window per two 64-sample steps: 127 steps + 2 chips <= 64 */
-    if (S * 127 + ((i128)2 << LIN_CODE_LGB) > ((i128)64 << LIN_CODE_LGB))
-        return 0;
-    lin->z0 = (uint64_t)L0;
-    lin->zs = (uint64_t)S;
     for (int i = ng; i < GSS_NGC; i++) {
         lin->gpos[i] = INT32_MAX;
         lin->gval[i] = g;
     }
+    (void)inexact;
     return 1;
 }
 
@@ -288,15 +319,12 @@ typedef struct {
     int n_nav, n_per_blk, b_lo, b_hi;
     gss_lin_t *lin;
     int32_t *fast;
-    int err;
 } lin_job;
 
 static void *lin_run(void *arg)
 {
     lin_job *j = arg;
-    lin_ws ws;
-    memset(&ws, 0, sizeof ws);
-    for (int b = j->b_lo; b < j->b_hi && !j->err; b++) {
+    for (int b = j->b_lo; b < j->b_hi; b++) {
         int ok = 1, gsum = 0;
         const int nc = j->nch[b];
         for (int k = 0; k < GSS_MAXCH; k++) {
@@ -304,6 +332,8 @@ static void *lin_run(void *arg)
             memset(l, 0, sizeof *l);
             for (int i = 0; i < GSS_NGC; i++)
                 l->gpos[i] = INT32_MAX;
+            for (int i = 0; i < GSS_NPATCH; i++)
+                l->ppos[i] = INT32_MAX;
         }
         if (nc < 0 || nc > GSS_MAXCH)
             ok = 0;
@@ -314,20 +344,14 @@ static void *lin_run(void *arg)
                 ok = 0;
                 break;
             }
-            int r = lin_channel(p, j->n_per_blk, j->nav + (size_t)p->nav_tbl * GSS_NAV_WORDS,
-                                &ws, &j->lin[(size_t)b * GSS_MAXCH + k]);
-            if (r < 0) {
-                j->err = GSS_E_NOMEM;
-                break;
-            }
-            ok = r;
+            ok = lin_channel(p, j->n_per_blk, j->nav + (size_t)p->nav_tbl * GSS_NAV_WORDS,
+                             &j->lin[(size_t)b * GSS_MAXCH + k]);
         }
         /* the packed I/Q accumulator (gss_lin_kernel) needs 250*sum|gain| + 64 < 2^21 */
         if (gsum > 8000)
             ok = 0;
         j->fast[b] = ok;
     }
-    free(ws.pc.p); free(ws.pc.u); free(ws.pz.p); free(ws.pz.u);
     return NULL;
 }
 
@@ -347,7 +371,7 @@ int gss_linearize(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n
     const int per = (nblk + threads - 1) / threads;
     for (int t = 0; t < threads; t++) {
         int lo = t * per, hi = lo + per > nblk ? nblk : lo + per;
-        job[t] = (lin_job){blk, nch, nav, n_nav, n_per_blk, lo, hi, lin, fast, 0};
+        job[t] = (lin_job){blk, nch, nav, n_nav, n_per_blk, lo, hi, lin, fast};
         if (lo >= hi)
             continue;
         if (threads == 1 || pthread_create(&tid[t], NULL, lin_run, &job[t]) != 0)
@@ -355,12 +379,8 @@ int gss_linearize(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n
         else
             started[t] = 1;
     }
-    int err = 0;
-    for (int t = 0; t < threads; t++) {
+    for (int t = 0; t < threads; t++)
         if (started[t])
             pthread_join(tid[t], NULL);
-        if (job[t].err)
-            err = job[t].err;
-    }
-    return err ? gss_fail(err, "out of memory in gss_linearize") : 0;
+    return 0;
 }

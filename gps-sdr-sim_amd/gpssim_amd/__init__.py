@@ -31,12 +31,14 @@ CHAN_DTYPE = np.dtype([
 assert CHAN_DTYPE.itemsize == 56
 
 NGC = 8                       # GSS_NGC: signed-gain schedule entries
-# gss_lin_t (96 bytes): certified integer lines of one block and channel, gpssim_amd.h
+NPATCH = 8                    # GSS_NPATCH: patched samples per block and channel
+# gss_lin_t (160 bytes): certified integer lines of one block and channel, gpssim_amd.h
 LIN_DTYPE = np.dtype([
     ("x0", "<u8"), ("xs", "<u8"), ("z0", "<u8"), ("zs", "<u8"),
     ("gpos", "<i4", (NGC,)), ("gval", "<i4", (NGC,)),
+    ("ppos", "<i4", (NPATCH,)), ("pval", "<i4", (NPATCH,)),
 ])
-assert LIN_DTYPE.itemsize == 96
+assert LIN_DTYPE.itemsize == 160
 
 
 class GssError(RuntimeError):

@@ -130,6 +130,7 @@ int gss_render_device(gss_dev *d, int set, const gss_chan_blk_t *blk, const int3
    arithmetic; gss_synth_lin_device renders the proven blocks with integer steps only and sends
    the rest (fast[b] == 0) through the exact walking path (Stage A + Stage B).  Same bytes.     */
 #define GSS_NGC 8                /* signed-gain schedule entries per block and channel        */
+#define GSS_NPATCH 8             /* patched samples per block and channel                     */
 typedef struct gss_lin {
     uint64_t x0, xs;             /* carrier line, 2^-64 cycle: LUT cell of sample p =
                                     ((x0 + p*xs) mod 2^64) >> 55  (= floor(512*carr_phase))    */
@@ -138,7 +139,11 @@ typedef struct gss_lin {
                                     mod 1023 and the k-th code wrap falls where it reaches 1023k */
     int32_t gpos[GSS_NGC];       /* gain*dataBit (gpssim.c:2186, 2234) is gval[i] for samples   */
     int32_t gval[GSS_NGC];       /* gpos[i] <= p < gpos[i+1]; gpos[0] = 0, unused = INT32_MAX   */
-} gss_lin_t;                     /* 96 bytes, laid out [nblk][GSS_MAXCH]                       */
+    int32_t ppos[GSS_NPATCH];    /* patched samples, ascending (unused = INT32_MAX), where the
+                                    line's cell or chip is not the exact one: sample ppos[i]     */
+    int32_t pval[GSS_NPATCH];    /* reads LUT cell pval & 0xFFFF (pval >> 16 == 0) or chip
+                                    pval & 0xFFFF (pval >> 16 == 1) instead                      */
+} gss_lin_t;                     /* 160 bytes, laid out [nblk][GSS_MAXCH]                      */
 
 /* Lines and proofs for nblk blocks (host arrays; nav = [n_nav][GSS_NAV_WORDS] rows as passed
    to the synth calls).  fast[b] = 1 if every channel of block b is certified (and the block's

@@ -1,7 +1,7 @@
 /* Test-only harness: renders blocks from the certified integer lines (gss_lin_t) with scalar C,
    exactly the arithmetic the GPU fast path (gss_lin_kernel) performs: LUT cell = high 9 bits of
    x0 + p*xs (mod 2^64), chip = floor((z0 + p*zs) / 2^50) mod 1023, signed gain from the
-   schedule.  tests/test_linearize.py compares its bytes with the scalar oracle of the reference
+   schedule, the patched samples.  tests/test_linearize.py compares its bytes with the scalar oracle of the reference
    loop (oracle/synth_oracle.c) on every block gss_linearize certifies. */
 #include <stdint.h>
 #include <stdlib.h>
@@ -29,9 +29,16 @@ int lc_render(const gss_chan_blk_t *blk, const int32_t *nch, const gss_lin_t *li
                 const gss_lin_t *l = &lin[(size_t)b * GSS_MAXCH + k];
                 const gss_chan_blk_t *c = &blk[(size_t)b * GSS_MAXCH + k];
                 const uint64_t x = l->x0 + (uint64_t)p * l->xs;
-                const int ti = (int)(x >> 55);
+                int ti = (int)(x >> 55);
                 const u128 z = (u128)l->z0 + (u128)p * l->zs;
-                const int chip = (int)((uint64_t)(z >> 50) % GSS_CA_LEN);
+                int chip = (int)((uint64_t)(z >> 50) % GSS_CA_LEN);
+                for (int j = 0; j < GSS_NPATCH; j++)
+                    if (l->ppos[j] == p) {                     /* the exact cell / chip */
+                        if (l->pval[j] >> 16)
+                            chip = l->pval[j] & 0xFFFF;
+                        else
+                            ti = l->pval[j] & 0xFFFF;
+                    }
                 const int ca = ca_chip(ca_bits + (size_t)c->ca_tbl * GSS_CA_WORDS, chip) * 2 - 1;
                 int g = l->gval[0];
                 for (int i = 1; i < GSS_NGC; i++)

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 from conftest import LOC, NAV
-from test_linearize import synth_params
+from test_linearize import boundary_params, synth_params
 
 import gpssim_amd as G
 import oracle
@@ -106,3 +106,19 @@ def test_lin_device_entry_scenario(dev, golden):
     hs = [hashlib.sha256(o[i * bb:(i + 1) * bb].tobytes()).hexdigest()[:16]
           for i in range(len(nch))]
     assert hs == golden["static_d30_b16"]["block_sha16"][:len(nch)]
+
+
+def test_lin_patched_samples_vs_oracle(dev):
+    """Code wraps (starting new data bits) and carrier cells placed within about 1e-11 of the
+    line: the kernel applies the exact values the proof found (patches); bytes equal the
+    oracle's."""
+    blk, nch, nav, n = boundary_params()
+    lin, fast = G.linearize(blk, nch, nav, n)
+    assert (lin["ppos"][fast.astype(bool)] != np.iinfo(np.int32).max).any()
+    ca = G.ca_table()
+    want, _ = oracle.synth(blk, nch, ca, nav, n, 16)
+    dev.timing_reset()
+    got = dev.synth_host(blk, nch, ca, nav, n, 16)
+    assert dev.timing_lin()[0] == 1
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:5]}"

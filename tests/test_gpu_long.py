@@ -11,6 +11,7 @@ disk.  A fixture that is absent (its reference run not made yet) skips its case.
 import hashlib
 import json
 import os
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 import pytest
@@ -23,6 +24,7 @@ pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 THREADS = 16
+PROGRESS = os.path.join(os.path.dirname(HERE), "gpurun_out", "long_progress.txt")
 
 
 def _fixture(name):
@@ -47,6 +49,7 @@ class BlockDigests:
         self.last = []
         self.n = 0
         self.head = None
+        self.t_note = time.time()
 
     def _span(self, mv, i0, i1):
         return [hashlib.sha256(mv[i * self.bb:(i + 1) * self.bb]).digest() for i in range(i0, i1)]
@@ -69,6 +72,11 @@ class BlockDigests:
                 if self.n % self.cb == 0:
                     self.chunks.append(self.chunk.hexdigest()[:16])
                     self.chunk = hashlib.sha256()
+        if time.time() - self.t_note > 20:            # a sign of life during long runs
+            self.t_note = time.time()
+            os.makedirs(os.path.dirname(PROGRESS), exist_ok=True)
+            with open(PROGRESS, "a") as f:
+                f.write(f"{time.strftime('%H:%M:%S')} {self.n} blocks\n")
 
     def finish(self):
         if self.n % self.cb:

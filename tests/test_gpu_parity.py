@@ -275,3 +275,18 @@ def test_cli_two_ranks_one_file(golden):
             assert p.returncode == 0, err[-2000:]
         h = hashlib.sha256(open(out, "rb").read()).hexdigest()
     assert h == golden["static_d30_b16"]["sha256"]
+
+
+def test_streaming_run_walk_path(dev, golden, monkeypatch):
+    """gss_run with GSS_PATH=walk (the exact path for every block): the same bytes."""
+    monkeypatch.setenv("GSS_PATH", "walk")
+    s = G.Scenario(NAV, llh=LOC, duration=30.0, data_format=8)
+    bb = G.block_bytes(s.n_per_blk, 8)
+    blocks = []
+
+    def sink(buf, first, nb):
+        for i in range(nb):
+            blocks.append(hashlib.sha256(buf[i * bb:(i + 1) * bb]).hexdigest()[:16])
+
+    dev.run(s, sink, first_block=200, n_blocks=40, batch=16)
+    assert blocks == golden["static_d30_b8"]["block_sha16"][200:240]

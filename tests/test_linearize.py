@@ -5,6 +5,8 @@
   arithmetic in scalar C) against the scalar oracle of the reference loop (gpssim.c:2190-2288)
   on synthetic parameter sweeps, and against the reference's own golden block hashes on the real
   static scenario;
+* samples where the line comes within the proof's Delta of a cell or chip boundary (code wraps
+  that start a new data bit included): decided exactly, patched where the line is wrong;
 * how many blocks the proof certifies on the BASELINE scenarios (the rest take the exact path).
 """
 import ctypes as C
@@ -159,7 +161,7 @@ def test_lines_real_scenario_vs_reference_golden(golden):
     s = G.Scenario(NAV, llh=LOC, duration=10.0, data_format=16)
     blk, nch = s.next(100)
     lin, fast = G.linearize(blk, nch, s.nav_table(), s.n_per_blk)
-    assert fast.mean() >= 0.95
+    assert fast.mean() >= 0.99
     got, _ = render_lin(blk, nch, lin, fast, G.ca_table(), s.n_per_blk, 16)
     bb = G.block_bytes(s.n_per_blk, 16)
     gold = golden["static_d30_b16"]["block_sha16"]
@@ -169,7 +171,7 @@ def test_lines_real_scenario_vs_reference_golden(golden):
 
 @pytest.mark.parametrize("kw,min_frac", [
     (dict(llh=LOC, duration=300.0, data_format=16), 0.99),
-    (dict(llh=LOC, duration=30.0, samp_freq=2.0e7, data_format=16), 0.8),
+    (dict(llh=LOC, duration=30.0, samp_freq=2.0e7, data_format=16), 0.97),
 ])
 def test_certified_fraction(kw, min_frac):
     s = G.Scenario(NAV, **kw)
@@ -178,3 +180,61 @@ def test_certified_fraction(kw, min_frac):
     frac = fast.mean()
     print(f"certified {fast.sum()}/{len(fast)} blocks ({frac:.4f})")
     assert frac >= min_frac
+
+
+# ---------------------------------------------------------------------------------------------
+def boundary_params(nb=36, n=26000, fs=2.6e6, seed=11):
+    """One-channel blocks whose code reaches 1023 (a wrap that starts a new data bit) and whose
+    carrier reaches a LUT cell boundary at one sample each, within about 1e-11 of the real line:
+    there the exact values may fall on either side of the line's."""
+    rng = np.random.default_rng(seed)
+    blk = np.zeros((nb, G.MAXCH), G.CHAN_DTYPE)
+    nch = np.ones(nb, np.int32)
+    nav = rng.integers(0, 1 << 30, size=(2, 60), dtype=np.uint32)
+    eps = [0.0, 1e-12, -1e-12, 1e-11, -1e-11, 3e-13]
+    for b in range(nb):
+        p = blk[b, 0]
+        f = rng.uniform(-4000, 4000)
+        cs, s = (1.023e6 + f / 1540.0) / fs, f / fs
+        q = int(rng.integers(100, 2500))
+        p["code0"], p["code_step"] = 1023.0 - q * cs + eps[b % 6], cs
+        qc = int(rng.integers(1, n))
+        c = (int(rng.integers(0, 512)) / 512.0 - qc * s + eps[(b // 6) % 6]) % 1.0
+        p["carr0"], p["carr_step"] = (c if c < 1.0 else 0.0), s
+        p["icode"], p["ibit"], p["iword"] = 19, int(rng.integers(0, 30)), int(rng.integers(0, 50))
+        p["gain"], p["ca_tbl"], p["nav_tbl"] = 100, int(rng.integers(0, 32)), b % 2
+    return blk, nch, nav, n
+
+
+def test_boundary_samples_like_oracle():
+    blk, nch, nav, n = boundary_params()
+    lin, fast = G.linearize(blk, nch, nav, n)
+    unused = np.iinfo(np.int32).max
+    npatched = int((lin["ppos"][:, 0, 0] != unused).sum())
+    print(f"certified {int(fast.sum())}/{len(fast)}, {npatched} channels patched")
+    assert fast.sum() >= len(fast) - 2
+    assert npatched > 0
+    ca = G.ca_table()
+    want, _ = oracle.synth(blk, nch, ca, nav, n, 16)
+    got, _ = render_lin(blk, nch, lin, fast, ca, n, 16)
+    bb = G.block_bytes(n, 16)
+    for b in np.nonzero(fast)[0]:
+        assert np.array_equal(got[b * bb:(b + 1) * bb], want[b * bb:(b + 1) * bb]), f"block {b}"
+
+
+def test_patched_real_blocks_vs_reference_golden(golden):
+    """20 MS/s blocks of the static scenario that carry patches, rendered with them, have the
+    reference's own block hashes."""
+    s = G.Scenario(NAV, llh=LOC, duration=30.0, samp_freq=2.0e7, data_format=16)
+    blk, nch = s.all_blocks(batch=1000)
+    lin, fast = G.linearize(blk, nch, s.nav_table(), s.n_per_blk)
+    unused = np.iinfo(np.int32).max
+    patched = [int(b) for b in np.nonzero(fast)[0] if (lin[b]["ppos"] != unused).any()]
+    print(f"{len(patched)} of {int(fast.sum())} certified blocks carry patches")
+    assert patched
+    sel = np.array(patched[:3])
+    got, _ = render_lin(blk[sel], nch[sel], lin[sel], fast[sel], G.ca_table(), s.n_per_blk, 16)
+    bb = G.block_bytes(s.n_per_blk, 16)
+    gold = golden["static_d30_s20M_b16"]["block_sha16"]
+    for i, b in enumerate(sel):
+        assert hashlib.sha256(got[i * bb:(i + 1) * bb].tobytes()).hexdigest()[:16] == gold[b], b

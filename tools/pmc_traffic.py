@@ -25,10 +25,15 @@ def main():
                     bench = json.loads(line)
         except OSError:
             pass
-    k = next(n for n in summ if n.startswith("gss_synth_kernel"))
+    want = "gss_lin_kernel" if bench and bench["config"].get("path") == "lin" else "gss_synth_kernel"
+    k = next(n for n in summ if n.startswith(want))
     e = summ[k]
     w, r = e["hbm_write_bytes"], e["hbm_read_bytes_corrected"]
-    alg = bench["config"]["samples_per_gpu"] * 4 if bench else None
+    alg = None
+    if bench:                 # -b 16: 4 B per sample; the fast path renders the certified blocks
+        share = (bench.get("blocks_fast_path", 0) / bench["blocks_total"]
+                 if want == "gss_lin_kernel" else 1.0)
+        alg = round(bench["config"]["samples_per_gpu"] * 4 * share)
     res = {"workload": bench["config"]["workload"] if bench else None, "kernel": k,
            "hbm_bytes_per_launch": round(w + r), "hbm_write_bytes_per_launch": round(w),
            "hbm_read_bytes_per_launch": round(r), "algorithmic_bytes_per_launch": alg,
