@@ -660,10 +660,10 @@ __device__ __forceinline__ void lin_patch_fix(int64_t (&acc)[LIN_CH], uint64_t X
         const int32_t d = s_lut[y1 >> 23] - s_lut[y0 >> 23];
         const int g = pp >= pos1 ? g1 : g0;
         const int64_t add = lane == (q & 63) ? (int64_t)g * (int64_t)d : 0;
+        const int sq = q >> 6;
 #pragma unroll
         for (int s = 0; s < LIN_CH; s++)
-            if (s == (q >> 6))
-                acc[s] += add;
+            acc[s] += add & -(int64_t)(s == sq);
     }
 }
 
