@@ -491,7 +491,9 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
 #define LIN_THREADS 256
 #define LIN_WAVES   (LIN_THREADS / 64)
 #define LIN_STEPS   64                     /* 64-sample steps per wave: 4096 samples            */
+#ifndef LIN_CH
 #define LIN_CH      16                     /* steps per chunk (one accumulator each)            */
+#endif
 #define CBW_X       3136                   /* windows per C/A row: chips E < 1023 + the reach of
                                               one wave (LIN_STEPS*64 samples * 0.49) + 64       */
 
@@ -714,7 +716,8 @@ __global__ __launch_bounds__(LIN_THREADS) void gss_lin_kernel(
             const bool chg = sk.pos1 < nb0 + 64 * LIN_CH;    /* a data bit by the chunk's end */
             lin_channel_chunk<false>(acc, X, Z, Zh, xs, zs, tab, chg && sk.pos1 <= nb0 ? g1 : g0,
                                      0, 0, 0, s_lut);
-            if (__builtin_expect(chg && sk.pos1 > nb0, 0)) {  /* ... inside it: add (g1-g0) e */
+            /* ... inside it, and the bit differs (half of the changes keep it): add (g1-g0) e */
+            if (__builtin_expect(chg && sk.pos1 > nb0 && g1 != g0, 0)) {
                 uint32_t l2 = (uint32_t)lane;
                 asm volatile("" : "+v"(l2));               /* recomputed: nothing stays live */
                 lin_channel_chunk<true>(acc, Xw + l2 * xs, Zw + l2 * zs, Zh, xs, zs, tab, 0,

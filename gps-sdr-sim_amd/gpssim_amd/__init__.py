@@ -13,7 +13,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libgpssim_amd.so")
+# GSS_LIB_PATH: an alternative build of the same library (kernel variants under measurement)
+LIB_PATH = os.environ.get("GSS_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libgpssim_amd.so")
 CLI_PATH = os.path.join(PKG_DIR, "bin", "gps-sdr-sim")
 
 MAXCH = 16
