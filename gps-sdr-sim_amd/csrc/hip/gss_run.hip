@@ -70,6 +70,7 @@ struct Run {
     std::mutex mu;
     std::condition_variable cv;
     int abort = 0;
+    uint32_t ca[32 * GSS_CA_WORDS];  /* C/A chips (gss_ca_table) for the proofs' patch terms */
     Slot slot[NSLOT];
 };
 
@@ -125,8 +126,8 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
             memcpy(sl.nav, rows, sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)n_rows);
         sl.n_nav = n_rows;
         if (r.use_lin) {                               /* the proofs, on the planner thread */
-            rc = gss_linearize(sl.blk, sl.nch, nb, r.n_per_blk, sl.nav, n_rows, sl.lin, sl.fast,
-                               r.threads);
+            rc = gss_linearize(sl.blk, sl.nch, nb, r.n_per_blk, r.ca, 32, sl.nav, n_rows, sl.lin,
+                               sl.fast, r.threads);
             if (rc)
                 return rc;
             int nf = 0;
@@ -307,10 +308,9 @@ extern "C" int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_bl
     };
     /* buffers */
     {
-        uint32_t ca[32 * GSS_CA_WORDS];
-        gss_ca_table(ca);
-        if (hipMalloc((void **)&d_ca, sizeof ca) != hipSuccess ||
-            hipMemcpy(d_ca, ca, sizeof ca, hipMemcpyHostToDevice) != hipSuccess ||
+        gss_ca_table(r.ca);
+        if (hipMalloc((void **)&d_ca, sizeof r.ca) != hipSuccess ||
+            hipMemcpy(d_ca, r.ca, sizeof r.ca, hipMemcpyHostToDevice) != hipSuccess ||
             hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
             err = gss_fail(GSS_E_HIP, "run setup failed");
         const size_t nb = (size_t)r.batch;

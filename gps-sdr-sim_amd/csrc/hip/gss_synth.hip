@@ -27,6 +27,7 @@
 #include <string.h>
 #include "gpssim_amd.h"
 #include "../common/gss_phase.h"
+#include "../common/gss_lin.h"
 
 #define SYNTH_THREADS  256
 #define SYNTH_WAVES    (SYNTH_THREADS / 64)
@@ -473,46 +474,72 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
 }
 
 /* ======================================================================================== */
-/* Fast path: certified integer lines (csrc/host/linearize.c)                               */
+/* Fast path: certified integer lines (csrc/host/linearize.c; render model common/gss_lin.h)  */
 /* ======================================================================================== */
-/* For a certified block, sample p of channel k reads LUT cell ((x0 + p xs) mod 2^64) >> 55 and
-   chip floor((z0 + p zs) / 2^50) mod 1023, with the signed gain of the schedule (gss_lin_t): no
-   floating point and no walk.  Lanes are consecutive samples: one wave step renders 64
-   consecutive samples, so the LUT reads of a wave hit a few neighbouring cells (no bank
-   conflicts) and the output leaves as one contiguous 256-B (-b 16) store per step.
-   A wave renders 64 steps (4096 samples) in chunks of LIN_CH steps.  Within a chunk the channel
-   loop is outermost: one channel's line parameters live in scalar registers at a time, its lane
-   phases X, Z (u64) are derived from the line at the chunk start, and each lane accumulates
-   LIN_CH samples (packed I/Q int64).  Chip signs: every lane's chip of two consecutive steps lies
-   in a 64-chip window starting at lane 0's chip E of the first (127 zs + 2 chips <= 64, checked by
-   gss_linearize), so one wave-uniform 64-bit window per step pair, read from the table cbw
-   (rotated: bit e mod 64 holds the sign of extended chip e, chip = e mod 1023), serves both steps
-   and a lane's sign is one 64-bit shift by its own chip index. */
+/* For a certified block, sample p of channel k reads the LUT cell and chip that gss_lin.h
+   defines from the block's two integer lines (gss_lin_t), with the signed gain of the schedule
+   and, at the rare patched samples, a correction to the exact term: no floating point and no
+   walk.  Lanes are consecutive samples: one wave step renders 64 consecutive samples, so the LUT
+   reads of a wave hit a few neighbouring cells and the output leaves as one contiguous 256-B
+   (-b 16) store per step.
+   A wave renders one 4096-sample segment in chunks of LIN_CH steps.  Within a chunk the channel
+   loop is outermost: one channel's line parameters live in scalar registers at a time; each lane
+   takes its chunk anchors from the lines (64-bit, once per chunk) and then steps
+       X = Xl + D.hi      carrier, 2^-32 cycle; D = 2^31 + s 64 xs is a
+                          scalar running sum (s_add_u32/s_addc_u32)    v_add_u32
+       Z += dZ            code, 32.32 fixed point (hi word = chip)     v_lshl_add_u64
+       t = W >> Z.hi      chip sign (bit 0) from the wave's 64-chip window   v_lshrrev_b64
+       a = alignbit(t, X, 21) & 0xFFC   LUT byte address: cell (X bits 23..31) at bits 2..10,
+                                        chip sign at bit 11 (second half of the LUT negated)
+       acc += g * LUT[a]  packed I/Q                                   v_mad_i64_i32
+   6 VALU + 1 LDS per channel-sample (the round-1 kernel needed 8, two of them 64-bit adds;
+   tools/ubench/body_ubench.hip: 1.55x fewer SIMD cycles).  Chip windows: every lane's chip of two
+   consecutive steps lies in a 64-chip window starting at lane 0's chip E of the first
+   (127 zs + 2 chips <= 64, checked by gss_linearize), so one wave-uniform 64-bit window per step
+   pair, read from the table cbw (rotated: bit e mod 64 holds the sign of extended chip e,
+   chip = e mod 1023), serves both steps; v_lshrrev_b64 takes the shift mod 64. */
 #define LIN_THREADS 256
 #define LIN_WAVES   (LIN_THREADS / 64)
-#define LIN_STEPS   64                     /* 64-sample steps per wave: 4096 samples            */
-#ifndef LIN_CH
-#define LIN_CH      16                     /* steps per chunk (one accumulator each)            */
+#define LIN_STEPS   64                     /* 64-sample steps per wave segment: 4096 samples    */
+#define LIN_CH      GSS_LIN_CH             /* steps per chunk (one accumulator each)            */
+#define CBW_PRE     8                      /* windows kept below chip 0 (window starts run up to
+                                              3 chips below lane 0's chip)                      */
+#define CBW_X       (3136 + CBW_PRE)       /* windows per C/A row: chips -8 <= E < 1023 + the
+                                              reach of one wave (LIN_STEPS*64 samples * 0.49)+64 */
+static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole chunks");
+/* LIN_ABLATE (measurement builds only, tools/ablate.sh; wrong output): 1 no output stores,
+   2 no chip-window loads, 4 no LUT reads */
+#ifndef LIN_ABLATE
+#define LIN_ABLATE 0
 #endif
-#define CBW_X       3136                   /* windows per C/A row: chips E < 1023 + the reach of
-                                              one wave (LIN_STEPS*64 samples * 0.49) + 64       */
 
-/* per (block, channel, wave segment of 64*LIN_STEPS samples): the lines evaluated at the
-   segment start, written by gss_linseg_kernel so that the render kernel needs no 128-bit
-   arithmetic and no schedule search */
+/* per (block, channel): the render constants of gss_lin.h (written by gss_linseg_kernel) */
+struct lin_chan {
+    uint64_t xs, zs;             /* the lines' per-sample steps                                 */
+    uint64_t dz;                 /* gss_lin_dz(zs): the code's 64-sample step, 32.32 chips       */
+    uint64_t pad0;
+    uint32_t dx;                 /* gss_lin_dx(xs): the carrier's 64-sample step, 2^-32 cycle    */
+    uint32_t dq;                 /* window start advance per step pair, 1/8 chip, rounded down   */
+    uint32_t tab;                /* byte offset of the channel's window row (chip -CBW_PRE)      */
+    uint32_t pad1[5];
+};
+/* per (block, channel, wave segment of 64*LIN_STEPS samples): the lines at the segment start,
+   so that the render kernel needs no 128-bit arithmetic and no schedule search */
 struct lin_seg {
-    uint64_t z;                  /* (E0 << 50) | fraction: E0 = chip at the start mod 1023       */
-    uint64_t x;                  /* carrier line at the segment start (mod 2^64)                 */
+    uint64_t x;                  /* X(n0) + gss_lin_xa(xs): the first chunk's carrier anchor base */
+    uint64_t z;                  /* ((E0 << 50) | fraction) + 2^17: the first chunk's code anchor
+                                    base, E0 = chip at the segment start mod 1023               */
     int32_t g01;                 /* signed gain at the start (low 16) and after pos1 (high 16)   */
     int32_t pos1;                /* sample of the first gain change in the segment, or INT32_MAX */
-    uint32_t tab;                /* row offset of the channel's C/A table in cbw (ca_tbl*CBW_X)  */
     uint32_t npatch;             /* patched samples of the channel inside the segment            */
+    uint32_t pad;
 };
 
 __global__ void gss_linseg_kernel(const gss_lin_t *__restrict__ lin,
                                   const gss_chan_blk_t *__restrict__ blk,
                                   const int32_t *__restrict__ nch, const int32_t *__restrict__ fast,
-                                  int nblk, int nseg, lin_seg *__restrict__ seg_out)
+                                  int nblk, int nseg, lin_seg *__restrict__ seg_out,
+                                  lin_chan *__restrict__ chan_out)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nblk * GSS_MAXCH * nseg)
@@ -521,13 +548,24 @@ __global__ void gss_linseg_kernel(const gss_lin_t *__restrict__ lin,
     if (!fast[b] || k >= nch[b])
         return;
     const gss_lin_t *L = lin + bk;
+    const uint64_t xa = gss_lin_xa(L->xs);
+    if (sg == 0) {
+        lin_chan c = {};
+        c.xs = L->xs;
+        c.zs = L->zs;
+        c.dz = gss_lin_dz(L->zs);
+        c.dx = gss_lin_dx(L->xs);
+        c.dq = (uint32_t)((L->zs * 128u) >> 47);
+        c.tab = (uint32_t)((size_t)blk[bk].ca_tbl * CBW_X * sizeof(uint64_t));
+        chan_out[bk] = c;
+    }
     const uint64_t n0 = (uint64_t)sg * (64 * LIN_STEPS);
     const uint64_t lo = L->z0 + n0 * L->zs;
     const uint64_t hi = __umul64hi(n0, L->zs) + (lo < L->z0 ? 1u : 0u);
     const uint32_t E0 = ((uint32_t)(hi << 14) | (uint32_t)(lo >> 50)) % (uint32_t)GSS_CA_LEN;
     lin_seg r;
-    r.z = ((uint64_t)E0 << 50) | (lo & ((1ull << 50) - 1));
-    r.x = L->x0 + n0 * L->xs;
+    r.z = (((uint64_t)E0 << 50) | (lo & ((1ull << 50) - 1))) + (1ull << 17);
+    r.x = L->x0 + n0 * L->xs + xa;
     int q = 0;
     while (q + 1 < GSS_NGC && L->gpos[q + 1] <= (int)n0)
         q++;
@@ -536,59 +574,64 @@ __global__ void gss_linseg_kernel(const gss_lin_t *__restrict__ lin,
     const int g1 = more ? L->gval[q + 1] : g0;
     r.g01 = (int32_t)(((uint32_t)g0 & 0xFFFFu) | ((uint32_t)g1 << 16));
     r.pos1 = more ? L->gpos[q + 1] : INT32_MAX;
-    r.tab = (uint32_t)blk[bk].ca_tbl * CBW_X;
     int np = 0;
     for (int j = 0; j < GSS_NPATCH; j++)
         np += L->ppos[j] >= (int)n0 && L->ppos[j] < (int)n0 + 64 * LIN_STEPS;
     r.npatch = (uint32_t)np;
+    r.pad = 0;
     seg_out[i] = r;
 }
 
+/* per C/A row, the rotated 64-bit chip-sign windows of extended chips E = -CBW_PRE .. */
 __global__ void gss_cbw_kernel(const uint32_t *__restrict__ ca_bits, int n_ca,
                                uint64_t *__restrict__ cbw)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_ca * CBW_X)
         return;
-    const int row = i / CBW_X, E = i - row * CBW_X;
+    const int row = i / CBW_X, E = i - row * CBW_X - CBW_PRE;
     const uint32_t *cb = ca_bits + (size_t)row * GSS_CA_WORDS;
     uint64_t w = 0;
     for (int q = 0; q < 64; q++) {
-        const int e = E + q, chip = e % GSS_CA_LEN;
+        const int e = E + q, chip = (e + GSS_CA_LEN) % GSS_CA_LEN;
         const uint64_t neg = ((cb[chip >> 5] >> (chip & 31)) & 1u) ^ 1u;   /* codeCA = -1 */
-        w |= neg << (e & 63);
+        w |= neg << ((e + 64) & 63);
     }
     cbw[i] = w;
 }
 
-/* one channel's contribution to LIN_CH steps of the wave: X, Z lane phases at the first step,
-   Zh = bits 32..63 of lane 0's code register, the window-table row, the signed gain (per lane
-   when a data bit changes inside the chunk) */
+/* one channel's contribution to the chunk's LIN_CH steps: lane anchors X (carrier, 2^-32
+   cycle) and Z (code, 32.32) and their 64-sample steps, the first pair's window start Q
+   (1/8 chip above chip -CBW_PRE, at most 3 chips below lane 0's chip) and its per-pair advance,
+   the channel's window row (chip -CBW_PRE), the signed gain (with LANE_GAIN: the gain difference, applied from sample
+   pos1 on) */
 template <bool LANE_GAIN>
-__device__ __forceinline__ void lin_channel_chunk(int64_t (&acc)[LIN_CH], uint64_t X, uint64_t Z,
-                                                  uint32_t Zh, uint64_t xs, uint64_t zs,
-                                                  const uint64_t *__restrict__ tab, int g0,
-                                                  int g1, int pos1, int p0,
+__device__ __forceinline__ void lin_channel_chunk(int64_t (&acc)[LIN_CH], uint32_t X, uint64_t Z,
+                                                  uint32_t dX, uint64_t dZ, uint32_t Q,
+                                                  uint32_t dq, const char *__restrict__ tab,
+                                                  int g, int pos1, int p0,
                                                   const int32_t *__restrict__ s_lut)
 {
-    const uint64_t dX = xs << 6, dZ = zs << 6;
-    /* lane 0's chip at step pair s/2, from 32-bit truncated values: at most one chip low, which
-       the window's slack (lanes need <= 52 of its 64 chips) absorbs */
-    const uint32_t dZh = (uint32_t)((dZ << 1) >> 32);
+    /* the chunk's chip windows, one per step pair, all loaded before the first use: a scalar
+       load can only be waited for together with every LDS read in flight (lgkmcnt) */
+    uint64_t W[LIN_CH / 2];
 #pragma unroll
-    for (int s = 0; s < LIN_CH; s += 2) {
-        const uint64_t W = tab[(Zh + (uint32_t)(s / 2) * dZh) >> 18];       /* scalar */
+    for (int j = 0; j < LIN_CH / 2; j++) {
+        if (LIN_ABLATE & 2)
+            W[j] = Q * 0x9E3779B97F4A7C15ull;
+        else
+            W[j] = *(const uint64_t *)(tab + (Q & ~7u));  /* scalar loads, SGPR offset */
+        Q += dq;
+    }
 #pragma unroll
-        for (int ss = 0; ss < 2; ss++) {
-            const uint32_t ci = (uint32_t)(Z >> 50);
-            const uint32_t t = (uint32_t)(W >> (ci & 63));               /* bit 0: chip sign */
-            const uint32_t y = (t << 31) + (uint32_t)(X >> 32);          /* + half a cycle */
-            const int32_t e = *(const int32_t *)((const char *)s_lut + ((y >> 21) & 0x7FCu));
-            const int g = LANE_GAIN ? (p0 + (s + ss) * 64 >= pos1 ? g1 : g0) : g0;
-            acc[s + ss] += (int64_t)g * (int64_t)e;
-            X += dX;
-            Z += dZ;
-        }
+    for (int s = 0; s < LIN_CH; s++) {
+        const uint32_t t = (uint32_t)(W[s / 2] >> ((uint32_t)(Z >> 32) & 63));   /* bit 0 */
+        const uint32_t a = __builtin_amdgcn_alignbit(t, X, 21) & 0xFFCu;
+        const int32_t e = (LIN_ABLATE & 4) ? (int32_t)a : *(const int32_t *)((const char *)s_lut + a);
+        const int gg = LANE_GAIN ? (p0 + s * 64 >= pos1 ? g : 0) : g;
+        acc[s] += (int64_t)gg * (int64_t)e;
+        X += dX;
+        Z += dZ;
     }
 }
 
@@ -632,36 +675,19 @@ __device__ __forceinline__ void lin_store(const int64_t (&acc)[LIN_CH], uint8_t 
     }
 }
 
-/* The chunk holds samples where the channel's line does not give the exact LUT cell or chip
-   (gss_lin_t ppos/pval, rare): in that lane and step, replace the line's term by the exact one.
-   A patched sample is the same for every lane, so its phases are wave-uniform. */
-__device__ __forceinline__ void lin_patch_fix(int64_t (&acc)[LIN_CH], uint64_t Xw, uint64_t Zw,
-                                              uint64_t xs, uint64_t zs,
-                                              const uint64_t *__restrict__ tab,
-                                              const gss_lin_t *__restrict__ Lk, int nb0, int lane,
-                                              int g0, int g1, int pos1,
-                                              const int32_t *__restrict__ s_lut)
+/* The chunk holds samples where the render arithmetic does not give the exact term (gss_lin_t
+   ppos/pdelta, rare): add the correction to that lane and step. */
+__device__ __forceinline__ void lin_patch_fix(int64_t (&acc)[LIN_CH],
+                                              const gss_lin_t *__restrict__ Lk, int nb0, int lane)
 {
     for (int j = 0; j < GSS_NPATCH; j++) {
-        const int pp = Lk->ppos[j];
-        if (pp < nb0 || pp >= nb0 + 64 * LIN_CH || (j > 0 && Lk->ppos[j - 1] == pp))
-            continue;                                 /* one pass per patched sample */
+        const int pp = Lk->ppos[j];                   /* ascending, unused = INT32_MAX */
+        if (pp >= nb0 + 64 * LIN_CH)
+            break;
+        if (pp < nb0)
+            continue;
         const int q = pp - nb0;
-        const uint64_t X = Xw + (uint64_t)q * xs, Z = Zw + (uint64_t)q * zs;
-        const uint32_t E = (uint32_t)(Z >> 50);       /* the line's chip (extended index) */
-        uint32_t t = (uint32_t)(tab[E] >> (E & 63)), hx = (uint32_t)(X >> 32);
-        const uint32_t y0 = (t << 31) + hx;
-        for (int i = j; i < GSS_NPATCH && Lk->ppos[i] == pp; i++) {
-            const int v = Lk->pval[i] & 0xFFFF;
-            if (Lk->pval[i] >> 16)
-                t = (uint32_t)(tab[v] >> (v & 63));   /* the exact chip */
-            else
-                hx = (uint32_t)v << 23;               /* the exact LUT cell */
-        }
-        const uint32_t y1 = (t << 31) + hx;
-        const int32_t d = s_lut[y1 >> 23] - s_lut[y0 >> 23];
-        const int g = pp >= pos1 ? g1 : g0;
-        const int64_t add = lane == (q & 63) ? (int64_t)g * (int64_t)d : 0;
+        const int64_t add = lane == (q & 63) ? Lk->pdelta[j] : 0;
         const int sq = q >> 6;
 #pragma unroll
         for (int s = 0; s < LIN_CH; s++)
@@ -672,25 +698,29 @@ __device__ __forceinline__ void lin_patch_fix(int64_t (&acc)[LIN_CH], uint64_t X
 template <int FMT>
 __global__ __launch_bounds__(LIN_THREADS) void gss_lin_kernel(
     const gss_lin_t *__restrict__ lin, const lin_seg *__restrict__ segs,
-    const int32_t *__restrict__ nch, const int32_t *__restrict__ fast,
-    const uint64_t *__restrict__ cbw, lut_arg lut, int n_per_blk, int nseg, int wg_per_blk,
-    uint8_t *__restrict__ out, size_t block_bytes)
+    const lin_chan *__restrict__ chans, const int32_t *__restrict__ nch,
+    const int32_t *__restrict__ fast, const uint64_t *__restrict__ cbw, lut_arg lut,
+    int n_per_blk, int nseg, int wg_per_blk, uint8_t *__restrict__ out, size_t block_bytes)
 {
-    __shared__ int32_t s_lut[512];                        /* cos + 2^22 sin */
+    __shared__ int32_t s_lut[1024];                       /* cos + 2^22 sin; [512+i] = -[i] */
     const int b = blockIdx.x / wg_per_blk;
     const int w = blockIdx.x - b * wg_per_blk;
     if (!fast[b])
         return;                                           /* the exact path renders it */
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);    /* wave-uniform: scalar */
-    for (int i = tid; i < 512; i += LIN_THREADS)
-        s_lut[i] = (int32_t)lut.cos512[i] + (int32_t)lut.sin512[i] * (1 << 22);
+    for (int i = tid; i < 512; i += LIN_THREADS) {
+        const int32_t v = (int32_t)lut.cos512[i] + (int32_t)lut.sin512[i] * (1 << 22);
+        s_lut[i] = v;
+        s_lut[512 + i] = -v;
+    }
     __syncthreads();
     const int sg = w * LIN_WAVES + wave;
     const int n0 = sg * (64 * LIN_STEPS);
     if (n0 >= n_per_blk)
         return;
     const gss_lin_t *L = lin + (size_t)b * GSS_MAXCH;
+    const lin_chan *CH = chans + (size_t)b * GSS_MAXCH;
     const lin_seg *S = segs + (size_t)b * GSS_MAXCH * nseg + sg;
     const int nc = nch[b];
     uint8_t *ob = out + (size_t)b * block_bytes;
@@ -704,29 +734,38 @@ __global__ __launch_bounds__(LIN_THREADS) void gss_lin_kernel(
         for (int s = 0; s < LIN_CH; s++)
             acc[s] = 64 + (1 << 21) + ((int64_t)64 << 22);
         for (int k = 0; k < nc; k++) {                    /* uniform channel loop */
-            const lin_seg sk = S[(size_t)k * nseg];       /* scalar loads */
-            const uint64_t xs = L[k].xs, zs = L[k].zs;
+            const lin_chan ck = CH[k];                    /* scalar loads */
+            const lin_seg sk = S[(size_t)k * nseg];
+            /* chunk anchor bases (gss_lin.h): the segment's, plus c chunks of 64 LIN_CH samples */
             const uint64_t off = (uint64_t)c * (64 * LIN_CH);
-            const uint64_t Zw = sk.z + off * zs, Xw = sk.x + off * xs;
-            const uint64_t X = Xw + (uint64_t)lane * xs;
-            const uint64_t Z = Zw + (uint64_t)lane * zs;
+            const uint64_t xb = sk.x + off * ck.xs;
+            const uint64_t zb = sk.z + off * ck.zs;
             const int g0 = (int)(int16_t)(sk.g01 & 0xFFFF), g1 = sk.g01 >> 16;
-            const uint64_t *tab = cbw + sk.tab;
-            const uint32_t Zh = (uint32_t)(Zw >> 32);
+            const char *tab = (const char *)cbw + ck.tab;
+            const uint32_t Q = (uint32_t)(zb >> 47) + (8 * CBW_PRE - 1);   /* below lane 0 */
             const bool chg = sk.pos1 < nb0 + 64 * LIN_CH;    /* a data bit by the chunk's end */
-            lin_channel_chunk<false>(acc, X, Z, Zh, xs, zs, tab, chg && sk.pos1 <= nb0 ? g1 : g0,
-                                     0, 0, 0, s_lut);
-            /* ... inside it, and the bit differs (half of the changes keep it): add (g1-g0) e */
-            if (__builtin_expect(chg && sk.pos1 > nb0 && g1 != g0, 0)) {
+            lin_channel_chunk<false>(acc, (uint32_t)((xb + (uint64_t)lane * ck.xs) >> 32),
+                                     (zb + (uint64_t)lane * ck.zs) >> 18, ck.dx, ck.dz, Q, ck.dq,
+                                     tab, chg && sk.pos1 <= nb0 ? g1 : g0, 0, 0, s_lut);
+            /* ... inside it: add (g1 - g0) e from sample pos1 on */
+            if (__builtin_expect(chg && sk.pos1 > nb0, 0)) {
                 uint32_t l2 = (uint32_t)lane;
                 asm volatile("" : "+v"(l2));               /* recomputed: nothing stays live */
-                lin_channel_chunk<true>(acc, Xw + l2 * xs, Zw + l2 * zs, Zh, xs, zs, tab, 0,
-                                        g1 - g0, sk.pos1, nb0 + (int)l2, s_lut);
+                lin_channel_chunk<true>(acc, (uint32_t)((xb + (uint64_t)l2 * ck.xs) >> 32),
+                                        (zb + (uint64_t)l2 * ck.zs) >> 18, ck.dx, ck.dz, Q, ck.dq,
+                                        tab, g1 - g0, sk.pos1, nb0 + (int)l2, s_lut);
             }
             if (__builtin_expect(sk.npatch != 0, 0))
-                lin_patch_fix(acc, Xw, Zw, xs, zs, tab, L + k, nb0, lane, g0, g1, sk.pos1, s_lut);
+                lin_patch_fix(acc, L + k, nb0, lane);
         }
-        if (nb0 + 64 * LIN_CH <= n_per_blk)
+        if (LIN_ABLATE & 1) {
+            int64_t x = 0;
+#pragma unroll
+            for (int s = 0; s < LIN_CH; s++)
+                x ^= acc[s];
+            if (x == 0x123456789)
+                ob[lane] = 1;
+        } else if (nb0 + 64 * LIN_CH <= n_per_blk)
             lin_store<FMT, false>(acc, ob, nb0, lane, n_per_blk);
         else
             lin_store<FMT, true>(acc, ob, nb0, lane, n_per_blk);
@@ -990,8 +1029,9 @@ extern "C" int gss_render_device(gss_dev *d, int set, const gss_chan_blk_t *blk,
 }
 
 /* ---- fast path -------------------------------------------------------------------------- */
-typedef void (*lin_fn)(const gss_lin_t *, const lin_seg *, const int32_t *, const int32_t *,
-                       const uint64_t *, lut_arg, int, int, int, uint8_t *, size_t);
+typedef void (*lin_fn)(const gss_lin_t *, const lin_seg *, const lin_chan *, const int32_t *,
+                       const int32_t *, const uint64_t *, lut_arg, int, int, int, uint8_t *,
+                       size_t);
 
 static lin_fn pick_lin(int fmt)
 {
@@ -1040,15 +1080,19 @@ extern "C" int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const
     const int segs = (n_per_blk + 64 * LIN_STEPS - 1) / (64 * LIN_STEPS);
     const int wg_per_blk = (segs + LIN_WAVES - 1) / LIN_WAVES;
     const size_t nsegrows = (size_t)nblk * GSS_MAXCH * segs;
-    if (nsegrows * sizeof(lin_seg) > d->d_seg_cap) {
+    const size_t seg_bytes = nsegrows * sizeof(lin_seg);
+    const size_t need_rows = seg_bytes + (size_t)nblk * GSS_MAXCH * sizeof(lin_chan);
+    if (need_rows > d->d_seg_cap) {
         (void)hipFree(d->d_seg);
         d->d_seg = nullptr;
         d->d_seg_cap = 0;
-        HIP_TRY(hipMalloc(&d->d_seg, nsegrows * sizeof(lin_seg)));
-        d->d_seg_cap = nsegrows * sizeof(lin_seg);
+        HIP_TRY(hipMalloc(&d->d_seg, need_rows));
+        d->d_seg_cap = need_rows;
     }
+    lin_seg *d_segs = (lin_seg *)d->d_seg;
+    lin_chan *d_chans = (lin_chan *)((char *)d->d_seg + seg_bytes);
     hipLaunchKernelGGL(gss_linseg_kernel, dim3((unsigned)((nsegrows + 255) / 256)), dim3(256), 0,
-                       st, lin, blk, nch, fast, nblk, segs, (lin_seg *)d->d_seg);
+                       st, lin, blk, nch, fast, nblk, segs, d_segs, d_chans);
     HIP_TRY(hipGetLastError());
     if (n_fb > 0) {          /* the exact path for the uncertified blocks, on the aux stream */
         HIP_TRY(hipEventRecord(d->ev_in, st));
@@ -1067,8 +1111,8 @@ extern "C" int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const
     d->n_l++;
     HIP_TRY(hipEventRecord(ev[0], st));
     hipLaunchKernelGGL(fn, dim3((unsigned)nblk * wg_per_blk), dim3(LIN_THREADS), 0, st, lin,
-                       (const lin_seg *)d->d_seg, nch, fast, d->d_cbw, d->lut, n_per_blk, segs,
-                       wg_per_blk, (uint8_t *)out, bb);
+                       (const lin_seg *)d_segs, (const lin_chan *)d_chans, nch, fast, d->d_cbw,
+                       d->lut, n_per_blk, segs, wg_per_blk, (uint8_t *)out, bb);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], st));
     if (n_fb > 0)                                 /* the call completes when both are done */
@@ -1210,7 +1254,7 @@ extern "C" int gss_synth_host(gss_dev *d, const gss_chan_blk_t *blk, const int32
             free(h_fast);
             return gss_fail(GSS_E_NOMEM, "out of memory");
         }
-        rc = gss_linearize(blk, nch, nblk, n_per_blk, nav, n_nav, h_lin, h_fast, 8);
+        rc = gss_linearize(blk, nch, nblk, n_per_blk, ca_bits, n_ca, nav, n_nav, h_lin, h_fast, 8);
         int n_fb = 0;
         for (int b = 0; b < nblk; b++)
             if (!h_fast[b])

@@ -9,27 +9,32 @@
  * fixed-point lines of the block's own start values and steps,
  *     carrier  X(p) = rnd(carr0 2^64) + p rnd(carr_step 2^64)  mod 2^64,  LUT cell X >> 55
  *     code     Z(p) = rnd(code0 2^50) + p rnd(code_step 2^50),            chip (Z >> 50) mod 1023
- * and proves, with exact integer arithmetic, at which samples they could select another LUT cell
- * or chip than the reference's doubles.  Those samples are decided exactly and, where the line is
- * wrong, patched (gss_lin_t ppos/pval).
+ * The kernel renders from chunk anchors of these lines plus 32-bit steps (gss_lin.h: the
+ * kernel's cell and chip at sample p are gss_lin_kcell / gss_lin_kchip, within
+ * GSS_LIN_KDEV_* of the lines).  This file proves, with exact integer arithmetic, at which samples
+ * the kernel could read another LUT cell or chip sign than the reference's doubles, decides those
+ * samples exactly and, where the kernel's term differs, stores the difference as a patch
+ * (gss_lin_t ppos/pdelta) that the kernel adds to that sample's accumulator.
  *
  * Proof, per chain and block of n samples:
  *   1. Each reference step is one IEEE addition (error <= 2^-53 cycle for sums below 2, <= 2^-44
  *      chip below 1024) plus a wrap that is exact (carr -= 1 and code -= 1023, Sterbenz) or
  *      rounded once (carr += 1, <= 2^-54).  So the unwrapped exact value moves by the step plus
  *      less than 2^12 units of 2^-64 cycle (2^7 units of 2^-50 chip) per sample, and the line by
- *      the step plus at most half a unit: |line - exact| <= Delta = 2 + n (err + 1) over the
- *      block, about 2^-34 cycle and 2^-25 chip for a 0.1 s block at 2.6 MS/s.
- *   2. A sample can read another cell than the line only if the line lies within Delta of a cell
- *      boundary (a multiple of B = 2^55, resp. 2^50): (line(p) + Delta) mod B < 2 Delta.  These
- *      samples are enumerated exactly: gss_minmod computes min over p of (a + p s) mod m in
- *      O(log m) steps (a Euclid-like reduction of the sawtooth), inside a binary search over
- *      prefixes.  At 2.6 MS/s about one chain in sixty has one.
- *   3. The exact value at each of them comes from the cycle-cached walks of gss_phase.h; where
- *      the line's cell or chip is not the exact one it becomes a patch.
+ *      the step plus at most half a unit: |line - exact| <= D1 = 2 + n (err + 1) over the block,
+ *      about 2^-34 cycle and 2^-25 chip for a 0.1 s block at 2.6 MS/s.  |kernel - line| <= D2
+ *      (GSS_LIN_KDEV_*: 2^-28 cycle, 2^-28 chip).
+ *   2. The exact value, the line and the kernel can fall into different cells only where the line
+ *      lies within D = D1 + D2 of a cell boundary (a multiple of B = 2^55, resp. 2^50):
+ *      (line(p) + D) mod B < 2 D.  These samples are enumerated exactly: gss_minmod computes the
+ *      min over p of (a + p s) mod m in O(log m) steps (a Euclid-like reduction of the sawtooth),
+ *      inside a binary search over prefixes.  At 2.6 MS/s about one carrier chain in two has one.
+ *   3. The exact value at each of them comes from the cycle-cached walks of gss_phase.h, the
+ *      kernel's from gss_lin.h; where the signed LUT term differs it becomes a patch.
  *   4. Code wraps are chip boundaries too: the k-th wrap falls where the line crosses
  *      1023 k 2^50, one sample earlier or later only where step 3 found the exact value on the
- *      other side.  The counters and the signed gain (gpssim.c:2186, 2219-2237) follow.
+ *      other side.  The counters and the signed gain (gpssim.c:2186, 2219-2237) follow; the
+ *      kernel applies the gain by sample position, so a patch only ever corrects cell and chip.
  * A channel with more than LIN_MAXHIT ambiguous samples or GSS_NPATCH patches, or failing a
  * precondition of the kernel (below), sends its block to the exact walking path (Stage A +
  * Stage B); gss_linearize reports that per block.  Cost: O(log B) per chain plus the rare walks.
@@ -40,6 +45,7 @@
 #include <string.h>
 #include "gss_host.h"
 #include "../common/gss_phase.h"
+#include "../common/gss_lin.h"
 
 typedef unsigned __int128 u128;
 typedef __int128 i128;
@@ -153,30 +159,11 @@ static int ambiguous(i128 L0, i128 S, i128 delta, int lgB, int64_t n, int64_t *h
 #define LIN_CODE_LGB 50          /* 2^50 units of 2^-50 chip = one chip */
 #define LIN_CARR_ERR ((i128)1 << 12)    /* one step's rounding (bound), units of 2^-64 cycle */
 #define LIN_CODE_ERR ((i128)1 << 7)     /* one step's rounding (bound), units of 2^-50 chip  */
-#define LIN_MAXHIT 16            /* ambiguous samples examined per chain */
+#define LIN_MAXHIT 64            /* ambiguous samples examined per chain */
 
 static int signed_gain(int gain, const uint32_t *nav, int iword, int ibit)
 {
     return ((nav[iword] >> (29 - ibit)) & 1u) ? gain : -gain;
-}
-
-/* Record that sample pos reads cell/chip `value` instead of the line's (kind 0: LUT cell,
-   kind 1: chip).  Patches stay sorted by position; 0 when the table is full. */
-static int add_patch(gss_lin_t *lin, int64_t pos, int kind, int value)
-{
-    int j = 0;
-    while (j < GSS_NPATCH && lin->ppos[j] != INT32_MAX)
-        j++;
-    if (j == GSS_NPATCH)
-        return 0;
-    while (j > 0 && lin->ppos[j - 1] > pos) {
-        lin->ppos[j] = lin->ppos[j - 1];
-        lin->pval[j] = lin->pval[j - 1];
-        j--;
-    }
-    lin->ppos[j] = (int32_t)pos;
-    lin->pval[j] = (kind << 16) | value;
-    return 1;
 }
 
 static int find_hit(const int64_t *hit, int nh, int64_t q)
@@ -194,39 +181,65 @@ static int64_t wraps_of(const gss_code_state *c, const gss_chan_blk_t *p)
            (c->icode - p->icode);
 }
 
+/* cos + 2^22 sin of LUT cell c (the kernel's packed I/Q term, gpssim.c:15-83) */
+static int64_t lut_packed(int c)
+{
+    static int32_t sinT[512], cosT[512];
+    static int ready;
+    if (!__atomic_load_n(&ready, __ATOMIC_ACQUIRE)) {
+        int32_t s[512], co[512];
+        gss_lut(s, co);
+        for (int i = 0; i < 512; i++) {
+            sinT[i] = s[i];
+            cosT[i] = co[i];
+        }
+        __atomic_store_n(&ready, 1, __ATOMIC_RELEASE);
+    }
+    return (int64_t)cosT[c] + (int64_t)sinT[c] * ((int64_t)1 << 22);
+}
+
+static int ca_sign(const uint32_t *ca, int chip)          /* codeCA (gpssim.c:2220) */
+{
+    return ((ca[chip >> 5] >> (chip & 31)) & 1u) ? 1 : -1;
+}
+
+/* 1 if the line value v lies within d of a multiple of 2^lgB */
+static int near_boundary(i128 v, i128 d, int lgB)
+{
+    const i128 B = (i128)1 << lgB;
+    return (((v + d) % B) + B) % B < 2 * d;
+}
+
+/* merge two ascending sample lists and {0}: ascending, no duplicates */
+static int merge_hits(const int64_t *a, int na, const int64_t *b, int nb, int64_t *out)
+{
+    int i = 0, j = 0, n = 0;
+    out[n++] = 0;
+    while (i < na || j < nb) {
+        int64_t v = (j >= nb || (i < na && a[i] <= b[j])) ? a[i++] : b[j++];
+        if (v != out[n - 1])
+            out[n++] = v;
+    }
+    return n;
+}
+
 /* 1 if certified (lin filled), 0 if this channel needs the exact path */
-static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, gss_lin_t *lin)
+static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, const uint32_t *ca,
+                       gss_lin_t *lin)
 {
     int inexact = 0;
-    int64_t hit[LIN_MAXHIT];
-    gss_code_state at_hit[LIN_MAXHIT];
+    int64_t hx[LIN_MAXHIT], hz[LIN_MAXHIT], hq[2 * LIN_MAXHIT + 1];
+    gss_code_state at_hz[LIN_MAXHIT];
 
-    /* ---- carrier (gpssim.c:2245-2250) ---- */
+    /* ---- the two lines and the samples where they decide nothing (gpssim.c:2212-2250) ---- */
     const double x0 = p->carr0, s = p->carr_step;
     if (!(x0 >= 0.0 && x0 < 1.0) || !(s > -0.5 && s < 0.5))
         return 0;
     const i128 X0 = to_fix(x0, 64, &inexact), XS = to_fix(s, 64, &inexact);
-    int nh = ambiguous(X0, XS, 2 + (i128)n * (LIN_CARR_ERR + 1), LIN_CARR_LGB, n, hit,
-                       LIN_MAXHIT);
-    if (nh < 0)
+    const i128 DX1 = 2 + (i128)n * (LIN_CARR_ERR + 1);           /* line vs reference */
+    const int nhx = ambiguous(X0, XS, DX1 + GSS_LIN_KDEV_CARR, LIN_CARR_LGB, n, hx, LIN_MAXHIT);
+    if (nhx < 0)
         return 0;
-    const int cell0 = (int)floor(x0 * 512.0);
-    if ((int)((uint64_t)X0 >> LIN_CARR_LGB) != cell0 && !add_patch(lin, 0, 0, cell0))
-        return 0;                                /* sample 0: the rounded start's own cell */
-    double x = x0;
-    int64_t at = 0;
-    for (int i = 0; i < nh; i++) {               /* the ambiguous samples, exactly */
-        x = gss_carr_walk_cc(x, s, hit[i] - at);
-        at = hit[i];
-        const int cell = (int)floor(x * 512.0);
-        const int line = (int)((uint64_t)(X0 + (i128)hit[i] * XS) >> LIN_CARR_LGB);
-        if (cell != line && !add_patch(lin, hit[i], 0, cell))
-            return 0;
-    }
-    lin->x0 = (uint64_t)X0;
-    lin->xs = (uint64_t)XS;
-
-    /* ---- code with its counters (gpssim.c:2212-2237) ---- */
     const double c0 = p->code0, cs = p->code_step;
     if (!(c0 >= 0.0 && c0 < GSS_CA_SEQ_LEN_D) || !(cs > 0.0 && cs < 1.0))
         return 0;
@@ -236,29 +249,28 @@ static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, gss_
     const int64_t Z0 = (int64_t)to_fix(c0, 50, &inexact);
     const int64_t ZS = (int64_t)to_fix(cs, 50, &inexact);
     const int64_t per = (int64_t)GSS_CA_LEN << LIN_CODE_LGB;
-    /* the kernel reads a 64-chip window per two 64-sample steps: 127 steps + 2 chips <= 64 */
+    /* the kernel reads a 64-chip window per two 64-sample steps, starting up to 3 chips below
+       lane 0's chip: 127 steps + 4 chips <= 64 */
     if (ZS <= 0 || Z0 >= per ||
-        ZS * 127 + ((int64_t)2 << LIN_CODE_LGB) > ((int64_t)64 << LIN_CODE_LGB))
+        ZS * 127 + ((int64_t)4 << LIN_CODE_LGB) > ((int64_t)64 << LIN_CODE_LGB))
         return 0;
-    nh = ambiguous(Z0, ZS, 2 + (i128)n * (LIN_CODE_ERR + 1), LIN_CODE_LGB, n, hit, LIN_MAXHIT);
-    if (nh < 0)
+    const int nhz = ambiguous(Z0, ZS, 2 + (i128)n * (LIN_CODE_ERR + 1) + GSS_LIN_KDEV_CODE,
+                              LIN_CODE_LGB, n, hz, LIN_MAXHIT);
+    if (nhz < 0)
         return 0;
-    const int chip0 = (int)floor(c0);
-    if ((int)(Z0 >> LIN_CODE_LGB) != chip0 && !add_patch(lin, 0, 1, chip0))
-        return 0;                                /* sample 0: the rounded start's own chip */
-    gss_code_state st = {c0, p->icode, p->ibit, p->iword};
-    at = 0;
-    for (int i = 0; i < nh; i++) {
-        gss_code_walk_cc(&st, cs, hit[i] - at);
-        at = hit[i];
-        at_hit[i] = st;
-        const int chip = (int)floor(st.ph);
-        const int line = (int)(((Z0 + (i128)hit[i] * ZS) >> LIN_CODE_LGB) % GSS_CA_LEN);
-        if (chip != line && !add_patch(lin, hit[i], 1, chip))
-            return 0;
-    }
+    lin->x0 = (uint64_t)X0;
+    lin->xs = (uint64_t)XS;
     lin->z0 = (uint64_t)Z0;
     lin->zs = (uint64_t)ZS;
+
+    /* exact code state at the code's ambiguous samples */
+    gss_code_state st = {c0, p->icode, p->ibit, p->iword};
+    int64_t at = 0;
+    for (int i = 0; i < nhz; i++) {
+        gss_code_walk_cc(&st, cs, hz[i] - at);
+        at = hz[i];
+        at_hz[i] = st;
+    }
 
     /* ---- code wraps, data bits and the signed-gain schedule ---- */
     int ng = 0;
@@ -274,10 +286,10 @@ static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, gss_
         int64_t q = u + (v > 0);
         if (q - 1 >= n)
             break;
-        int j = find_hit(hit, nh, q - 1);
-        if (j >= 0 && wraps_of(&at_hit[j], p) >= k)
+        int j = find_hit(hz, nhz, q - 1);
+        if (j >= 0 && wraps_of(&at_hz[j], p) >= k)
             q--;                                 /* the exact value wrapped one sample earlier */
-        else if ((j = find_hit(hit, nh, q)) >= 0 && wraps_of(&at_hit[j], p) < k)
+        else if ((j = find_hit(hz, nhz, q)) >= 0 && wraps_of(&at_hz[j], p) < k)
             q++;                                 /* ... or one sample later */
         if (q >= n)
             break;
@@ -308,6 +320,44 @@ static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, gss_
         lin->gpos[i] = INT32_MAX;
         lin->gval[i] = g;
     }
+
+    /* ---- patches: the exact term where the kernel's differs ---- */
+    const int nq = merge_hits(hx, nhx, hz, nhz, hq);
+    double x = x0;
+    int64_t xat = 0;
+    int np = 0, gi = 0;
+    for (int i = 0; i < nq; i++) {
+        const int64_t q = hq[i];
+        int cell, chip;
+        if (q == 0) {
+            cell = (int)floor(x0 * 512.0);
+        } else if (near_boundary(X0 + (i128)q * XS, DX1, LIN_CARR_LGB)) {
+            x = gss_carr_walk_cc(x, s, q - xat);     /* the reference may differ from the line */
+            xat = q;
+            cell = (int)floor(x * 512.0);
+        } else {                                 /* proven: exact = line */
+            cell = (int)((uint64_t)(X0 + (i128)q * XS) >> LIN_CARR_LGB);
+        }
+        int j;
+        if (q == 0)
+            chip = (int)floor(c0);
+        else if ((j = find_hit(hz, nhz, q)) >= 0)
+            chip = (int)floor(at_hz[j].ph);
+        else
+            chip = (int)(((Z0 + (i128)q * ZS) >> LIN_CODE_LGB) % GSS_CA_LEN);
+        const int kcell = gss_lin_kcell((uint64_t)X0, (uint64_t)XS, q);
+        const int kchip = gss_lin_kchip((uint64_t)Z0, (uint64_t)ZS, q);
+        const int64_t te = ca_sign(ca, chip) * lut_packed(cell);
+        const int64_t tk = ca_sign(ca, kchip) * lut_packed(kcell);
+        if (te == tk)
+            continue;
+        while (gi + 1 < GSS_NGC && lin->gpos[gi + 1] <= q)
+            gi++;
+        if (np == GSS_NPATCH)
+            return 0;
+        lin->ppos[np] = (int32_t)q;
+        lin->pdelta[np++] = (int64_t)lin->gval[gi] * (te - tk);
+    }
     (void)inexact;
     return 1;
 }
@@ -315,8 +365,8 @@ static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, gss_
 typedef struct {
     const gss_chan_blk_t *blk;
     const int32_t *nch;
-    const uint32_t *nav;
-    int n_nav, n_per_blk, b_lo, b_hi;
+    const uint32_t *nav, *ca;
+    int n_nav, n_ca, n_per_blk, b_lo, b_hi;
     gss_lin_t *lin;
     int32_t *fast;
 } lin_job;
@@ -340,11 +390,13 @@ static void *lin_run(void *arg)
         for (int k = 0; ok && k < nc; k++) {
             const gss_chan_blk_t *p = &j->blk[(size_t)b * GSS_MAXCH + k];
             gsum += p->gain < 0 ? -p->gain : p->gain;
-            if (p->nav_tbl < 0 || p->nav_tbl >= j->n_nav) {
+            if (p->nav_tbl < 0 || p->nav_tbl >= j->n_nav || p->ca_tbl < 0 ||
+                p->ca_tbl >= j->n_ca) {
                 ok = 0;
                 break;
             }
             ok = lin_channel(p, j->n_per_blk, j->nav + (size_t)p->nav_tbl * GSS_NAV_WORDS,
+                             j->ca + (size_t)p->ca_tbl * GSS_CA_WORDS,
                              &j->lin[(size_t)b * GSS_MAXCH + k]);
         }
         /* the packed I/Q accumulator (gss_lin_kernel) needs 250*sum|gain| + 64 < 2^21 */
@@ -356,9 +408,11 @@ static void *lin_run(void *arg)
 }
 
 int gss_linearize(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
-                  const uint32_t *nav, int n_nav, gss_lin_t *lin, int32_t *fast, int threads)
+                  const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
+                  gss_lin_t *lin, int32_t *fast, int threads)
 {
-    if (!blk || !nch || !lin || !fast || nblk < 0 || n_per_blk <= 0 || (n_nav > 0 && !nav))
+    if (!blk || !nch || !lin || !fast || nblk < 0 || n_per_blk <= 0 || (n_nav > 0 && !nav) ||
+        (n_ca > 0 && !ca_bits) || n_ca < 0)
         return gss_fail(GSS_E_ARG, "invalid linearize arguments");
     if (nblk == 0)
         return 0;
@@ -371,7 +425,7 @@ int gss_linearize(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n
     const int per = (nblk + threads - 1) / threads;
     for (int t = 0; t < threads; t++) {
         int lo = t * per, hi = lo + per > nblk ? nblk : lo + per;
-        job[t] = (lin_job){blk, nch, nav, n_nav, n_per_blk, lo, hi, lin, fast};
+        job[t] = (lin_job){blk, nch, nav, ca_bits, n_nav, n_ca, n_per_blk, lo, hi, lin, fast};
         if (lo >= hi)
             continue;
         if (threads == 1 || pthread_create(&tid[t], NULL, lin_run, &job[t]) != 0)

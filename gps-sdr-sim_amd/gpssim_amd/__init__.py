@@ -33,13 +33,13 @@ assert CHAN_DTYPE.itemsize == 56
 
 NGC = 8                       # GSS_NGC: signed-gain schedule entries
 NPATCH = 8                    # GSS_NPATCH: patched samples per block and channel
-# gss_lin_t (160 bytes): certified integer lines of one block and channel, gpssim_amd.h
+# gss_lin_t (192 bytes): certified integer lines of one block and channel, gpssim_amd.h
 LIN_DTYPE = np.dtype([
     ("x0", "<u8"), ("xs", "<u8"), ("z0", "<u8"), ("zs", "<u8"),
-    ("gpos", "<i4", (NGC,)), ("gval", "<i4", (NGC,)),
-    ("ppos", "<i4", (NPATCH,)), ("pval", "<i4", (NPATCH,)),
+    ("pdelta", "<i8", (NPATCH,)),
+    ("gpos", "<i4", (NGC,)), ("gval", "<i4", (NGC,)), ("ppos", "<i4", (NPATCH,)),
 ])
-assert LIN_DTYPE.itemsize == 160
+assert LIN_DTYPE.itemsize == 192
 
 
 class GssError(RuntimeError):
@@ -85,7 +85,8 @@ _SIGS = {
                                    C.c_int, C.c_int, C.c_int, _P, _P, _P, _P]),
     "gss_synth_host": (C.c_int, [_P, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int,
                                  C.c_int, _P, _P]),
-    "gss_linearize": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_int, _P, _P, C.c_int]),
+    "gss_linearize": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_int, _P, C.c_int, _P, _P,
+                                C.c_int]),
     "gss_synth_lin_device": (C.c_int, [_P, _P, _P, C.c_int, _P, _P, _P, C.c_int, _P, _P,
                                        C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P,
                                        _P]),
@@ -161,16 +162,18 @@ def lut():
     return s, c
 
 
-def linearize(blk, nch, nav, n_per_blk, threads=8):
+def linearize(blk, nch, nav, n_per_blk, threads=8, ca=None):
     """(lin[nblk, 16] LIN_DTYPE, fast[nblk] int32): the certified integer lines of every block
-    (gss_linearize); fast[b] == 1 where the fast path renders block b exactly."""
+    (gss_linearize); fast[b] == 1 where the fast path renders block b exactly.  ca: the C/A
+    table the blocks' ca_tbl index (default: ca_table(), PRN 1..32)."""
     blk = np.ascontiguousarray(blk, CHAN_DTYPE)
     nch = np.ascontiguousarray(nch, np.int32)
     nav = np.ascontiguousarray(nav, np.uint32)
+    ca = np.ascontiguousarray(ca_table() if ca is None else ca, np.uint32)
     lin = np.zeros((len(nch), MAXCH), LIN_DTYPE)
     fast = np.zeros(len(nch), np.int32)
-    _check(lib().gss_linearize(_ptr(blk), _ptr(nch), len(nch), n_per_blk, _ptr(nav), len(nav),
-                               _ptr(lin), _ptr(fast), threads))
+    _check(lib().gss_linearize(_ptr(blk), _ptr(nch), len(nch), n_per_blk, _ptr(ca), len(ca),
+                               _ptr(nav), len(nav), _ptr(lin), _ptr(fast), threads))
     return lin, fast
 
 

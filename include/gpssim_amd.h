@@ -132,24 +132,25 @@ int gss_render_device(gss_dev *d, int set, const gss_chan_blk_t *blk, const int3
 #define GSS_NGC 8                /* signed-gain schedule entries per block and channel        */
 #define GSS_NPATCH 8             /* patched samples per block and channel                     */
 typedef struct gss_lin {
-    uint64_t x0, xs;             /* carrier line, 2^-64 cycle: LUT cell of sample p =
-                                    ((x0 + p*xs) mod 2^64) >> 55  (= floor(512*carr_phase))    */
+    uint64_t x0, xs;             /* carrier line, 2^-64 cycle: x0 + p*xs mod 2^64              */
     uint64_t z0, zs;             /* code line, 2^-50 chip, unwrapped: floor((z0 + p*zs) / 2^50)
                                     = chips since the block's code wrap base; chip index is that
                                     mod 1023 and the k-th code wrap falls where it reaches 1023k */
+    int64_t pdelta[GSS_NPATCH];  /* correction of sample ppos[i]'s packed I/Q term (exact minus
+                                    what the kernel's render arithmetic reads there, both
+                                    gain * codeCA * (cos + 2^22 sin), gpssim.c:2190-2256)      */
     int32_t gpos[GSS_NGC];       /* gain*dataBit (gpssim.c:2186, 2234) is gval[i] for samples   */
     int32_t gval[GSS_NGC];       /* gpos[i] <= p < gpos[i+1]; gpos[0] = 0, unused = INT32_MAX   */
-    int32_t ppos[GSS_NPATCH];    /* patched samples, ascending (unused = INT32_MAX), where the
-                                    line's cell or chip is not the exact one: sample ppos[i]     */
-    int32_t pval[GSS_NPATCH];    /* reads LUT cell pval & 0xFFFF (pval >> 16 == 0) or chip
-                                    pval & 0xFFFF (pval >> 16 == 1) instead                      */
-} gss_lin_t;                     /* 160 bytes, laid out [nblk][GSS_MAXCH]                      */
+    int32_t ppos[GSS_NPATCH];    /* patched samples, ascending (unused = INT32_MAX)             */
+} gss_lin_t;                     /* 192 bytes, laid out [nblk][GSS_MAXCH]                      */
 
-/* Lines and proofs for nblk blocks (host arrays; nav = [n_nav][GSS_NAV_WORDS] rows as passed
-   to the synth calls).  fast[b] = 1 if every channel of block b is certified (and the block's
-   gains fit the packed accumulator), else 0.  Runs on `threads` host threads.                 */
+/* Lines and proofs for nblk blocks (host arrays; ca_bits = [n_ca][GSS_CA_WORDS] and nav =
+   [n_nav][GSS_NAV_WORDS] rows as passed to the synth calls).  fast[b] = 1 if every channel of
+   block b is certified (and the block's gains fit the packed accumulator), else 0.  Runs on
+   `threads` host threads.                                                                     */
 int gss_linearize(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
-                  const uint32_t *nav, int n_nav, gss_lin_t *lin, int32_t *fast, int threads);
+                  const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
+                  gss_lin_t *lin, int32_t *fast, int threads);
 
 /* gss_synth_device over the certified fast path.  Device pointers as gss_synth_device, plus
    lin [nblk][GSS_MAXCH] and fast [nblk] from gss_linearize, and the exact path's block list

@@ -1,14 +1,15 @@
 /* Test-only harness: renders blocks from the certified integer lines (gss_lin_t) with scalar C,
-   exactly the arithmetic the GPU fast path (gss_lin_kernel) performs: LUT cell = high 9 bits of
-   x0 + p*xs (mod 2^64), chip = floor((z0 + p*zs) / 2^50) mod 1023, signed gain from the
-   schedule, the patched samples.  tests/test_linearize.py compares its bytes with the scalar oracle of the reference
-   loop (oracle/synth_oracle.c) on every block gss_linearize certifies. */
+   exactly the arithmetic the GPU fast path (gss_lin_kernel) performs: the kernel's LUT cell and
+   chip at each sample (gss_lin_kcell / gss_lin_kchip, csrc/common/gss_lin.h: chunk anchors plus
+   32-bit steps), the signed gain from the schedule, the packed I/Q accumulator
+   (64 + 2^21) + 2^22 (64 + ...) and the patch corrections.  tests/test_linearize.py compares its
+   bytes with the scalar oracle of the reference loop (oracle/synth_oracle.c) on every block
+   gss_linearize certifies. */
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 #include "../../include/gpssim_amd.h"
-
-typedef unsigned __int128 u128;
+#include "../../gps-sdr-sim_amd/csrc/common/gss_lin.h"
 
 static int ca_chip(const uint32_t *bits, int i) { return (int)((bits[i >> 5] >> (i & 31)) & 1u); }
 
@@ -24,31 +25,26 @@ int lc_render(const gss_chan_blk_t *blk, const int32_t *nch, const gss_lin_t *li
             continue;
         rendered++;
         for (int p = 0; p < n; p++) {
-            int i_acc = 64, q_acc = 64;
+            int64_t acc = 64 + (1 << 21) + ((int64_t)64 << 22);
             for (int k = 0; k < nch[b]; k++) {
                 const gss_lin_t *l = &lin[(size_t)b * GSS_MAXCH + k];
                 const gss_chan_blk_t *c = &blk[(size_t)b * GSS_MAXCH + k];
-                const uint64_t x = l->x0 + (uint64_t)p * l->xs;
-                int ti = (int)(x >> 55);
-                const u128 z = (u128)l->z0 + (u128)p * l->zs;
-                int chip = (int)((uint64_t)(z >> 50) % GSS_CA_LEN);
-                for (int j = 0; j < GSS_NPATCH; j++)
-                    if (l->ppos[j] == p) {                     /* the exact cell / chip */
-                        if (l->pval[j] >> 16)
-                            chip = l->pval[j] & 0xFFFF;
-                        else
-                            ti = l->pval[j] & 0xFFFF;
-                    }
+                const int ti = gss_lin_kcell(l->x0, l->xs, p);
+                const int chip = gss_lin_kchip(l->z0, l->zs, p);
                 const int ca = ca_chip(ca_bits + (size_t)c->ca_tbl * GSS_CA_WORDS, chip) * 2 - 1;
                 int g = l->gval[0];
                 for (int i = 1; i < GSS_NGC; i++)
                     if (l->gpos[i] <= p)
                         g = l->gval[i];
-                i_acc += g * ca * cosT[ti];
-                q_acc += g * ca * sinT[ti];
+                acc += (int64_t)(g * ca) * ((int64_t)cosT[ti] + ((int64_t)sinT[ti] << 22));
+                for (int j = 0; j < GSS_NPATCH; j++)
+                    if (l->ppos[j] == p)
+                        acc += l->pdelta[j];
             }
-            iq[2 * p] = (int16_t)(i_acc >> 7);
-            iq[2 * p + 1] = (int16_t)(q_acc >> 7);
+            /* the kernel's epilogue: I field (sum I + 64 + 2^21) in bits 0..21, Q above */
+            const int64_t fi = (acc & ((1 << 22) - 1)) - (1 << 21);
+            iq[2 * p] = (int16_t)(fi >> 7);
+            iq[2 * p + 1] = (int16_t)(acc >> 29);
         }
         uint8_t *dst = out + (size_t)b * bb;
         if (fmt == 16) {

@@ -32,9 +32,10 @@ def lc():
     if _lc is None:
         src = os.path.join(HELP, "lin_check.c")
         so = os.path.join(HELP, "_lin_check.so")
-        hdr = os.path.join(REPO, "include", "gpssim_amd.h")
-        if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(src),
-                                                                  os.path.getmtime(hdr)):
+        hdrs = [os.path.join(REPO, "include", "gpssim_amd.h"),
+                os.path.join(PKG, "csrc", "common", "gss_lin.h")]
+        if not os.path.exists(so) or os.path.getmtime(so) < max(
+                [os.path.getmtime(src)] + [os.path.getmtime(h) for h in hdrs]):
             subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-o", so, src])
         L = C.CDLL(so)
         L.lc_render.restype = C.c_int

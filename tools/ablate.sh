@@ -1,0 +1,14 @@
+#!/bin/bash
+# Build measurement variants of the library into _var/<name>/ (ablations of the fast-path kernel,
+# or other LIN_CH): usage  bash tools/ablate.sh name "EXTRA_HIPFLAGS"
+# The variant is loaded by bench.py through GSS_LIB_PATH=_var/<name>/libgpssim_amd.so.
+set -e
+cd "$(dirname "$0")/.."
+name=$1; flags=$2
+mkdir -p _var/$name/obj
+HIPCC=/opt/rocm/bin/hipcc
+F="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Iinclude -Wno-unused-result $flags"
+$HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_synth.hip -o _var/$name/obj/gss_synth.o
+$HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_run.hip -o _var/$name/obj/gss_run.o
+$HIPCC -shared -fPIC --offload-arch=gfx950 -o _var/$name/libgpssim_amd.so gps-sdr-sim_amd/obj/host/*.o \
+    _var/$name/obj/gss_synth.o _var/$name/obj/gss_run.o -lm -lpthread

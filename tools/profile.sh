@@ -1,11 +1,11 @@
 #!/bin/bash
 # Profiling session on the GPU box (rocprofv3): kernel trace + stats, then one PMC pass per
-# counter group (never combined with other trace domains).  Outputs under gpurun_out/prof/.
+# counter group (never combined with other trace domains).  Outputs under gpurun_out/prof_<tag>/.
 # Usage: bash tools/profile.sh [tag]   (bench args via BENCH_ARGS)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-TAG=${1:-r1}
+TAG=${1:-r2}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 BA=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --no-exact}
@@ -20,4 +20,5 @@ run pmc_write --pmc WRITE_SIZE --kernel-trace || exit $?
 run pmc_fetch --pmc FETCH_SIZE --kernel-trace || exit $?
 run pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_WR --kernel-trace || exit $?
 run pmc_lds --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAIT_ANY GRBM_GUI_ACTIVE --kernel-trace || exit $?
+[ -n "$PMC_STALL" ] && { run pmc_stall --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU SQ_WAVE_CYCLES --kernel-trace || exit $?; }
 echo done >> $OUT/session.log
