@@ -508,7 +508,7 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
                                               reach of one wave (LIN_STEPS*64 samples * 0.49)+64 */
 static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole chunks");
 /* LIN_ABLATE (measurement builds only, tools/ablate.sh; wrong output): 1 no output stores,
-   2 no chip-window loads, 4 no LUT reads */
+   2 no chip-window loads, 4 no LUT reads, 8 every block stores into one of 8 blocks (L2) */
 #ifndef LIN_ABLATE
 #define LIN_ABLATE 0
 #endif
@@ -635,10 +635,29 @@ __device__ __forceinline__ void lin_channel_chunk(int64_t (&acc)[LIN_CH], uint32
     }
 }
 
+/* output stores: the stream is written once and never read back by this kernel, while each
+   XCD's L2 must keep the chip-window table warm.  LIN_STORE_POLICY: 0 plain,
+   1 nt, 2 sc1 (drops the line from L2), 3 sc0 sc1 */
+#ifndef LIN_STORE_POLICY
+#define LIN_STORE_POLICY 1
+#endif
+__device__ __forceinline__ void lin_put(uint32_t *p, uint32_t v)
+{
+    if (LIN_STORE_POLICY == 1)
+        __builtin_nontemporal_store(v, p);
+    else if (LIN_STORE_POLICY == 2)
+        asm volatile("global_store_dword %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
+    else if (LIN_STORE_POLICY == 3)
+        asm volatile("global_store_dword %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+    else
+        *p = v;
+}
+
 template <int FMT, bool TAIL>
 __device__ __forceinline__ void lin_store(const int64_t (&acc)[LIN_CH], uint8_t *__restrict__ ob,
                                           int nb0, int lane, int n_per_blk)
 {
+    uint32_t pk[LIN_CH];
 #pragma unroll
     for (int s = 0; s < LIN_CH; s++) {
         /* acc = (sum I + 64 + 2^21) + 2^22 (sum Q + 64): the 2^21 bias keeps the I field
@@ -648,10 +667,11 @@ __device__ __forceinline__ void lin_store(const int64_t (&acc)[LIN_CH], uint8_t 
         const int nb = nb0 + s * 64, p = nb + lane;
         const bool in = !TAIL || p < n_per_blk;
         if (FMT == 16) {
+            /* packed first, stored after the loop: distinct data registers, so a store never
+               holds up the next pack (a VMEM store reads its data VGPR after issue) */
             const int i16 = __builtin_amdgcn_sbfe((int)(lo ^ (1u << 21)), 7, 15);
             const uint32_t q16 = __builtin_amdgcn_alignbit(hi, lo, 29);
-            if (in)
-                ((uint32_t *)ob)[p] = __builtin_amdgcn_perm(q16, (uint32_t)i16, 0x05040100u);
+            pk[s] = __builtin_amdgcn_perm(q16, (uint32_t)i16, 0x05040100u);
         } else if (FMT == 8) {                            /* iq_buff >> 4 → signed char */
             const int i8 = __builtin_amdgcn_sbfe((int)(lo ^ (1u << 21)), 11, 11);
             const uint32_t q8 = (uint32_t)((int)hi >> 1);
@@ -671,6 +691,15 @@ __device__ __forceinline__ void lin_store(const int64_t (&acc)[LIN_CH], uint8_t 
                                               ((c & 1u) << 6) | ((c & 2u) << 3) | (c & 4u) |
                                               ((c & 8u) >> 3));
             }
+        }
+    }
+    if (FMT == 16) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < LIN_CH; s++) {
+            const int p = nb0 + s * 64 + lane;
+            if (!TAIL || p < n_per_blk)
+                lin_put(((uint32_t *)ob) + p, pk[s]);
         }
     }
 }
@@ -723,7 +752,7 @@ __global__ __launch_bounds__(LIN_THREADS) void gss_lin_kernel(
     const lin_chan *CH = chans + (size_t)b * GSS_MAXCH;
     const lin_seg *S = segs + (size_t)b * GSS_MAXCH * nseg + sg;
     const int nc = nch[b];
-    uint8_t *ob = out + (size_t)b * block_bytes;
+    uint8_t *ob = out + ((LIN_ABLATE & 8) ? (size_t)(b & 7) : (size_t)b) * block_bytes;
 
     for (int c = 0; c < LIN_STEPS / LIN_CH; c++) {
         const int nb0 = n0 + c * (64 * LIN_CH);           /* first sample of the chunk */

@@ -71,3 +71,17 @@ def test_cpu_restatement_dynamic_prefix(golden):
     g = golden["circle_b8"]
     out = run_cpu_restatement(["-u", CIRCLE, "-d", "2", "-b", "8"])
     assert block_hashes(out, 520000) == g["block_sha16"][:19]
+
+
+@pytest.mark.parametrize("name,args,nblk", [
+    ("static_d300_b16", ["-l", ",".join(map(str, LOC)), "-d", "31", "-b", "16"], 309),
+    ("circle_b8", ["-u", CIRCLE, "-d", "31", "-b", "8"], 309),
+])
+def test_cpu_restatement_across_first_nav_update(golden, name, args, nblk):
+    """Past the first 30 s boundary: the nav-message regeneration and channel re-allocation that
+    run after block 299 (gpssim.c:2294-2332) feed blocks 300..308, byte for byte."""
+    g = golden[name]
+    out = run_cpu_restatement(args)
+    bb = g["bytes"] // g["blocks"]
+    assert len(out) == nblk * bb
+    assert block_hashes(out, bb) == g["block_sha16"][:nblk]
