@@ -5,19 +5,33 @@ Workload (BASELINE.json configs[1]): static receiver -l 30.286502,120.032669,100
 -b 16, 300 s per GPU = 2999 blocks x 260000 samples (11-12 satellites; ephemeris
 brdc3540.14n).  The scenario is deterministic; there is no dataset.
 
-One step = one pass of the hot path over the rank's whole 300 s window: checkpoint stage +
-synthesis stage (gss_synth_device) from per-block parameters already resident in HBM, writing
-the exact -b 16 byte stream (3.12 GB) to HBM.  Multi-GPU (torchrun, one process per GPU):
-rank r owns the time window [300 r, 300 (r+1)) s of one longer static run — a weak-scaling
-time-window shard with no data-path collective; RCCL is used only for the
-barrier and the max-over-ranks timing.  The host control plane (ephemeris, ranges, nav words,
-exact carrier planner) runs before the timed region; its wall time is reported as host_plan_s
-and folded into e2e_msps.
+One step = one pass of the hot path over the rank's whole 300 s window from per-block parameters
+already resident in HBM: gss_synth_lin_device (the certified fast path, gss_lin_kernel; blocks the
+host proof does not certify take the exact path inside the same call), writing the exact -b 16
+byte stream (3.12 GB) to HBM.  Multi-GPU (torchrun, one process per GPU): rank r owns the time
+window [300 r, 300 (r+1)) s of one longer static run -- a weak-scaling time-window shard with no
+data-path collective; RCCL is used only for the barrier and the max-over-ranks
+timing.  The host control plane (ephemeris, ranges, nav words, exact carrier planner) and the
+host proof run before the timed region (host_plan_s, host_linearize_s).
 
-Extra JSON fields besides the driver contract: x_realtime, stages_ms, host_plan_s, e2e_msps,
-roofline (synthesis kernel: algorithmic output bytes per launch / its average HIP-event
-duration over the timed steps), cpu_baseline (the reference binary itself, oracle/_ref/
-gps-sdr-sim, on a bounded 60 s sample, rank 0 only, before the GPU is initialised).
+Extra JSON fields besides the driver contract:
+  x_realtime, stages_ms, host_plan_s, host_linearize_s, lib (the library that was measured);
+  roofline      fast-path kernel: algorithmic output bytes per launch / its average HIP-event
+                duration over the timed steps; traffic = HBM bytes per launch from the PMC
+                passes in profiles/pmc_traffic.json when that profile is of this kernel build
+                and its kernel time agrees with this run's within 5 %;
+  per_config    rank 0 at N=1: the other BASELINE configurations on the same path, each timed
+                the same way (configs[2] circle -b 8, configs[3] 20 MS/s -b 16 per-GPU share of
+                3600 s over 8 GPUs, configs[4] 24 h -b 1), with their own algorithmic bytes and
+                roofline fraction;
+  e2e           rank 0 at N=1: gss_run (planner thread + proofs + H2D + kernels + D2H into
+                pinned host buffers + a discarding sink, all overlapped) over the 300 s run,
+                wall-clocked: the PCIe-inclusive rate (a 1800 s run, so that the pinned
+                buffers' setup is amortised as in a real run);
+  cpu_baseline  the reference program built from its own sources (oracle/_ref/gps-sdr-sim) on a
+                bounded sample, on 1 core and as C concurrent processes on C host cores, rank 0
+                only, before the GPU is initialised;
+  exact_path    the same resident batch through the exact walking path alone.
 """
 import argparse
 import json
@@ -30,47 +44,164 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "gps-sdr-sim_amd"))
 
 NAV = os.path.join(REPO, "tests", "golden", "data", "brdc3540.14n")
+CIRCLE = os.path.join(REPO, "tests", "golden", "data", "circle.csv")
 LOC = (30.286502, 120.032669, 100.0)
 FS = 2.6e6
 WINDOW_S = 300.0
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters
 METRIC = "IQ MSamples/s (and × real-time) at 2.6 MS/s, 12 sats, -b 16; 1/2/4/8 GPU"
+BOX_CORES = 16                 # the GPU box's host CPU share for one GPU
+
+# BASELINE.json configs[2..4] (per_config); configs[1] is the headline, configs[0] the CPU case
+CONFIGS = [
+    {"name": "configs[2]", "desc": "dynamic -u circle.csv -s 2600000 -b 8, 300 s",
+     "kw": {"motion_file": CIRCLE}, "fs": 2.6e6, "fmt": 8, "window": 300.0},
+    {"name": "configs[3]", "desc": "static -s 20000000 -b 16, 3600 s over 8 GPUs: the 450 s "
+     "per-GPU share (4499 blocks x 2000000 samples)", "kw": {"llh": LOC}, "fs": 2.0e7,
+     "fmt": 16, "window": 450.0},
+    {"name": "configs[4]", "desc": "static -s 2600000 -b 1, 86400 s (863999 blocks)",
+     "kw": {"llh": LOC}, "fs": 2.6e6, "fmt": 1, "window": 86400.0},
+]
 
 
-def cpu_baseline(seconds=60):
-    """The reference program (compiled from its own sources by oracle/Makefile) timed on one
-    host core over a bounded sample; falls back to the repo's CPU restatement ("port")."""
+def cpu_baseline(seconds=30, cores=BOX_CORES):
+    """The reference program (compiled from its own sources by oracle/Makefile) on a bounded
+    sample of the static scenario to /dev/null: one process on one core, then `cores` concurrent
+    processes pinned to cores 0..cores-1 (it is single-threaded by construction).  Falls back to
+    the repo's CPU restatement ("port") when the reference binary is absent."""
     ref = os.path.join(REPO, "oracle", "_ref", "gps-sdr-sim")
     port = os.path.join(REPO, "oracle", "_ref", "gss_oracle_cli")
     kind, exe = ("reference", ref) if os.path.exists(ref) else ("port", port)
     if not os.path.exists(exe):
         return None
+    try:
+        avail = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = list(range(os.cpu_count() or 1))
+    cores = max(1, min(cores, len(avail)))
     args = [exe, "-e", NAV, "-l", ",".join(map(str, LOC)), "-d", str(seconds), "-s",
             str(int(FS)), "-b", "16", "-o", "/dev/null"]
     env = dict(os.environ, GSS_THREADS="1")
-    t0 = time.perf_counter()
-    r = subprocess.run(["taskset", "-c", "0"] + args, capture_output=True, env=env)
-    wall = time.perf_counter() - t0
-    if r.returncode != 0:
-        return None
     blocks = int(seconds * 10) - 1
-    msps = blocks * FS / 10 / wall / 1e6
-    return {"value": round(msps, 3), "unit": "MS/s", "cores": 1, "kind": kind,
+    samples = blocks * FS / 10
+
+    def run(n):
+        t0 = time.perf_counter()
+        ps = [subprocess.Popen(["taskset", "-c", str(avail[i])] + args, env=env,
+                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+              for i in range(n)]
+        ok = all(p.wait() == 0 for p in ps)
+        return (time.perf_counter() - t0) if ok else None
+
+    w1 = run(1)
+    wn = run(cores) if w1 is not None and cores > 1 else w1
+    if w1 is None or wn is None:
+        return None
+    one = samples / w1 / 1e6
+    agg = cores * samples / wn / 1e6
+    return {"value": round(agg, 2), "unit": "MS/s", "cores": cores, "kind": kind,
+            "single_core": {"value": round(one, 3), "cores": 1,
+                            "x_realtime": round(one / (FS / 1e6), 2)},
+            "x_realtime": round(agg / (FS / 1e6), 2),
             "sample": f"static -d {seconds} -b 16 -o /dev/null ({blocks} blocks x 260000 "
-                      f"samples), wall {wall:.2f} s, x_realtime {msps / 2.6:.2f}"}
+                      f"samples) per process; 1 process: wall {w1:.2f} s; {cores} concurrent "
+                      f"processes on cores {avail[0]}..{avail[cores - 1]}: wall {wn:.2f} s"}
 
 
-def load_traffic(workload, kernel):
-    """HBM bytes per launch of `kernel` from the PMC passes (profiles/pmc_traffic.json), when
-    they were taken on this workload"""
+def lib_sha16(path):
+    import hashlib
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def load_traffic(workload, kernel, kern_ms, lib_sha):
+    """HBM bytes per launch of `kernel` from the PMC passes (profiles/pmc_traffic.json), only
+    when they were taken on this workload and this kernel build (same library sha256, average
+    kernel time within 5 % of this run's)"""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
-        if d.get("workload") == workload and str(d.get("kernel", "")).startswith(kernel):
-            return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        pass
-    return None
+        return None, "no profiles/pmc_traffic.json"
+    if d.get("workload") != workload or not str(d.get("kernel", "")).startswith(kernel):
+        return None, "profile of another workload"
+    if d.get("lib_sha16") != lib_sha:
+        return None, "profile of another build"
+    prof_ms = (d.get("kernel_avg_ns") or 0) / 1e6
+    if kern_ms <= 0 or abs(prof_ms - kern_ms) > 0.05 * kern_ms:
+        return None, f"profile kernel time {prof_ms:.3f} ms vs {kern_ms:.3f} ms here"
+    return d.get("hbm_bytes_per_launch"), d.get("source")
+
+
+def time_steps(torch, dev, dev_t, res, steps, warmup, stream):
+    for _ in range(warmup):
+        res.step(stream)
+    torch.cuda.synchronize(dev_t)
+    dev.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res.step(stream)
+    torch.cuda.synchronize(dev_t)
+    el = time.perf_counter() - t0
+    n_lin, lin_ms = dev.timing_lin()
+    return el, n_lin, lin_ms
+
+
+def per_config(G, torch, dev, dev_t, stream, steps, warmup, threads):
+    from gpssim_amd.render import DeviceWindow
+    from gpssim_amd.shard import blocks_per_rank
+    out = []
+    for c in CONFIGS:
+        t0 = time.perf_counter()
+        s = G.Scenario(NAV, duration=c["window"], samp_freq=c["fs"], data_format=c["fmt"],
+                       **c["kw"])
+        want = blocks_per_rank(c["window"])
+        blk, nch = s.all_blocks(batch=2000, threads=threads)
+        plan_s = time.perf_counter() - t0
+        assert len(nch) == want, (c["name"], len(nch), want)
+        res = DeviceWindow(torch, dev, dev_t, blk, nch, s.nav_table(), s.n_per_blk, c["fmt"],
+                           threads=threads, batch=3000)
+        el, n_lin, lin_ms = time_steps(torch, dev, dev_t, res, steps, warmup, stream)
+        samples = res.nblk * res.npb
+        msps = samples * steps / el / 1e6
+        per_launch = (res.n_fast * res.bb) / len(res.batches)
+        achieved = per_launch / (lin_ms * 1e-3) / 1e9 if lin_ms > 0 else 0.0
+        out.append({
+            "config": c["name"], "workload": c["desc"], "fmt": c["fmt"],
+            "value": round(msps, 2), "unit": "MS/s", "x_realtime": round(msps / (c["fs"] / 1e6), 1),
+            "ms_per_step": round(el / steps * 1e3, 3), "steps": steps,
+            "blocks_fast_path": res.n_fast, "blocks_total": res.nblk,
+            "launches_per_step": len(res.batches), "channels_max": res.nch_max,
+            "bytes_per_step": res.nblk * res.bb,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "algorithmic_bytes_per_sample": res.bb / res.npb,
+                         "kernel_ms_per_launch": round(lin_ms, 3)},
+            "host_plan_s": round(plan_s, 3), "host_linearize_s": round(res.lin_s, 3)})
+        res.free()
+        del blk, nch, s
+    return out
+
+
+def e2e_run(G, dev, threads, window=1800.0):
+    """gss_run over the whole static run into a discarding sink, wall-clocked (planner, proofs,
+    uploads, kernels, D2H into pinned buffers and the sink, overlapped)."""
+    s = G.Scenario(NAV, llh=LOC, duration=window, samp_freq=FS, data_format=16)
+    got = {"bytes": 0, "blocks": 0}
+
+    def sink(mv, first, nb):
+        got["bytes"] += len(mv)
+        got["blocks"] += nb
+
+    t0 = time.perf_counter()
+    dev.run(s, sink, batch=256, threads=threads)
+    wall = time.perf_counter() - t0
+    samples = got["blocks"] * s.n_per_blk
+    return {"value": round(samples / wall / 1e6, 2), "unit": "MS/s",
+            "x_realtime": round(samples / wall / FS, 1), "wall_s": round(wall, 3),
+            "blocks": got["blocks"], "d2h_GBps": round(got["bytes"] / wall / 1e9, 2),
+            "workload": f"static -b 16, {window:g} s through gss_run (batch 256 blocks), "
+                        "discarding sink"}
 
 
 def main():
@@ -82,33 +213,26 @@ def main():
     ap.add_argument("--fmt", type=int, default=16, choices=[1, 8, 16])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-exact", action="store_true",
-                    help="lin path: skip the exact-path run on the same batch (exact_path)")
-    ap.add_argument("--no-ck", action="store_true",
-                    help="do not pass the planner's carrier checkpoints (GPU walks whole blocks)")
-    ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 8))
-    ap.add_argument("--path", choices=["lin", "walk"], default="lin",
-                    help="lin: certified integer fast path (gss_linearize + gss_synth_lin_device; "
-                         "uncertified blocks take the exact path inside the same call); walk: "
-                         "the exact walking path only (Stage A + Stage B, gss_synth_device)")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="run Stage A of batch k+1 on a second stream beside Stage B of batch k "
-                         "(gss_anchor_device/gss_render_device) instead of one gss_synth_device "
-                         "call per step; slower on MI355X today (Stage A waves displace Stage B "
-                         "workgroups), kept for measurement")
+                    help="skip the exact-path run on the same batch (exact_path)")
+    ap.add_argument("--no-configs", action="store_true", help="skip per_config")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the gss_run end-to-end run")
+    ap.add_argument("--e2e-window", type=float, default=1800.0)
+    ap.add_argument("--threads", type=int, default=BOX_CORES)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    single = rank == 0 and world == 1
 
-    # CPU baseline first: a child process, before this process touches the GPU
+    # CPU baseline first: child processes, before this process touches the GPU
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if single and not args.no_cpu_baseline:
         cpu = cpu_baseline()
 
-    import numpy as np
     import torch                      # loads the HIP runtime our library then shares
     import gpssim_amd as G
+    from gpssim_amd.render import DeviceWindow
 
     dist = world > 1
     if dist:
@@ -123,83 +247,21 @@ def main():
     blk, nch, ck, nav, npb = plan_rank(NAV, rank, world, args.window, llh=LOC, samp_freq=FS,
                                        data_format=args.fmt, threads=args.threads)
     host_plan_s = time.perf_counter() - t_plan0
-    nblk = len(nch)
-    lin_s, n_fast = 0.0, 0
-    if args.path == "lin":
-        t_lin0 = time.perf_counter()
-        lin, fast = G.linearize(blk, nch, nav, npb, threads=args.threads)
-        lin_s = time.perf_counter() - t_lin0
-        host_plan_s += lin_s
-        n_fast = int(fast.sum())
-        fb = np.nonzero(fast == 0)[0].astype(np.int32)
 
-    # ---- inputs resident in HBM ----
     dev = G.Device(local)
-    ca = G.ca_table()
-    d_blk = torch.from_numpy(blk.view(np.uint8).reshape(-1)).to(dev_t)
-    d_nch = torch.from_numpy(nch).to(dev_t)
-    d_ck = torch.from_numpy(ck).to(dev_t)        # planner carrier checkpoints (host-computed)
-    d_ca = torch.from_numpy(ca.view(np.int32)).to(dev_t)
-    d_nav = torch.from_numpy(nav.view(np.int32)).to(dev_t)
-    bb = G.block_bytes(npb, args.fmt)
-    out = torch.empty(nblk * bb, dtype=torch.uint8, device=dev_t)
-    dev.reserve(nblk, npb)
-    nch_max = int(nch.max())
     stream = torch.cuda.current_stream(dev_t).cuda_stream
-
-    ck_ptr = 0 if args.no_ck else d_ck.data_ptr()
-    if args.path == "lin":
-        d_lin = torch.from_numpy(lin.view(np.uint8).reshape(-1)).to(dev_t)
-        d_fast = torch.from_numpy(fast).to(dev_t)
-        d_fb = torch.from_numpy(fb if len(fb) else np.zeros(1, np.int32)).to(dev_t)
-
-    def step_lin():
-        dev.synth_lin_device(d_blk.data_ptr(), d_nch.data_ptr(), nch_max, d_lin.data_ptr(),
-                             d_fast.data_ptr(), d_fb.data_ptr(), len(fb), d_ca.data_ptr(),
-                             len(ca), d_nav.data_ptr(), len(nav), nblk, npb, args.fmt,
-                             out.data_ptr(), stream=stream, ck_ptr=ck_ptr)
+    res = DeviceWindow(torch, dev, dev_t, blk, nch, nav, npb, args.fmt, ck=ck,
+                       threads=args.threads, batch=len(nch))
+    nblk = res.nblk
 
     def step_serial():
-        dev.synth_device(d_blk.data_ptr(), d_nch.data_ptr(), nch_max, d_ca.data_ptr(), len(ca),
-                         d_nav.data_ptr(), len(nav), nblk, npb, args.fmt, out.data_ptr(),
-                         0, 0, stream, ck_ptr=ck_ptr)
+        dev.synth_device(res.d_blk.data_ptr(), res.d_nch.data_ptr(), res.nch_max,
+                         res.d_ca.data_ptr(), res.n_ca, res.d_nav.data_ptr(), res.n_nav, nblk,
+                         npb, args.fmt, res.out.data_ptr(), 0, 0, stream,
+                         ck_ptr=res.d_ck.data_ptr())
 
-    # --pipeline: batch k is rendered (Stage B) on the main stream while Stage A of batch k+1
-    # runs on a second, higher-priority stream into the other anchor set.  Every step still runs
-    # one full Stage A and one full Stage B; events order the ping-pong sets.
-    s_b = torch.cuda.current_stream(dev_t)
-    s_a = torch.cuda.Stream(dev_t, priority=-1)
-    ev_a = [torch.cuda.Event() for _ in range(2)]
-    ev_b = [torch.cuda.Event() for _ in range(2)]
-    pipe = {"k": 0}
-
-    def anchor(k):
-        st = k % 2
-        if k >= 2:                    # set st was last read by render(k-2)
-            s_a.wait_event(ev_b[st])
-        dev.anchor_device(st, d_blk.data_ptr(), d_nch.data_ptr(), nch_max, nblk, npb,
-                          ck_ptr=ck_ptr, stream=s_a.cuda_stream)
-        ev_a[st].record(s_a)
-
-    def render(k):
-        st = k % 2
-        s_b.wait_event(ev_a[st])
-        dev.render_device(st, d_blk.data_ptr(), d_nch.data_ptr(), nch_max, d_ca.data_ptr(),
-                          len(ca), d_nav.data_ptr(), len(nav), nblk, npb, args.fmt,
-                          out.data_ptr(), stream=s_b.cuda_stream)
-        ev_b[st].record(s_b)
-
-    def step_pipelined():
-        k = pipe["k"]
-        render(k)
-        anchor(k + 1)
-        pipe["k"] = k + 1
-
-    step = step_lin if args.path == "lin" else (step_pipelined if args.pipeline else step_serial)
-    if args.pipeline:
-        anchor(0)                     # pipeline prologue (untimed)
     for _ in range(args.warmup):
-        step()
+        res.step(stream)
     torch.cuda.synchronize(dev_t)
     dev.timing_reset()
     if dist:
@@ -207,22 +269,23 @@ def main():
     torch.cuda.synchronize(dev_t)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        res.step(stream)
     torch.cuda.synchronize(dev_t)
     if dist:
         td.barrier()
     elapsed = time.perf_counter() - t0
     n_launch, ck_ms, syn_ms = dev.timing()
     n_lin, lin_ms = dev.timing_lin()
+    host_lin_s = res.lin_s
     if dist:
-        t = torch.tensor([elapsed, ck_ms, syn_ms, host_plan_s, lin_ms], dtype=torch.float64,
-                         device=dev_t)
+        t = torch.tensor([elapsed, ck_ms, syn_ms, host_plan_s, lin_ms, host_lin_s],
+                         dtype=torch.float64, device=dev_t)
         td.all_reduce(t, op=td.ReduceOp.MAX)
-        elapsed, ck_ms, syn_ms, host_plan_s, lin_ms = t.tolist()
+        elapsed, ck_ms, syn_ms, host_plan_s, lin_ms, host_lin_s = t.tolist()
 
     samples_rank = nblk * npb
     exact = None
-    if args.path == "lin" and not dist and not args.no_exact:
+    if single and not args.no_exact:
         # the same resident batch through the exact path alone (Stage A + Stage B for every
         # block, no host-side line proofs), timed the same way
         for _ in range(args.warmup):
@@ -237,17 +300,23 @@ def main():
                  "ms_per_step": round(el / args.steps * 1e3, 3)}
     ms_per_step = elapsed / args.steps * 1e3
     value = world * samples_rank * args.steps / elapsed / 1e6          # MS/s, whole job
-    if args.path == "lin":
-        # the dominant kernel is gss_lin_kernel; its algorithmic bytes are the certified blocks'
-        kern_ms, bytes_launch = lin_ms, n_fast * bb
-    else:
-        kern_ms, bytes_launch = syn_ms, nblk * bb                       # algorithmic bytes
-    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
-    e2e = world * samples_rank / (host_plan_s + ms_per_step * 1e-3) / 1e6
+    # the dominant kernel is gss_lin_kernel; its algorithmic bytes are the certified blocks'
+    bytes_launch = res.n_fast * res.bb
+    achieved = bytes_launch / (lin_ms * 1e-3) / 1e9 if lin_ms > 0 else 0.0
     workload = (f"static -l {LOC[0]},{LOC[1]},{LOC[2]:g} -s 2600000 -b {args.fmt}, "
                 f"{args.window:g} s per GPU ({nblk} blocks x {npb} samples)")
-    traffic = load_traffic(workload, "gss_lin_kernel" if args.path == "lin" else "gss_synth_kernel")
-    res = {
+    version = G.lib().gss_version().decode()
+    sha = lib_sha16(G.LIB_PATH)
+    traffic, traffic_src = load_traffic(workload, "gss_lin_kernel", lin_ms, sha)
+    res.free()
+
+    configs = e2e = None
+    if single and not args.no_configs:
+        configs = per_config(G, torch, dev, dev_t, stream, min(args.steps, 3), 1, args.threads)
+    if single and not args.no_e2e:
+        e2e = e2e_run(G, dev, args.threads, args.e2e_window)
+
+    out = {
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "MS/s",
@@ -258,29 +327,28 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": "int64",
         "data": "synthetic: deterministic static-receiver scenario (brdc3540.14n), no dataset",
-        "config": {"workload": workload, "samples_per_gpu": samples_rank,
-                   "path": args.path,
-                   "carrier_checkpoints": 0 if args.no_ck else 8,
-                   "channels_max": nch_max, "parallelism": f"time-window shards x{world}",
-                   "stages": "pipelined (A of batch k+1 beside B of k)" if args.pipeline
-                   else "serial (A then B, one stream)"},
+        "config": {"workload": workload, "samples_per_gpu": samples_rank, "path": "lin",
+                   "channels_max": res.nch_max, "parallelism": f"time-window shards x{world}"},
         "x_realtime": round(value / (FS / 1e6), 1),
-        "stages_ms": {"fast_path": round(lin_ms, 3), "checkpoint": round(ck_ms, 3),
-                      "synthesis": round(syn_ms, 3), "launches_timed": max(n_launch, n_lin)},
-        "blocks_fast_path": n_fast if args.path == "lin" else 0, "blocks_total": nblk,
-        "host_linearize_s": round(lin_s, 3),
+        "stages_ms": {"fast_path": round(lin_ms, 3), "exact_leftovers_checkpoint": round(ck_ms, 3),
+                      "exact_leftovers_synthesis": round(syn_ms, 3),
+                      "launches_timed": max(n_launch, n_lin)},
+        "blocks_fast_path": res.n_fast, "blocks_total": nblk,
         "host_plan_s": round(host_plan_s, 3),
-        "e2e_msps": round(e2e, 2),
+        "host_linearize_s": round(host_lin_s, 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic},
+                     "traffic": traffic, "traffic_source": traffic_src},
         "cpu_baseline": cpu,
+        "per_config": configs,
+        "e2e": e2e,
         "exact_path": exact,
+        "lib": {"path": os.path.relpath(G.LIB_PATH, REPO), "version": version, "sha16": sha},
     }
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        print(json.dumps(out), flush=True)
     dev.close()
     if dist:
         td.destroy_process_group()

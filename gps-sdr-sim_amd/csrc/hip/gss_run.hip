@@ -5,15 +5,15 @@
  *
  *   planner thread   gss_scn_next into pinned slot buffers (+ a snapshot of the nav table),
  *                    then gss_linearize: the fast path's certified lines and patches
- *   main thread      per slot: async H2D, gss_synth_lin_device (certified blocks on the integer
- *                    fast path, the rest on Stage A + B; with GSS_PATH=walk gss_synth_device
- *                    renders every block), async D2H into a
- *                    pinned output buffer; then, while the next slot is on the GPU, hands the
- *                    previous slot's bytes to the sink in run order
+ *   main thread      per slot: async H2D and gss_synth_lin_device on the compute stream
+ *                    (certified blocks on the integer fast path, the rest on Stage A + B; with
+ *                    GSS_PATH=walk gss_synth_device renders every block), then async D2H into a
+ *                    pinned output buffer on the copy stream (after an event); while the next
+ *                    slot renders, hands the previous slot's bytes to the sink in run order
  *
  * Slots cycle planner -> main -> sink -> planner; a slot's buffers belong to exactly one side at
- * a time (state under a mutex).  One HIP stream, so H2D(i+1) and the kernels of i+1 queue behind
- * D2H(i) on the device while the host runs the sink on i-1.
+ * a time (state under a mutex).  Two HIP streams: the D2H of slot i (PCIe) overlaps the kernels
+ * of slot i+1; a slot's device output buffer is rewritten only after its own D2H (event).
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -60,7 +60,8 @@ struct Slot {
     size_t d_in_cap = 0;
     uint8_t *d_out = nullptr, *h_out = nullptr;
     int32_t *d_status = nullptr, *h_status = nullptr;
-    hipEvent_t done = nullptr;
+    hipEvent_t rendered = nullptr;   /* compute stream: the slot's kernels are done      */
+    hipEvent_t done = nullptr;       /* copy stream: the slot's bytes are in h_out        */
 };
 
 struct Run {
@@ -167,8 +168,10 @@ void planner(Run *r)
 }
 
 int submit(gss_dev *d, Slot &sl, const uint32_t *d_ca, int n_per_blk, int fmt, size_t bb,
-           hipStream_t st)
+           hipStream_t st, hipStream_t cp)
 {
+    /* the slot's previous D2H must have read d_out before the kernels rewrite it */
+    RUN_TRY(hipStreamWaitEvent(st, sl.done, 0));
     const size_t s_blk = sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)sl.nb;
     const size_t s_nch = sizeof(int32_t) * (size_t)sl.nb;
     const size_t s_ck = sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb;
@@ -214,9 +217,11 @@ int submit(gss_dev *d, Slot &sl, const uint32_t *d_ca, int n_per_blk, int fmt, s
     }
     if (rc)
         return rc;
-    RUN_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, bb * (size_t)sl.nb, hipMemcpyDeviceToHost, st));
-    RUN_TRY(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    RUN_TRY(hipEventRecord(sl.done, st));
+    RUN_TRY(hipEventRecord(sl.rendered, st));
+    RUN_TRY(hipStreamWaitEvent(cp, sl.rendered, 0));
+    RUN_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, bb * (size_t)sl.nb, hipMemcpyDeviceToHost, cp));
+    RUN_TRY(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int32_t), hipMemcpyDeviceToHost, cp));
+    RUN_TRY(hipEventRecord(sl.done, cp));
     return 0;
 }
 
@@ -236,7 +241,7 @@ int drain(Run &r, Slot &sl, size_t bb, gss_sink_fn sink, void *user)
 }
 
 int run_main(gss_dev *d, Run &r, int n_per_blk, int fmt, size_t bb, gss_sink_fn sink,
-             void *user, hipStream_t st, const uint32_t *d_ca)
+             void *user, hipStream_t st, hipStream_t cp, const uint32_t *d_ca)
 {
     int pending = -1;                                  /* slot submitted, not yet drained */
     for (int i = 0;; i++) {
@@ -249,7 +254,7 @@ int run_main(gss_dev *d, Run &r, int n_per_blk, int fmt, size_t bb, gss_sink_fn 
             int rc = pending >= 0 ? drain(r, r.slot[pending], bb, sink, user) : 0;
             return sl.err ? sl.err : rc;
         }
-        int rc = submit(d, sl, d_ca, n_per_blk, fmt, bb, st);
+        int rc = submit(d, sl, d_ca, n_per_blk, fmt, bb, st, cp);
         if (rc)
             return rc;
         if (pending >= 0) {                            /* previous slot overlaps this one */
@@ -291,27 +296,31 @@ extern "C" int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_bl
 
     int ordinal = 0;
     RUN_TRY(hipGetDevice(&ordinal));
-    hipStream_t st = nullptr;
+    hipStream_t st = nullptr, cp = nullptr;
     uint32_t *d_ca = nullptr;
     int err = 0;
     auto cleanup = [&]() {
         if (st) (void)hipStreamSynchronize(st);
+        if (cp) (void)hipStreamSynchronize(cp);
         for (Slot &sl : r.slot) {
             (void)hipHostFree(sl.blk); (void)hipHostFree(sl.nch); (void)hipHostFree(sl.ck);
             (void)hipHostFree(sl.nav); (void)hipHostFree(sl.h_out); (void)hipHostFree(sl.h_status);
             (void)hipHostFree(sl.lin); (void)hipHostFree(sl.fast);
             (void)hipFree(sl.d_in); (void)hipFree(sl.d_out); (void)hipFree(sl.d_status);
             if (sl.done) (void)hipEventDestroy(sl.done);
+            if (sl.rendered) (void)hipEventDestroy(sl.rendered);
         }
         (void)hipFree(d_ca);
         if (st) (void)hipStreamDestroy(st);
+        if (cp) (void)hipStreamDestroy(cp);
     };
     /* buffers */
     {
         gss_ca_table(r.ca);
         if (hipMalloc((void **)&d_ca, sizeof r.ca) != hipSuccess ||
             hipMemcpy(d_ca, r.ca, sizeof r.ca, hipMemcpyHostToDevice) != hipSuccess ||
-            hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
+            hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&cp, hipStreamNonBlocking) != hipSuccess)
             err = gss_fail(GSS_E_HIP, "run setup failed");
         const size_t nb = (size_t)r.batch;
         for (Slot &sl : r.slot) {
@@ -327,7 +336,8 @@ extern "C" int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_bl
                     hipSuccess ||
                 hipMalloc((void **)&sl.d_out, bb * nb) != hipSuccess ||
                 hipMalloc((void **)&sl.d_status, sizeof(int32_t)) != hipSuccess ||
-                hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess)
+                hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&sl.rendered, hipEventDisableTiming) != hipSuccess)
                 err = gss_fail(GSS_E_NOMEM, "run buffers (%zu B per slot)", bb * nb);
             if (!err && r.use_lin &&
                 (hipHostMalloc((void **)&sl.lin, sizeof(gss_lin_t) * GSS_MAXCH * nb,
@@ -348,7 +358,7 @@ extern "C" int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_bl
         (void)hipSetDevice(ordinal);                   /* pinned reallocations */
         planner(&r);
     });
-    err = run_main(d, r, info.n_per_blk, info.data_format, bb, sink, user, st, d_ca);
+    err = run_main(d, r, info.n_per_blk, info.data_format, bb, sink, user, st, cp, d_ca);
     {
         std::lock_guard<std::mutex> lk(r.mu);
         r.abort = 1;

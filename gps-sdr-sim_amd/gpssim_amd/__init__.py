@@ -13,8 +13,15 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
-# GSS_LIB_PATH: an alternative build of the same library (kernel variants under measurement)
-LIB_PATH = os.environ.get("GSS_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libgpssim_amd.so")
+# The in-tree build (make -C gps-sdr-sim_amd).  Measurement builds of kernel variants
+# (tools/ablate.sh) load only with both GSS_LIB_PATH and GSS_ALLOW_LIB_OVERRIDE=1 set; bench.py
+# records the path it measured and the tests refuse to run on anything but the in-tree build.
+_INTREE = os.path.join(PKG_DIR, "lib", "libgpssim_amd.so")
+if os.environ.get("GSS_LIB_PATH") and os.environ.get("GSS_ALLOW_LIB_OVERRIDE") != "1":
+    raise ImportError("GSS_LIB_PATH is set without GSS_ALLOW_LIB_OVERRIDE=1: refusing to load a "
+                      "library other than the in-tree build " + _INTREE)
+LIB_PATH = os.environ.get("GSS_LIB_PATH") or _INTREE
+IN_TREE = os.path.abspath(LIB_PATH) == os.path.abspath(_INTREE)
 CLI_PATH = os.path.join(PKG_DIR, "bin", "gps-sdr-sim")
 
 MAXCH = 16
@@ -57,6 +64,11 @@ class _Opts(C.Structure):
         ("start", C.c_int * 6), ("start_sec", C.c_double), ("iono_disable", C.c_int),
         ("verbose", C.c_int), ("user_motion_size", C.c_int), ("quiet", C.c_int),
     ]
+
+
+class _Cli(C.Structure):
+    _fields_ = [("opt", _Opts), ("nav_file", C.c_char * 256), ("motion_file", C.c_char * 256),
+                ("out_file", C.c_char * 256)]
 
 
 class _Info(C.Structure):
@@ -108,6 +120,8 @@ _SIGS = {
                                       C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                       C.POINTER(C.c_int32)]),
     "gss_lut": (C.c_int, [_P, _P]),
+    "gss_cli_parse": (C.c_int, [C.c_int, C.POINTER(C.c_char_p), C.POINTER(_Cli)]),
+    "gss_cli_usage": (None, []),
     "gss_last_error": (C.c_char_p, []),
     "gss_version": (C.c_char_p, []),
 }
@@ -233,6 +247,26 @@ class Scenario:
         o.quiet = int(bool(quiet))
         self._h = C.c_void_p()
         _check(lib().gss_scn_open(C.byref(self._h), C.byref(o)))
+        self._init_info()
+
+    @classmethod
+    def from_cli(cls, argv):
+        """(Scenario, output path) from the reference's command line (gss_cli_parse: same
+        options, defaults and error messages, gpssim.c:1650-1852).  Raises SystemExit(1) where
+        the reference exits 1."""
+        cli = _Cli()
+        args = [b"gps-sdr-sim"] + [str(a).encode() for a in argv]
+        arr = (C.c_char_p * len(args))(*args)
+        if lib().gss_cli_parse(len(args), arr, C.byref(cli)):
+            raise SystemExit(1)
+        self = cls.__new__(cls)
+        self._keep = [cli]
+        self._h = C.c_void_p()
+        _check(lib().gss_scn_open(C.byref(self._h), C.byref(cli.opt)))
+        self._init_info()
+        return self, cli.out_file.decode()
+
+    def _init_info(self):
         inf = _Info()
         _check(lib().gss_scn_info(self._h, C.byref(inf)))
         self.n_per_blk, self.n_blocks = inf.n_per_blk, inf.n_blocks

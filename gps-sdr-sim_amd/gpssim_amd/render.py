@@ -1,0 +1,94 @@
+"""Device-resident rendering of a block range: the host plane (Scenario), the host proof
+(gss_linearize) and gss_synth_lin_device in batches, output left in HBM (a torch uint8 tensor).
+
+Used by bench.py (timed steps over a resident window) and gpssim_amd.node (each rank renders its
+time-window shard before the ordered gather to rank 0).  torch is only the allocator and stream
+here; the kernels run through the C ABI.
+"""
+import time
+
+import numpy as np
+
+from . import (CHAN_DTYPE, LIN_DTYPE, MAXCH, NCK, block_bytes, ca_table, linearize)
+
+
+def plan_range(scn, first, count, threads=8, batch=2000, with_ck=False):
+    """Blocks [first, first + count) of Scenario scn (count < 0: to the end): blk, nch (and the
+    carrier checkpoints when with_ck).  Blocks before `first` are planned and dropped: the
+    carrier chain is serial (gpssim.c:2245-2250 carries carr_phase across blocks)."""
+    done, parts = 0, []
+    want = None if count < 0 else first + count
+    while want is None or done < want:
+        ask = batch if want is None else min(batch, want - done)
+        r = scn.next(ask, threads=threads, with_ck=with_ck)
+        nb = len(r[1])
+        if nb == 0:
+            break
+        lo = max(0, first - done)
+        if lo < nb:
+            parts.append(tuple(a[lo:] for a in r))
+        done += nb
+    if not parts:
+        empty = [np.zeros((0, MAXCH), CHAN_DTYPE), np.zeros(0, np.int32)]
+        if with_ck:
+            empty.append(np.zeros((0, MAXCH, NCK)))
+        return tuple(empty)
+    return tuple(np.concatenate([p[i] for p in parts]) for i in range(len(parts[0])))
+
+
+class DeviceWindow:
+    """One window of blocks, proven and resident in HBM, rendered in calls of at most `batch`
+    blocks (each call's fast-path scratch rows scale with its block count)."""
+
+    def __init__(self, torch, dev, dev_t, blk, nch, nav, n_per_blk, fmt, ck=None, threads=8,
+                 batch=3000, out=None):
+        self.torch, self.dev, self.fmt, self.npb = torch, dev, fmt, n_per_blk
+        t0 = time.perf_counter()
+        lin, fast = linearize(blk, nch, nav, n_per_blk, threads=threads)
+        self.lin_s = time.perf_counter() - t0
+        self.nblk = len(nch)
+        self.n_fast = int(fast.sum())
+        self.nch_max = int(nch.max()) if len(nch) else 1
+        ca = ca_table()
+        self.n_ca, self.n_nav = len(ca), len(nav)
+        self.bb = block_bytes(n_per_blk, fmt)
+
+        def up(a):
+            return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev_t)
+
+        self.d_blk, self.d_nch, self.d_lin = up(blk), up(nch), up(lin)
+        self.d_ck = up(ck) if ck is not None else None
+        self.d_ca, self.d_nav, self.d_fast = up(ca), up(nav), up(fast)
+        self.out = out if out is not None else torch.empty(self.nblk * self.bb, dtype=torch.uint8,
+                                                           device=dev_t)
+        assert self.out.numel() >= self.nblk * self.bb
+        self.batches = []
+        for b0 in range(0, self.nblk, batch):
+            b1 = min(self.nblk, b0 + batch)
+            fb = np.nonzero(fast[b0:b1] == 0)[0].astype(np.int32)
+            d_fb = torch.from_numpy(fb if len(fb) else np.zeros(1, np.int32)).to(dev_t)
+            self.batches.append((b0, b1, d_fb, len(fb)))
+        if self.nblk:
+            dev.reserve(min(batch, self.nblk), n_per_blk)
+
+    def step(self, stream=0):
+        """Render every block of the window into self.out (stream-ordered)."""
+        cs, ls, ks = CHAN_DTYPE.itemsize * MAXCH, LIN_DTYPE.itemsize * MAXCH, 8 * MAXCH * NCK
+        for b0, b1, d_fb, n_fb in self.batches:
+            self.dev.synth_lin_device(
+                self.d_blk.data_ptr() + b0 * cs, self.d_nch.data_ptr() + b0 * 4, self.nch_max,
+                self.d_lin.data_ptr() + b0 * ls, self.d_fast.data_ptr() + b0 * 4,
+                d_fb.data_ptr(), n_fb, self.d_ca.data_ptr(), self.n_ca, self.d_nav.data_ptr(),
+                self.n_nav, b1 - b0, self.npb, self.fmt, self.out.data_ptr() + b0 * self.bb,
+                stream=stream,
+                ck_ptr=(self.d_ck.data_ptr() + b0 * ks) if self.d_ck is not None else 0)
+
+    def free_inputs(self):
+        for a in ("d_blk", "d_nch", "d_lin", "d_ck", "d_ca", "d_nav", "d_fast"):
+            setattr(self, a, None)
+        self.batches = []
+
+    def free(self):
+        self.free_inputs()
+        self.out = None
+        self.torch.cuda.empty_cache()

@@ -207,6 +207,17 @@ typedef struct gss_opts {
     int    quiet;               /* suppress the reference's stderr chatter (library use)       */
 } gss_opts_t;
 
+/* The reference command line (getopt "e:u:g:c:l:o:s:b:T:t:d:iv", gpssim.c:1650-1852) parsed
+   into options, with the reference's validation messages on stderr.  Returns 0 to run, 1 after
+   printing usage or an error (the reference then exits with status 1).  The strings opt points
+   at live in the struct.                                                                       */
+typedef struct gss_cli {
+    gss_opts_t opt;
+    char nav_file[256], motion_file[256], out_file[256];
+} gss_cli_t;
+int gss_cli_parse(int argc, char **argv, gss_cli_t *cli);
+void gss_cli_usage(void);
+
 typedef struct gss_scn_info {
     int    n_per_blk;           /* iq_buff_size = floor(fs/10) (gpssim.c:1877-1878)            */
     int    n_blocks;            /* numd-1: blocks the run writes (gpssim.c:2154)               */

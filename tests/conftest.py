@@ -40,6 +40,8 @@ def _ensure_built():
 @pytest.fixture(scope="session", autouse=True)
 def built():
     _ensure_built()
+    import gpssim_amd
+    assert gpssim_amd.IN_TREE, f"tests must run on the in-tree build, not {gpssim_amd.LIB_PATH}"
 
 
 @pytest.fixture(scope="session")

@@ -25,7 +25,7 @@ def main():
                     bench = json.loads(line)
         except OSError:
             pass
-    want = "gss_lin_kernel" if bench and bench["config"].get("path") == "lin" else "gss_synth_kernel"
+    want = "gss_lin_kernel" if bench and bench["config"].get("path", "lin") == "lin" else "gss_synth_kernel"
     k = next(n for n in summ if n.startswith(want))
     e = summ[k]
     w, r = e["hbm_write_bytes"], e["hbm_read_bytes_corrected"]
@@ -38,6 +38,7 @@ def main():
            "hbm_bytes_per_launch": round(w + r), "hbm_write_bytes_per_launch": round(w),
            "hbm_read_bytes_per_launch": round(r), "algorithmic_bytes_per_launch": alg,
            "kernel_avg_ns": e.get("avg_ns"), "valu_issue_frac": e.get("valu_issue_frac"),
+           "lib_sha16": (bench or {}).get("lib", {}).get("sha16"),
            "lds_busy_frac": e.get("lds_busy_frac"), "lds_conflict_frac": e.get("lds_conflict_frac"),
            "method": "rocprofv3 --pmc WRITE_SIZE / --pmc FETCH_SIZE in separate passes "
                      "(--kernel-trace only), KiB x1024, FETCH_SIZE x2 (gfx950 correction)",

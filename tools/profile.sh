@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 TAG=${1:-r2}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BA=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --no-exact}
+BA=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --no-exact --no-configs --no-e2e}
 run() {  # name, rocprofv3 args...
     local name=$1; shift
     timeout -k 10 400 rocprofv3 "$@" -d $OUT/$name -o $name -f csv -- python3 bench.py $BA \
