@@ -28,6 +28,12 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD Instinct MI355X (gfx950)")
 
 
+def pytest_collection_modifyitems(config, items):
+    """The long full-stream digests (test_gpu_long.py, 344 GB hashed) run last, so that with -x
+    every BASELINE-config and CLI parity test has reported before them."""
+    items.sort(key=lambda it: "test_gpu_long" in it.nodeid)
+
+
 def _ensure_built():
     lib = os.path.join(PKG, "lib", "libgpssim_amd.so")
     ora = os.path.join(REPO, "oracle", "_ref", "libgss_oracle.so")

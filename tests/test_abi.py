@@ -46,3 +46,16 @@ def test_no_gpu_fails_loudly():
         assert e.code == -7
     else:
         raise AssertionError("gss_dev_open succeeded without a GPU")
+
+
+def test_integration_patch_compiles_and_links():
+    """INTEGRATION.md §2 applied to a /tmp copy of the reference's gpssim.c, compiled with the
+    reference's flags and linked against the library (tools/integration/build_integ.py)."""
+    import pytest
+    import subprocess
+    import sys
+    if not os.path.exists("/root/reference/gpssim.c"):
+        pytest.skip("reference sources absent (GPU box): the binary is built in the container")
+    subprocess.check_call([sys.executable, os.path.join(REPO, "tools", "integration",
+                                                        "build_integ.py")])
+    assert os.path.exists(os.path.join(REPO, "oracle", "_ref", "gps-sdr-sim-integ"))

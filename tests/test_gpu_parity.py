@@ -290,3 +290,23 @@ def test_streaming_run_walk_path(dev, golden, monkeypatch):
 
     dev.run(s, sink, first_block=200, n_blocks=40, batch=16)
     assert blocks == golden["static_d30_b8"]["block_sha16"][200:240]
+
+
+INTEG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle",
+                     "_ref", "gps-sdr-sim-integ")
+
+
+@pytest.mark.parametrize("name,args", [
+    ("static_d30_b16", ["-l", ",".join(map(str, LOC)), "-d", "30", "-b", "16"]),
+    ("circle_b8", ["-u", CIRCLE, "-b", "8"]),
+])
+def test_integration_patch_bit_exact(golden, name, args):
+    """INTEGRATION.md applied to the reference's own gpssim.c (tools/integration/build_integ.py:
+    its sample loop replaced by gss_integ_block, batches flushed at every 30 s update) writes the
+    reference's bytes; circle.csv crosses nine nav/allocation updates."""
+    if not os.path.exists(INTEG):
+        pytest.skip("oracle/_ref/gps-sdr-sim-integ not built (needs the reference sources)")
+    p = subprocess.run([INTEG, "-e", NAV] + args + ["-o", "-"], capture_output=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert hashlib.sha256(p.stdout).hexdigest() == golden[name]["sha256"]

@@ -85,3 +85,51 @@ def test_cpu_restatement_across_first_nav_update(golden, name, args, nblk):
     bb = g["bytes"] // g["blocks"]
     assert len(out) == nblk * bb
     assert block_hashes(out, bb) == g["block_sha16"][:nblk]
+
+
+# the rest of the CLI surface (tests/golden/make_golden.py): NMEA input, valid -t, -T, a
+# USER_MOTION_SIZE=4000 build for rocket.csv, the LEO satellite.csv run with -i
+DATA = os.path.join(REPO, "tests", "golden", "data")
+CLI_CASES = ["nmea_triumph_b8", "static_t0200_d30_b8", "static_T1221_d30_b8",
+             "rocket_um4000_b8", "satellite_i_b8"]
+
+
+def fixture_argv(g):
+    """the fixture's command line with the reference's data files mapped to tests/golden/data"""
+    return [os.path.join(DATA, a) if os.path.exists(os.path.join(DATA, a)) else a
+            for a in g["argv"]]
+
+
+def limit_duration(argv, seconds):
+    a = list(argv)
+    if "-d" in a:
+        a[a.index("-d") + 1] = str(seconds)
+    else:
+        a += ["-d", str(seconds)]
+    return a
+
+
+@pytest.mark.parametrize("name", CLI_CASES)
+def test_cpu_restatement_cli_surface_prefix(golden, name, monkeypatch):
+    """The first 2.9 s of each run, byte for byte (the GPU tests check whole runs)."""
+    g = golden[name]
+    monkeypatch.setenv("GSS_USER_MOTION_SIZE", str(g["user_motion_size"]))
+    out = run_cpu_restatement(limit_duration(fixture_argv(g), 3))
+    bb = G.block_bytes(g["n_per_blk"], g["fmt"])
+    assert len(out) == 29 * bb
+    assert block_hashes(out, bb) == g["block_sha16"][:29]
+
+
+@pytest.mark.parametrize("name", ["static_d31_v", "circle_d31"])
+def test_cpu_restatement_stderr_matches_reference(name):
+    """Banner, ephemeris/iono/UTC lines (-v), the channel table, its 30 s reprint (-v) and the
+    progress lines, as the reference prints them (gpssim.c:1939-1948, 2037-2039, 2131-2136,
+    2335-2352), minus the CPU-time line."""
+    e = json.load(open(os.path.join(REPO, "tests", "golden", "stderr.json")))[name]
+    argv = [os.path.join(DATA, a) if os.path.exists(os.path.join(DATA, a)) else a
+            for a in e["argv"]]
+    p = subprocess.run([oracle.CLI, "-e", NAV] + argv + ["-o", "/dev/null"],
+                       capture_output=True, check=True)
+    got = "".join(l for l in p.stderr.decode().splitlines(True)
+                  if not l.startswith("Process time"))
+    assert got == e["stderr"]
