@@ -605,6 +605,8 @@ __global__ void gss_cbw_kernel(const uint32_t *__restrict__ ca_bits, int n_ca,
    (1/8 chip above chip -CBW_PRE, at most 3 chips below lane 0's chip) and its per-pair advance,
    the channel's window row (chip -CBW_PRE), the signed gain (with LANE_GAIN: the gain difference, applied from sample
    pos1 on) */
+#define LIN_ACC0 (64 + (1 << 21) + ((int64_t)64 << 22))   /* (0 + 64 + 2^21) + 2^22 (0 + 64) */
+
 template <bool LANE_GAIN>
 __device__ __forceinline__ void lin_channel_chunk(int64_t (&acc)[LIN_CH], uint32_t X, uint64_t Z,
                                                   uint32_t dX, uint64_t dZ, uint32_t Q,
@@ -758,10 +760,12 @@ __global__ __launch_bounds__(LIN_THREADS) void gss_lin_kernel(
         const int nb0 = n0 + c * (64 * LIN_CH);           /* first sample of the chunk */
         if (nb0 >= n_per_blk)
             break;
+        /* (peeling the first channel to fold this into its multiply-adds measured 3.5 %
+           slower: profiles/round2/ablate_a6.log) */
         int64_t acc[LIN_CH];
 #pragma unroll
         for (int s = 0; s < LIN_CH; s++)
-            acc[s] = 64 + (1 << 21) + ((int64_t)64 << 22);
+            acc[s] = LIN_ACC0;
         for (int k = 0; k < nc; k++) {                    /* uniform channel loop */
             const lin_chan ck = CH[k];                    /* scalar loads */
             const lin_seg sk = S[(size_t)k * nseg];
