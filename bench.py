@@ -183,26 +183,53 @@ def per_config(G, torch, dev, dev_t, stream, steps, warmup, threads):
     return out
 
 
+def d2h_ceiling(nbytes, reps=8):
+    """device -> pinned host copy rate of one gss_run slot (the PCIe ceiling of e2e_run)"""
+    import torch
+    src = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    dst = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    rate = nbytes * reps / (time.perf_counter() - t0) / 1e9
+    del src, dst
+    return round(rate, 2)
+
+
 def e2e_run(G, dev, threads, window=1800.0):
     """gss_run over the whole static run into a discarding sink, wall-clocked (planner, proofs,
-    uploads, kernels, D2H into pinned buffers and the sink, overlapped)."""
-    s = G.Scenario(NAV, llh=LOC, duration=window, samp_freq=FS, data_format=16)
-    got = {"bytes": 0, "blocks": 0}
+    uploads, kernels, D2H into pinned buffers and the sink, overlapped).  A second run of a third
+    of the length gives the steady-state rate (the slope; the rest is the fixed start-up), to be
+    read against d2h_ceiling_GBps, the measured device -> pinned host copy rate."""
 
-    def sink(mv, first, nb):
-        got["bytes"] += len(mv)
-        got["blocks"] += nb
+    def one(w):
+        s = G.Scenario(NAV, llh=LOC, duration=w, samp_freq=FS, data_format=16)
+        got = {"bytes": 0, "blocks": 0}
 
-    t0 = time.perf_counter()
-    dev.run(s, sink, batch=256, threads=threads)
-    wall = time.perf_counter() - t0
-    samples = got["blocks"] * s.n_per_blk
+        def sink(mv, first, nb):
+            got["bytes"] += len(mv)
+            got["blocks"] += nb
+
+        t0 = time.perf_counter()
+        dev.run(s, sink, batch=256, threads=threads)
+        return time.perf_counter() - t0, got["blocks"], got["bytes"], s.n_per_blk
+
+    ws, bs, _, _ = one(window / 3)
+    wall, blocks, nbytes, n_per_blk = one(window)
+    samples = blocks * n_per_blk
+    slope = (blocks - bs) / (wall - ws)
     return {"value": round(samples / wall / 1e6, 2), "unit": "MS/s",
             "x_realtime": round(samples / wall / FS, 1), "wall_s": round(wall, 3),
-            "blocks": got["blocks"], "d2h_GBps": round(got["bytes"] / wall / 1e9, 2),
+            "blocks": blocks, "d2h_GBps": round(nbytes / wall / 1e9, 2),
+            "steady_MSps": round(slope * n_per_blk / 1e6, 1),
+            "steady_d2h_GBps": round(slope * nbytes / blocks / 1e9, 2),
+            "startup_s": round(wall - blocks / slope, 3),
+            "d2h_ceiling_GBps": d2h_ceiling(256 * n_per_blk * 4),
             "workload": f"static -b 16, {window:g} s through gss_run (batch 256 blocks), "
                         "discarding sink"}
-
 
 def main():
     ap = argparse.ArgumentParser()

@@ -12,8 +12,10 @@
  *                    slot renders, hands the previous slot's bytes to the sink in run order
  *
  * Slots cycle planner -> main -> sink -> planner; a slot's buffers belong to exactly one side at
- * a time (state under a mutex).  Two HIP streams: the D2H of slot i (PCIe) overlaps the kernels
- * of slot i+1; a slot's device output buffer is rewritten only after its own D2H (event).
+ * a time (state under a mutex).  One compute stream and two copy streams (alternating slots, so
+ * two DMA engines share the PCIe link): the D2H of slots i and i-1 overlap the kernels of slot
+ * i+1; up to DEPTH slots are submitted before the oldest is handed to the sink; a slot's device
+ * output buffer is rewritten only after its own D2H (event).
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -36,7 +38,15 @@ extern "C" int gss_fail(int code, const char *fmt, ...);
 
 namespace {
 
-constexpr int NSLOT = 3;
+#ifndef GSS_RUN_NCOPY
+#define GSS_RUN_NCOPY 1
+#endif
+#ifndef GSS_RUN_DEPTH
+#define GSS_RUN_DEPTH 1
+#endif
+constexpr int NCOPY = GSS_RUN_NCOPY;                   /* copy streams (DMA engines) */
+constexpr int DEPTH = GSS_RUN_DEPTH;                   /* slots submitted, not yet drained */
+constexpr int NSLOT = DEPTH + 2;
 constexpr size_t SLOT_OUT_MAX = (size_t)256 << 20;     /* pinned output bytes per slot */
 
 enum { FREE, PLANNED };
@@ -240,10 +250,18 @@ int drain(Run &r, Slot &sl, size_t bb, gss_sink_fn sink, void *user)
     return 0;
 }
 
-int run_main(gss_dev *d, Run &r, int n_per_blk, int fmt, size_t bb, gss_sink_fn sink,
-             void *user, hipStream_t st, hipStream_t cp, const uint32_t *d_ca)
+bool make_streams(hipStream_t *cp)
 {
-    int pending = -1;                                  /* slot submitted, not yet drained */
+    for (int k = 0; k < NCOPY; k++)
+        if (hipStreamCreateWithFlags(&cp[k], hipStreamNonBlocking) != hipSuccess)
+            return false;
+    return true;
+}
+
+int run_main(gss_dev *d, Run &r, int n_per_blk, int fmt, size_t bb, gss_sink_fn sink,
+             void *user, hipStream_t st, hipStream_t *cp, const uint32_t *d_ca)
+{
+    int pending[DEPTH], np = 0, head = 0;              /* submitted, not yet drained (FIFO) */
     for (int i = 0;; i++) {
         Slot &sl = r.slot[i % NSLOT];
         {
@@ -251,18 +269,23 @@ int run_main(gss_dev *d, Run &r, int n_per_blk, int fmt, size_t bb, gss_sink_fn 
             r.cv.wait(lk, [&] { return sl.state == PLANNED; });
         }
         if (sl.end) {
-            int rc = pending >= 0 ? drain(r, r.slot[pending], bb, sink, user) : 0;
+            int rc = 0;
+            for (; np > 0 && rc == 0; np--, head = (head + 1) % DEPTH)
+                rc = drain(r, r.slot[pending[head]], bb, sink, user);
             return sl.err ? sl.err : rc;
         }
-        int rc = submit(d, sl, d_ca, n_per_blk, fmt, bb, st, cp);
-        if (rc)
-            return rc;
-        if (pending >= 0) {                            /* previous slot overlaps this one */
-            rc = drain(r, r.slot[pending], bb, sink, user);
+        if (np == DEPTH) {                             /* oldest slot out to the sink */
+            int rc = drain(r, r.slot[pending[head]], bb, sink, user);
             if (rc)
                 return rc;
+            head = (head + 1) % DEPTH;
+            np--;
         }
-        pending = i % NSLOT;
+        int rc = submit(d, sl, d_ca, n_per_blk, fmt, bb, st, cp[i % NCOPY]);
+        if (rc)
+            return rc;
+        pending[(head + np) % DEPTH] = i % NSLOT;
+        np++;
     }
 }
 
@@ -296,12 +319,13 @@ extern "C" int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_bl
 
     int ordinal = 0;
     RUN_TRY(hipGetDevice(&ordinal));
-    hipStream_t st = nullptr, cp = nullptr;
+    hipStream_t st = nullptr, cp[NCOPY] = {};
     uint32_t *d_ca = nullptr;
     int err = 0;
     auto cleanup = [&]() {
         if (st) (void)hipStreamSynchronize(st);
-        if (cp) (void)hipStreamSynchronize(cp);
+        for (hipStream_t c : cp)
+            if (c) (void)hipStreamSynchronize(c);
         for (Slot &sl : r.slot) {
             (void)hipHostFree(sl.blk); (void)hipHostFree(sl.nch); (void)hipHostFree(sl.ck);
             (void)hipHostFree(sl.nav); (void)hipHostFree(sl.h_out); (void)hipHostFree(sl.h_status);
@@ -312,7 +336,8 @@ extern "C" int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_bl
         }
         (void)hipFree(d_ca);
         if (st) (void)hipStreamDestroy(st);
-        if (cp) (void)hipStreamDestroy(cp);
+        for (hipStream_t c : cp)
+            if (c) (void)hipStreamDestroy(c);
     };
     /* buffers */
     {
@@ -320,7 +345,7 @@ extern "C" int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_bl
         if (hipMalloc((void **)&d_ca, sizeof r.ca) != hipSuccess ||
             hipMemcpy(d_ca, r.ca, sizeof r.ca, hipMemcpyHostToDevice) != hipSuccess ||
             hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
-            hipStreamCreateWithFlags(&cp, hipStreamNonBlocking) != hipSuccess)
+            !make_streams(cp))
             err = gss_fail(GSS_E_HIP, "run setup failed");
         const size_t nb = (size_t)r.batch;
         for (Slot &sl : r.slot) {
