@@ -482,52 +482,75 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
    walk.  Lanes are consecutive samples: one wave step renders 64 consecutive samples, so the LUT
    reads of a wave hit a few neighbouring cells and the output leaves as one contiguous 256-B
    (-b 16) store per step.
-   A wave renders one 4096-sample segment in chunks of LIN_CH steps.  Within a chunk the channel
-   loop is outermost: one channel's line parameters live in scalar registers at a time; each lane
-   takes its chunk anchors from the lines (64-bit, once per chunk) and then steps
-       X = Xl + D.hi      carrier, 2^-32 cycle; D = 2^31 + s 64 xs is a
-                          scalar running sum (s_add_u32/s_addc_u32)    v_add_u32
-       Z += dZ            code, 32.32 fixed point (hi word = chip)     v_lshl_add_u64
-       t = W >> Z.hi      chip sign (bit 0) from the wave's 64-chip window   v_lshrrev_b64
-       a = alignbit(t, X, 21) & 0xFFC   LUT byte address: cell (X bits 23..31) at bits 2..10,
-                                        chip sign at bit 11 (second half of the LUT negated)
-       acc += g * LUT[a]  packed I/Q                                   v_mad_i64_i32
-   6 VALU + 1 LDS per channel-sample (the round-1 kernel needed 8, two of them 64-bit adds;
-   tools/ubench/body_ubench.hip: 1.55x fewer SIMD cycles).  Chip windows: every lane's chip of two
-   consecutive steps lies in a 64-chip window starting at lane 0's chip E of the first
-   (127 zs + 2 chips <= 64, checked by gss_linearize), so one wave-uniform 64-bit window per step
-   pair, read from the table cbw (rotated: bit e mod 64 holds the sign of extended chip e,
-   chip = e mod 1023), serves both steps; v_lshrrev_b64 takes the shift mod 64. */
+   A wave renders one 4096-sample segment in chunks of LIN_CH steps.  Per chunk, the wave's
+   lanes first build every channel's parameters in parallel (lin_ct in LDS: the chunk base, the
+   step, the gain, and the 16 chip windows from vector loads of the window table); then, channel
+   by channel, each lane forms its anchor P (carrier in the low word, code in the high word,
+   gss_lin.h) with one 64-bit add of the base to its entry of the workgroup's lane table (LDS),
+   and per 64-sample step
+       t = W_s >> byte3(P.hi)  chip sign at bit 0, from the step's window       v_lshrrev_b32_sdwa
+       a = alignbit(t, P.lo, 21) & M   LUT byte address: cell (carrier bits 23..31) at bits
+                                    2..10, chip sign at bit 11 (second half of the LUT negated)
+       acc += g * LUT[a]       packed I/Q                                       v_mad_i64_i32
+       P += D                  carrier and code together                        v_lshl_add_u64
+   5 VALU + 1 LDS per channel-sample.  Measured (profiles/round2/ablate_b1.log, ablate_b2.log):
+   without any memory access the kernel still takes 75-80 % of its time, and the scalar unit,
+   one per CU for four SIMDs, was the next limit once the loop lost its 64-bit code add (the
+   per-channel scalar work of a chunk, ~90 instructions, cost more than the steps' VALU).  So the
+   code is a 32-bit word beside the carrier (a carry out of the carrier adds 2^-24 chip, which the
+   render model counts), and everything wave-uniform that used to be scalar per channel is built
+   once per chunk by the lanes in parallel.
+   Chip windows (table cbw, one row per C/A table row, 4 entries per chip): entry q holds the 32
+   chips from extended chip E = q/4 - CBW_PRE on, rotated (bit e mod 32 = sign of chip e mod 1023,
+   1 = negative), so that any lane whose chip e lies in [E, E + 32) takes its sign with a shift by
+   e mod 32 = byte 3 of the code word mod 32.  Step s reads entry floor(Q_s/4), Q_s = Q_0 + s dq
+   in 1/16 chip (Q_0 1/16 below lane 0's first chip, dq = floor(64 zs / 2^46)).  The window then
+   starts at most two chips below lane 0's chip and every lane's chip of the step lies inside it
+   when 63 zs + 3 chips <= 31 (GSS_LIN_WIN_OK, checked by gss_linearize); the index is clamped to
+   the row, which a certified channel never needs. */
 #define LIN_THREADS 256
 #define LIN_WAVES   (LIN_THREADS / 64)
 #define LIN_STEPS   64                     /* 64-sample steps per wave segment: 4096 samples    */
 #define LIN_CH      GSS_LIN_CH             /* steps per chunk (one accumulator each)            */
-#define CBW_PRE     8                      /* windows kept below chip 0 (window starts run up to
-                                              3 chips below lane 0's chip)                      */
-#define CBW_X       (3136 + CBW_PRE)       /* windows per C/A row: chips -8 <= E < 1023 + the
-                                              reach of one wave (LIN_STEPS*64 samples * 0.49)+64 */
+#define CBW_PRE     2                      /* chips of windows kept below extended chip 0       */
+#define CBW_CHIPS   3072                   /* window starts per row: E0 <= 1022 plus a segment's
+                                              reach (4160 samples * 0.46 chip) plus a window     */
+#define CBW_ROW     (4 * (CBW_CHIPS + CBW_PRE))     /* entries (32-bit) per row            */
 static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole chunks");
 /* LIN_ABLATE (measurement builds only, tools/ablate.sh; wrong output): 1 no output stores,
-   2 no chip-window loads, 4 no LUT reads, 8 every block stores into one of 8 blocks (L2) */
+   2 no chip-window loads, 4 no LUT reads, 8 every block stores into one of 8 blocks (L2),
+   32 no alignbit (VALU work), 64 no window reads in the render loop (LDS work) */
 #ifndef LIN_ABLATE
 #define LIN_ABLATE 0
 #endif
 
+/* per (block, segment wave, chunk, channel): the chunk's render parameters, built by the wave's
+   lanes in parallel (vector loads and VALU) and read back by the render loop with broadcast LDS
+   reads, so that the scalar unit (one per CU, shared by its four SIMDs) does no per-channel
+   work */
+struct lin_ct {
+    uint64_t B;                  /* the chunk's base (gss_lin.h)                                */
+    uint64_t D;                  /* the 64-sample step dC : dX                                  */
+    int32_t g;                   /* signed gain at the chunk start                              */
+    int32_t gd;                  /* gain change inside the chunk (g1 - g0), from sample pos1 on */
+    int32_t pos1;
+    uint32_t flags;              /* 1: a gain change inside the chunk, 2: patched samples       */
+    uint32_t q0, dq, tab, pad;   /* first window offset (1/16 chip), its step, the row          */
+    uint32_t W[LIN_CH];          /* the steps' chip windows                                     */
+};
+
 /* per (block, channel): the render constants of gss_lin.h (written by gss_linseg_kernel) */
 struct lin_chan {
     uint64_t xs, zs;             /* the lines' per-sample steps                                 */
-    uint64_t dz;                 /* gss_lin_dz(zs): the code's 64-sample step, 32.32 chips       */
-    uint64_t pad0;
-    uint32_t dx;                 /* gss_lin_dx(xs): the carrier's 64-sample step, 2^-32 cycle    */
-    uint32_t dq;                 /* window start advance per step pair, 1/8 chip, rounded down   */
-    uint32_t tab;                /* byte offset of the channel's window row (chip -CBW_PRE)      */
-    uint32_t pad1[5];
+    uint64_t d;                  /* the 64-sample step dC : dX of P (gss_lin_dz : gss_lin_dx)    */
+    uint32_t dq;                 /* window offset advance per step, 1/16 chip, rounded down      */
+    uint32_t tab;                /* byte offset of the channel's window row                      */
 };
 /* per (block, channel, wave segment of 64*LIN_STEPS samples): the lines at the segment start,
    so that the render kernel needs no 128-bit arithmetic and no schedule search */
 struct lin_seg {
     uint64_t x;                  /* X(n0) + gss_lin_xa(xs): the first chunk's carrier anchor base */
-    uint64_t z;                  /* ((E0 << 50) | fraction) + 2^17: the first chunk's code anchor
+    uint64_t z;                  /* ((E0 << 50) | fraction) + 2^25: the first chunk's code anchor
                                     base, E0 = chip at the segment start mod 1023               */
     int32_t g01;                 /* signed gain at the start (low 16) and after pos1 (high 16)   */
     int32_t pos1;                /* sample of the first gain change in the segment, or INT32_MAX */
@@ -550,13 +573,12 @@ __global__ void gss_linseg_kernel(const gss_lin_t *__restrict__ lin,
     const gss_lin_t *L = lin + bk;
     const uint64_t xa = gss_lin_xa(L->xs);
     if (sg == 0) {
-        lin_chan c = {};
+        lin_chan c;
         c.xs = L->xs;
         c.zs = L->zs;
-        c.dz = gss_lin_dz(L->zs);
-        c.dx = gss_lin_dx(L->xs);
-        c.dq = (uint32_t)((L->zs * 128u) >> 47);
-        c.tab = (uint32_t)((size_t)blk[bk].ca_tbl * CBW_X * sizeof(uint64_t));
+        c.d = ((uint64_t)gss_lin_dz(L->zs) << 32) | gss_lin_dx(L->xs);
+        c.dq = (uint32_t)((L->zs * 64u) >> 46);
+        c.tab = (uint32_t)((size_t)blk[bk].ca_tbl * CBW_ROW * sizeof(uint32_t));
         chan_out[bk] = c;
     }
     const uint64_t n0 = (uint64_t)sg * (64 * LIN_STEPS);
@@ -564,7 +586,7 @@ __global__ void gss_linseg_kernel(const gss_lin_t *__restrict__ lin,
     const uint64_t hi = __umul64hi(n0, L->zs) + (lo < L->z0 ? 1u : 0u);
     const uint32_t E0 = ((uint32_t)(hi << 14) | (uint32_t)(lo >> 50)) % (uint32_t)GSS_CA_LEN;
     lin_seg r;
-    r.z = (((uint64_t)E0 << 50) | (lo & ((1ull << 50) - 1))) + (1ull << 17);
+    r.z = (((uint64_t)E0 << 50) | (lo & ((1ull << 50) - 1))) + (1ull << (GSS_LIN_CSH - 1));
     r.x = L->x0 + n0 * L->xs + xa;
     int q = 0;
     while (q + 1 < GSS_NGC && L->gpos[q + 1] <= (int)n0)
@@ -582,58 +604,54 @@ __global__ void gss_linseg_kernel(const gss_lin_t *__restrict__ lin,
     seg_out[i] = r;
 }
 
-/* per C/A row, the rotated 64-bit chip-sign windows of extended chips E = -CBW_PRE .. */
+/* per C/A row, the rotated 32-chip windows, 4 entries per chip: entry q starts at extended chip
+   E = q/4 - CBW_PRE */
 __global__ void gss_cbw_kernel(const uint32_t *__restrict__ ca_bits, int n_ca,
-                               uint64_t *__restrict__ cbw)
+                               uint32_t *__restrict__ cbw)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_ca * CBW_X)
+    if (i >= n_ca * CBW_ROW)
         return;
-    const int row = i / CBW_X, E = i - row * CBW_X - CBW_PRE;
+    const int row = i / CBW_ROW, E = (i - row * CBW_ROW) / 4 - CBW_PRE;
     const uint32_t *cb = ca_bits + (size_t)row * GSS_CA_WORDS;
-    uint64_t w = 0;
-    for (int q = 0; q < 64; q++) {
-        const int e = E + q, chip = (e + GSS_CA_LEN) % GSS_CA_LEN;
-        const uint64_t neg = ((cb[chip >> 5] >> (chip & 31)) & 1u) ^ 1u;   /* codeCA = -1 */
-        w |= neg << ((e + 64) & 63);
+    uint32_t w = 0;
+    for (int q = 0; q < 32; q++) {
+        const int e = E + q, chip = ((e % GSS_CA_LEN) + GSS_CA_LEN) % GSS_CA_LEN;
+        const uint32_t neg = ((cb[chip >> 5] >> (chip & 31)) & 1u) ^ 1u;   /* codeCA = -1 */
+        w |= neg << (e & 31);
     }
     cbw[i] = w;
 }
 
-/* one channel's contribution to the chunk's LIN_CH steps: lane anchors X (carrier, 2^-32
-   cycle) and Z (code, 32.32) and their 64-sample steps, the first pair's window start Q
-   (1/8 chip above chip -CBW_PRE, at most 3 chips below lane 0's chip) and its per-pair advance,
-   the channel's window row (chip -CBW_PRE), the signed gain (with LANE_GAIN: the gain difference, applied from sample
+/* one channel's contribution to the chunk's LIN_CH steps: the lane's anchor P (carrier : code,
+   gss_lin.h) and its 64-sample step D, the steps' chip windows (LDS, the same for every lane),
+   the LUT mask M, the signed gain (with LANE_GAIN: the gain difference, applied from sample
    pos1 on) */
 #define LIN_ACC0 (64 + (1 << 21) + ((int64_t)64 << 22))   /* (0 + 64 + 2^21) + 2^22 (0 + 64) */
 
 template <bool LANE_GAIN>
-__device__ __forceinline__ void lin_channel_chunk(int64_t (&acc)[LIN_CH], uint32_t X, uint64_t Z,
-                                                  uint32_t dX, uint64_t dZ, uint32_t Q,
-                                                  uint32_t dq, const char *__restrict__ tab,
-                                                  int g, int pos1, int p0,
-                                                  const int32_t *__restrict__ s_lut)
+__device__ __forceinline__ void lin_channel_chunk(int64_t (&acc)[LIN_CH], uint64_t P, uint64_t D,
+                                                  const uint32_t *W, uint32_t M, int g, int pos1,
+                                                  int p0, const int32_t *__restrict__ s_lut)
 {
-    /* the chunk's chip windows, one per step pair, all loaded before the first use: a scalar
-       load can only be waited for together with every LDS read in flight (lgkmcnt) */
-    uint64_t W[LIN_CH / 2];
-#pragma unroll
-    for (int j = 0; j < LIN_CH / 2; j++) {
-        if (LIN_ABLATE & 2)
-            W[j] = Q * 0x9E3779B97F4A7C15ull;
-        else
-            W[j] = *(const uint64_t *)(tab + (Q & ~7u));  /* scalar loads, SGPR offset */
-        Q += dq;
-    }
+    uint4 w4;
 #pragma unroll
     for (int s = 0; s < LIN_CH; s++) {
-        const uint32_t t = (uint32_t)(W[s / 2] >> ((uint32_t)(Z >> 32) & 63));   /* bit 0 */
-        const uint32_t a = __builtin_amdgcn_alignbit(t, X, 21) & 0xFFCu;
+        if (s % 4 == 0) {                                 /* four windows per broadcast read */
+            if (LIN_ABLATE & 64)
+                w4 = make_uint4(M * (s + 1), M * (s + 3), M * (s + 5), M * (s + 7));
+            else
+                w4 = ((const uint4 *)W)[s / 4];
+        }
+        const uint32_t ws = s % 4 == 0 ? w4.x : s % 4 == 1 ? w4.y : s % 4 == 2 ? w4.z : w4.w;
+        uint32_t t;
+        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
+            "src1_sel:DWORD" : "=v"(t) : "v"((uint32_t)(P >> 32)), "v"(ws));     /* bit 0: sign */
+        const uint32_t a = ((LIN_ABLATE & 32) ? t : __builtin_amdgcn_alignbit(t, (uint32_t)P, 21)) & M;
         const int32_t e = (LIN_ABLATE & 4) ? (int32_t)a : *(const int32_t *)((const char *)s_lut + a);
         const int gg = LANE_GAIN ? (p0 + s * 64 >= pos1 ? g : 0) : g;
         acc[s] += (int64_t)gg * (int64_t)e;
-        X += dX;
-        Z += dZ;
+        P += D;
     }
 }
 
@@ -727,13 +745,18 @@ __device__ __forceinline__ void lin_patch_fix(int64_t (&acc)[LIN_CH],
 }
 
 template <int FMT>
-__global__ __launch_bounds__(LIN_THREADS) void gss_lin_kernel(
+#ifndef LIN_MINB
+#define LIN_MINB 8                         /* workgroups per CU the register budget must allow  */
+#endif
+__global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
     const gss_lin_t *__restrict__ lin, const lin_seg *__restrict__ segs,
     const lin_chan *__restrict__ chans, const int32_t *__restrict__ nch,
-    const int32_t *__restrict__ fast, const uint64_t *__restrict__ cbw, lut_arg lut,
+    const int32_t *__restrict__ fast, const uint32_t *__restrict__ cbw, lut_arg lut,
     int n_per_blk, int nseg, int wg_per_blk, uint8_t *__restrict__ out, size_t block_bytes)
 {
     __shared__ int32_t s_lut[1024];                       /* cos + 2^22 sin; [512+i] = -[i] */
+    __shared__ uint64_t s_lane[GSS_MAXCH * 64];           /* lane offsets L(l) per channel    */
+    __shared__ lin_ct s_ct[LIN_WAVES][GSS_MAXCH];         /* the current chunk, per wave      */
     const int b = blockIdx.x / wg_per_blk;
     const int w = blockIdx.x - b * wg_per_blk;
     if (!fast[b])
@@ -745,52 +768,83 @@ __global__ __launch_bounds__(LIN_THREADS) void gss_lin_kernel(
         s_lut[i] = v;
         s_lut[512 + i] = -v;
     }
+    const lin_chan *CH = chans + (size_t)b * GSS_MAXCH;
+    const int nc = nch[b];
+    for (int i = tid; i < nc * 64; i += LIN_THREADS)
+        s_lane[i] = gss_lin_lane(CH[i >> 6].xs, CH[i >> 6].zs, (uint32_t)(i & 63));
     __syncthreads();
+    uint32_t M = 0xFFCu;                                  /* LUT address mask, in a VGPR */
+    asm volatile("" : "+v"(M));
     const int sg = w * LIN_WAVES + wave;
     const int n0 = sg * (64 * LIN_STEPS);
     if (n0 >= n_per_blk)
         return;
     const gss_lin_t *L = lin + (size_t)b * GSS_MAXCH;
-    const lin_chan *CH = chans + (size_t)b * GSS_MAXCH;
     const lin_seg *S = segs + (size_t)b * GSS_MAXCH * nseg + sg;
-    const int nc = nch[b];
+    lin_ct *T = s_ct[wave];
     uint8_t *ob = out + ((LIN_ABLATE & 8) ? (size_t)(b & 7) : (size_t)b) * block_bytes;
 
     for (int c = 0; c < LIN_STEPS / LIN_CH; c++) {
         const int nb0 = n0 + c * (64 * LIN_CH);           /* first sample of the chunk */
         if (nb0 >= n_per_blk)
             break;
-        /* (peeling the first channel to fold this into its multiply-adds measured 3.5 %
-           slower: profiles/round2/ablate_a6.log) */
-        int64_t acc[LIN_CH];
-#pragma unroll
-        for (int s = 0; s < LIN_CH; s++)
-            acc[s] = LIN_ACC0;
-        for (int k = 0; k < nc; k++) {                    /* uniform channel loop */
-            const lin_chan ck = CH[k];                    /* scalar loads */
-            const lin_seg sk = S[(size_t)k * nseg];
-            /* chunk anchor bases (gss_lin.h): the segment's, plus c chunks of 64 LIN_CH samples */
+        /* ---- the chunk's parameters, lane k for channel k ---- */
+        if (lane < nc) {
+            const lin_chan ck = CH[lane];
+            const lin_seg sk = S[(size_t)lane * nseg];
+            /* the chunk's base B (gss_lin.h): the segment's lines plus c chunks */
             const uint64_t off = (uint64_t)c * (64 * LIN_CH);
             const uint64_t xb = sk.x + off * ck.xs;
             const uint64_t zb = sk.z + off * ck.zs;
             const int g0 = (int)(int16_t)(sk.g01 & 0xFFFF), g1 = sk.g01 >> 16;
-            const char *tab = (const char *)cbw + ck.tab;
-            const uint32_t Q = (uint32_t)(zb >> 47) + (8 * CBW_PRE - 1);   /* below lane 0 */
             const bool chg = sk.pos1 < nb0 + 64 * LIN_CH;    /* a data bit by the chunk's end */
-            lin_channel_chunk<false>(acc, (uint32_t)((xb + (uint64_t)lane * ck.xs) >> 32),
-                                     (zb + (uint64_t)lane * ck.zs) >> 18, ck.dx, ck.dz, Q, ck.dq,
-                                     tab, chg && sk.pos1 <= nb0 ? g1 : g0, 0, 0, s_lut);
+            lin_ct &t = T[lane];
+            t.B = ((uint64_t)(uint32_t)(zb >> GSS_LIN_CSH) << 32) | (xb >> 32);
+            t.D = ck.d;
+            t.g = chg && sk.pos1 <= nb0 ? g1 : g0;
+            t.gd = g1 - g0;
+            t.pos1 = sk.pos1;
+            t.flags = (chg && sk.pos1 > nb0 ? 1u : 0u) | (sk.npatch != 0 ? 2u : 0u);
+            /* 1/16 chip below lane 0's first chip, plus the row's CBW_PRE chips */
+            t.q0 = (uint32_t)(zb >> 46) + (16 * CBW_PRE - 1);
+            t.dq = ck.dq;
+            t.tab = ck.tab;
+        }
+        wave_sync_lds();
+        /* ---- the chip windows, lane (k, s) ---- */
+        for (int i = lane; i < nc * LIN_CH; i += 64) {
+            const lin_ct &t = T[i / LIN_CH];
+            const uint32_t q = (t.q0 + (uint32_t)(i % LIN_CH) * t.dq) >> 2;
+            uint32_t wv;
+            if (LIN_ABLATE & 2)
+                wv = q * 0x9E3779B9u;
+            else
+                wv = cbw[t.tab / 4u + min(q, (uint32_t)CBW_ROW - 1u)];
+            T[i / LIN_CH].W[i % LIN_CH] = wv;
+        }
+        wave_sync_lds();
+        int64_t acc[LIN_CH];
+#pragma unroll
+        for (int s = 0; s < LIN_CH; s++) {
+            acc[s] = LIN_ACC0;
+            asm volatile("" : "+v"(acc[s]));              /* one move each, no copies */
+        }
+        for (int k = 0; k < nc; k++) {                    /* uniform channel loop */
+            const lin_ct &t = T[k];                       /* broadcast LDS reads */
+            const uint64_t B = t.B, D = t.D;
+            const uint32_t fl = __builtin_amdgcn_readfirstlane(t.flags);
+            lin_channel_chunk<false>(acc, s_lane[k * 64 + lane] + B, D, t.W, M, t.g, 0, 0, s_lut);
             /* ... inside it: add (g1 - g0) e from sample pos1 on */
-            if (__builtin_expect(chg && sk.pos1 > nb0, 0)) {
+            if (__builtin_expect(fl & 1u, 0)) {
                 uint32_t l2 = (uint32_t)lane;
                 asm volatile("" : "+v"(l2));               /* recomputed: nothing stays live */
-                lin_channel_chunk<true>(acc, (uint32_t)((xb + (uint64_t)l2 * ck.xs) >> 32),
-                                        (zb + (uint64_t)l2 * ck.zs) >> 18, ck.dx, ck.dz, Q, ck.dq,
-                                        tab, g1 - g0, sk.pos1, nb0 + (int)l2, s_lut);
+                lin_channel_chunk<true>(acc, s_lane[k * 64 + l2] + B, D, t.W, M, t.gd, t.pos1,
+                                        nb0 + (int)l2, s_lut);
             }
-            if (__builtin_expect(sk.npatch != 0, 0))
+            if (__builtin_expect(fl & 2u, 0))
                 lin_patch_fix(acc, L + k, nb0, lane);
         }
+        wave_sync_lds();                                  /* T is rewritten by the next chunk */
         if (LIN_ABLATE & 1) {
             int64_t x = 0;
 #pragma unroll
@@ -824,7 +878,7 @@ struct gss_dev {
     void *h_in = nullptr; size_t h_in_cap = 0;
     void *d_out = nullptr; size_t d_out_cap = 0;
     double *d_cend = nullptr; size_t d_cend_cap = 0;
-    uint64_t *d_cbw = nullptr; size_t d_cbw_cap = 0;   /* chip-sign windows (gss_cbw_kernel) */
+    uint32_t *d_cbw = nullptr; size_t d_cbw_cap = 0;   /* chip-sign windows (gss_cbw_kernel) */
     void *d_seg = nullptr; size_t d_seg_cap = 0;       /* lin_seg rows (gss_linseg_kernel)   */
     int32_t *d_status = nullptr;
     /* the exact path's leftovers of a fast-path call run on their own stream beside the fast
@@ -1063,7 +1117,7 @@ extern "C" int gss_render_device(gss_dev *d, int set, const gss_chan_blk_t *blk,
 
 /* ---- fast path -------------------------------------------------------------------------- */
 typedef void (*lin_fn)(const gss_lin_t *, const lin_seg *, const lin_chan *, const int32_t *,
-                       const int32_t *, const uint64_t *, lut_arg, int, int, int, uint8_t *,
+                       const int32_t *, const uint32_t *, lut_arg, int, int, int, uint8_t *,
                        size_t);
 
 static lin_fn pick_lin(int fmt)
@@ -1098,14 +1152,14 @@ extern "C" int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const
         return gss_fail(GSS_E_ARG, "no fast kernel for fmt=%d nch=%d", fmt, nchp);
     HIP_TRY(hipSetDevice(d->ordinal));
     hipStream_t st = (hipStream_t)stream;
-    /* chip-sign windows of every C/A table row (32 x 1600 x 8 B; rebuilt per call: ~µs) */
-    const size_t ncbw = (size_t)n_ca * CBW_X;
-    if (ncbw * sizeof(uint64_t) > d->d_cbw_cap) {
+    /* chip-sign windows of every C/A table row (32 x 12296 x 4 B; rebuilt per call: ~µs) */
+    const size_t ncbw = (size_t)n_ca * CBW_ROW;
+    if (ncbw * sizeof(uint32_t) > d->d_cbw_cap) {
         (void)hipFree(d->d_cbw);
         d->d_cbw = nullptr;
         d->d_cbw_cap = 0;
-        HIP_TRY(hipMalloc(&d->d_cbw, ncbw * sizeof(uint64_t)));
-        d->d_cbw_cap = ncbw * sizeof(uint64_t);
+        HIP_TRY(hipMalloc(&d->d_cbw, ncbw * sizeof(uint32_t)));
+        d->d_cbw_cap = ncbw * sizeof(uint32_t);
     }
     hipLaunchKernelGGL(gss_cbw_kernel, dim3((unsigned)((ncbw + 255) / 256)), dim3(256), 0, st,
                        ca_bits, n_ca, d->d_cbw);

@@ -10,7 +10,7 @@
  *     carrier  X(p) = rnd(carr0 2^64) + p rnd(carr_step 2^64)  mod 2^64,  LUT cell X >> 55
  *     code     Z(p) = rnd(code0 2^50) + p rnd(code_step 2^50),            chip (Z >> 50) mod 1023
  * The kernel renders from chunk anchors of these lines plus 32-bit steps (gss_lin.h: the
- * kernel's cell and chip at sample p are gss_lin_kcell / gss_lin_kchip, within
+ * kernel's cell and chip at sample p are gss_lin_kernel_at, within
  * GSS_LIN_KDEV_* of the lines).  This file proves, with exact integer arithmetic, at which samples
  * the kernel could read another LUT cell or chip sign than the reference's doubles, decides those
  * samples exactly and, where the kernel's term differs, stores the difference as a patch
@@ -23,7 +23,7 @@
  *      less than 2^12 units of 2^-64 cycle (2^7 units of 2^-50 chip) per sample, and the line by
  *      the step plus at most half a unit: |line - exact| <= D1 = 2 + n (err + 1) over the block,
  *      about 2^-34 cycle and 2^-25 chip for a 0.1 s block at 2.6 MS/s.  |kernel - line| <= D2
- *      (GSS_LIN_KDEV_*: 2^-28 cycle, 2^-28 chip).
+ *      (GSS_LIN_KDEV_*: about 2^-30 cycle and 2^-21 chip).
  *   2. The exact value, the line and the kernel can fall into different cells only where the line
  *      lies within D = D1 + D2 of a cell boundary (a multiple of B = 2^55, resp. 2^50):
  *      (line(p) + D) mod B < 2 D.  These samples are enumerated exactly: gss_minmod computes the
@@ -249,10 +249,9 @@ static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
     const int64_t Z0 = (int64_t)to_fix(c0, 50, &inexact);
     const int64_t ZS = (int64_t)to_fix(cs, 50, &inexact);
     const int64_t per = (int64_t)GSS_CA_LEN << LIN_CODE_LGB;
-    /* the kernel reads a 64-chip window per two 64-sample steps, starting up to 3 chips below
-       lane 0's chip: 127 steps + 4 chips <= 64 */
-    if (ZS <= 0 || Z0 >= per ||
-        ZS * 127 + ((int64_t)4 << LIN_CODE_LGB) > ((int64_t)64 << LIN_CODE_LGB))
+    /* the kernel reads one 32-chip window per 64-sample step, starting up to 2 chips below
+       lane 0's chip (gss_lin.h) */
+    if (ZS <= 0 || Z0 >= per || !GSS_LIN_WIN_OK((uint64_t)ZS))
         return 0;
     const int nhz = ambiguous(Z0, ZS, 2 + (i128)n * (LIN_CODE_ERR + 1) + GSS_LIN_KDEV_CODE,
                               LIN_CODE_LGB, n, hz, LIN_MAXHIT);
@@ -345,8 +344,9 @@ static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
             chip = (int)floor(at_hz[j].ph);
         else
             chip = (int)(((Z0 + (i128)q * ZS) >> LIN_CODE_LGB) % GSS_CA_LEN);
-        const int kcell = gss_lin_kcell((uint64_t)X0, (uint64_t)XS, q);
-        const int kchip = gss_lin_kchip((uint64_t)Z0, (uint64_t)ZS, q);
+        const gss_lin_kc kk = gss_lin_kernel_at((uint64_t)X0, (uint64_t)XS, (uint64_t)Z0,
+                                                 (uint64_t)ZS, q);
+        const int kcell = kk.cell, kchip = kk.chip;
         const int64_t te = ca_sign(ca, chip) * lut_packed(cell);
         const int64_t tk = ca_sign(ca, kchip) * lut_packed(kcell);
         if (te == tk)

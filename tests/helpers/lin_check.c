@@ -1,6 +1,6 @@
 /* Test-only harness: renders blocks from the certified integer lines (gss_lin_t) with scalar C,
    exactly the arithmetic the GPU fast path (gss_lin_kernel) performs: the kernel's LUT cell and
-   chip at each sample (gss_lin_kcell / gss_lin_kchip, csrc/common/gss_lin.h: chunk anchors plus
+   chip at each sample (gss_lin_kernel_at, csrc/common/gss_lin.h: chunk anchors plus
    32-bit steps), the signed gain from the schedule, the packed I/Q accumulator
    (64 + 2^21) + 2^22 (64 + ...) and the patch corrections.  tests/test_linearize.py compares its
    bytes with the scalar oracle of the reference loop (oracle/synth_oracle.c) on every block
@@ -29,8 +29,8 @@ int lc_render(const gss_chan_blk_t *blk, const int32_t *nch, const gss_lin_t *li
             for (int k = 0; k < nch[b]; k++) {
                 const gss_lin_t *l = &lin[(size_t)b * GSS_MAXCH + k];
                 const gss_chan_blk_t *c = &blk[(size_t)b * GSS_MAXCH + k];
-                const int ti = gss_lin_kcell(l->x0, l->xs, p);
-                const int chip = gss_lin_kchip(l->z0, l->zs, p);
+                const gss_lin_kc kk = gss_lin_kernel_at(l->x0, l->xs, l->z0, l->zs, p);
+                const int ti = kk.cell, chip = kk.chip;
                 const int ca = ca_chip(ca_bits + (size_t)c->ca_tbl * GSS_CA_WORDS, chip) * 2 - 1;
                 int g = l->gval[0];
                 for (int i = 1; i < GSS_NGC; i++)

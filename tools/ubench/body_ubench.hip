@@ -8,11 +8,24 @@
 //           addr = alignbit(t, X, 21) & 0xFFC into a 1024-entry LUT (second half negated)
 //   cnd   : as alb but the chip sign selects the signed gain with v_cndmask (sign mask from
 //           v_cmp on t), LUT address from X alone
+//   sdw   : X 32-bit, code C 32-bit 8.24 (byte 3 = chip mod 256), one rotated 32-bit window per
+//           step in an SGPR (scalar running byte offset, 2 SALU per step), t = W >> byte3(C) by
+//           SDWA, addr = alignbit(t, X, 21) & M with M, dX, dC, g in VGPRs (all-VGPR VOP2 forms)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
 
 #define NSTEP 16
+/* scalar buffer load with an SGPR byte offset (SMEM), seen by the compiler's lgkmcnt tracking */
+typedef int gss_v4i __attribute__((ext_vector_type(4)));
+extern "C" __device__ int gss_s_buffer_load_i32(gss_v4i, int, int)
+    __asm("llvm.amdgcn.s.buffer.load.i32");
+__device__ inline gss_v4i gss_rsrc(const void *p, uint32_t bytes)
+{
+    const uint64_t a = (uint64_t)p;
+    gss_v4i r = {(int)(uint32_t)a, (int)(uint32_t)(a >> 32) & 0xFFFF, (int)bytes, 0x00020000};
+    return r;
+}
 #define NCH 12
 
 template <int V>
@@ -48,6 +61,32 @@ __global__ __launch_bounds__(256) void body(const uint64_t *__restrict__ tab, co
                         acc[s + ss] += (int64_t)g * e;
                         X += dX; Z += dZ;
                     }
+                }
+            } else if (V == 3) {
+                uint32_t X = (uint32_t)((x0 + lane * xs) >> 32);
+                uint32_t C = (uint32_t)((z0 + lane * zs) >> 26);
+                uint32_t dX = (uint32_t)((xs << 6) >> 32), dC = (uint32_t)((zs << 6) >> 26);
+                uint32_t M = 0xFFCu;
+                int gv = g;
+                asm volatile("" : "+v"(dX), "+v"(dC), "+v"(M), "+v"(gv));
+                const gss_v4i rs = gss_rsrc(T, 3136 * 8);
+                uint32_t Qb = (uint32_t)__builtin_amdgcn_readfirstlane(C >> 20) & 0x3ffcu;
+                const uint32_t dq = __builtin_amdgcn_readfirstlane((uint32_t)((zs << 6) >> 46));
+                uint32_t W[NSTEP];
+#pragma unroll
+                for (int s = 0; s < NSTEP; s++) {
+                    W[s] = (uint32_t)gss_s_buffer_load_i32(rs, (int)Qb, 0);
+                    Qb += dq;
+                }
+#pragma unroll
+                for (int s = 0; s < NSTEP; s++) {
+                    uint32_t t;
+                    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD "
+                        "src0_sel:BYTE_3 src1_sel:DWORD" : "=v"(t) : "v"(C), "s"(W[s]));
+                    const uint32_t a = __builtin_amdgcn_alignbit(t, X, 21) & M;
+                    const int32_t e = *(const int32_t *)((const char *)lut + a);
+                    acc[s] += (int64_t)gv * e;
+                    X += dX; C += dC;
                 }
             } else {
                 uint32_t X = (uint32_t)((x0 + lane * xs) >> 32);
@@ -98,10 +137,10 @@ int main()
     const int grid = 256 * 8 * 4;       /* 8 waves/SIMD resident x 4 rounds */
     (void)hipMalloc(&out, (size_t)grid * 256 * 8);
     const int chunks = 32;
-    const char *names[] = {"cur", "alb", "cnd"};
-    for (int v = 0; v < 3; v++) {
+    const char *names[] = {"cur", "alb", "cnd", "sdw"};
+    for (int v = 0; v < 4; v++) {
         void (*f)(const uint64_t *, const uint64_t *, int64_t *, int) =
-            v == 0 ? body<0> : v == 1 ? body<1> : body<2>;
+            v == 0 ? body<0> : v == 1 ? body<1> : v == 2 ? body<2> : body<3>;
         hipLaunchKernelGGL(f, grid, 256, 0, 0, tab, prm, out, chunks);
         hipEvent_t a, b; (void)hipEventCreate(&a); (void)hipEventCreate(&b);
         (void)hipEventRecord(a);

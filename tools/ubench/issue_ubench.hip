@@ -80,6 +80,45 @@ KERN(mix_add_mad,
      asm volatile("v_add_u32 %0, %0, %10\n v_mad_i64_i32 %4, vcc, %10, %10, %4\n v_add_u32 %1, %1, %10\n v_mad_i64_i32 %5, vcc, %10, %10, %5\n v_add_u32 %2, %2, %10\n v_mad_i64_i32 %6, vcc, %10, %10, %6\n v_add_u32 %3, %3, %10\n v_mad_i64_i32 %7, vcc, %10, %10, %7"
                   : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]) : "v"(u[4]), "v"(u[5]), "v"(sc) : "vcc");)
 
+
+// round 3 candidates: a 32-bit window shift taking the chip from byte 3 of a 32-bit code
+// accumulator (SDWA), shifts with the value in an SGPR, VOP2 carry adds, dot2c, MFMA issue cost
+#define OP_S(fmt) \
+    asm volatile(fmt(0) "\n" fmt(1) "\n" fmt(2) "\n" fmt(3) "\n" fmt(4) "\n" fmt(5) "\n" fmt(6) "\n" fmt(7) \
+                 : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]),       \
+                   "+v"(u[6]), "+v"(u[7]) : "s"(sc));
+#define F_LSHR_E64(i) "v_lshrrev_b32_e64 %" #i ", %" #i ", %8"
+#define F_LSHR_SDWA(i) "v_lshrrev_b32_sdwa %" #i ", %" #i ", %8 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+#define F_ADD_SDWA(i) "v_add_u32_sdwa %" #i ", %" #i ", %8 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+#define F_ADDCO(i) "v_add_co_u32 %" #i ", vcc, %8, %" #i
+#define F_DOT2C(i) "v_dot2c_f32_f16 %" #i ", %8, %" #i
+#define F_ALIGN_S(i) "v_alignbit_b32 %" #i ", %8, %" #i ", 21"
+KERN(lshr_e64_s, OP_S(F_LSHR_E64))
+KERN(lshr_sdwa_s, OP_S(F_LSHR_SDWA))
+KERN(add_sdwa_s, OP_S(F_ADD_SDWA))
+KERN(add_co_vop2, asm volatile(F_ADDCO(0) "\n" F_ADDCO(1) "\n" F_ADDCO(2) "\n" F_ADDCO(3) "\n" F_ADDCO(4) "\n" F_ADDCO(5) "\n" F_ADDCO(6) "\n" F_ADDCO(7)
+                          : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]) : "s"(sc) : "vcc");)
+KERN(dot2c_f32_f16, asm volatile(F_DOT2C(0) "\n" F_DOT2C(1) "\n" F_DOT2C(2) "\n" F_DOT2C(3) "\n" F_DOT2C(4) "\n" F_DOT2C(5) "\n" F_DOT2C(6) "\n" F_DOT2C(7)
+                            : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]) : "v"(sc));)
+KERN(alignbit_s, OP_S(F_ALIGN_S))
+KERN(lshrrev_b64_s,
+     asm volatile("v_lshrrev_b64 %0, %8, %16\n v_lshrrev_b64 %1, %9, %16\n v_lshrrev_b64 %2, %10, %16\n v_lshrrev_b64 %3, %11, %16\n v_lshrrev_b64 %4, %12, %16\n v_lshrrev_b64 %5, %13, %16\n v_lshrrev_b64 %6, %14, %16\n v_lshrrev_b64 %7, %15, %16"
+                  : "=v"(d[0]), "=v"(d[1]), "=v"(d[2]), "=v"(d[3]), "=v"(d[4]), "=v"(d[5]), "=v"(d[6]), "=v"(d[7])
+                  : "v"(u[0]), "v"(u[1]), "v"(u[2]), "v"(u[3]), "v"(u[4]), "v"(u[5]), "v"(u[6]), "v"(u[7]), "s"((uint64_t)sc * 7u));
+     _Pragma("unroll") for (int i = 0; i < 8; i++) u[i] ^= (uint32_t)d[i];)
+KERN(mov_b64,
+     asm volatile("v_mov_b64 %0, %8\n v_mov_b64 %1, %8\n v_mov_b64 %2, %8\n v_mov_b64 %3, %8\n v_mov_b64 %4, %8\n v_mov_b64 %5, %8\n v_mov_b64 %6, %8\n v_mov_b64 %7, %8"
+                  : "=v"(d[0]), "=v"(d[1]), "=v"(d[2]), "=v"(d[3]), "=v"(d[4]), "=v"(d[5]), "=v"(d[6]), "=v"(d[7]) : "s"((uint64_t)sc * 5u));)
+// 8 VOP2 adds plus 2 independent MFMA 4x4x4 (16 blocks) per group: the MFMAs' issue cost over add_u32
+typedef float f4_t __attribute__((ext_vector_type(4)));
+#define MFMA_BODY \
+     f4_t a0 = {f[0][0], f[0][1], f[1][0], f[1][1]}; f4_t a1 = {f[2][0], f[2][1], f[3][0], f[3][1]}; \
+     asm volatile("v_add_u32 %0, %0, %12\n v_mfma_f32_4x4x4_16b_f16 %8, %10, %11, %8\n v_add_u32 %1, %1, %12\n v_add_u32 %2, %2, %12\n v_add_u32 %3, %3, %12\n v_mfma_f32_4x4x4_16b_f16 %9, %11, %10, %9\n v_add_u32 %4, %4, %12\n v_add_u32 %5, %5, %12\n v_add_u32 %6, %6, %12\n v_add_u32 %7, %7, %12" \
+                  : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]), "+v"(a0), "+v"(a1) \
+                  : "v"(d[0]), "v"(d[1]), "v"(sc)); \
+     f[0][0] = a0[0] + a1[3]; f[1][1] = a0[2] + a1[1];
+KERN(mix_add_mfma4, MFMA_BODY)
+
 typedef void (*kfn)(uint32_t *, long long *);
 static void run(const char *name, kfn f)
 {
@@ -109,5 +148,7 @@ int main()
     RUN(alignbit) RUN(bfe_u32) RUN(and_or) RUN(lshl_add_u32) RUN(perm_b32) RUN(add3_u32)
     RUN(lshl_add_u64) RUN(add_co_pair) RUN(lshrrev_b64) RUN(mad_i64_i32) RUN(mad_u32_u24)
     RUN(pk_add_f32) RUN(dot2_i32_i16) RUN(cndmask) RUN(mix_add_mad)
+    RUN(lshr_e64_s) RUN(lshr_sdwa_s) RUN(add_sdwa_s) RUN(add_co_vop2) RUN(dot2c_f32_f16)
+    RUN(alignbit_s) RUN(lshrrev_b64_s) RUN(mov_b64) RUN(mix_add_mfma4)
     return 0;
 }
