@@ -116,8 +116,10 @@ def lib_sha16(path):
 
 def load_traffic(workload, kernel, kern_ms, lib_sha):
     """HBM bytes per launch of `kernel` from the PMC passes (profiles/pmc_traffic.json), only
-    when they were taken on this workload and this kernel build (same library sha256, average
-    kernel time within 5 % of this run's)"""
+    when they were taken on this workload and this kernel build (same library sha256).  Bytes
+    per launch do not depend on the box's speed; the profiled run's kernel time (a few % slower
+    under rocprofv3, and boxes differ) only has to be within 25 % of this run's as a sanity
+    check, and is reported beside it."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
@@ -128,9 +130,9 @@ def load_traffic(workload, kernel, kern_ms, lib_sha):
     if d.get("lib_sha16") != lib_sha:
         return None, "profile of another build"
     prof_ms = (d.get("kernel_avg_ns") or 0) / 1e6
-    if kern_ms <= 0 or abs(prof_ms - kern_ms) > 0.05 * kern_ms:
+    if kern_ms <= 0 or abs(prof_ms - kern_ms) > 0.25 * kern_ms:
         return None, f"profile kernel time {prof_ms:.3f} ms vs {kern_ms:.3f} ms here"
-    return d.get("hbm_bytes_per_launch"), d.get("source")
+    return d.get("hbm_bytes_per_launch"), f"{d.get('source')}; profiled kernel {prof_ms:.3f} ms"
 
 
 def time_steps(torch, dev, dev_t, res, steps, warmup, stream):

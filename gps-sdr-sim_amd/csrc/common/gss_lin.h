@@ -9,21 +9,25 @@
  * (linearize.c proves how close they stay to the reference's double recurrences,
  * gpssim.c:2212-2250).  The kernel does not evaluate them at every sample.  Samples are grouped
  * in chunks of GSS_LIN_CHUNK (block-relative, aligned), a chunk in GSS_LIN_CH steps of 64 (lane l
- * of step s renders sample p = c + 64 s + l), and each lane keeps carrier and code in ONE 64-bit
- * register P (carrier in the low word, 2^-32 cycle; code in the high word, 8.24 fixed point with
- * byte 3 = chip mod 256) that advances by one 64-bit add per step:
+ * of step s renders sample p = c + 64 s + l), and each lane keeps code and carrier in ONE 64-bit
+ * register P (code in the low word, 8.24 fixed point with byte 3 = chip mod 256; carrier in the
+ * high word, 2^-32 cycle) that advances by one 64-bit add per step:
  *   anchor   P(c, l) = B(c) + L(l)  mod 2^64, from the chunk's base and the lane's offset
- *              B = lo32((Z(c) + 2^25) >> 26) : hi32(X(c) + A)
- *              L = lo32((l zs) >> 26)        : hi32(l xs + 2^31)
- *   step     P += dC : dX,   dX = hi32(64 xs + 2^31) [2^-32 cycle],
+ *              B = hi32(X(c) + A) : lo32((Z(c) + Ac) >> 26)
+ *              L = hi32(l xs + 2^31) : lo32((l zs) >> 26)
+ *   step     P += dX : dC,   dX = hi32(64 xs + 2^31) [2^-32 cycle],
  *                            dC = (64 zs + 2^25) >> 26 [2^-24 chip]
- *            A = 2^31 - (GSS_LIN_CH - 1) e / 2 centres the carrier steps' error
- *            e = dX 2^32 - 64 xs.
- *   LUT cell = low word >> 23;  chip = (unwrapped high word >> 24) mod 1023, where every carry
- *   out of the low word (at the anchor add and at each step) adds 2^-24 chip to the code.
- * Each rounding is at most one unit and the carries only add, so the carrier is within
- * (GSS_LIN_CH/2 + 3) 2^31 and the code within 3 GSS_LIN_CH 2^25 of the lines (GSS_LIN_KDEV_*,
- * 2^-64 cycle and 2^-50 chip); the proof adds these to its own line-versus-reference bound.
+ *            A = 2^31 - (GSS_LIN_CH - 1) e / 2 and Ac = 2^25 - (GSS_LIN_CH - 1) ec / 2 centre
+ *            the steps' errors e = dX 2^32 - 64 xs and ec = dC 2^26 - 64 zs.
+ *   Z(c) is the code line reduced at its wave segment's start (GSS_LIN_SEG samples, aligned)
+ *   to the chip there mod 1023 (1023 for chip 0: gss_lin_e0), plus the fraction.
+ *   LUT cell = high word >> 23, where every carry out of the low word (at the anchor add and at
+ *   each step, one per 256 chips) adds 2^-32 cycle to the carrier; chip = (unwrapped low word
+ *   >> 24) mod 1023.
+ * Each rounding is at most one unit (half a unit where rounded to nearest) and the carries only
+ * add, so the carrier is within (GSS_LIN_CH/2 + 3) 2^31 + (2 + (GSS_LIN_CH - 1) dC / 2^32) 2^32
+ * and the code within (GSS_LIN_CH/2 + 3) 2^25 of the lines (GSS_LIN_KDEV_*, 2^-64 cycle and 2^-50 chip); the
+ * proof adds these to its own line-versus-reference bound.
  * The kernel reads each step's chip sign from a 32-chip window (gss_lin_kernel): every lane's
  * chip of one step must lie in it, which linearize.c checks as 63 zs + 3 chips <= 31
  * (GSS_LIN_WIN_OK).
@@ -37,6 +41,8 @@
 #define GSS_LIN_CH     16                      /* 64-sample steps per chunk                   */
 #endif
 #define GSS_LIN_CHUNK  (64 * GSS_LIN_CH)       /* samples per chunk (block-relative, aligned) */
+#define GSS_LIN_SEG    4096                    /* samples per wave segment: the code line is
+                                                  taken mod 1023 chips at each segment start   */
 
 #if defined(__HIPCC__)
 #define GSS_LIN_FN static __host__ __device__ inline
@@ -57,20 +63,38 @@ GSS_LIN_FN uint64_t gss_lin_xa(uint64_t xs)
     const int64_t e = (int64_t)(((uint64_t)gss_lin_dx(xs) << 32) - xs * 64u);
     return (1ull << 31) - (uint64_t)((e * (GSS_LIN_CH - 1)) / 2);
 }
+/* the code's anchor offset Ac (rounding and centring), added to Z(c) before >> 26 */
+GSS_LIN_FN uint64_t gss_lin_za(uint64_t zs)
+{
+    const int64_t ec = (int64_t)(((uint64_t)gss_lin_dz(zs) << GSS_LIN_CSH) - zs * 64u);
+    return (1ull << (GSS_LIN_CSH - 1)) - (uint64_t)((ec * (GSS_LIN_CH - 1)) / 2);
+}
+
+/* the chip the code line is reduced to at a segment start: the chip there mod 1023, taken as 1023
+   for chip 0 so that the (possibly negative) anchor offset keeps the reduced line positive */
+GSS_LIN_FN uint32_t gss_lin_e0(uint64_t chips)
+{
+    const uint32_t e = (uint32_t)(chips % 1023u);
+    return e ? e : 1023u;
+}
 
 /* worst-case distance of the kernel's values from the lines, in line units (2^-64 cycle,
    2^-50 chip) */
-#define GSS_LIN_KDEV_CARR (((uint64_t)GSS_LIN_CH / 2 + 3) << 31)
-#define GSS_LIN_KDEV_CODE ((uint64_t)(3 * GSS_LIN_CH) << (GSS_LIN_CSH - 1))
+/* carrier: roundings plus the carries of the code word, at most one at the anchor and one per
+   2^32 of code advance over the chunk's steps (zs: the code line's step, 2^-50 chip per sample) */
+#define GSS_LIN_KDEV_CARR(zs)                                                                      \
+    ((((uint64_t)GSS_LIN_CH / 2 + 3) << 31) +                                                     \
+     ((2 + (((uint64_t)gss_lin_dz(zs) * (GSS_LIN_CH - 1)) >> 32)) << 32))
+#define GSS_LIN_KDEV_CODE (((uint64_t)GSS_LIN_CH / 2 + 3) << (GSS_LIN_CSH - 1))
 /* the 32-chip step window holds every lane's chip (zs in 2^-50 chip per sample, < 1 chip) */
 #define GSS_LIN_WIN_OK(zs) ((zs) * 63u + (3ull << 50) <= (31ull << 50))
 
-/* the lane offset L(l) of gss_lin.h: code word (high) and carrier word (low) */
+/* the lane offset L(l) of gss_lin.h: carrier word (high) and code word (low) */
 GSS_LIN_FN uint64_t gss_lin_lane(uint64_t xs, uint64_t zs, uint32_t l)
 {
     const uint32_t lx = (uint32_t)(((uint64_t)l * xs + (1ull << 31)) >> 32);
     const uint32_t lz = (uint32_t)(((uint64_t)l * zs) >> GSS_LIN_CSH);
-    return ((uint64_t)lz << 32) | lx;
+    return ((uint64_t)lx << 32) | lz;
 }
 
 #if !defined(__HIP_DEVICE_COMPILE__)
@@ -85,16 +109,23 @@ GSS_LIN_FN gss_lin_kc gss_lin_kernel_at(uint64_t x0, uint64_t xs, uint64_t z0, u
     const int64_t c = p & ~(int64_t)(GSS_LIN_CHUNK - 1);
     const int64_t l = p & 63, s = (p - c) >> 6;
     const uint64_t lane = gss_lin_lane(xs, zs, (uint32_t)l);
+    /* code: the low word, unwrapped (no carries in), from the line reduced at the segment start */
+    const int64_t n0 = p & ~(int64_t)(GSS_LIN_SEG - 1);
+    const unsigned __int128 zn = (unsigned __int128)z0 + (unsigned __int128)(uint64_t)n0 * zs;
+    const int64_t chips = (int64_t)(zn >> 50), e0 = gss_lin_e0((uint64_t)chips);
+    const __int128 z = (__int128)z0 + (__int128)c * (__int128)zs - ((__int128)(chips - e0) << 50);
+    const unsigned __int128 zk = (unsigned __int128)((z + (int64_t)gss_lin_za(zs)) >> GSS_LIN_CSH);
+    const uint64_t za = (uint64_t)(uint32_t)zk + (uint32_t)lane;       /* anchor add, carry */
+    const uint64_t zw = (uint64_t)(uint32_t)za + (uint64_t)s * gss_lin_dz(zs);   /* low word */
+    const unsigned __int128 kz = zk + (uint32_t)lane + (unsigned __int128)(uint64_t)s *
+                                 gss_lin_dz(zs);
+    /* carrier: the high word plus the low word's carries */
     const uint32_t xb = (uint32_t)((x0 + (uint64_t)c * xs + gss_lin_xa(xs)) >> 32);
-    const uint64_t xa = (uint64_t)xb + (uint32_t)lane;         /* anchor add, with its carry */
-    const uint64_t xk = (uint64_t)(uint32_t)xa + (uint64_t)s * gss_lin_dx(xs);
-    const unsigned __int128 z = (unsigned __int128)z0 + (unsigned __int128)(uint64_t)c * zs;
-    const unsigned __int128 k = ((z + (1u << (GSS_LIN_CSH - 1))) >> GSS_LIN_CSH) +
-                                (lane >> 32) + (xa >> 32) +
-                                (unsigned __int128)(uint64_t)s * gss_lin_dz(zs) + (xk >> 32);
+    const uint32_t xk = xb + (uint32_t)(lane >> 32) + (uint32_t)(za >> 32) +
+                        (uint32_t)s * gss_lin_dx(xs) + (uint32_t)(zw >> 32);
     gss_lin_kc r;
-    r.cell = (int)((uint32_t)xk >> 23);
-    r.chip = (int)((uint64_t)(k >> 24) % 1023u);
+    r.cell = (int)(xk >> 23);
+    r.chip = (int)((uint64_t)(kz >> 24) % 1023u);
     return r;
 }
 #endif

@@ -485,11 +485,11 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
    A wave renders one 4096-sample segment in chunks of LIN_CH steps.  Per chunk, the wave's
    lanes first build every channel's parameters in parallel (lin_ct in LDS: the chunk base, the
    step, the gain, and the 16 chip windows from vector loads of the window table); then, channel
-   by channel, each lane forms its anchor P (carrier in the low word, code in the high word,
+   by channel, each lane forms its anchor P (code in the low word, carrier in the high word,
    gss_lin.h) with one 64-bit add of the base to its entry of the workgroup's lane table (LDS),
    and per 64-sample step
-       t = W_s >> byte3(P.hi)  chip sign at bit 0, from the step's window       v_lshrrev_b32_sdwa
-       a = alignbit(t, P.lo, 21) & M   LUT byte address: cell (carrier bits 23..31) at bits
+       t = W_s >> byte3(P.lo)  chip sign at bit 0, from the step's window       v_lshrrev_b32_sdwa
+       a = alignbit(t, P.hi, 21) & M   LUT byte address: cell (carrier bits 23..31) at bits
                                     2..10, chip sign at bit 11 (second half of the LUT negated)
        acc += g * LUT[a]       packed I/Q                                       v_mad_i64_i32
        P += D                  carrier and code together                        v_lshl_add_u64
@@ -497,25 +497,27 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
    without any memory access the kernel still takes 75-80 % of its time, and the scalar unit,
    one per CU for four SIMDs, was the next limit once the loop lost its 64-bit code add (the
    per-channel scalar work of a chunk, ~90 instructions, cost more than the steps' VALU).  So the
-   code is a 32-bit word beside the carrier (a carry out of the carrier adds 2^-24 chip, which the
-   render model counts), and everything wave-uniform that used to be scalar per channel is built
+   code is a 32-bit word beside the carrier (a carry out of the code word adds 2^-32 cycle to the
+   carrier, which the render model counts), and everything wave-uniform that used to be scalar per channel is built
    once per chunk by the lanes in parallel.
-   Chip windows (table cbw, one row per C/A table row, 4 entries per chip): entry q holds the 32
-   chips from extended chip E = q/4 - CBW_PRE on, rotated (bit e mod 32 = sign of chip e mod 1023,
-   1 = negative), so that any lane whose chip e lies in [E, E + 32) takes its sign with a shift by
-   e mod 32 = byte 3 of the code word mod 32.  Step s reads entry floor(Q_s/4), Q_s = Q_0 + s dq
+   Chip windows: the window of extended chip E holds the 32 chips from E on, rotated (bit e mod 32
+   = sign of chip e mod 1023, 1 = negative), so that any lane whose chip e lies in [E, E + 32)
+   takes its sign with a shift by e mod 32 = byte 3 of the code word mod 32.  Lanes build them in
+   the chunk's parameter pass from the channel's sign bit-stream (table cab: one row of CAB_W words
+   per C/A table row, bit j = sign of extended chip j - 32, copied to LDS per workgroup): two LDS
+   words and two alignbits (extract the 32 bits at E, rotate by E mod 32).  Step s reads entry floor(Q_s/4), Q_s = Q_0 + s dq
    in 1/16 chip (Q_0 1/16 below lane 0's first chip, dq = floor(64 zs / 2^46)).  The window then
    starts at most two chips below lane 0's chip and every lane's chip of the step lies inside it
    when 63 zs + 3 chips <= 31 (GSS_LIN_WIN_OK, checked by gss_linearize); the index is clamped to
    the row, which a certified channel never needs. */
 #define LIN_THREADS 256
 #define LIN_WAVES   (LIN_THREADS / 64)
-#define LIN_STEPS   64                     /* 64-sample steps per wave segment: 4096 samples    */
+#define LIN_STEPS   (GSS_LIN_SEG / 64)     /* 64-sample steps per wave segment: 4096 samples    */
 #define LIN_CH      GSS_LIN_CH             /* steps per chunk (one accumulator each)            */
-#define CBW_PRE     2                      /* chips of windows kept below extended chip 0       */
-#define CBW_CHIPS   3072                   /* window starts per row: E0 <= 1022 plus a segment's
+#define CBW_PRE     2                      /* a window starts at most this far below chip 0      */
+#define CBW_CHIPS   3072                   /* window starts per row: E0 <= 1023 plus a segment's
                                               reach (4160 samples * 0.46 chip) plus a window     */
-#define CBW_ROW     (4 * (CBW_CHIPS + CBW_PRE))     /* entries (32-bit) per row            */
+#define CAB_W       ((CBW_CHIPS + 96) / 32)    /* sign words per row: chips -32 .. CBW_CHIPS + 63 */
 static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole chunks");
 /* LIN_ABLATE (measurement builds only, tools/ablate.sh; wrong output): 1 no output stores,
    2 no chip-window loads, 4 no LUT reads, 8 every block stores into one of 8 blocks (L2),
@@ -542,16 +544,16 @@ struct lin_ct {
 /* per (block, channel): the render constants of gss_lin.h (written by gss_linseg_kernel) */
 struct lin_chan {
     uint64_t xs, zs;             /* the lines' per-sample steps                                 */
-    uint64_t d;                  /* the 64-sample step dC : dX of P (gss_lin_dz : gss_lin_dx)    */
+    uint64_t d;                  /* the 64-sample step dX : dC of P (gss_lin_dx : gss_lin_dz)    */
     uint32_t dq;                 /* window offset advance per step, 1/16 chip, rounded down      */
-    uint32_t tab;                /* byte offset of the channel's window row                      */
+    uint32_t tab;                /* the channel's C/A table row                                  */
 };
 /* per (block, channel, wave segment of 64*LIN_STEPS samples): the lines at the segment start,
    so that the render kernel needs no 128-bit arithmetic and no schedule search */
 struct lin_seg {
     uint64_t x;                  /* X(n0) + gss_lin_xa(xs): the first chunk's carrier anchor base */
-    uint64_t z;                  /* ((E0 << 50) | fraction) + 2^25: the first chunk's code anchor
-                                    base, E0 = chip at the segment start mod 1023               */
+    uint64_t z;                  /* ((E0 << 50) | fraction) + gss_lin_za(zs): the first chunk's
+                                    code anchor base, E0 = gss_lin_e0(chip at the segment start) */
     int32_t g01;                 /* signed gain at the start (low 16) and after pos1 (high 16)   */
     int32_t pos1;                /* sample of the first gain change in the segment, or INT32_MAX */
     uint32_t npatch;             /* patched samples of the channel inside the segment            */
@@ -576,17 +578,17 @@ __global__ void gss_linseg_kernel(const gss_lin_t *__restrict__ lin,
         lin_chan c;
         c.xs = L->xs;
         c.zs = L->zs;
-        c.d = ((uint64_t)gss_lin_dz(L->zs) << 32) | gss_lin_dx(L->xs);
+        c.d = ((uint64_t)gss_lin_dx(L->xs) << 32) | gss_lin_dz(L->zs);
         c.dq = (uint32_t)((L->zs * 64u) >> 46);
-        c.tab = (uint32_t)((size_t)blk[bk].ca_tbl * CBW_ROW * sizeof(uint32_t));
+        c.tab = (uint32_t)blk[bk].ca_tbl;
         chan_out[bk] = c;
     }
     const uint64_t n0 = (uint64_t)sg * (64 * LIN_STEPS);
     const uint64_t lo = L->z0 + n0 * L->zs;
     const uint64_t hi = __umul64hi(n0, L->zs) + (lo < L->z0 ? 1u : 0u);
-    const uint32_t E0 = ((uint32_t)(hi << 14) | (uint32_t)(lo >> 50)) % (uint32_t)GSS_CA_LEN;
+    const uint32_t E0 = gss_lin_e0((hi << 14) | (lo >> 50));
     lin_seg r;
-    r.z = (((uint64_t)E0 << 50) | (lo & ((1ull << 50) - 1))) + (1ull << (GSS_LIN_CSH - 1));
+    r.z = (((uint64_t)E0 << 50) | (lo & ((1ull << 50) - 1))) + gss_lin_za(L->zs);
     r.x = L->x0 + n0 * L->xs + xa;
     int q = 0;
     while (q + 1 < GSS_NGC && L->gpos[q + 1] <= (int)n0)
@@ -604,27 +606,26 @@ __global__ void gss_linseg_kernel(const gss_lin_t *__restrict__ lin,
     seg_out[i] = r;
 }
 
-/* per C/A row, the rotated 32-chip windows, 4 entries per chip: entry q starts at extended chip
-   E = q/4 - CBW_PRE */
-__global__ void gss_cbw_kernel(const uint32_t *__restrict__ ca_bits, int n_ca,
-                               uint32_t *__restrict__ cbw)
+/* per C/A row, the chip-sign bit-stream extended cyclically: bit j of the row = sign of extended
+   chip j - 32 (chip (j - 32) mod 1023, 1 = codeCA -1) */
+__global__ void gss_cab_kernel(const uint32_t *__restrict__ ca_bits, int n_ca,
+                               uint32_t *__restrict__ cab)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_ca * CBW_ROW)
+    if (i >= n_ca * CAB_W)
         return;
-    const int row = i / CBW_ROW, E = (i - row * CBW_ROW) / 4 - CBW_PRE;
+    const int row = i / CAB_W, j0 = (i - row * CAB_W) * 32 - 32;
     const uint32_t *cb = ca_bits + (size_t)row * GSS_CA_WORDS;
     uint32_t w = 0;
     for (int q = 0; q < 32; q++) {
-        const int e = E + q, chip = ((e % GSS_CA_LEN) + GSS_CA_LEN) % GSS_CA_LEN;
-        const uint32_t neg = ((cb[chip >> 5] >> (chip & 31)) & 1u) ^ 1u;   /* codeCA = -1 */
-        w |= neg << (e & 31);
+        const int e = j0 + q, chip = ((e % GSS_CA_LEN) + GSS_CA_LEN) % GSS_CA_LEN;
+        w |= (((cb[chip >> 5] >> (chip & 31)) & 1u) ^ 1u) << q;
     }
-    cbw[i] = w;
+    cab[i] = w;
 }
 
 /* one channel's contribution to the chunk's LIN_CH steps: the lane's anchor P (carrier : code,
-   gss_lin.h) and its 64-sample step D, the steps' chip windows (LDS, the same for every lane),
+   high : low word, gss_lin.h) and its 64-sample step D, the steps' chip windows (LDS, the same for every lane),
    the LUT mask M, the signed gain (with LANE_GAIN: the gain difference, applied from sample
    pos1 on) */
 #define LIN_ACC0 (64 + (1 << 21) + ((int64_t)64 << 22))   /* (0 + 64 + 2^21) + 2^22 (0 + 64) */
@@ -646,8 +647,8 @@ __device__ __forceinline__ void lin_channel_chunk(int64_t (&acc)[LIN_CH], uint64
         const uint32_t ws = s % 4 == 0 ? w4.x : s % 4 == 1 ? w4.y : s % 4 == 2 ? w4.z : w4.w;
         uint32_t t;
         asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
-            "src1_sel:DWORD" : "=v"(t) : "v"((uint32_t)(P >> 32)), "v"(ws));     /* bit 0: sign */
-        const uint32_t a = ((LIN_ABLATE & 32) ? t : __builtin_amdgcn_alignbit(t, (uint32_t)P, 21)) & M;
+            "src1_sel:DWORD" : "=v"(t) : "v"((uint32_t)P), "v"(ws));             /* bit 0: sign */
+        const uint32_t a = ((LIN_ABLATE & 32) ? t : __builtin_amdgcn_alignbit(t, (uint32_t)(P >> 32), 21)) & M;
         const int32_t e = (LIN_ABLATE & 4) ? (int32_t)a : *(const int32_t *)((const char *)s_lut + a);
         const int gg = LANE_GAIN ? (p0 + s * 64 >= pos1 ? g : 0) : g;
         acc[s] += (int64_t)gg * (int64_t)e;
@@ -751,12 +752,13 @@ template <int FMT>
 __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
     const gss_lin_t *__restrict__ lin, const lin_seg *__restrict__ segs,
     const lin_chan *__restrict__ chans, const int32_t *__restrict__ nch,
-    const int32_t *__restrict__ fast, const uint32_t *__restrict__ cbw, lut_arg lut,
+    const int32_t *__restrict__ fast, const uint32_t *__restrict__ cab, lut_arg lut,
     int n_per_blk, int nseg, int wg_per_blk, uint8_t *__restrict__ out, size_t block_bytes)
 {
     __shared__ int32_t s_lut[1024];                       /* cos + 2^22 sin; [512+i] = -[i] */
     __shared__ uint64_t s_lane[GSS_MAXCH * 64];           /* lane offsets L(l) per channel    */
     __shared__ lin_ct s_ct[LIN_WAVES][GSS_MAXCH];         /* the current chunk, per wave      */
+    __shared__ uint32_t s_cab[GSS_MAXCH][CAB_W];          /* the channels' sign bit-streams   */
     const int b = blockIdx.x / wg_per_blk;
     const int w = blockIdx.x - b * wg_per_blk;
     if (!fast[b])
@@ -772,6 +774,8 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
     const int nc = nch[b];
     for (int i = tid; i < nc * 64; i += LIN_THREADS)
         s_lane[i] = gss_lin_lane(CH[i >> 6].xs, CH[i >> 6].zs, (uint32_t)(i & 63));
+    for (int i = tid; i < nc * CAB_W; i += LIN_THREADS)
+        s_cab[i / CAB_W][i % CAB_W] = cab[(size_t)CH[i / CAB_W].tab * CAB_W + i % CAB_W];
     __syncthreads();
     uint32_t M = 0xFFCu;                                  /* LUT address mask, in a VGPR */
     asm volatile("" : "+v"(M));
@@ -799,13 +803,13 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
             const int g0 = (int)(int16_t)(sk.g01 & 0xFFFF), g1 = sk.g01 >> 16;
             const bool chg = sk.pos1 < nb0 + 64 * LIN_CH;    /* a data bit by the chunk's end */
             lin_ct &t = T[lane];
-            t.B = ((uint64_t)(uint32_t)(zb >> GSS_LIN_CSH) << 32) | (xb >> 32);
+            t.B = (xb & ~0xFFFFFFFFull) | (uint32_t)(zb >> GSS_LIN_CSH);
             t.D = ck.d;
             t.g = chg && sk.pos1 <= nb0 ? g1 : g0;
             t.gd = g1 - g0;
             t.pos1 = sk.pos1;
             t.flags = (chg && sk.pos1 > nb0 ? 1u : 0u) | (sk.npatch != 0 ? 2u : 0u);
-            /* 1/16 chip below lane 0's first chip, plus the row's CBW_PRE chips */
+            /* 1/16 chip below lane 0's first chip, plus CBW_PRE chips */
             t.q0 = (uint32_t)(zb >> 46) + (16 * CBW_PRE - 1);
             t.dq = ck.dq;
             t.tab = ck.tab;
@@ -813,14 +817,21 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
         wave_sync_lds();
         /* ---- the chip windows, lane (k, s) ---- */
         for (int i = lane; i < nc * LIN_CH; i += 64) {
-            const lin_ct &t = T[i / LIN_CH];
-            const uint32_t q = (t.q0 + (uint32_t)(i % LIN_CH) * t.dq) >> 2;
+            const int k = i / LIN_CH;
+            const lin_ct &t = T[k];
+            /* the window's first extended chip E (1/16 chip offsets, CBW_PRE chips below 0) and
+               its bit in the row, j = E + 32 */
+            const uint32_t j = min(((t.q0 + (uint32_t)(i % LIN_CH) * t.dq) >> 4) + (32 - CBW_PRE),
+                                   (uint32_t)(32 * CAB_W - 64));
             uint32_t wv;
-            if (LIN_ABLATE & 2)
-                wv = q * 0x9E3779B9u;
-            else
-                wv = cbw[t.tab / 4u + min(q, (uint32_t)CBW_ROW - 1u)];
-            T[i / LIN_CH].W[i % LIN_CH] = wv;
+            if (LIN_ABLATE & 2) {
+                wv = j * 0x9E3779B9u;
+            } else {
+                const uint32_t lin = __builtin_amdgcn_alignbit(s_cab[k][(j >> 5) + 1],
+                                                              s_cab[k][j >> 5], j & 31);
+                wv = __builtin_amdgcn_alignbit(lin, lin, (32u - j) & 31u);   /* rotl by E mod 32 */
+            }
+            T[k].W[i % LIN_CH] = wv;
         }
         wave_sync_lds();
         int64_t acc[LIN_CH];
@@ -878,7 +889,7 @@ struct gss_dev {
     void *h_in = nullptr; size_t h_in_cap = 0;
     void *d_out = nullptr; size_t d_out_cap = 0;
     double *d_cend = nullptr; size_t d_cend_cap = 0;
-    uint32_t *d_cbw = nullptr; size_t d_cbw_cap = 0;   /* chip-sign windows (gss_cbw_kernel) */
+    uint32_t *d_cbw = nullptr; size_t d_cbw_cap = 0;   /* chip-sign bit-streams (gss_cab_kernel) */
     void *d_seg = nullptr; size_t d_seg_cap = 0;       /* lin_seg rows (gss_linseg_kernel)   */
     int32_t *d_status = nullptr;
     /* the exact path's leftovers of a fast-path call run on their own stream beside the fast
@@ -1152,8 +1163,8 @@ extern "C" int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const
         return gss_fail(GSS_E_ARG, "no fast kernel for fmt=%d nch=%d", fmt, nchp);
     HIP_TRY(hipSetDevice(d->ordinal));
     hipStream_t st = (hipStream_t)stream;
-    /* chip-sign windows of every C/A table row (32 x 12296 x 4 B; rebuilt per call: ~µs) */
-    const size_t ncbw = (size_t)n_ca * CBW_ROW;
+    /* chip-sign bit-streams of every C/A table row (32 x 99 x 4 B; rebuilt per call: ~µs) */
+    const size_t ncbw = (size_t)n_ca * CAB_W;
     if (ncbw * sizeof(uint32_t) > d->d_cbw_cap) {
         (void)hipFree(d->d_cbw);
         d->d_cbw = nullptr;
@@ -1161,7 +1172,7 @@ extern "C" int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const
         HIP_TRY(hipMalloc(&d->d_cbw, ncbw * sizeof(uint32_t)));
         d->d_cbw_cap = ncbw * sizeof(uint32_t);
     }
-    hipLaunchKernelGGL(gss_cbw_kernel, dim3((unsigned)((ncbw + 255) / 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(gss_cab_kernel, dim3((unsigned)((ncbw + 255) / 256)), dim3(256), 0, st,
                        ca_bits, n_ca, d->d_cbw);
     HIP_TRY(hipGetLastError());
     const int segs = (n_per_blk + 64 * LIN_STEPS - 1) / (64 * LIN_STEPS);

@@ -237,17 +237,18 @@ static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
         return 0;
     const i128 X0 = to_fix(x0, 64, &inexact), XS = to_fix(s, 64, &inexact);
     const i128 DX1 = 2 + (i128)n * (LIN_CARR_ERR + 1);           /* line vs reference */
-    const int nhx = ambiguous(X0, XS, DX1 + GSS_LIN_KDEV_CARR, LIN_CARR_LGB, n, hx, LIN_MAXHIT);
-    if (nhx < 0)
-        return 0;
     const double c0 = p->code0, cs = p->code_step;
     if (!(c0 >= 0.0 && c0 < GSS_CA_SEQ_LEN_D) || !(cs > 0.0 && cs < 1.0))
+        return 0;
+    const int64_t ZS = (int64_t)to_fix(cs, 50, &inexact);
+    const int nhx = ambiguous(X0, XS, DX1 + GSS_LIN_KDEV_CARR((uint64_t)ZS), LIN_CARR_LGB, n, hx,
+                              LIN_MAXHIT);
+    if (nhx < 0)
         return 0;
     if (p->iword < 0 || p->iword >= GSS_NAV_WORDS || p->ibit < 0 || p->ibit >= 30 ||
         p->icode < 0 || p->icode >= 20)
         return 0;
     const int64_t Z0 = (int64_t)to_fix(c0, 50, &inexact);
-    const int64_t ZS = (int64_t)to_fix(cs, 50, &inexact);
     const int64_t per = (int64_t)GSS_CA_LEN << LIN_CODE_LGB;
     /* the kernel reads one 32-chip window per 64-sample step, starting up to 2 chips below
        lane 0's chip (gss_lin.h) */
