@@ -335,6 +335,9 @@ static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
             x = gss_carr_walk_cc(x, s, q - xat);     /* the reference may differ from the line */
             xat = q;
             cell = (int)floor(x * 512.0);
+            if (cell > 511)      /* carr += 1.0 rounded to 1.0: the reference reads cosTable512[512]
+                                    (SURVEY A.7); the exact path renders it */
+                return 0;
         } else {                                 /* proven: exact = line */
             cell = (int)((uint64_t)(X0 + (i128)q * XS) >> LIN_CARR_LGB);
         }
