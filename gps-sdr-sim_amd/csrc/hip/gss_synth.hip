@@ -674,11 +674,15 @@ __device__ __forceinline__ void lin_put(uint32_t *p, uint32_t v)
         *p = v;
 }
 
+/* v_writelane_b32: a wave-uniform value into one lane (no clang builtin in this toolchain) */
+extern "C" __device__ int gss_writelane(int, int, int) __asm("llvm.amdgcn.writelane.i32");
+
 template <int FMT, bool TAIL>
 __device__ __forceinline__ void lin_store(const int64_t (&acc)[LIN_CH], uint8_t *__restrict__ ob,
                                           int nb0, int lane, int n_per_blk)
 {
     uint32_t pk[LIN_CH];
+    pk[0] = 0;
 #pragma unroll
     for (int s = 0; s < LIN_CH; s++) {
         /* acc = (sum I + 64 + 2^21) + 2^22 (sum Q + 64): the 2^21 bias keeps the I field
@@ -700,18 +704,42 @@ __device__ __forceinline__ void lin_store(const int64_t (&acc)[LIN_CH], uint8_t 
                 ((uint16_t *)ob)[p] =
                     (uint16_t)__builtin_amdgcn_perm(q8, (uint32_t)i8, 0x0c0c0400u);
         } else {                                          /* {I0 Q0 I1 Q1 ...} MSB first */
-            const int i16 = __builtin_amdgcn_sbfe((int)(lo ^ (1u << 21)), 7, 15);
-            const int q16 = (int)__builtin_amdgcn_alignbit(hi, lo, 29);
-            const uint64_t mi = __builtin_amdgcn_ballot_w64(in && i16 > 0);
-            const uint64_t mq = __builtin_amdgcn_ballot_w64(in && q16 > 0);
-            if (lane < 16 && (!TAIL || nb + 4 * lane < n_per_blk)) {
-                const uint32_t a = (uint32_t)(mi >> (4 * lane)) & 15u;
-                const uint32_t c = (uint32_t)(mq >> (4 * lane)) & 15u;
-                ob[nb / 4 + lane] = (uint8_t)(((a & 1u) << 7) | ((a & 2u) << 4) |
-                                              ((a & 4u) << 1) | ((a & 8u) >> 2) |
-                                              ((c & 1u) << 6) | ((c & 2u) << 3) | (c & 4u) |
-                                              ((c & 8u) >> 3));
-            }
+            /* I16 > 0 <=> sum I + 64 >= 128 <=> the I field (low 22 bits) >= 2^21 + 128;
+               Q16 > 0 <=> acc >= 2^29 (gpssim.c:2266-2276: bit = iq_buff[] > 0) */
+            const uint64_t mi = __builtin_amdgcn_ballot_w64((lo & 0x3FFFFFu) >= (1u << 21) + 128u);
+            const uint64_t mq = __builtin_amdgcn_ballot_w64(acc[s] >= ((int64_t)1 << 29));
+            /* lane 4s + j collects the I (low half) and Q (high half) sign bits of samples
+               64 s + 16 j .. + 15: scalar packs, one lane write each */
+            const uint32_t ilo = (uint32_t)mi, ihi = (uint32_t)(mi >> 32);
+            const uint32_t qlo = (uint32_t)mq, qhi = (uint32_t)(mq >> 32);
+            pk[0] = (uint32_t)gss_writelane((int)((ilo & 0xFFFFu) | (qlo << 16)), 4 * s, (int)pk[0]);
+            pk[0] = (uint32_t)gss_writelane((int)((ilo >> 16) | (qlo & 0xFFFF0000u)), 4 * s + 1, (int)pk[0]);
+            pk[0] = (uint32_t)gss_writelane((int)((ihi & 0xFFFFu) | (qhi << 16)), 4 * s + 2, (int)pk[0]);
+            pk[0] = (uint32_t)gss_writelane((int)((ihi >> 16) | (qhi & 0xFFFF0000u)), 4 * s + 3, (int)pk[0]);
+            (void)in;
+        }
+    }
+    if (FMT == 1) {
+        /* each lane now holds 16 samples' I bits (low) and Q bits (high): interleave them into the
+           reference's bytes (sample 4b + m: I at bit 7 - 2m, Q at bit 6 - 2m) and store the
+           chunk's 256 bytes with one dword per lane */
+        uint32_t vi = pk[0] & 0xFFFFu, vq = pk[0] >> 16;
+        vi = (vi | (vi << 8)) & 0x00FF00FFu; vq = (vq | (vq << 8)) & 0x00FF00FFu;
+        vi = (vi | (vi << 4)) & 0x0F0F0F0Fu; vq = (vq | (vq << 4)) & 0x0F0F0F0Fu;
+        vi = (vi | (vi << 2)) & 0x33333333u; vq = (vq | (vq << 2)) & 0x33333333u;
+        vi = (vi | (vi << 1)) & 0x55555555u; vq = (vq | (vq << 1)) & 0x55555555u;
+        const uint32_t x = (vi << 1) | vq;                  /* bit 2k + 1 = I_k, bit 2k = Q_k */
+        const uint32_t y = ((x & 0x03030303u) << 6) | ((x & 0x0C0C0C0Cu) << 2) |
+                           ((x >> 2) & 0x0C0C0C0Cu) | ((x >> 6) & 0x03030303u);
+        uint8_t *dst = ob + nb0 / 4 + 4 * lane;
+        const int first = nb0 + 16 * lane;                  /* this lane's first sample */
+        const bool whole = !TAIL || first + 16 <= n_per_blk;
+        if (whole && ((uintptr_t)(ob + nb0 / 4) & 3u) == 0) {
+            lin_put((uint32_t *)dst, y);
+        } else {
+            for (int b = 0; b < 4; b++)                     /* ragged tail or unaligned block */
+                if (first + 4 * b < n_per_blk)
+                    dst[b] = (uint8_t)(y >> (8 * b));
         }
     }
     if (FMT == 16) {
