@@ -54,6 +54,28 @@ int gss_cli_parse(int argc, char **argv, gss_cli_t *c)
     if (ums && atoi(ums) > 0)
         c->opt.user_motion_size = atoi(ums);
 
+    /* --carrier=float|int (an extension: the reference chooses at compile time, gpssim.h:4) is
+       taken out before the reference's getopt loop sees the arguments */
+    char *av[argc + 1];
+    int ac = 0;
+    for (int i = 0; i < argc; i++) {
+        if (i > 0 && strncmp(argv[i], "--carrier=", 10) == 0) {
+            if (strcmp(argv[i] + 10, "int") == 0)
+                c->opt.carrier_int = 1;
+            else if (strcmp(argv[i] + 10, "float") == 0)
+                c->opt.carrier_int = 0;
+            else {
+                fprintf(stderr, "ERROR: Invalid carrier mode (float or int).\n");
+                return 1;
+            }
+            continue;
+        }
+        av[ac++] = argv[i];
+    }
+    av[ac] = NULL;
+    argc = ac;
+    argv = av;
+
     if (argc < 3) {
         gss_cli_usage();
         return 1;

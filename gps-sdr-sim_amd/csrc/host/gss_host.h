@@ -21,6 +21,7 @@
 #define K_N_DWRD_SBF        10
 #define K_N_DWRD            GSS_NAV_WORDS
 #define K_CA_LEN            GSS_CA_LEN
+#define K_CARR_INT_ONE      33554432.0      /* 512*65536: one cycle of the integer carrier */
 #define K_EPH_SETS          13           /* EPHEM_ARRAY_SIZE */
 
 #define K_SEC_WEEK          604800.0

@@ -241,8 +241,17 @@ static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
     if (!(c0 >= 0.0 && c0 < GSS_CA_SEQ_LEN_D) || !(cs > 0.0 && cs < 1.0))
         return 0;
     const int64_t ZS = (int64_t)to_fix(cs, 50, &inexact);
-    const int nhx = ambiguous(X0, XS, DX1 + GSS_LIN_KDEV_CARR((uint64_t)ZS), LIN_CARR_LGB, n, hx,
-                              LIN_MAXHIT);
+    /* An exact chain: the integer-carrier variant's rows (--carrier=int, gpssim.c:2252) are
+       multiples of 2^-25 cycle, so every IEEE step and wrap of the reference is exact and the
+       line IS the reference.  The kernel then rounds nothing either (xs is a multiple of 2^39,
+       gss_lin.h): its carrier word is the line's, a multiple of 2^7, plus the code word's
+       carries, fewer than 2^7 (KDEV below 2^39 units of 2^-64): no sample can change cell. */
+    int ix = 0;
+    (void)to_fix(x0, 25, &ix);
+    (void)to_fix(s, 25, &ix);
+    const int exact_carr = !ix && GSS_LIN_KDEV_CARR((uint64_t)ZS) < ((uint64_t)1 << 39);
+    const int nhx = exact_carr ? 0 : ambiguous(X0, XS, DX1 + GSS_LIN_KDEV_CARR((uint64_t)ZS),
+                                               LIN_CARR_LGB, n, hx, LIN_MAXHIT);
     if (nhx < 0)
         return 0;
     if (p->iword < 0 || p->iword >= GSS_NAV_WORDS || p->ibit < 0 || p->ibit >= 30 ||

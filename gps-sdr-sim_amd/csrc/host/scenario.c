@@ -138,6 +138,9 @@ static int allocate_channels(gss_scn *s, const eph_t *eset, gtime_t grx, const d
                 double r_ref = rho.range;
                 double ph = (2.0 * r_ref - r_xyz) / K_LAMBDA_L1;
                 ch->carr_phase = ph - floor(ph);
+                if (s->opt.carrier_int)   /* #else branch: (unsigned int)(512*65536*phase) */
+                    ch->carr_phase = (double)(unsigned int)(512.0 * 65536.0 * ch->carr_phase) /
+                                     K_CARR_INT_ONE;
                 ch->carr_fresh = 1;
                 break;
             }
@@ -365,6 +368,20 @@ int gss_scn_info(const gss_scn *s, gss_scn_info_t *info)
 /* ---- exact carrier planner ------------------------------------------------------------------
  * One chain per channel slot; a slot's chain restarts whenever allocateChannel re-initialises
  * its carr_phase.  Slots are independent, so the planner runs one slot per thread. */
+/* The integer carrier (FLOAT_CARR_PHASE undefined): carr_phase += carr_phasestep per sample in
+   a uint32 whose bits 16..24 index the LUT (gpssim.c:2202, 2252), i.e. a chain mod 2^25.  Rows
+   carry it as multiples of 2^-25 cycle; n steps from x is (x + n step) mod 1, exactly. */
+static double carr_int_walk(double x, double step, int n, double *ck)
+{
+    const uint32_t xi = (uint32_t)(x * K_CARR_INT_ONE);
+    const int64_t si = (int64_t)(step * K_CARR_INT_ONE);
+    if (ck)
+        for (int j = 0; j < GSS_NCK; j++)
+            ck[j] = (double)((xi + (uint32_t)(si * gss_ck_pos(j, n))) & 0x1FFFFFFu) /
+                    K_CARR_INT_ONE;
+    return (double)((xi + (uint32_t)(si * n)) & 0x1FFFFFFu) / K_CARR_INT_ONE;
+}
+
 typedef struct {
     gss_scn *s;
     gss_chan_blk_t *blk;
@@ -387,7 +404,10 @@ static void *plan_slots(void *arg)
                 if (s->b_reset[e])
                     x = s->b_init[e];
                 j->blk[e].carr0 = x;
-                if (j->ck)      /* same walk, recording the sub-block checkpoints on the way */
+                if (s->opt.carrier_int)    /* exact integer chain, checkpoints included */
+                    x = carr_int_walk(x, j->blk[e].carr_step, s->n_per_blk,
+                                      j->ck ? j->ck + e * GSS_NCK : NULL);
+                else if (j->ck) /* same walk, recording the sub-block checkpoints on the way */
                     x = gss_carr_walk_ck(x, j->blk[e].carr_step, s->n_per_blk,
                                          j->ck + e * GSS_NCK);
                 else
@@ -485,6 +505,9 @@ int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, 
             gss_chan_blk_t *p = &row[k];
             p->carr0 = 0.0;                        /* filled by the planner */
             p->carr_step = ch->f_carr * s->delt;
+            if (s->opt.carrier_int)       /* carr_phasestep (gpssim.c:2175-2177) */
+                p->carr_step = (double)(int)round(512.0 * 65536.0 * ch->f_carr * s->delt) /
+                               K_CARR_INT_ONE;
             p->code0 = ch->code_phase;
             p->code_step = ch->f_code * s->delt;
             p->icode = ch->icode;

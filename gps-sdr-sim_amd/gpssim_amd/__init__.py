@@ -63,6 +63,7 @@ class _Opts(C.Structure):
         ("duration", C.c_double), ("has_start", C.c_int), ("time_overwrite", C.c_int),
         ("start", C.c_int * 6), ("start_sec", C.c_double), ("iono_disable", C.c_int),
         ("verbose", C.c_int), ("user_motion_size", C.c_int), ("quiet", C.c_int),
+        ("carrier_int", C.c_int),
     ]
 
 
@@ -221,7 +222,9 @@ class Scenario:
     def __init__(self, nav_file, *, llh=None, xyz=None, motion_file=None, nmea=False,
                  samp_freq=2.6e6, data_format=16, duration=None, start=None,
                  time_overwrite=False, iono=True, verbose=False, quiet=True,
-                 user_motion_size=3000):
+                 user_motion_size=3000, carrier="float"):
+        if carrier not in ("float", "int"):
+            raise ValueError(f"carrier must be 'float' or 'int', not {carrier!r}")
         self._keep = []
         o = _Opts()
         o.nav_file = self._s(nav_file)
@@ -245,6 +248,7 @@ class Scenario:
         o.verbose = int(bool(verbose))
         o.user_motion_size = int(user_motion_size)
         o.quiet = int(bool(quiet))
+        o.carrier_int = int(carrier == "int")      # FLOAT_CARR_PHASE off (gpssim.h:4)
         self._h = C.c_void_p()
         _check(lib().gss_scn_open(C.byref(self._h), C.byref(o)))
         self._init_info()

@@ -205,6 +205,14 @@ typedef struct gss_opts {
     int    verbose;             /* -v                                                          */
     int    user_motion_size;    /* USER_MOTION_SIZE (gpssim.h:19-21), 0 → 3000                 */
     int    quiet;               /* suppress the reference's stderr chatter (library use)       */
+    int    carrier_int;         /* 1: the reference built without FLOAT_CARR_PHASE (gpssim.h:4):
+                                   32-bit integer carrier in 2^-25 cycle, step
+                                   (int)round(2^25 f_carr delt) (gpssim.c:1623-1626, 2175-2177,
+                                   2201-2202, 2252).  CLI: --carrier=int (default float).  The
+                                   rows then carry that integer chain as exact doubles, carr0 =
+                                   (carr_phase mod 2^25) / 2^25 and carr_step = step / 2^25, whose
+                                   IEEE recurrence is the integer one, so every kernel renders it
+                                   unchanged.                                                   */
 } gss_opts_t;
 
 /* The reference command line (getopt "e:u:g:c:l:o:s:b:T:t:d:iv", gpssim.c:1650-1852) parsed

@@ -56,7 +56,20 @@ CONFIGS.update({
     "satellite_i_b8": (["-u", os.path.join(REF_SRC, "satellite.csv"), "-i", "-s", "2600000",
                         "-b", "8"], 260000, 8),
 })
-BINARY = {"rocket_um4000_b8": REF_UM4000}
+# the integer-carrier build (FLOAT_CARR_PHASE off, gpssim.h:4; oracle/Makefile), which the
+# product renders with --carrier=int
+REF_INT = os.path.join(REPO, "oracle", "_ref", "gps-sdr-sim-intcarr")
+CONFIGS.update({
+    "intcarr_static_d30_b16": (["-l", LOC, "-d", "30", "-s", "2600000", "-b", "16"], 260000, 16),
+    "intcarr_static_d65_b8": (["-l", LOC, "-d", "65", "-s", "2600000", "-b", "8"], 260000, 8),
+    "intcarr_circle_b8": (["-u", os.path.join(REF_SRC, "circle.csv"), "-s", "2600000", "-b",
+                           "8"], 260000, 8),
+    "intcarr_static_d30_s20M_b1": (["-l", LOC, "-d", "30", "-s", "20000000", "-b", "1"],
+                                   2000000, 1),
+})
+BINARY = {"rocket_um4000_b8": REF_UM4000, "intcarr_static_d30_b16": REF_INT,
+          "intcarr_static_d65_b8": REF_INT, "intcarr_circle_b8": REF_INT,
+          "intcarr_static_d30_s20M_b1": REF_INT}
 # reference stderr (banner, channel table, -v details, progress), minus the timing line
 STDERR = {
     "static_d31_v": ["-l", LOC, "-d", "31", "-b", "1", "-v"],
@@ -90,7 +103,8 @@ def run(name, tail, n, fmt):
     return {"argv": [os.path.basename(a) if a.startswith(REF_SRC) else a for a in tail],
             "n_per_blk": n, "fmt": fmt, "bytes": total, "blocks": len(blocks),
             "sha256": full.hexdigest(), "block_sha16": blocks, "head_hex": head,
-            "user_motion_size": 4000 if name in BINARY else 3000}
+            "user_motion_size": 4000 if name == "rocket_um4000_b8" else 3000,
+            "carrier": "int" if name.startswith("intcarr_") else "float"}
 
 
 def stderr_of(tail):

@@ -19,7 +19,10 @@ pytestmark = pytest.mark.gpu
 
 DATA = os.path.join(REPO, "tests", "golden", "data")
 CASES = ["nmea_triumph_b8", "static_t0200_d30_b8", "static_T1221_d30_b8", "rocket_um4000_b8",
-         "satellite_i_b8"]
+         "satellite_i_b8",
+         # --carrier=int vs the reference built with FLOAT_CARR_PHASE off (gpssim.h:4)
+         "intcarr_static_d30_b16", "intcarr_static_d65_b8", "intcarr_circle_b8",
+         "intcarr_static_d30_s20M_b1"]
 
 
 def _argv(args):
@@ -32,7 +35,8 @@ def test_cli_surface_whole_run(golden, name, tmp_path):
     bb = G.block_bytes(g["n_per_blk"], g["fmt"])
     env = dict(os.environ, GSS_USER_MOTION_SIZE=str(g["user_motion_size"]))
     errf = open(tmp_path / "stderr.txt", "w+b")      # a file: a pipe would fill and stall it
-    p = subprocess.Popen([G.CLI_PATH, "-e", NAV] + _argv(g["argv"]) + ["-o", "-"], env=env,
+    mode = ["--carrier=int"] if g.get("carrier") == "int" else []
+    p = subprocess.Popen([G.CLI_PATH, "-e", NAV] + _argv(g["argv"]) + mode + ["-o", "-"], env=env,
                          stdout=subprocess.PIPE, stderr=errf)
     h, blocks, total = hashlib.sha256(), [], 0
     while True:

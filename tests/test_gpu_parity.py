@@ -165,6 +165,23 @@ def test_baseline_configs_bit_exact(dev, golden, name, kw):
     assert total == g["bytes"] and sha == g["sha256"]
 
 
+@pytest.mark.parametrize("name,kw", [
+    ("intcarr_static_d30_b16", dict(llh=LOC, duration=30.0, data_format=16)),
+    ("intcarr_static_d65_b8", dict(llh=LOC, duration=65.0, data_format=8)),
+    ("intcarr_circle_b8", dict(motion_file=CIRCLE, data_format=8)),
+    ("intcarr_static_d30_s20M_b1", dict(llh=LOC, duration=30.0, samp_freq=2.0e7, data_format=1)),
+])
+def test_integer_carrier_bit_exact(dev, golden, name, kw):
+    """--carrier=int against the reference built with FLOAT_CARR_PHASE off (gpssim.h:4): the
+    integer chain travels as exact doubles, so the same kernels render it"""
+    sha, total, blocks = run_scenario(dev, batch=100, carrier="int", **kw)
+    g = golden[name]
+    if blocks != g["block_sha16"]:
+        first = next(i for i, (a, b) in enumerate(zip(blocks, g["block_sha16"])) if a != b)
+        raise AssertionError(f"{name}: first differing block {first}")
+    assert total == g["bytes"] and sha == g["sha256"]
+
+
 def test_cli_end_to_end(golden):
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "gpssim.bin")

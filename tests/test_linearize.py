@@ -239,3 +239,46 @@ def test_patched_real_blocks_vs_reference_golden(golden):
     gold = golden["static_d30_s20M_b16"]["block_sha16"]
     for i, b in enumerate(sel):
         assert hashlib.sha256(got[i * bb:(i + 1) * bb].tobytes()).hexdigest()[:16] == gold[b], b
+
+
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name,fs,nb", [("intcarr_static_d30_b16", 2.6e6, 40),
+                                        ("intcarr_static_d30_s20M_b1", 2.0e7, 6)])
+def test_integer_carrier_lines_vs_reference_golden(golden, name, fs, nb):
+    """--carrier=int: the chain is exact (multiples of 2^-25 cycle), so the proof certifies every
+    block with no ambiguous carrier sample, and the render model reproduces the reference built
+    with FLOAT_CARR_PHASE off (gpssim.h:4), block for block."""
+    g = golden[name]
+    s = G.Scenario(NAV, llh=LOC, duration=30.0, samp_freq=fs, data_format=g["fmt"],
+                   carrier="int")
+    blk, nch = s.next(nb)
+    lin, fast = G.linearize(blk, nch, s.nav_table(), s.n_per_blk)
+    assert fast.all(), fast
+    got, _ = render_lin(blk, nch, lin, fast, G.ca_table(), s.n_per_blk, g["fmt"])
+    bb = G.block_bytes(s.n_per_blk, g["fmt"])
+    for i in range(nb):
+        assert hashlib.sha256(got[i * bb:(i + 1) * bb].tobytes()).hexdigest()[:16] == \
+            g["block_sha16"][i], i
+
+
+def test_integer_carrier_on_cell_boundaries_like_oracle():
+    """Exact integer chains that sit exactly on LUT cell boundaries at many samples (steps with
+    large powers of two, starts on a boundary): every block certified, bytes equal the oracle's
+    (patches come only from the code chain here)."""
+    rng = np.random.default_rng(17)
+    n = 26000
+    blk, nch, nav = synth_params(rng, 4, [12, 12, 12, 12], n)
+    one = float(1 << 25)
+    for b in range(4):
+        for k in range(12):
+            p = blk[b, k]
+            step = int(rng.integers(-20000, 20000)) & ~((1 << (4 * (k % 4))) - 1)
+            p["carr_step"] = step / one
+            p["carr0"] = (int(rng.integers(0, 512)) << 16) / one if k % 2 else \
+                int(rng.integers(0, 1 << 25)) / one
+    lin, fast = G.linearize(blk, nch, nav, n)
+    assert fast.all(), fast
+    ca = G.ca_table()
+    want, _ = oracle.synth(blk, nch, ca, nav, n, 16)
+    got, _ = render_lin(blk, nch, lin, fast, ca, n, 16)
+    assert np.array_equal(got, want)

@@ -133,3 +133,38 @@ def test_cpu_restatement_stderr_matches_reference(name):
     got = "".join(l for l in p.stderr.decode().splitlines(True)
                   if not l.startswith("Process time"))
     assert got == e["stderr"]
+
+
+# the integer-carrier variant: the reference built with FLOAT_CARR_PHASE off (gpssim.h:4,
+# oracle/Makefile _ref/gps-sdr-sim-intcarr), rendered by the product with --carrier=int
+INT_CASES = [
+    ("intcarr_static_d30_b16", ["-d", "3"], 29),
+    ("intcarr_static_d65_b8", ["-d", "31"], 309),      # across the first nav/allocation update
+    ("intcarr_circle_b8", ["-d", "2"], 19),
+    ("intcarr_static_d30_s20M_b1", ["-d", "1"], 9),
+]
+
+
+@pytest.mark.parametrize("name,dur,nblk", INT_CASES)
+def test_cpu_restatement_integer_carrier_prefix(golden, name, dur, nblk):
+    g = golden[name]
+    assert g["carrier"] == "int"
+    argv = fixture_argv(g)
+    out = run_cpu_restatement(["--carrier=int"] + limit_duration(argv, dur[1]))
+    bb = G.block_bytes(g["n_per_blk"], g["fmt"])
+    assert len(out) == nblk * bb
+    assert block_hashes(out, bb) == g["block_sha16"][:nblk]
+
+
+def test_integer_carrier_differs_from_float(golden):
+    """the two reference builds give different streams, so the flag is honoured"""
+    assert golden["intcarr_static_d30_b16"]["sha256"] != golden["static_d30_b16"]["sha256"]
+    out = run_cpu_restatement(["-l", ",".join(map(str, LOC)), "-d", "1", "-b", "16",
+                               "--carrier=float"])
+    assert block_hashes(out, 1040000) == golden["static_d30_b16"]["block_sha16"][:9]
+
+
+def test_carrier_flag_rejects_unknown_mode():
+    p = subprocess.run([oracle.CLI, "-e", NAV, "-l", "30,120,100", "-d", "1", "--carrier=fixed",
+                        "-o", "/dev/null"], capture_output=True)
+    assert p.returncode == 1 and b"Invalid carrier mode" in p.stderr
