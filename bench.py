@@ -117,7 +117,9 @@ def lib_sha16(path):
 def load_traffic(workload, kernel, kern_ms, lib_sha):
     """HBM bytes per launch of `kernel` from a committed profile (profiles/pmc_traffic.json), only
     when it was taken on this workload and this kernel build (same library sha256) and its kernel
-    time is within 5 % of this run's.  Fallback for live_traffic."""
+    time (warm launches) is within 5 % of the profiled run's own HIP-event time (rocprofv3 slows
+    the kernel by a few %, so the profile is checked against the run it profiled; this run's
+    time is reported beside it).  Fallback for live_traffic."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
@@ -127,10 +129,13 @@ def load_traffic(workload, kernel, kern_ms, lib_sha):
         return None, "profile of another workload"
     if d.get("lib_sha16") != lib_sha:
         return None, "profile of another build"
-    prof_ms = (d.get("kernel_avg_ns") or 0) / 1e6
-    if kern_ms <= 0 or abs(prof_ms - kern_ms) > 0.05 * kern_ms:
-        return None, f"profile kernel time {prof_ms:.3f} ms vs {kern_ms:.3f} ms here"
-    return d.get("hbm_bytes_per_launch"), f"{d.get('source')}; profiled kernel {prof_ms:.3f} ms"
+    prof_ms = (d.get("kernel_warm_avg_ns") or d.get("kernel_avg_ns") or 0) / 1e6
+    ev_ms = d.get("profiled_run_event_ms") or 0
+    if ev_ms <= 0 or abs(prof_ms - ev_ms) > 0.05 * ev_ms:
+        return None, f"profile kernel time {prof_ms:.3f} ms vs {ev_ms:.3f} ms of its own run"
+    return d.get("hbm_bytes_per_launch"), (f"{d.get('source')}; profiled kernel {prof_ms:.3f} ms "
+                                           f"(its run's events {ev_ms:.3f} ms; this run "
+                                           f"{kern_ms:.3f} ms)")
 
 
 def live_traffic(fmt, window, threads, kern_ms, timeout=150):
@@ -147,7 +152,7 @@ def live_traffic(fmt, window, threads, kern_ms, timeout=150):
     if not shutil.which("rocprofv3"):
         return None, "rocprofv3 not found"
     top = tempfile.mkdtemp(prefix="gss_pmc_", dir="/tmp")
-    child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
+    child = [sys.executable, os.path.abspath(__file__), "--steps", "4", "--warmup", "1",
              "--fmt", str(fmt), "--window", str(window), "--threads", str(threads),
              "--no-cpu-baseline", "--no-exact", "--no-configs", "--no-e2e", "--no-pmc"]
     env = dict(os.environ, TMPDIR="/tmp")
@@ -158,7 +163,8 @@ def live_traffic(fmt, window, threads, kern_ms, timeout=150):
         for name, opts in passes:
             cmd = ["rocprofv3"] + opts + ["-d", os.path.join(top, name), "-o", name, "-f", "csv",
                                           "--"] + child
-            p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
+            outf = os.path.join(top, name + ".out")
+            p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=open(outf, "w"),
                                  stderr=subprocess.DEVNULL, start_new_session=True)
             try:
                 rc = p.wait(timeout=timeout)
@@ -168,18 +174,30 @@ def live_traffic(fmt, window, threads, kern_ms, timeout=150):
                 return None, f"rocprofv3 {name} pass timed out"
             if rc != 0:
                 return None, f"rocprofv3 {name} pass exited {rc}"
-        ks, cs = PS.kernel_stats(top), PS.counters(top)
+        ks, kd, cs = PS.kernel_stats(top), PS.kernel_durations(top), PS.counters(top)
         k = next((n for n in cs if n.startswith("gss_lin_kernel")), None)
         if k is None or "WRITE_SIZE" not in cs[k] or "FETCH_SIZE" not in cs[k] or k not in ks:
             return None, "rocprofv3 passes gave no gss_lin_kernel counters"
-        prof_ms = ks[k]["avg_ns"] / 1e6
-        if kern_ms <= 0 or abs(prof_ms - kern_ms) > 0.05 * kern_ms:
-            return None, f"live profile kernel time {prof_ms:.3f} ms vs {kern_ms:.3f} ms here"
+        # the warm launches (the child's first launch runs from cold caches and clocks), against
+        # the child's own HIP-event time of the same launches: under rocprofv3 the kernel runs a
+        # few % slower than without it, so the profile is checked against the run it profiled
+        prof_ms = (PS.warm_avg_ns(kd[k]) if kd.get(k) else ks[k]["avg_ns"]) / 1e6
+        try:
+            line = [l for l in open(os.path.join(top, "kt.out")) if l.startswith("{")][-1]
+            child_ms = json.loads(line)["stages_ms"]["fast_path"]
+        except (IndexError, KeyError, ValueError):
+            return None, "profiled run printed no bench line"
+        if child_ms <= 0 or abs(prof_ms - child_ms) > 0.05 * child_ms:
+            return None, (f"live profile kernel time {prof_ms:.3f} ms vs {child_ms:.3f} ms of "
+                          "the profiled run's own events")
         traffic = round((cs[k]["WRITE_SIZE"] + 2 * cs[k]["FETCH_SIZE"]) * 1024)
         return traffic, (f"live rocprofv3 passes on this box and build ({k}: write "
                          f"{cs[k]['WRITE_SIZE'] * 1024 / 1e9:.3f} GB + read "
                          f"{2 * cs[k]['FETCH_SIZE'] * 1024 / 1e9:.3f} GB per launch, "
-                         f"profiled kernel {prof_ms:.3f} ms)")
+                         f"profiled kernel {prof_ms:.3f} ms over its warm launches "
+                         f"({ks[k]['avg_ns'] / 1e6:.3f} ms over all {ks[k]['calls']}), the "
+                         f"profiled run's own events {child_ms:.3f} ms; this run without the "
+                         f"profiler {kern_ms:.3f} ms)")
     finally:
         shutil.rmtree(top, ignore_errors=True)
 

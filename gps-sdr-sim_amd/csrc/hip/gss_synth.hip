@@ -521,7 +521,8 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
 static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole chunks");
 /* LIN_ABLATE (measurement builds only, tools/ablate.sh; wrong output): 1 no output stores,
    2 no chip-window loads, 4 no LUT reads, 8 every block stores into one of 8 blocks (L2),
-   32 no alignbit (VALU work), 64 no window reads in the render loop (LDS work) */
+   32 no alignbit (VALU work), 64 no window reads in the render loop (LDS work), 128 the LUT
+   address without the chip sign (no bank conflicts between a cell's two signs) */
 #ifndef LIN_ABLATE
 #define LIN_ABLATE 0
 #endif
@@ -674,6 +675,9 @@ __device__ __forceinline__ void lin_put(uint32_t *p, uint32_t v)
         *p = v;
 }
 
+#ifndef LIN_SADDR
+#define LIN_SADDR 1
+#endif
 /* v_writelane_b32: a wave-uniform value into one lane (no clang builtin in this toolchain) */
 extern "C" __device__ int gss_writelane(int, int, int) __asm("llvm.amdgcn.writelane.i32");
 
@@ -744,11 +748,22 @@ __device__ __forceinline__ void lin_store(const int64_t (&acc)[LIN_CH], uint8_t 
     }
     if (FMT == 16) {
         __builtin_amdgcn_sched_barrier(0);
+        if (!TAIL && LIN_SADDR) {
+            /* uniform base in SGPRs, 32-bit lane offset: no 64-bit address VGPRs per store */
+            uint32_t *base = (uint32_t *)ob + nb0;
+            const uint32_t off = (uint32_t)lane * 4u;
 #pragma unroll
-        for (int s = 0; s < LIN_CH; s++) {
-            const int p = nb0 + s * 64 + lane;
-            if (!TAIL || p < n_per_blk)
-                lin_put(((uint32_t *)ob) + p, pk[s]);
+            for (int s = 0; s < LIN_CH; s++)
+                asm volatile("global_store_dword %0, %1, %2 offset:%3 nt"   /* 13-bit offset */
+                             : : "v"(off), "v"(pk[s]), "s"(base + (s >> 4) * 1024),
+                               "i"((s & 15) * 256) : "memory");
+        } else {
+#pragma unroll
+            for (int s = 0; s < LIN_CH; s++) {
+                const int p = nb0 + s * 64 + lane;
+                if (!TAIL || p < n_per_blk)
+                    lin_put(((uint32_t *)ob) + p, pk[s]);
+            }
         }
     }
 }
@@ -805,7 +820,7 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
     for (int i = tid; i < nc * CAB_W; i += LIN_THREADS)
         s_cab[i / CAB_W][i % CAB_W] = cab[(size_t)CH[i / CAB_W].tab * CAB_W + i % CAB_W];
     __syncthreads();
-    uint32_t M = 0xFFCu;                                  /* LUT address mask, in a VGPR */
+    uint32_t M = (LIN_ABLATE & 128) ? 0x7FCu : 0xFFCu;   /* LUT address mask, in a VGPR */
     asm volatile("" : "+v"(M));
     const int sg = w * LIN_WAVES + wave;
     const int n0 = sg * (64 * LIN_STEPS);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build measurement variants of the library into _var/<name>/ (ablations of the fast-path kernel,
-# or other LIN_CH): usage  bash tools/ablate.sh name "EXTRA_HIPFLAGS"
+# or other LIN_CH): usage  [HOSTFLAGS="-D..."] bash tools/ablate.sh name "EXTRA_HIPFLAGS"
 # The variant is loaded by bench.py through GSS_LIB_PATH=_var/<name>/libgpssim_amd.so.
 set -e
 cd "$(dirname "$0")/.."
@@ -10,5 +10,14 @@ HIPCC=/opt/rocm/bin/hipcc
 F="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Iinclude -Wno-unused-result $flags"
 $HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_synth.hip -o _var/$name/obj/gss_synth.o
 $HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_run.hip -o _var/$name/obj/gss_run.o
-$HIPCC -shared -fPIC --offload-arch=gfx950 -o _var/$name/libgpssim_amd.so gps-sdr-sim_amd/obj/host/*.o \
+HOSTOBJ=gps-sdr-sim_amd/obj/host/*.o
+if [ -n "$HOSTFLAGS" ]; then          # the host proof must agree with the kernel (e.g. GSS_LIN_CH)
+    mkdir -p _var/$name/obj/host
+    for f in gps-sdr-sim_amd/csrc/host/*.c gps-sdr-sim_amd/csrc/cli/cli_args.c; do
+        gcc -O2 -fPIC -ffp-contract=off -fno-fast-math -D_FILE_OFFSET_BITS=64 -Iinclude $HOSTFLAGS \
+            -c $f -o _var/$name/obj/host/$(basename ${f%.c}).o
+    done
+    HOSTOBJ=_var/$name/obj/host/*.o
+fi
+$HIPCC -shared -fPIC --offload-arch=gfx950 -o _var/$name/libgpssim_amd.so $HOSTOBJ \
     _var/$name/obj/gss_synth.o _var/$name/obj/gss_run.o -lm -lpthread

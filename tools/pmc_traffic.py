@@ -37,7 +37,9 @@ def main():
     res = {"workload": bench["config"]["workload"] if bench else None, "kernel": k,
            "hbm_bytes_per_launch": round(w + r), "hbm_write_bytes_per_launch": round(w),
            "hbm_read_bytes_per_launch": round(r), "algorithmic_bytes_per_launch": alg,
-           "kernel_avg_ns": e.get("avg_ns"), "valu_issue_frac": e.get("valu_issue_frac"),
+           "kernel_avg_ns": e.get("avg_ns"), "kernel_warm_avg_ns": e.get("warm_avg_ns"),
+           "profiled_run_event_ms": (bench or {}).get("stages_ms", {}).get("fast_path"),
+           "valu_issue_frac": e.get("valu_issue_frac"),
            "lib_sha16": (bench or {}).get("lib", {}).get("sha16"),
            "lds_busy_frac": e.get("lds_busy_frac"), "lds_conflict_frac": e.get("lds_conflict_frac"),
            "method": "rocprofv3 --pmc WRITE_SIZE / --pmc FETCH_SIZE in separate passes "

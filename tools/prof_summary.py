@@ -24,6 +24,26 @@ def kernel_stats(d):
     return out
 
 
+def kernel_durations(d):
+    """per-dispatch durations [ns] in dispatch order, per kernel (kernel trace of the kt pass)"""
+    out = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(d, "kt", "*kernel_trace.csv")):
+        try:
+            rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
+            for r in rows:
+                out[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) -
+                                                    int(r["Start_Timestamp"]))
+        except (KeyError, ValueError):       # an unexpected trace layout: no per-dispatch data
+            return {}
+    return dict(out)
+
+
+def warm_avg_ns(durs):
+    """mean duration of the dispatches after the first (the cold warm-up launch)"""
+    w = durs[1:] if len(durs) > 1 else durs
+    return sum(w) / len(w) if w else 0.0
+
+
 def counters(d):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     meta = {}
@@ -44,10 +64,13 @@ def counters(d):
 def main():
     d = sys.argv[1]
     ks = kernel_stats(d)
+    kd = kernel_durations(d)
     cs = counters(d)
     summary = {}
     for k in sorted(set(ks) | set(cs)):
         e = dict(ks.get(k, {}))
+        if k in kd:
+            e["warm_avg_ns"] = warm_avg_ns(kd[k])
         c = cs.get(k, {})
         e.update({"meta": c.get("_meta")})
         e["counters"] = {n: v for n, v in c.items() if n != "_meta"}
