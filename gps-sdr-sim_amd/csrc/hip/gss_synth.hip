@@ -704,9 +704,14 @@ __device__ __forceinline__ void lin_store(const int64_t (&acc)[LIN_CH], uint8_t 
         } else if (FMT == 8) {                            /* iq_buff >> 4 → signed char */
             const int i8 = __builtin_amdgcn_sbfe((int)(lo ^ (1u << 21)), 11, 11);
             const uint32_t q8 = (uint32_t)((int)hi >> 1);
-            if (in)
-                ((uint16_t *)ob)[p] =
-                    (uint16_t)__builtin_amdgcn_perm(q8, (uint32_t)i8, 0x0c0c0400u);
+            const uint32_t v = __builtin_amdgcn_perm(q8, (uint32_t)i8, 0x0c0c0400u);
+            if (!TAIL && LIN_SADDR)               /* SGPR base, 32-bit lane offset, as -b 16 */
+                asm volatile("global_store_short %0, %1, %2 offset:%3"
+                             : : "v"((uint32_t)lane * 2u), "v"(v),
+                               "s"((uint16_t *)ob + nb0 + (s >> 4) * 2048), "i"((s & 15) * 128)
+                             : "memory");
+            else if (in)
+                ((uint16_t *)ob)[p] = (uint16_t)v;
         } else {                                          /* {I0 Q0 I1 Q1 ...} MSB first */
             /* I16 > 0 <=> sum I + 64 >= 128 <=> the I field (low 22 bits) >= 2^21 + 128;
                Q16 > 0 <=> acc >= 2^29 (gpssim.c:2266-2276: bit = iq_buff[] > 0) */
