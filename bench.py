@@ -283,7 +283,7 @@ def e2e_run(G, dev, threads, window=1800.0):
             got["blocks"] += nb
 
         t0 = time.perf_counter()
-        dev.run(s, sink, batch=256, threads=threads)
+        dev.run(s, sink, batch=128, threads=threads)
         return time.perf_counter() - t0, got["blocks"], got["bytes"], s.n_per_blk
 
     ws, bs, _, _ = one(window / 3)
@@ -296,7 +296,7 @@ def e2e_run(G, dev, threads, window=1800.0):
             "steady_MSps": round(slope * n_per_blk / 1e6, 1),
             "steady_d2h_GBps": round(slope * nbytes / blocks / 1e9, 2),
             "startup_s": round(wall - blocks / slope, 3),
-            "d2h_ceiling_GBps": d2h_ceiling(256 * n_per_blk * 4),
+            "d2h_ceiling_GBps": d2h_ceiling(128 * n_per_blk * 4),
             "workload": f"static -b 16, {window:g} s through gss_run (batch 256 blocks), "
                         "discarding sink"}
 

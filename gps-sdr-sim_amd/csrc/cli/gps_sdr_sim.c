@@ -73,7 +73,7 @@ static int run_rank(const gss_cli_t *cli, gss_scn *scn, const gss_scn_info_t *in
         fprintf(stderr, "ERROR: Failed to open output file.\n");
         return 1;
     }
-    if (gss_run(dev, scn, first, last - first, env_int("GSS_BATCH", 100),
+    if (gss_run(dev, scn, first, last - first, env_int("GSS_BATCH", 128),
                 env_int("GSS_THREADS", 8), pwrite_sink, &c)) {
         fprintf(stderr, "\nERROR: rank %d: %s\n", rank, gss_last_error());
         return 1;
@@ -124,7 +124,7 @@ int main(int argc, char **argv)
             return 1;
         }
     }
-    int batch = env_int("GSS_BATCH", 100);
+    int batch = env_int("GSS_BATCH", 128);
     int threads = env_int("GSS_THREADS", 8);
     if (batch < 1) batch = 1;
     clock_t t0 = clock();

@@ -20,7 +20,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
+#include <time.h>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -37,6 +39,23 @@ extern "C" int gss_fail(int code, const char *fmt, ...);
     } while (0)
 
 namespace {
+
+/* GSS_RUN_TRACE=1: per-slot timestamps on stderr (planner start/end, submit, drain wait/end) */
+static double tnow()
+{
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+static int trace_on()
+{
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("GSS_RUN_TRACE");
+        on = e && e[0] == '1';
+    }
+    return on;
+}
 
 #ifndef GSS_RUN_NCOPY
 #define GSS_RUN_NCOPY 1
@@ -102,7 +121,9 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
         if (*cursor < r.first && r.first - *cursor < ask)
             ask = (int)(r.first - *cursor);            /* stop exactly at the range start */
         int nb = 0;
-        int rc = gss_scn_next(r.scn, ask, sl.blk, sl.nch, sl.ck, &nb, r.threads);
+        /* before the range only the carrier chain matters: no checkpoints recorded */
+        int rc = gss_scn_next(r.scn, ask, sl.blk, sl.nch, *cursor < r.first ? nullptr : sl.ck,
+                              &nb, r.threads);
         if (rc)
             return rc;
         if (nb == 0) {
@@ -162,7 +183,10 @@ void planner(Run *r)
             if (r->abort)
                 return;
         }
+        const double t0 = trace_on() ? tnow() : 0.0;
         int rc = plan_into(*r, sl, &cursor);
+        if (trace_on())
+            fprintf(stderr, "trace plan slot %d nb %d %.6f %.6f\n", i % NSLOT, sl.nb, t0, tnow());
         {
             std::lock_guard<std::mutex> lk(r->mu);
             if (rc) {
@@ -237,11 +261,16 @@ int submit(gss_dev *d, Slot &sl, const uint32_t *d_ca, int n_per_blk, int fmt, s
 
 int drain(Run &r, Slot &sl, size_t bb, gss_sink_fn sink, void *user)
 {
+    const double t0 = trace_on() ? tnow() : 0.0;
     RUN_TRY(hipEventSynchronize(sl.done));
+    const double t1 = trace_on() ? tnow() : 0.0;
     if (*sl.h_status)
         return gss_fail(GSS_E_RANGE, "nav word index ran past dwrd[59]");
     if (sink(user, sl.h_out, bb * (size_t)sl.nb, sl.first, sl.nb))
         return gss_fail(GSS_E_IO, "sink failed at block %lld", (long long)sl.first);
+    if (trace_on())
+        fprintf(stderr, "trace drain first %lld wait %.6f %.6f sink_end %.6f\n",
+                (long long)sl.first, t0, t1, tnow());
     {
         std::lock_guard<std::mutex> lk(r.mu);
         sl.state = FREE;
@@ -281,7 +310,10 @@ int run_main(gss_dev *d, Run &r, int n_per_blk, int fmt, size_t bb, gss_sink_fn 
             head = (head + 1) % DEPTH;
             np--;
         }
+        const double ts0 = trace_on() ? tnow() : 0.0;
         int rc = submit(d, sl, d_ca, n_per_blk, fmt, bb, st, cp[i % NCOPY]);
+        if (trace_on())
+            fprintf(stderr, "trace submit slot %d %.6f %.6f\n", i % NSLOT, ts0, tnow());
         if (rc)
             return rc;
         pending[(head + np) % DEPTH] = i % NSLOT;

@@ -73,6 +73,9 @@ struct gss_scn {
     int8_t *b_slot;                         /* [b][k] slot of entry k */
     uint8_t *b_reset;                       /* [b][k] 1 if the slot's chain restarts here */
     double *b_init;                         /* [b][k] restart value */
+    /* ranges of the blocks up to the next 30 s update, computed in parallel (range_pass) */
+    rng_t *rg;                              /* [j][slot] */
+    int rg_cap;
 };
 
 static void msg(const gss_scn *s, const char *fmt, ...)
@@ -448,6 +451,80 @@ static void plan_batch(gss_scn *s, gss_chan_blk_t *blk, const int32_t *nch, doub
             pthread_join(tid[t], NULL);
 }
 
+/* ---- per-block ranges in parallel --------------------------------------------------------------
+ * The per-block refresh (gpssim.c:2156-2188) needs computeRange for every active channel of
+ * every block, and block b only uses its own range and block b-1's.  Between two 30 s updates the
+ * channel set, the ephemeris set and the receiver positions are fixed, so the ranges of a run of
+ * blocks up to the next update are independent: threads compute them (range_pass), then the
+ * refresh walks the run in order with the same arithmetic as before. */
+typedef struct {
+    const gss_scn *s;
+    const gtime_t *g;                       /* [j] receiver time of block j of the run */
+    int j0, nj, jstep;
+    int iumd0;
+} range_job;
+
+static void *range_worker(void *arg)
+{
+    range_job *r = arg;
+    const gss_scn *s = r->s;
+    for (int j = r->j0; j < r->nj; j += r->jstep) {
+        const double *xyz = s->static_mode ? s->xyz[0] : s->xyz[r->iumd0 + j];
+        for (int i = 0; i < K_MAX_CHAN; i++) {
+            const chan_t *ch = &s->chan[i];
+            if (ch->prn > 0)
+                sv_range(&s->rg[(size_t)j * K_MAX_CHAN + i], &s->eph[s->ieph][ch->prn - 1],
+                         &s->io, r->g[j], xyz);
+        }
+    }
+    return NULL;
+}
+
+/* blocks of the run from the current one that share its channel set (the last is the one after
+   which the 30 s update runs), at most max_j; their ranges into s->rg */
+static int range_pass(gss_scn *s, int max_j, int threads)
+{
+    gtime_t gbuf[300 + 1];
+    int nj = 0;
+    gtime_t g = s->grx;
+    while (nj < max_j && nj < 300 && s->iumd + nj < s->numd) {
+        gbuf[nj++] = g;
+        if ((int)(g.sec * 10.0 + 0.5) % 300 == 0)
+            break;
+        g = gt_add(g, 0.1);
+    }
+    if (nj > s->rg_cap) {
+        free(s->rg);
+        s->rg = malloc((size_t)nj * K_MAX_CHAN * sizeof(rng_t));
+        if (s->rg == NULL) {
+            s->rg_cap = 0;
+            return gss_fail(GSS_E_NOMEM, "out of memory");
+        }
+        s->rg_cap = nj;
+    }
+    if (threads < 1)
+        threads = 1;
+    if (threads > 32)
+        threads = 32;
+    if (threads > nj)
+        threads = nj;
+    pthread_t tid[32];
+    range_job job[32];
+    int started = 0;
+    for (int t = 0; t < threads; t++) {
+        job[t] = (range_job){s, gbuf, t, nj, threads, s->iumd};
+        if (t > 0 && pthread_create(&tid[t], NULL, range_worker, &job[t]) == 0)
+            started |= 1u << t;
+        else if (t > 0)
+            range_worker(&job[t]);
+    }
+    range_worker(&job[0]);
+    for (int t = 1; t < threads; t++)
+        if (started & (1u << t))
+            pthread_join(tid[t], NULL);
+    return nj;
+}
+
 int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, double *carr_ck,
                  int *n_out, int threads)
 {
@@ -466,19 +543,25 @@ int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, 
         s->batch_cap = max_blocks;
     }
 
-    int nb = 0;
+    int nb = 0, jr = 0, nr = 0;                /* block jr of a range pass of nr blocks */
     while (nb < max_blocks && s->iumd < s->numd) {
         const double *xyz = s->static_mode ? s->xyz[0] : s->xyz[s->iumd];
         gss_chan_blk_t *row = blk + (size_t)nb * GSS_MAXCH;
         int k = 0;
+        if (jr == nr) {
+            nr = range_pass(s, max_blocks - nb, threads);
+            if (nr < 0)
+                return nr;
+            jr = 0;
+        }
+        const rng_t *rg = s->rg + (size_t)jr++ * K_MAX_CHAN;
 
         /* ---- per-block refresh (gpssim.c:2156-2188) ---- */
         for (int i = 0; i < K_MAX_CHAN; i++) {
             chan_t *ch = &s->chan[i];
             if (ch->prn <= 0)
                 continue;
-            rng_t rho;
-            sv_range(&rho, &s->eph[s->ieph][ch->prn - 1], &s->io, s->grx, xyz);
+            const rng_t rho = rg[i];           /* sv_range at s->grx, xyz (range_pass) */
             ch->azel[0] = rho.azel[0];
             ch->azel[1] = rho.azel[1];
 
@@ -597,6 +680,7 @@ int gss_scn_close(gss_scn *s)
     free(s->b_slot);
     free(s->b_reset);
     free(s->b_init);
+    free(s->rg);
     free(s);
     return 0;
 }

@@ -36,6 +36,13 @@ def plan_rank(nav_file, rank, world, window_s, *, llh, samp_freq=2.6e6, data_for
                    samp_freq=samp_freq, data_format=data_format)
     done, keep_b, keep_n, keep_c = 0, [], [], []
     while done < first + count:
+        if done < first:             # before the window only the carrier chain matters
+            ask = min(batch, first - done)
+            b, n = scn.next(ask, threads=threads)
+            if len(n) == 0:
+                break
+            done += len(n)
+            continue
         b, n, c = scn.next(min(batch, first + count - done), threads=threads, with_ck=True)
         if len(n) == 0:
             break

@@ -23,7 +23,7 @@ for window in [float(w) for w in (sys.argv[1:] or ["60", "600", "1800", "3600"])
             t["first"] = time.perf_counter() - t0
         t["blocks"] += nb
 
-    dev.run(s, sink, batch=256, threads=16)
+    dev.run(s, sink, batch=int(os.environ.get("GSS_PROBE_BATCH", "256")), threads=16)
     wall = time.perf_counter() - t0
     rows.append((window, wall, t["first"], t["blocks"]))
     print(f"window {window:7.0f} s  wall {wall:.3f} s  first sink {t['first']:.3f} s  "
