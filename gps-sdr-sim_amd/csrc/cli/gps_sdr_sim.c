@@ -10,7 +10,7 @@
  * (every rank ftruncate()s FILE to the run's size first, safe in any order): the same file as
  * one process writes, with no collective.
  * Env: GSS_DEVICE (ordinal; default LOCAL_RANK or 0), GSS_BATCH (blocks per launch, default
- *      100), GSS_THREADS (planner threads, default 8).
+ *      128), GSS_THREADS (planner threads, default 8).
  */
 #include <fcntl.h>
 #include <stdio.h>
