@@ -87,8 +87,11 @@ def cpu_baseline(seconds=30, cores=BOX_CORES):
 
     def run(n):
         t0 = time.perf_counter()
-        ps = [subprocess.Popen(["taskset", "-c", str(avail[i])] + args, env=env,
-                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        # pinned in the child before it runs the program (no launcher such as taskset, whose
+        # own exec would be one more hop)
+        ps = [subprocess.Popen(args, env=env, stdout=subprocess.DEVNULL,
+                               stderr=subprocess.DEVNULL,
+                               preexec_fn=(lambda c=avail[i]: os.sched_setaffinity(0, {c})))
               for i in range(n)]
         ok = all(p.wait() == 0 for p in ps)
         return (time.perf_counter() - t0) if ok else None
@@ -161,8 +164,10 @@ def live_traffic(fmt, window, threads, kern_ms, timeout=150):
               ("pmc_fetch", ["--pmc", "FETCH_SIZE", "--kernel-trace"])]
     try:
         for name, opts in passes:
-            cmd = ["rocprofv3"] + opts + ["-d", os.path.join(top, name), "-o", name, "-f", "csv",
-                                          "--"] + child
+            # the rocprofv3 script run by this interpreter directly (its `#!/usr/bin/env python3`
+            # line would be one more exec hop)
+            cmd = [sys.executable, shutil.which("rocprofv3")] + opts + [
+                "-d", os.path.join(top, name), "-o", name, "-f", "csv", "--"] + child
             outf = os.path.join(top, name + ".out")
             p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=open(outf, "w"),
                                  stderr=subprocess.DEVNULL, start_new_session=True)

@@ -1,14 +1,15 @@
 #!/bin/bash
 # Profiling session on the GPU box (rocprofv3): kernel trace + stats, then one PMC pass per
 # counter group (never combined with other trace domains).  Outputs under gpurun_out/prof_<tag>/.
-# Usage: bash tools/profile.sh [tag]   (bench args via BENCH_ARGS)
+# Usage: bash tools/profile.sh [tag]   (bench args via PROF_BENCH_ARGS; never the CPU baseline
+# or the live PMC passes: a profiled process has the GPU initialised, so it must start no programs)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-r2}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BA=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --no-exact --no-configs --no-e2e}
+BA="${PROF_BENCH_ARGS:---steps 3 --warmup 1 --no-exact --no-configs --no-e2e} --no-cpu-baseline --no-pmc"
 run() {  # name, rocprofv3 args...
     local name=$1; shift
     timeout -k 10 400 rocprofv3 "$@" -d $OUT/$name -o $name -f csv -- python3 bench.py $BA \
