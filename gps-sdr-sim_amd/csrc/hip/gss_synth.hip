@@ -526,6 +526,23 @@ static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole ch
 #ifndef LIN_ABLATE
 #define LIN_ABLATE 0
 #endif
+/* LIN_MFMA 1: the gain x LUT accumulation runs on the matrix cores instead of v_mad_i64_i32.
+   The LUT holds (cos, sin) as an f16 pair (exact integers, |v| <= 250); per channel and pair of
+   steps one v_mfma_f32_4x4x4_16b_f16 takes B = the lane's two LUT words (K = cos_s, sin_s,
+   cos_s+1, sin_s+1) and A = the gain placed at slot i of lane 4b + i (f16, exact for
+   |g| <= 2048; the proof certifies |g| <= 1024 so that gain differences stay exact too), so
+   block b's column j -- lane 4b + j's own sample -- receives rows (I_s, Q_s, I_s+1, Q_s+1).
+   The f32 accumulators start at 1.5 2^23 + 64: every partial sum is an integer below 2^24 in
+   magnitude, so the matrix core's sums are exact in any order, and the IEEE bits of the result
+   are 0x4B400000 + (sum + 64), from which (sum + 64) >> 7 is a shift
+   (tools/ubench/mfma_probe.hip: operand layout and exactness on gfx950). */
+#ifndef LIN_MFMA
+#define LIN_MFMA 0
+#endif
+typedef _Float16 lin_half4 __attribute__((ext_vector_type(4)));
+typedef float lin_f4 __attribute__((ext_vector_type(4)));
+#define LIN_MAGF  12582976.0f                   /* 1.5 2^23 + 64                          */
+#define LIN_MAGB  0x4B400000u                   /* IEEE bits of 1.5 2^23                  */
 
 /* per (block, segment wave, chunk, channel): the chunk's render parameters, built by the wave's
    lanes in parallel (vector loads and VALU) and read back by the render loop with broadcast LDS
@@ -540,6 +557,9 @@ struct lin_ct {
     uint32_t flags;              /* 1: a gain change inside the chunk, 2: patched samples       */
     uint32_t q0, dq, tab, pad;   /* first window offset (1/16 chip), its step, the row          */
     uint32_t W[LIN_CH];          /* the steps' chip windows                                     */
+#if LIN_MFMA
+    uint32_t A[4][2];            /* the MFMA gain operand of lane 4b + i: g (f16) at slot i      */
+#endif
 };
 
 /* per (block, channel): the render constants of gss_lin.h (written by gss_linseg_kernel) */
@@ -657,6 +677,56 @@ __device__ __forceinline__ void lin_channel_chunk(int64_t (&acc)[LIN_CH], uint64
     }
 }
 
+/* LIN_MFMA: the same steps, the accumulation on the matrix cores (one MFMA per two steps; with
+   LANE_GAIN the LUT words of samples before pos1 are zeroed and A carries the gain difference) */
+template <bool LANE_GAIN>
+__device__ __forceinline__ void lin_channel_chunk_m(lin_f4 (&cq)[LIN_CH / 2], uint64_t P,
+                                                    uint64_t D, const uint32_t *W, uint32_t M,
+                                                    lin_half4 A, int pos1, int p0,
+                                                    const int32_t *__restrict__ s_lut)
+{
+    uint4 w4;
+    uint32_t e0 = 0;
+#pragma unroll
+    for (int s = 0; s < LIN_CH; s++) {
+        if (s % 4 == 0) {
+            if (LIN_ABLATE & 64)
+                w4 = make_uint4(M * (s + 1), M * (s + 3), M * (s + 5), M * (s + 7));
+            else
+                w4 = ((const uint4 *)W)[s / 4];
+        }
+        const uint32_t ws = s % 4 == 0 ? w4.x : s % 4 == 1 ? w4.y : s % 4 == 2 ? w4.z : w4.w;
+        uint32_t t;
+        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
+            "src1_sel:DWORD" : "=v"(t) : "v"((uint32_t)P), "v"(ws));             /* bit 0: sign */
+        const uint32_t a = __builtin_amdgcn_alignbit(t, (uint32_t)(P >> 32), 21) & M;
+        uint32_t e = *(const uint32_t *)((const char *)s_lut + a);
+        if (LANE_GAIN)
+            e = p0 + s * 64 >= pos1 ? e : 0u;
+        if (s & 1) {
+            const uint2 bb = make_uint2(e0, e);
+            cq[s / 2] = __builtin_amdgcn_mfma_f32_4x4x4f16(A, __builtin_bit_cast(lin_half4, bb),
+                                                          cq[s / 2], 0, 0, 0);
+        } else {
+            e0 = e;
+        }
+        P += D;
+    }
+}
+
+/* the MFMA gain operand of this lane (g at slot lane mod 4, f16 bits gh) */
+__device__ __forceinline__ lin_half4 lin_gain_operand(uint32_t gh, int lane)
+{
+    const uint32_t x = gh << ((lane & 1) * 16);
+    const uint2 v = (lane & 2) ? make_uint2(0u, x) : make_uint2(x, 0u);
+    return __builtin_bit_cast(lin_half4, v);
+}
+
+__device__ __forceinline__ uint32_t lin_f16_bits(int g)
+{
+    return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)g);
+}
+
 /* output stores: the stream is written once and never read back by this kernel, while each
    XCD's L2 must keep the chip-window table warm.  LIN_STORE_POLICY: 0 plain,
    1 nt, 2 sc1 (drops the line from L2), 3 sc0 sc1 */
@@ -681,30 +751,78 @@ __device__ __forceinline__ void lin_put(uint32_t *p, uint32_t v)
 /* v_writelane_b32: a wave-uniform value into one lane (no clang builtin in this toolchain) */
 extern "C" __device__ int gss_writelane(int, int, int) __asm("llvm.amdgcn.writelane.i32");
 
-template <int FMT, bool TAIL>
-__device__ __forceinline__ void lin_store(const int64_t (&acc)[LIN_CH], uint8_t *__restrict__ ob,
+/* Per step s of a chunk, from either accumulator: the -b 16 sample word (I16 | Q16 << 16), the
+   -b 8 halfword (I8 | Q8 << 8) and the -b 1 signs (I16 > 0, Q16 > 0), gpssim.c:2257-2287.
+   Packed int64: acc = (sum I + 64 + 2^21) + 2^22 (sum Q + 64); the 2^21 bias keeps the I field
+   non-negative, so (sum Q + 64) >> 7 is bits 29.. of acc and (sum I + 64) >> 7 is the 15-bit
+   field at bit 7 with its top bit flipped.
+   MFMA f32 (LIN_MFMA): the IEEE bits of 1.5 2^23 + (sum + 64) are 0x4B400000 + (sum + 64), so
+   (sum + 64) >> n is the word shifted by n, offset by 0x4B400000 >> n (whose low 16 bits are
+   0x8000 for n = 7 and whose low byte is 0 for n = 11). */
+__device__ __forceinline__ uint32_t lin_w16(const int64_t (&acc)[LIN_CH], int s)
+{
+    const uint32_t lo = (uint32_t)acc[s], hi = (uint32_t)(acc[s] >> 32);
+    const int i16 = __builtin_amdgcn_sbfe((int)(lo ^ (1u << 21)), 7, 15);
+    const uint32_t q16 = __builtin_amdgcn_alignbit(hi, lo, 29);
+    return __builtin_amdgcn_perm(q16, (uint32_t)i16, 0x05040100u);
+}
+__device__ __forceinline__ uint32_t lin_w8(const int64_t (&acc)[LIN_CH], int s)
+{
+    const uint32_t lo = (uint32_t)acc[s], hi = (uint32_t)(acc[s] >> 32);
+    const int i8 = __builtin_amdgcn_sbfe((int)(lo ^ (1u << 21)), 11, 11);
+    const uint32_t q8 = (uint32_t)((int)hi >> 1);
+    return __builtin_amdgcn_perm(q8, (uint32_t)i8, 0x0c0c0400u);
+}
+__device__ __forceinline__ bool lin_ipos(const int64_t (&acc)[LIN_CH], int s)
+{
+    return ((uint32_t)acc[s] & 0x3FFFFFu) >= (1u << 21) + 128u;
+}
+__device__ __forceinline__ bool lin_qpos(const int64_t (&acc)[LIN_CH], int s)
+{
+    return acc[s] >= ((int64_t)1 << 29);
+}
+__device__ __forceinline__ uint32_t lin_ib(const lin_f4 (&cq)[LIN_CH / 2], int s)
+{
+    return __float_as_uint(cq[s / 2][2 * (s & 1)]);
+}
+__device__ __forceinline__ uint32_t lin_qb(const lin_f4 (&cq)[LIN_CH / 2], int s)
+{
+    return __float_as_uint(cq[s / 2][2 * (s & 1) + 1]);
+}
+__device__ __forceinline__ uint32_t lin_w16(const lin_f4 (&cq)[LIN_CH / 2], int s)
+{
+    return __builtin_amdgcn_perm(lin_qb(cq, s) >> 7, lin_ib(cq, s) >> 7, 0x05040100u) ^
+           0x80008000u;
+}
+__device__ __forceinline__ uint32_t lin_w8(const lin_f4 (&cq)[LIN_CH / 2], int s)
+{
+    return __builtin_amdgcn_perm(lin_qb(cq, s) >> 11, lin_ib(cq, s) >> 11, 0x0c0c0400u);
+}
+__device__ __forceinline__ bool lin_ipos(const lin_f4 (&cq)[LIN_CH / 2], int s)
+{
+    return lin_ib(cq, s) >= LIN_MAGB + 128u;
+}
+__device__ __forceinline__ bool lin_qpos(const lin_f4 (&cq)[LIN_CH / 2], int s)
+{
+    return lin_qb(cq, s) >= LIN_MAGB + 128u;
+}
+
+template <int FMT, bool TAIL, class ACC>
+__device__ __forceinline__ void lin_store(const ACC &acc, uint8_t *__restrict__ ob,
                                           int nb0, int lane, int n_per_blk)
 {
     uint32_t pk[LIN_CH];
     pk[0] = 0;
 #pragma unroll
     for (int s = 0; s < LIN_CH; s++) {
-        /* acc = (sum I + 64 + 2^21) + 2^22 (sum Q + 64): the 2^21 bias keeps the I field
-           non-negative, so (sum Q + 64) >> 7 is bits 29.. of acc and (sum I + 64) >> 7 is the
-           15-bit field at bit 7 with its top bit flipped (gpssim.c:2257-2263) */
-        const uint32_t lo = (uint32_t)acc[s], hi = (uint32_t)(acc[s] >> 32);
         const int nb = nb0 + s * 64, p = nb + lane;
         const bool in = !TAIL || p < n_per_blk;
         if (FMT == 16) {
             /* packed first, stored after the loop: distinct data registers, so a store never
                holds up the next pack (a VMEM store reads its data VGPR after issue) */
-            const int i16 = __builtin_amdgcn_sbfe((int)(lo ^ (1u << 21)), 7, 15);
-            const uint32_t q16 = __builtin_amdgcn_alignbit(hi, lo, 29);
-            pk[s] = __builtin_amdgcn_perm(q16, (uint32_t)i16, 0x05040100u);
+            pk[s] = lin_w16(acc, s);
         } else if (FMT == 8) {                            /* iq_buff >> 4 → signed char */
-            const int i8 = __builtin_amdgcn_sbfe((int)(lo ^ (1u << 21)), 11, 11);
-            const uint32_t q8 = (uint32_t)((int)hi >> 1);
-            const uint32_t v = __builtin_amdgcn_perm(q8, (uint32_t)i8, 0x0c0c0400u);
+            const uint32_t v = lin_w8(acc, s);
             if (!TAIL && LIN_SADDR)               /* SGPR base, 32-bit lane offset, as -b 16 */
                 asm volatile("global_store_short %0, %1, %2 offset:%3"
                              : : "v"((uint32_t)lane * 2u), "v"(v),
@@ -715,8 +833,8 @@ __device__ __forceinline__ void lin_store(const int64_t (&acc)[LIN_CH], uint8_t 
         } else {                                          /* {I0 Q0 I1 Q1 ...} MSB first */
             /* I16 > 0 <=> sum I + 64 >= 128 <=> the I field (low 22 bits) >= 2^21 + 128;
                Q16 > 0 <=> acc >= 2^29 (gpssim.c:2266-2276: bit = iq_buff[] > 0) */
-            const uint64_t mi = __builtin_amdgcn_ballot_w64((lo & 0x3FFFFFu) >= (1u << 21) + 128u);
-            const uint64_t mq = __builtin_amdgcn_ballot_w64(acc[s] >= ((int64_t)1 << 29));
+            const uint64_t mi = __builtin_amdgcn_ballot_w64(lin_ipos(acc, s));
+            const uint64_t mq = __builtin_amdgcn_ballot_w64(lin_qpos(acc, s));
             /* lane 4s + j collects the I (low half) and Q (high half) sign bits of samples
                64 s + 16 j .. + 15: scalar packs, one lane write each */
             const uint32_t ilo = (uint32_t)mi, ihi = (uint32_t)(mi >> 32);
@@ -793,6 +911,34 @@ __device__ __forceinline__ void lin_patch_fix(int64_t (&acc)[LIN_CH],
     }
 }
 
+/* ... the same on the MFMA accumulators: the packed delta dI + 2^22 dQ split into its two exact
+   integers, added in f32 (exact: integers below 2^24) */
+__device__ __forceinline__ void lin_patch_fix(lin_f4 (&cq)[LIN_CH / 2],
+                                              const gss_lin_t *__restrict__ Lk, int nb0, int lane)
+{
+    for (int j = 0; j < GSS_NPATCH; j++) {
+        const int pp = Lk->ppos[j];                   /* ascending, unused = INT32_MAX */
+        if (pp >= nb0 + 64 * LIN_CH)
+            break;
+        if (pp < nb0)
+            continue;
+        const int q = pp - nb0;
+        const int64_t d = lane == (q & 63) ? Lk->pdelta[j] : 0;
+        const int di = (int)((uint32_t)d << 10) >> 10;
+        const float fi = (float)di, fq = (float)(int)((d - di) >> 22);
+        /* every accumulator takes fi (fq) times a wave-uniform 0 or 1: in-place multiply-adds
+           (exact), no branches and no selects that would keep two copies of the set live */
+        const int sq = __builtin_amdgcn_readfirstlane(q >> 6);
+#pragma unroll
+        for (int s = 0; s < LIN_CH; s++) {
+            const float m = s == sq ? 1.0f : 0.0f;
+            cq[s / 2][2 * (s & 1)] = __builtin_fmaf(m, fi, cq[s / 2][2 * (s & 1)]);
+            cq[s / 2][2 * (s & 1) + 1] = __builtin_fmaf(m, fq, cq[s / 2][2 * (s & 1) + 1]);
+        }
+    }
+}
+
+
 template <int FMT>
 #ifndef LIN_MINB
 #define LIN_MINB 8                         /* workgroups per CU the register budget must allow  */
@@ -814,9 +960,15 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);    /* wave-uniform: scalar */
     for (int i = tid; i < 512; i += LIN_THREADS) {
-        const int32_t v = (int32_t)lut.cos512[i] + (int32_t)lut.sin512[i] * (1 << 22);
-        s_lut[i] = v;
-        s_lut[512 + i] = -v;
+        if (LIN_MFMA) {                                   /* (cos, sin) f16; [512+i] negated */
+            const uint32_t v = lin_f16_bits(lut.cos512[i]) | (lin_f16_bits(lut.sin512[i]) << 16);
+            s_lut[i] = (int32_t)v;
+            s_lut[512 + i] = (int32_t)(v ^ 0x80008000u);
+        } else {
+            const int32_t v = (int32_t)lut.cos512[i] + (int32_t)lut.sin512[i] * (1 << 22);
+            s_lut[i] = v;
+            s_lut[512 + i] = -v;
+        }
     }
     const lin_chan *CH = chans + (size_t)b * GSS_MAXCH;
     const int nc = nch[b];
@@ -861,6 +1013,13 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
             t.q0 = (uint32_t)(zb >> 46) + (16 * CBW_PRE - 1);
             t.dq = ck.dq;
             t.tab = ck.tab;
+#if LIN_MFMA
+            const uint32_t gh = lin_f16_bits(t.g);        /* lane 4b + i's gain operand */
+            t.A[0][0] = gh;         t.A[0][1] = 0;
+            t.A[1][0] = gh << 16;   t.A[1][1] = 0;
+            t.A[2][0] = 0;          t.A[2][1] = gh;
+            t.A[3][0] = 0;          t.A[3][1] = gh << 16;
+#endif
         }
         wave_sync_lds();
         /* ---- the chip windows, lane (k, s) ---- */
@@ -882,6 +1041,31 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
             T[k].W[i % LIN_CH] = wv;
         }
         wave_sync_lds();
+#if LIN_MFMA
+        lin_f4 acc[LIN_CH / 2];
+#pragma unroll
+        for (int s = 0; s < LIN_CH / 2; s++) {
+            acc[s] = lin_f4{LIN_MAGF, LIN_MAGF, LIN_MAGF, LIN_MAGF};
+            asm volatile("" : "+v"(acc[s]));
+        }
+        for (int k = 0; k < nc; k++) {                    /* uniform channel loop */
+            const lin_ct &t = T[k];
+            const uint64_t B = t.B, D = t.D;
+            const uint32_t fl = __builtin_amdgcn_readfirstlane(t.flags);
+            const uint2 a2 = *(const uint2 *)t.A[lane & 3];
+            lin_channel_chunk_m<false>(acc, s_lane[k * 64 + lane] + B, D, t.W, M,
+                                       __builtin_bit_cast(lin_half4, a2), 0, 0, s_lut);
+            if (__builtin_expect(fl & 1u, 0)) {
+                uint32_t l2 = (uint32_t)lane;
+                asm volatile("" : "+v"(l2));
+                lin_channel_chunk_m<true>(acc, s_lane[k * 64 + l2] + B, D, t.W, M,
+                                          lin_gain_operand(lin_f16_bits(t.gd), (int)l2), t.pos1,
+                                          nb0 + (int)l2, s_lut);
+            }
+            if (__builtin_expect(fl & 2u, 0))
+                lin_patch_fix(acc, L + k, nb0, lane);
+        }
+#else
         int64_t acc[LIN_CH];
 #pragma unroll
         for (int s = 0; s < LIN_CH; s++) {
@@ -903,13 +1087,14 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
             if (__builtin_expect(fl & 2u, 0))
                 lin_patch_fix(acc, L + k, nb0, lane);
         }
+#endif
         wave_sync_lds();                                  /* T is rewritten by the next chunk */
         if (LIN_ABLATE & 1) {
-            int64_t x = 0;
+            uint32_t x = 0;
 #pragma unroll
             for (int s = 0; s < LIN_CH; s++)
-                x ^= acc[s];
-            if (x == 0x123456789)
+                x ^= lin_w16(acc, s);
+            if (x == 0x12345678u)
                 ob[lane] = 1;
         } else if (nb0 + 64 * LIN_CH <= n_per_blk)
             lin_store<FMT, false>(acc, ob, nb0, lane, n_per_blk);

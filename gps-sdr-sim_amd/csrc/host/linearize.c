@@ -411,6 +411,9 @@ static void *lin_run(void *arg)
             ok = lin_channel(p, j->n_per_blk, j->nav + (size_t)p->nav_tbl * GSS_NAV_WORDS,
                              j->ca + (size_t)p->ca_tbl * GSS_CA_WORDS,
                              &j->lin[(size_t)b * GSS_MAXCH + k]);
+            if (p->gain > 1024 || p->gain < -1024)    /* an exact f16 MFMA operand, and so is
+                                                         its doubled data-bit difference */
+                ok = 0;
         }
         /* the packed I/Q accumulator (gss_lin_kernel) needs 250*sum|gain| + 64 < 2^21 */
         if (gsum > 8000)

@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 name=$1; flags=$2
 mkdir -p _var/$name/obj
 HIPCC=/opt/rocm/bin/hipcc
-F="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Iinclude -Wno-unused-result $flags"
+F="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Iinclude -Wno-unused-result -mllvm -amdgpu-mfma-vgpr-form=1 $flags"
 $HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_synth.hip -o _var/$name/obj/gss_synth.o
 $HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_run.hip -o _var/$name/obj/gss_run.o
 HOSTOBJ=gps-sdr-sim_amd/obj/host/*.o
