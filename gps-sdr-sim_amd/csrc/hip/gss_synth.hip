@@ -19,7 +19,8 @@
  *                               over channels with v_dot2 on packed int16, (acc+64)>>7,
  *                               SC16/SC08/SC01 packing.  Output is staged per lane in LDS
  *                               (128 B) and stored by the wave as whole 128-B lines.
- * Integer/byte work on f64 phases: no MFMA.
+ * gss_lin_kernel (the fast path, below) renders the blocks the host proof certifies: integer
+ * phase lines, LDS LUT reads, and the gain x LUT sums on the matrix cores (LIN_MFMA).
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -493,7 +494,8 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
                                     2..10, chip sign at bit 11 (second half of the LUT negated)
        acc += g * LUT[a]       packed I/Q                                       v_mad_i64_i32
        P += D                  carrier and code together                        v_lshl_add_u64
-   5 VALU + 1 LDS per channel-sample.  Measured (profiles/round2/ablate_b1.log, ablate_b2.log):
+   5 VALU + 1 LDS per channel-sample; with LIN_MFMA (the default build) the accumulate is one
+   v_mfma_f32_4x4x4_16b_f16 per channel and two steps instead (4 VALU + 1 LDS + 1/2 MFMA).  Measured (profiles/round2/ablate_b1.log, ablate_b2.log):
    without any memory access the kernel still takes 75-80 % of its time, and the scalar unit,
    one per CU for four SIMDs, was the next limit once the loop lost its 64-bit code add (the
    per-channel scalar work of a chunk, ~90 instructions, cost more than the steps' VALU).  So the
