@@ -122,3 +122,25 @@ def test_lin_patched_samples_vs_oracle(dev):
     assert dev.timing_lin()[0] == 1
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:5]}"
+
+
+@pytest.mark.parametrize("fmt", [16, 8, 1])
+def test_lin_mfma_sum_extremes_vs_oracle(dev, fmt):
+    """The largest certified sums: 7 channels at |gain| 1024 (sum 7168, |sum I| up to 1.8 M),
+    mixed signs and data-bit flips, against the oracle's integer loop: the matrix cores' f32
+    sums from 1.5 2^23 + 64 stay exact integers and the packing from the f32 bits is the
+    reference's (sum + 64) >> 7 (gpssim.c:2257-2287)."""
+    rng = np.random.default_rng(1024 + fmt)
+    n = 26004
+    blk, nch, nav = synth_params(rng, 4, [7, 7, 7, 12], n)
+    blk[0, :7]["gain"] = 1024
+    blk[1, :7]["gain"] = [1024, -1024, 1024, -1024, 1000, -999, 1]
+    blk[2, :7]["gain"] = -1024
+    ca = G.ca_table()
+    _, fast = G.linearize(blk, nch, nav, n)
+    assert fast.sum() >= 3
+    want, rc = oracle.synth(blk, nch, ca, nav, n, fmt)
+    assert rc == 0
+    got = dev.synth_host(blk, nch, ca, nav, n, fmt)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:5]}"

@@ -282,3 +282,18 @@ def test_integer_carrier_on_cell_boundaries_like_oracle():
     want, _ = oracle.synth(blk, nch, ca, nav, n, 16)
     got, _ = render_lin(blk, nch, lin, fast, ca, n, 16)
     assert np.array_equal(got, want)
+
+
+def test_gain_bound_of_the_mfma_operand():
+    """The fast kernel's gains are f16 MFMA operands (gss_synth.hip, LIN_MFMA): the proof
+    certifies a block only when every |gain| <= 1024, so that the gain and its doubled
+    data-bit difference are exact f16 integers; larger gains go to the exact path."""
+    rng = np.random.default_rng(7)
+    n = 26000
+    blk, nch, nav = synth_params(rng, 4, [7, 7, 7, 3], n)
+    blk[0, :7]["gain"] = 1024                          # sum 7168 <= 8000: certified
+    blk[1, :7]["gain"] = -1024
+    blk[2, 2]["gain"] = 1025                           # one channel above the bound
+    blk[3, 0]["gain"] = -1025
+    _, fast = G.linearize(blk, nch, nav, n)
+    assert list(fast) == [1, 1, 0, 0]
