@@ -158,6 +158,8 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
             memcpy(sl.nav, rows, sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)n_rows);
         sl.n_nav = n_rows;
         if (r.use_lin) {                               /* the proofs, on the planner thread */
+            if (trace_on())
+                fprintf(stderr, "trace scn_done %.6f\n", tnow());
             rc = gss_linearize(sl.blk, sl.nch, nb, r.n_per_blk, r.ca, 32, sl.nav, n_rows, sl.lin,
                                sl.fast, r.threads);
             if (rc)
