@@ -955,6 +955,10 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
     __shared__ uint64_t s_lane[GSS_MAXCH * 64];           /* lane offsets L(l) per channel    */
     __shared__ lin_ct s_ct[LIN_WAVES][GSS_MAXCH];         /* the current chunk, per wave      */
     __shared__ uint32_t s_cab[GSS_MAXCH][CAB_W];          /* the channels' sign bit-streams   */
+#ifdef LIN_LDS_PAD                                        /* occupancy measurements only      */
+    __shared__ uint32_t s_pad[LIN_LDS_PAD];
+    if (threadIdx.x == 1023) s_pad[blockIdx.x % LIN_LDS_PAD] = 0;
+#endif
     const int b = blockIdx.x / wg_per_blk;
     const int w = blockIdx.x - b * wg_per_blk;
     if (!fast[b])

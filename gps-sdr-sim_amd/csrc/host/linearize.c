@@ -415,7 +415,8 @@ static void *lin_run(void *arg)
                                                          its doubled data-bit difference */
                 ok = 0;
         }
-        /* the packed I/Q accumulator (gss_lin_kernel) needs 250*sum|gain| + 64 < 2^21 */
+        /* the kernel's sums: the packed int64 I/Q accumulator (LIN_MFMA=0) needs
+           250*sum|gain| + 64 < 2^21; the MFMA build's f32 sums from 1.5 2^23 need < 2^22 */
         if (gsum > 8000)
             ok = 0;
         j->fast[b] = ok;
