@@ -495,7 +495,8 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
        acc += g * LUT[a]       packed I/Q                                       v_mad_i64_i32
        P += D                  carrier and code together                        v_lshl_add_u64
    5 VALU + 1 LDS per channel-sample; with LIN_MFMA (the default build) the accumulate is one
-   v_mfma_f32_4x4x4_16b_f16 per channel and two steps instead (4 VALU + 1 LDS + 1/2 MFMA).  Measured (profiles/round2/ablate_b1.log, ablate_b2.log):
+   v_mfma_f32_4x4x4_16b_f16 per channel and two steps instead (4 VALU + 1 LDS + 1/2 MFMA).
+   Measured on the int64 build (profiles/round2/ablate_b1.log, ablate_b2.log):
    without any memory access the kernel still takes 75-80 % of its time, and the scalar unit,
    one per CU for four SIMDs, was the next limit once the loop lost its 64-bit code add (the
    per-channel scalar work of a chunk, ~90 instructions, cost more than the steps' VALU).  So the
