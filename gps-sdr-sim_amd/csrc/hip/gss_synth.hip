@@ -792,14 +792,21 @@ __device__ __forceinline__ uint32_t lin_qb(const lin_f4 (&cq)[LIN_CH / 2], int s
 {
     return __float_as_uint(cq[s / 2][2 * (s & 1) + 1]);
 }
+/* the Q half (byte) is shifted straight into place by an SDWA shift that preserves the rest of
+   the destination: two shifts, no perm */
 __device__ __forceinline__ uint32_t lin_w16(const lin_f4 (&cq)[LIN_CH / 2], int s)
 {
-    return __builtin_amdgcn_perm(lin_qb(cq, s) >> 7, lin_ib(cq, s) >> 7, 0x05040100u) ^
-           0x80008000u;
+    uint32_t d = lin_ib(cq, s) >> 7;
+    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "
+        "src1_sel:DWORD" : "+v"(d) : "v"(7u), "v"(lin_qb(cq, s)));
+    return d ^ 0x80008000u;
 }
 __device__ __forceinline__ uint32_t lin_w8(const lin_f4 (&cq)[LIN_CH / 2], int s)
 {
-    return __builtin_amdgcn_perm(lin_qb(cq, s) >> 11, lin_ib(cq, s) >> 11, 0x0c0c0400u);
+    uint32_t d = lin_ib(cq, s) >> 11;                 /* bytes 2, 3: not stored */
+    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "
+        "src1_sel:DWORD" : "+v"(d) : "v"(11u), "v"(lin_qb(cq, s)));
+    return d;
 }
 __device__ __forceinline__ bool lin_ipos(const lin_f4 (&cq)[LIN_CH / 2], int s)
 {
