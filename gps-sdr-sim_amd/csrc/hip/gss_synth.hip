@@ -748,6 +748,15 @@ __device__ __forceinline__ void lin_put(uint32_t *p, uint32_t v)
         *p = v;
 }
 
+#if LIN_STORE_POLICY == 1
+#define LIN_ST_MOD "nt"
+#elif LIN_STORE_POLICY == 2
+#define LIN_ST_MOD "sc1"
+#elif LIN_STORE_POLICY == 3
+#define LIN_ST_MOD "sc0 sc1"
+#else
+#define LIN_ST_MOD ""
+#endif
 #ifndef LIN_SADDR
 #define LIN_SADDR 1
 #endif
@@ -887,7 +896,7 @@ __device__ __forceinline__ void lin_store(const ACC &acc, uint8_t *__restrict__ 
             const uint32_t off = (uint32_t)lane * 4u;
 #pragma unroll
             for (int s = 0; s < LIN_CH; s++)
-                asm volatile("global_store_dword %0, %1, %2 offset:%3 nt"   /* 13-bit offset */
+                asm volatile("global_store_dword %0, %1, %2 offset:%3 " LIN_ST_MOD  /* 13-bit offset */
                              : : "v"(off), "v"(pk[s]), "s"(base + (s >> 4) * 1024),
                                "i"((s & 15) * 256) : "memory");
         } else {
