@@ -1,0 +1,45 @@
+"""bench.py pieces that need no GPU: the metric is BASELINE.json's, the committed PMC traffic
+record (profiles/pmc_traffic.json) is attached only to the workload, kernel and library build it
+was measured on and only when its kernel time agrees with its own run's events, and the CPU
+baseline runs the reference binary pinned per core without a launcher hop."""
+import json
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+
+def test_metric_is_baselines():
+    base = json.load(open(os.path.join(REPO, "BASELINE.json")))
+    assert bench.METRIC == base["metric"]
+
+
+def test_traffic_record_matches_its_build_only():
+    rec = json.load(open(os.path.join(REPO, "profiles", "pmc_traffic.json")))
+    wl, sha = rec["workload"], rec["lib_sha16"]
+    got, src = bench.load_traffic(wl, "gss_lin_kernel", 1.8, sha)
+    assert got == rec["hbm_bytes_per_launch"] and "profiled kernel" in src
+    # HBM bytes within a few % of the algorithmic bytes: no wasted re-reads
+    assert 1.0 <= got / rec["algorithmic_bytes_per_launch"] < 1.05
+    assert bench.load_traffic(wl, "gss_lin_kernel", 1.8, "0" * 16)[0] is None
+    assert bench.load_traffic(wl + " x", "gss_lin_kernel", 1.8, sha)[0] is None
+    assert bench.load_traffic(wl, "gss_synth_kernel", 1.8, sha)[0] is None
+
+
+def test_committed_profile_agrees_with_its_run():
+    """the profile's warm kernel time is within 5 % of the profiled run's own HIP events"""
+    rec = json.load(open(os.path.join(REPO, "profiles", "pmc_traffic.json")))
+    prof = rec["kernel_warm_avg_ns"] / 1e6
+    assert abs(prof - rec["profiled_run_event_ms"]) <= 0.05 * rec["profiled_run_event_ms"]
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REPO, "oracle", "_ref", "gss_oracle_cli")),
+                    reason="oracle not built")
+def test_cpu_baseline_short_sample():
+    r = bench.cpu_baseline(seconds=1, cores=2)
+    assert r is not None and r["cores"] == 2 and r["value"] > 0
+    assert r["single_core"]["cores"] == 1 and r["kind"] in ("reference", "port")
