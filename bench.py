@@ -50,7 +50,7 @@ FS = 2.6e6
 WINDOW_S = 300.0
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters
 METRIC = "IQ MSamples/s (and × real-time) at 2.6 MS/s, 12 sats, -b 16; 1/2/4/8 GPU"
-BOX_CORES = 16                 # the GPU box's host CPU share for one GPU
+BOX_CORES = 16                 # host threads for the planner/proofs (the box's CPU share per GPU)
 
 # BASELINE.json configs[2..4] (per_config); configs[1] is the headline, configs[0] the CPU case
 CONFIGS = [
@@ -64,11 +64,22 @@ CONFIGS = [
 ]
 
 
-def cpu_baseline(seconds=30, cores=BOX_CORES):
+def cpu_quota():
+    """CPUs' worth of time the cgroup grants this process tree (cgroup v2 cpu.max), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(seconds=30):
     """The reference program (compiled from its own sources by oracle/Makefile) on a bounded
-    sample of the static scenario to /dev/null: one process on one core, then `cores` concurrent
-    processes pinned to cores 0..cores-1 (it is single-threaded by construction).  Falls back to
-    the repo's CPU restatement ("port") when the reference binary is absent."""
+    sample of the static scenario to /dev/null: one process on one core, then one process per
+    core the affinity mask offers (it is single-threaded by construction), each pinned to its
+    core.  `cores` is the affinity size; `cpu_quota` the cgroup's CPU limit when one is set (the
+    aggregate can never exceed it).  Falls back to the repo's CPU restatement ("port") when the
+    reference binary is absent."""
     ref = os.path.join(REPO, "oracle", "_ref", "gps-sdr-sim")
     port = os.path.join(REPO, "oracle", "_ref", "gss_oracle_cli")
     kind, exe = ("reference", ref) if os.path.exists(ref) else ("port", port)
@@ -78,7 +89,7 @@ def cpu_baseline(seconds=30, cores=BOX_CORES):
         avail = sorted(os.sched_getaffinity(0))
     except AttributeError:
         avail = list(range(os.cpu_count() or 1))
-    cores = max(1, min(cores, len(avail)))
+    cores = len(avail)
     args = [exe, "-e", NAV, "-l", ",".join(map(str, LOC)), "-d", str(seconds), "-s",
             str(int(FS)), "-b", "16", "-o", "/dev/null"]
     env = dict(os.environ, GSS_THREADS="1")
@@ -103,12 +114,14 @@ def cpu_baseline(seconds=30, cores=BOX_CORES):
     one = samples / w1 / 1e6
     agg = cores * samples / wn / 1e6
     return {"value": round(agg, 2), "unit": "MS/s", "cores": cores, "kind": kind,
+            "cpu_quota": cpu_quota(),
             "single_core": {"value": round(one, 3), "cores": 1,
                             "x_realtime": round(one / (FS / 1e6), 2)},
             "x_realtime": round(agg / (FS / 1e6), 2),
             "sample": f"static -d {seconds} -b 16 -o /dev/null ({blocks} blocks x 260000 "
                       f"samples) per process; 1 process: wall {w1:.2f} s; {cores} concurrent "
-                      f"processes on cores {avail[0]}..{avail[cores - 1]}: wall {wn:.2f} s"}
+                      f"processes, one per core of the affinity mask (cores {avail[0]}.."
+                      f"{avail[-1]}): wall {wn:.2f} s"}
 
 
 def lib_sha16(path):
@@ -273,7 +286,7 @@ def d2h_ceiling(nbytes, reps=8):
     return round(rate, 2)
 
 
-def e2e_run(G, dev, threads, window=1800.0):
+def e2e_run(G, dev, threads, window=1800.0, batch=128):
     """gss_run over the whole static run into a discarding sink, wall-clocked (planner, proofs,
     uploads, kernels, D2H into pinned buffers and the sink, overlapped).  A second run of a third
     of the length gives the steady-state rate (the slope; the rest is the fixed start-up), to be
@@ -288,7 +301,7 @@ def e2e_run(G, dev, threads, window=1800.0):
             got["blocks"] += nb
 
         t0 = time.perf_counter()
-        dev.run(s, sink, batch=128, threads=threads)
+        dev.run(s, sink, batch=batch, threads=threads)
         return time.perf_counter() - t0, got["blocks"], got["bytes"], s.n_per_blk
 
     ws, bs, _, _ = one(window / 3)
@@ -301,8 +314,8 @@ def e2e_run(G, dev, threads, window=1800.0):
             "steady_MSps": round(slope * n_per_blk / 1e6, 1),
             "steady_d2h_GBps": round(slope * nbytes / blocks / 1e9, 2),
             "startup_s": round(wall - blocks / slope, 3),
-            "d2h_ceiling_GBps": d2h_ceiling(128 * n_per_blk * 4),
-            "workload": f"static -b 16, {window:g} s through gss_run (batch 256 blocks), "
+            "d2h_ceiling_GBps": d2h_ceiling(batch * n_per_blk * 4),
+            "workload": f"static -b 16, {window:g} s through gss_run (batch {batch} blocks), "
                         "discarding sink"}
 
 def main():
@@ -438,7 +451,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int64",
+        "dtype": ("int64 phases + f16 x f16 -> f32 MFMA accumulate (exact integer sums)"
+                  if G.lib_mfma() else "int64 phases + int64 accumulate"),
         "data": "synthetic: deterministic static-receiver scenario (brdc3540.14n), no dataset",
         "config": {"workload": workload, "samples_per_gpu": samples_rank, "path": "lin",
                    "channels_max": res.nch_max, "parallelism": f"time-window shards x{world}"},

@@ -12,9 +12,11 @@
  *                    slot renders, hands the previous slot's bytes to the sink in run order
  *
  * Slots cycle planner -> main -> sink -> planner; a slot's buffers belong to exactly one side at
- * a time (state under a mutex).  One compute stream and two copy streams (alternating slots, so
- * two DMA engines share the PCIe link): the D2H of slots i and i-1 overlap the kernels of slot
- * i+1; up to DEPTH slots are submitted before the oldest is handed to the sink; a slot's device
+ * a time (state under a mutex).  Shipped defaults (GSS_RUN_NCOPY = 1, GSS_RUN_DEPTH = 1): one
+ * compute stream and one copy stream, NSLOT = DEPTH + 2 = 3 slots; the D2H of slot i overlaps
+ * the kernels of slot i+1 and the planning of slot i+2; DEPTH slots are submitted before the
+ * oldest is handed to the sink.  NCOPY = 2 alternates slots over two copy streams (two DMA
+ * engines on the link; measured no faster, profiles/round2/ablate_e2e*.log).  A slot's device
  * output buffer is rewritten only after its own D2H (event).
  */
 #include <hip/hip_runtime.h>

@@ -830,6 +830,8 @@ template <int FMT, bool TAIL, class ACC>
 __device__ __forceinline__ void lin_store(const ACC &acc, uint8_t *__restrict__ ob,
                                           int nb0, int lane, int n_per_blk)
 {
+    /* the -b 1 epilogue hands lane 4 s + j the 16 samples 64 s + 16 j .. + 15: 4 LIN_CH lanes */
+    static_assert(FMT != 1 || LIN_CH == 16, "-b 1 packing assumes 16-step chunks");
     uint32_t pk[LIN_CH];
     pk[0] = 0;
 #pragma unroll
@@ -1163,6 +1165,13 @@ extern "C" int gss_fail(int code, const char *fmt, ...);
             return gss_fail(GSS_E_HIP, "HIP error %s at %s:%d", hipGetErrorString(e_),      \
                             __FILE__, __LINE__);                                             \
     } while (0)
+
+#define GSS_STR2(x) #x
+#define GSS_STR(x) GSS_STR2(x)
+extern "C" const char *gss_build_info(void)
+{
+    return "lin_mfma=" GSS_STR(LIN_MFMA) " lin_ch=" GSS_STR(LIN_CH) " arch=gfx950";
+}
 
 extern "C" size_t gss_block_bytes(int n, int fmt)
 {

@@ -181,21 +181,16 @@ static int64_t wraps_of(const gss_code_state *c, const gss_chan_blk_t *p)
            (c->icode - p->icode);
 }
 
-/* cos + 2^22 sin of LUT cell c (the kernel's packed I/Q term, gpssim.c:15-83) */
+/* cos + 2^22 sin of LUT cell c (the kernel's packed I/Q term, gpssim.c:15-83); the tables are
+   filled once, by pthread_once, before any worker reads them */
+static int32_t lut_sinT[512], lut_cosT[512];
+static pthread_once_t lut_once = PTHREAD_ONCE_INIT;
+
+static void lut_fill(void) { gss_lut(lut_sinT, lut_cosT); }
+
 static int64_t lut_packed(int c)
 {
-    static int32_t sinT[512], cosT[512];
-    static int ready;
-    if (!__atomic_load_n(&ready, __ATOMIC_ACQUIRE)) {
-        int32_t s[512], co[512];
-        gss_lut(s, co);
-        for (int i = 0; i < 512; i++) {
-            sinT[i] = s[i];
-            cosT[i] = co[i];
-        }
-        __atomic_store_n(&ready, 1, __ATOMIC_RELEASE);
-    }
-    return (int64_t)cosT[c] + (int64_t)sinT[c] * ((int64_t)1 << 22);
+    return (int64_t)lut_cosT[c] + (int64_t)lut_sinT[c] * ((int64_t)1 << 22);
 }
 
 static int ca_sign(const uint32_t *ca, int chip)          /* codeCA (gpssim.c:2220) */
@@ -433,6 +428,7 @@ int gss_linearize(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n
         return gss_fail(GSS_E_ARG, "invalid linearize arguments");
     if (nblk == 0)
         return 0;
+    pthread_once(&lut_once, lut_fill);                /* before any worker thread starts */
     if (threads < 1) threads = 1;
     if (threads > 64) threads = 64;
     if (threads > nblk) threads = nblk;

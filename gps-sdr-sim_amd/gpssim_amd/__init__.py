@@ -125,6 +125,7 @@ _SIGS = {
     "gss_cli_usage": (None, []),
     "gss_last_error": (C.c_char_p, []),
     "gss_version": (C.c_char_p, []),
+    "gss_build_info": (C.c_char_p, []),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -149,6 +150,16 @@ def lib():
             f.restype, f.argtypes = res, args
         _lib = L
     return _lib
+
+
+def build_info():
+    """The kernels' build configuration as a dict, e.g. {"lin_mfma": "1", "lin_ch": "16", ...}."""
+    return dict(kv.split("=", 1) for kv in lib().gss_build_info().decode().split())
+
+
+def lib_mfma():
+    """True when the fast path accumulates on the matrix cores (LIN_MFMA build)."""
+    return build_info().get("lin_mfma") == "1"
 
 
 def _check(rc):

@@ -295,6 +295,10 @@ int gss_lut(int32_t *sin512, int32_t *cos512);
 
 const char *gss_last_error(void);
 const char *gss_version(void);
+/* Build configuration of the kernels, e.g. "lin_mfma=1 lin_ch=16 arch=gfx950" (lin_mfma: the fast
+   path accumulates f16 x f16 products in f32 on the matrix cores, exact integer sums; 0: int64
+   multiply-adds on the VALU).                                                                 */
+const char *gss_build_info(void);
 
 #ifdef __cplusplus
 }

@@ -14,6 +14,7 @@ import hashlib
 import math
 import os
 import subprocess
+import zlib
 
 import numpy as np
 import pytest
@@ -127,20 +128,22 @@ def synth_params(rng, nblk, nch_list, n_per_blk, ties=False, tiny=False, fs=2.6e
 @pytest.mark.parametrize("fmt", [16, 8, 1])
 @pytest.mark.parametrize("case", ["mixed", "ties_tiny"])
 def test_lines_render_like_oracle(fmt, case):
-    rng = np.random.default_rng(abs(hash((fmt, case))) % (1 << 32))
+    seed = zlib.crc32(f"{fmt}:{case}".encode())      # stable across processes (no hash())
+    rng = np.random.default_rng(seed)
     n = 26000
     nch = [12, 0, 1, 7, 12, 3, 16, 11]
     blk, nchv, nav = synth_params(rng, len(nch), nch, n, ties=case == "ties_tiny",
                                   tiny=case == "ties_tiny")
     ca = G.ca_table()
     lin, fast = G.linearize(blk, nchv, nav, n)
-    assert fast.sum() >= len(nch) - 2, fast          # the proof rarely fails
+    assert fast.sum() >= len(nch) - 2, (seed, fast)  # the proof rarely fails
     want, rc = oracle.synth(blk, nchv, ca, nav, n, fmt)
     got, nr = render_lin(blk, nchv, lin, fast, ca, n, fmt)
     assert nr == fast.sum()
     bb = G.block_bytes(n, fmt)
     for b in np.nonzero(fast)[0]:
-        assert np.array_equal(got[b * bb:(b + 1) * bb], want[b * bb:(b + 1) * bb]), f"block {b}"
+        assert np.array_equal(got[b * bb:(b + 1) * bb], want[b * bb:(b + 1) * bb]), \
+            f"seed {seed}: block {b}"
 
 
 def test_lines_full_blocks_like_oracle():

@@ -10,7 +10,10 @@ copied to /tmp/gss_integ/ and edited there:
   3. `gss_integ_flush(fp);` before the reference's `tend = clock();`.
 Then gcc builds it with the reference's flags together with tools/integration/gss_integ.c,
 linked against gps-sdr-sim_amd/lib/libgpssim_amd.so, into oracle/_ref/gps-sdr-sim-integ
-(git-ignored, travels to the GPU box; tests/test_gpu_parity.py runs it there).
+(git-ignored, travels to the GPU box; tests/test_gpu_parity.py runs it there).  A second build,
+oracle/_ref/gps-sdr-sim-integ-intcarr, is the same patch on the reference's other carrier mode:
+the one `#define FLOAT_CARR_PHASE` line of the gpssim.h copy dropped (as oracle/Makefile does for
+its _ref/gps-sdr-sim-intcarr), so gss_integ.c's integer-carrier branch is built and tested too.
 Usage: python tools/integration/build_integ.py [--check]   (--check: compile and link only)
 """
 import os
@@ -24,6 +27,7 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 WORK = "/tmp/gss_integ"
 OUT = os.path.join(REPO, "oracle", "_ref", "gps-sdr-sim-integ")
+OUT_INT = OUT + "-intcarr"
 
 
 def patch(src):
@@ -43,23 +47,32 @@ def patch(src):
     return src
 
 
-def main():
-    if not os.path.exists(os.path.join(REF, "gpssim.c")):
-        sys.exit("no reference sources at " + REF)
-    os.makedirs(WORK, exist_ok=True)
-    shutil.copy(os.path.join(REF, "gpssim.h"), WORK)
-    open(os.path.join(WORK, "gpssim.c"), "w").write(
+def build(work, out, drop_float_carr):
+    os.makedirs(work, exist_ok=True)
+    hdr = open(os.path.join(REF, "gpssim.h")).read()
+    if drop_float_carr:
+        hdr = re.sub(r"(?m)^#define FLOAT_CARR_PHASE.*\n", "", hdr)
+        assert "#define FLOAT_CARR_PHASE" not in hdr
+    open(os.path.join(work, "gpssim.h"), "w").write(hdr)
+    open(os.path.join(work, "gpssim.c"), "w").write(
         patch(open(os.path.join(REF, "gpssim.c")).read()))
     lib = os.path.join(REPO, "gps-sdr-sim_amd", "lib")
     if not os.path.exists(os.path.join(lib, "libgpssim_amd.so")):
         subprocess.check_call(["make", "-C", os.path.join(REPO, "gps-sdr-sim_amd")])
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = ["gcc", "-O3", "-Wall", "-Wno-unused-variable", "-Wno-unused-but-set-variable",
-           "-D_FILE_OFFSET_BITS=64", "-I" + WORK, "-I" + os.path.join(REPO, "include"),
-           os.path.join(WORK, "gpssim.c"), os.path.join(HERE, "gss_integ.c"), "-L" + lib,
-           "-lgpssim_amd", "-Wl,-rpath,$ORIGIN/../../gps-sdr-sim_amd/lib", "-lm", "-o", OUT]
+           "-D_FILE_OFFSET_BITS=64", "-I" + work, "-I" + os.path.join(REPO, "include"),
+           os.path.join(work, "gpssim.c"), os.path.join(HERE, "gss_integ.c"), "-L" + lib,
+           "-lgpssim_amd", "-Wl,-rpath,$ORIGIN/../../gps-sdr-sim_amd/lib", "-lm", "-o", out]
     subprocess.check_call(cmd)
-    print("built", OUT)
+    print("built", out)
+
+
+def main():
+    if not os.path.exists(os.path.join(REF, "gpssim.c")):
+        sys.exit("no reference sources at " + REF)
+    build(WORK, OUT, False)
+    build(WORK + "_intcarr", OUT_INT, True)
 
 
 if __name__ == "__main__":

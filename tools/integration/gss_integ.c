@@ -13,8 +13,14 @@
  * The carrier phase is the only state the reference loop carries into the next block
  * (gpssim.c:2245-2250); gss_carr_advance_ck advances it exactly, without running the loop, and
  * records the block's GSS_NCK carrier checkpoints for the GPU.
+ * Both carrier builds of the reference are handled (gpssim.h:4): with FLOAT_CARR_PHASE the
+ * double carr_phase is advanced by gss_carr_advance_ck; without it chan[i].carr_phase is the
+ * uint32 chain of 2^-25 cycle steps carr_phasestep (gpssim.c:1625, 2176, 2202, 2252), which the
+ * rows carry as exact multiples of 2^-25 (carr0 = (carr_phase mod 2^25) / 2^25, carr_step =
+ * carr_phasestep / 2^25, the library's --carrier=int convention) and which is advanced here by
+ * the same integer additions the loop would make.
  * Compiled together with the maintainer's gpssim.c/gpssim.h (channel_t, MAX_CHAN, CA_SEQ_LEN);
- * tools/integration/build_integ.sh does that against a /tmp copy of the reference.
+ * tools/integration/build_integ.py does that against a /tmp copy of the reference.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -84,8 +90,13 @@ void gss_integ_block(channel_t *chan, const int *gain, int iq_buff_size, int dat
         }
         for (int w = 0; w < N_DWRD; w++)
             g.nav[row][w] = (uint32_t)chan[i].dwrd[w];
+#ifdef FLOAT_CARR_PHASE
         p->carr0 = chan[i].carr_phase;
         p->carr_step = chan[i].f_carr * delt;        /* the loop's own products */
+#else
+        p->carr0 = (double)(chan[i].carr_phase & 0x1FFFFFFu) / 33554432.0;
+        p->carr_step = (double)chan[i].carr_phasestep / 33554432.0;
+#endif
         p->code0 = chan[i].code_phase;
         p->code_step = chan[i].f_code * delt;
         p->icode = chan[i].icode;
@@ -95,8 +106,17 @@ void gss_integ_block(channel_t *chan, const int *gain, int iq_buff_size, int dat
         p->ca_tbl = sv;
         p->nav_tbl = row;
         /* the carrier the reference loop would leave behind, exactly */
+#ifdef FLOAT_CARR_PHASE
         chan[i].carr_phase = gss_carr_advance_ck(chan[i].carr_phase, p->carr_step, iq_buff_size,
                                                  &g.ck[(size_t)row * GSS_NCK]);
+#else
+        for (int j = 0; j < GSS_NCK; j++) {      /* phase at sample (j n) / GSS_NCK */
+            const unsigned int at = chan[i].carr_phase +
+                (unsigned int)chan[i].carr_phasestep * (unsigned int)(((long long)j * iq_buff_size) / GSS_NCK);
+            g.ck[(size_t)row * GSS_NCK + j] = (double)(at & 0x1FFFFFFu) / 33554432.0;
+        }
+        chan[i].carr_phase += (unsigned int)chan[i].carr_phasestep * (unsigned int)iq_buff_size;
+#endif
         c++;
     }
     for (int k = c; k < GSS_MAXCH; k++)
