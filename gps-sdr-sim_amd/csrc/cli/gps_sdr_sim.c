@@ -8,9 +8,15 @@
  * --no-python --nproc-per-node N gps-sdr-sim ... -o FILE`), process r synthesises the contiguous
  * block range [B r/N, B (r+1)/N) on GPU LOCAL_RANK and pwrite()s it at its byte offset of FILE
  * (every rank ftruncate()s FILE to the run's size first, safe in any order): the same file as
- * one process writes, with no collective.
+ * one process writes, with no collective.  Planned once per node: rank r seeks to
+ * its first block and plans only its own range; the 16 slot carriers at its first block (the one
+ * state the sample loop carries across blocks, gpssim.c:2245-2250) come from rank r-1 through a
+ * hand-off file next to FILE, FILE.gss-carr-<run id>-<block>, written atomically (tmp + rename)
+ * and removed by its reader.  The run id is torchrun's TORCHELASTIC_RUN_ID (or GSS_RUN_ID);
+ * without one every rank plans the blocks before its range itself.
  * Env: GSS_DEVICE (ordinal; default LOCAL_RANK or 0), GSS_BATCH (blocks per launch, default
- *      128), GSS_THREADS (planner threads, default 8).
+ *      128), GSS_THREADS (planner threads, default 8), GSS_HANDOFF_TIMEOUT (seconds a rank waits
+ *      for its carriers, default 3600).
  */
 #include <fcntl.h>
 #include <stdio.h>
@@ -52,6 +58,58 @@ static int env_int(const char *name, int dflt)
     return v && *v ? atoi(v) : dflt;
 }
 
+/* The carrier hand-off between ranks (plan once per node): a 16-double file per boundary. */
+typedef struct {
+    gss_scn *scn;
+    char in_path[600], out_path[600];      /* empty: none (rank 0 / last rank) */
+    double timeout_s;
+} handoff_ctx;
+
+#define HANDOFF_MAGIC 0x67737363u          /* "gssc" */
+
+static int handoff_in(void *user, double *carr)
+{
+    const handoff_ctx *h = (const handoff_ctx *)user;
+    if (!h->in_path[0])                    /* rank 0: every slot starts with a reset */
+        return gss_scn_carrier(h->scn, carr);
+    struct timespec nap = {0, 1000000};
+    double waited = 0.0;
+    for (;;) {
+        FILE *f = fopen(h->in_path, "rb");
+        if (f) {
+            uint32_t magic = 0;
+            size_t ok = fread(&magic, sizeof magic, 1, f) == 1 &&
+                        fread(carr, sizeof(double), GSS_MAXCH, f) == GSS_MAXCH;
+            fclose(f);
+            if (!ok || magic != HANDOFF_MAGIC)
+                return 1;
+            unlink(h->in_path);
+            return 0;
+        }
+        if (waited > h->timeout_s)
+            return 1;
+        nanosleep(&nap, NULL);
+        waited += 1e-3;
+    }
+}
+
+static int handoff_out(void *user, const double *carr)
+{
+    const handoff_ctx *h = (const handoff_ctx *)user;
+    if (!h->out_path[0])
+        return 0;
+    char tmp[640];
+    snprintf(tmp, sizeof tmp, "%s.tmp", h->out_path);
+    FILE *f = fopen(tmp, "wb");
+    if (!f)
+        return 1;
+    const uint32_t magic = HANDOFF_MAGIC;
+    int ok = fwrite(&magic, sizeof magic, 1, f) == 1 &&
+             fwrite(carr, sizeof(double), GSS_MAXCH, f) == GSS_MAXCH;
+    ok = (fclose(f) == 0) && ok;
+    return (ok && rename(tmp, h->out_path) == 0) ? 0 : 1;
+}
+
 /* One process of a multi-GPU run: its block range, pwrite()n at its offset of the output file. */
 static int run_rank(const gss_cli_t *cli, gss_scn *scn, const gss_scn_info_t *info, int rank,
                     int world)
@@ -73,8 +131,25 @@ static int run_rank(const gss_cli_t *cli, gss_scn *scn, const gss_scn_info_t *in
         fprintf(stderr, "ERROR: Failed to open output file.\n");
         return 1;
     }
-    if (gss_run(dev, scn, first, last - first, env_int("GSS_BATCH", 128),
-                env_int("GSS_THREADS", 8), pwrite_sink, &c)) {
+    const char *run_id = getenv("TORCHELASTIC_RUN_ID");
+    if (!run_id || !*run_id)
+        run_id = getenv("GSS_RUN_ID");
+    handoff_ctx h;
+    memset(&h, 0, sizeof h);
+    h.scn = scn;
+    h.timeout_s = env_int("GSS_HANDOFF_TIMEOUT", 3600);
+    gss_run_opts_t ro = {handoff_in, handoff_out, &h};
+    if (run_id && *run_id) {
+        if (rank > 0)
+            snprintf(h.in_path, sizeof h.in_path, "%s.gss-carr-%s-%lld", cli->out_file, run_id,
+                     (long long)first);
+        if (rank + 1 < world)
+            snprintf(h.out_path, sizeof h.out_path, "%s.gss-carr-%s-%lld", cli->out_file,
+                     run_id, (long long)last);
+    }
+    if (gss_run_ex(dev, scn, first, last - first, env_int("GSS_BATCH", 128),
+                   env_int("GSS_THREADS", 8), pwrite_sink, &c,
+                   run_id && *run_id ? &ro : NULL)) {
         fprintf(stderr, "\nERROR: rank %d: %s\n", rank, gss_last_error());
         return 1;
     }

@@ -28,6 +28,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <thread>
+#include <vector>
 #include "gpssim_amd.h"
 
 extern "C" int gss_fail(int code, const char *fmt, ...);
@@ -97,8 +98,14 @@ struct Slot {
 
 struct Run {
     gss_scn *scn;
-    int batch, threads, n_per_blk, use_lin;
+    int batch, threads, n_per_blk, use_lin, carrier_int;
     int64_t first, last;             /* [first, last) block range of the run */
+    const gss_run_opts_t *opts;      /* carrier hand-off (gss_run_ex), or null */
+    /* with opts->carr_in: the whole range planned up front (rows, carriers, checkpoints) */
+    std::vector<gss_chan_blk_t> pre_blk;
+    std::vector<int32_t> pre_nch;
+    std::vector<double> pre_ck;
+    int64_t pre_n = 0, pre_at = 0;
     std::mutex mu;
     std::condition_variable cv;
     int abort = 0;
@@ -108,10 +115,129 @@ struct Run {
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-/* Fill slot k's pinned buffers with the next batch inside [first, last); blocks before `first`
-   are planned (the carrier chain is serial) and dropped. */
+/* gss_run_ex with a carrier hand-off: seek to the range, produce its rows, take the slot
+   carriers at its first block from carr_in, walk the chain, give the end state to carr_out. */
+int plan_range_upfront(Run &r)
+{
+    int rc = gss_scn_seek(r.scn, r.first, r.threads);
+    if (rc)
+        return rc;
+    std::vector<gss_chain_t> chain;
+    const int step = 4096;
+    for (;;) {
+        const int64_t want = r.last - r.first - r.pre_n;
+        if (want <= 0)
+            break;
+        const int ask = want < step ? (int)want : step;
+        r.pre_blk.resize((size_t)(r.pre_n + ask) * GSS_MAXCH);
+        r.pre_nch.resize((size_t)(r.pre_n + ask));
+        chain.resize((size_t)(r.pre_n + ask) * GSS_MAXCH);
+        int nb = 0;
+        rc = gss_scn_next_deferred(r.scn, ask, &r.pre_blk[(size_t)r.pre_n * GSS_MAXCH],
+                                   &r.pre_nch[(size_t)r.pre_n],
+                                   &chain[(size_t)r.pre_n * GSS_MAXCH], &nb, r.threads);
+        if (rc)
+            return rc;
+        r.pre_n += nb;
+        if (nb < ask)
+            break;                                     /* end of the run */
+    }
+    double carr[GSS_MAXCH];
+    if (r.opts->carr_in(r.opts->carr_user, carr))
+        return gss_fail(GSS_E_IO, "carrier hand-off (in) failed at block %lld",
+                        (long long)r.first);
+    r.pre_ck.resize((size_t)r.pre_n * GSS_MAXCH * GSS_NCK);
+    rc = gss_carr_chain(carr, r.pre_blk.data(), r.pre_nch.data(), chain.data(), (int)r.pre_n,
+                        r.n_per_blk, r.carrier_int, r.pre_ck.data(), r.threads);
+    if (rc)
+        return rc;
+    if (r.opts->carr_out && r.opts->carr_out(r.opts->carr_user, carr))
+        return gss_fail(GSS_E_IO, "carrier hand-off (out) failed after block %lld",
+                        (long long)(r.first + r.pre_n - 1));
+    return 0;
+}
+
+/* the slot's batch from the up-front plan; its nav rows are the contiguous table range its rows
+   reference (rows are appended in run order), renumbered from 0 */
+int take_upfront(Run &r, Slot &sl, int *nb_out)
+{
+    const int64_t left = r.pre_n - r.pre_at;
+    const int nb = left < r.batch ? (int)left : r.batch;
+    *nb_out = nb;
+    if (nb <= 0)
+        return 0;
+    const size_t rows = (size_t)nb * GSS_MAXCH;
+    memcpy(sl.blk, &r.pre_blk[(size_t)r.pre_at * GSS_MAXCH], rows * sizeof(gss_chan_blk_t));
+    memcpy(sl.nch, &r.pre_nch[(size_t)r.pre_at], (size_t)nb * sizeof(int32_t));
+    memcpy(sl.ck, &r.pre_ck[(size_t)r.pre_at * GSS_MAXCH * GSS_NCK],
+           rows * GSS_NCK * sizeof(double));
+    int lo = INT32_MAX, hi = -1;
+    for (int b = 0; b < nb; b++)
+        for (int k = 0; k < sl.nch[b]; k++) {
+            const int t = sl.blk[(size_t)b * GSS_MAXCH + k].nav_tbl;
+            lo = t < lo ? t : lo;
+            hi = t > hi ? t : hi;
+        }
+    if (hi < lo)
+        lo = hi = 0;
+    for (int b = 0; b < nb; b++)
+        for (int k = 0; k < sl.nch[b]; k++)
+            sl.blk[(size_t)b * GSS_MAXCH + k].nav_tbl -= lo;
+    const uint32_t *all = nullptr;
+    int n_all = 0;
+    gss_scn_nav_table(r.scn, &all, &n_all);
+    const int n_rows = n_all > 0 ? hi - lo + 1 : 0;
+    if (n_rows > sl.nav_cap) {
+        (void)hipHostFree(sl.nav);
+        sl.nav = nullptr;
+        sl.nav_cap = 0;
+        const int cap = n_rows * 2 + 16;
+        if (hipHostMalloc((void **)&sl.nav, sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)cap,
+                          hipHostMallocDefault) != hipSuccess)
+            return gss_fail(GSS_E_NOMEM, "pinned nav table");
+        sl.nav_cap = cap;
+    }
+    if (n_rows > 0)
+        memcpy(sl.nav, all + (size_t)lo * GSS_NAV_WORDS,
+               sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)n_rows);
+    sl.n_nav = n_rows;
+    sl.first = r.first + r.pre_at;
+    r.pre_at += nb;
+    return 0;
+}
+
+/* Fill slot k's pinned buffers with the next batch inside [first, last); without a carrier
+   hand-off, blocks before `first` are planned (the carrier chain is serial) and dropped. */
 int plan_into(Run &r, Slot &sl, int64_t *cursor)
 {
+    if (r.opts && r.opts->carr_in) {
+        int nb = 0;
+        int rc = take_upfront(r, sl, &nb);
+        if (rc)
+            return rc;
+        if (nb == 0) {
+            sl.nb = 0;
+            sl.end = 1;
+            return 0;
+        }
+        sl.nb = nb;
+        int m = 1;
+        for (int i = 0; i < nb; i++)
+            m = sl.nch[i] > m ? sl.nch[i] : m;
+        sl.nch_max = m;
+        if (r.use_lin) {
+            rc = gss_linearize(sl.blk, sl.nch, nb, r.n_per_blk, r.ca, 32, sl.nav, sl.n_nav,
+                               sl.lin, sl.fast, r.threads);
+            if (rc)
+                return rc;
+            int nf = 0;
+            for (int i = 0; i < nb; i++)
+                if (!sl.fast[i])
+                    sl.fast[nb + nf++] = i;
+            sl.n_fb = nf;
+        }
+        return 0;
+    }
     for (;;) {
         int64_t want = r.last - *cursor;
         if (want <= 0) {
@@ -179,6 +305,7 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
 void planner(Run *r)
 {
     int64_t cursor = 0;
+    int up_rc = (r->opts && r->opts->carr_in) ? plan_range_upfront(*r) : 0;
     for (int i = 0;; i++) {
         Slot &sl = r->slot[i % NSLOT];
         {
@@ -188,7 +315,7 @@ void planner(Run *r)
                 return;
         }
         const double t0 = trace_on() ? tnow() : 0.0;
-        int rc = plan_into(*r, sl, &cursor);
+        int rc = up_rc ? up_rc : plan_into(*r, sl, &cursor);
         if (trace_on())
             fprintf(stderr, "trace plan slot %d nb %d %.6f %.6f\n", i % NSLOT, sl.nb, t0, tnow());
         {
@@ -330,6 +457,13 @@ int run_main(gss_dev *d, Run &r, int n_per_blk, int fmt, size_t bb, gss_sink_fn 
 extern "C" int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_blocks, int batch,
                        int threads, gss_sink_fn sink, void *user)
 {
+    return gss_run_ex(d, s, first_block, n_blocks, batch, threads, sink, user, nullptr);
+}
+
+extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_blocks,
+                          int batch, int threads, gss_sink_fn sink, void *user,
+                          const gss_run_opts_t *opts)
+{
     if (!d || !s || !sink || first_block < 0)
         return gss_fail(GSS_E_ARG, "invalid run arguments");
     gss_scn_info_t info;
@@ -341,6 +475,8 @@ extern "C" int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_bl
                         info.n_per_blk);
     Run r;
     r.scn = s;
+    r.opts = opts;
+    r.carrier_int = info.carrier_int;
     r.threads = threads > 0 ? threads : 1;
     r.n_per_blk = info.n_per_blk;
     {

@@ -539,10 +539,22 @@ static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole ch
    magnitude, so the matrix core's sums are exact in any order, and the IEEE bits of the result
    are 0x4B400000 + (sum + 64), from which (sum + 64) >> 7 is a shift
    (tools/ubench/mfma_probe.hip: operand layout and exactness on gfx950). */
+/* LIN_MFMA 2 (the default build): channels in pairs on v_mfma_f32_16x16x32_f16.  Lane l holds
+   B[8 (l>>4) + j][l & 15] (j = 0..7) and C[4 (l>>4) + r][l & 15] (r = 0..3), so a lane's four
+   outputs depend only on its own eight B values when A row 4q + r is zero outside K columns
+   8q .. 8q+7 (tools/ubench/mfma16_probe.hip checks the map and the exact sums on gfx950).  B is
+   the lane's four LUT words -- channel a at steps s, s+1, channel b at steps s, s+1 -- and A
+   puts g_a at column 8q + r and g_b at 8q + 4 + r of row 4q + r: the lanes 20q + r hold those
+   two gains (elements r and 4 + r), every other lane zeros.  One MFMA per two channels and two
+   steps instead of one per channel and two steps: the 4x4x4 MFMA holds the SIMD's vector issue
+   about 9 cycles, the 16x16x32 one about 11 (tools/ubench/mfma_issue_ubench.hip), so the
+   accumulate costs ~2.8 instead of ~4.6 issue cycles per channel-step.  A lone last channel, and
+   the rare gain-change reruns, keep the 4x4x4 form. */
 #ifndef LIN_MFMA
 #define LIN_MFMA 0
 #endif
 typedef _Float16 lin_half4 __attribute__((ext_vector_type(4)));
+typedef _Float16 lin_half8 __attribute__((ext_vector_type(8)));
 typedef float lin_f4 __attribute__((ext_vector_type(4)));
 #define LIN_MAGF  12582976.0f                   /* 1.5 2^23 + 64                          */
 #define LIN_MAGB  0x4B400000u                   /* IEEE bits of 1.5 2^23                  */
@@ -562,6 +574,7 @@ struct lin_ct {
     uint32_t W[LIN_CH];          /* the steps' chip windows                                     */
 #if LIN_MFMA
     uint32_t A[4][2];            /* the MFMA gain operand of lane 4b + i: g (f16) at slot i      */
+    uint32_t g2, pad2[3];        /* g as an f16 pair (both halves), the pair MFMA's gain         */
 #endif
 };
 
@@ -715,6 +728,64 @@ __device__ __forceinline__ void lin_channel_chunk_m(lin_f4 (&cq)[LIN_CH / 2], ui
         }
         P += D;
     }
+}
+
+/* LIN_MFMA 2: two channels' steps, one v_mfma_f32_16x16x32_f16 per two steps (B = channel a's
+   words of steps s, s+1 and channel b's; A = the pair's gains, lin_pair_gains) */
+__device__ __forceinline__ void lin_pair_chunk(lin_f4 (&cq)[LIN_CH / 2], uint64_t Pa, uint64_t Da,
+                                               const uint32_t *Wa, uint64_t Pb, uint64_t Db,
+                                               const uint32_t *Wb, uint32_t M, lin_half8 A,
+                                               const int32_t *__restrict__ s_lut)
+{
+    uint4 wa4, wb4;
+    uint32_t ea0 = 0, eb0 = 0;
+#pragma unroll
+    for (int s = 0; s < LIN_CH; s++) {
+        if (s % 4 == 0) {
+            wa4 = ((const uint4 *)Wa)[s / 4];
+            wb4 = ((const uint4 *)Wb)[s / 4];
+        }
+        const uint32_t wa = s % 4 == 0 ? wa4.x : s % 4 == 1 ? wa4.y : s % 4 == 2 ? wa4.z : wa4.w;
+        const uint32_t wb = s % 4 == 0 ? wb4.x : s % 4 == 1 ? wb4.y : s % 4 == 2 ? wb4.z : wb4.w;
+        uint32_t ta, tb;
+        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
+            "src1_sel:DWORD" : "=v"(ta) : "v"((uint32_t)Pa), "v"(wa));
+        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
+            "src1_sel:DWORD" : "=v"(tb) : "v"((uint32_t)Pb), "v"(wb));
+        const uint32_t aa = __builtin_amdgcn_alignbit(ta, (uint32_t)(Pa >> 32), 21) & M;
+        const uint32_t ab = __builtin_amdgcn_alignbit(tb, (uint32_t)(Pb >> 32), 21) & M;
+        const uint32_t ea = *(const uint32_t *)((const char *)s_lut + aa);
+        const uint32_t eb = *(const uint32_t *)((const char *)s_lut + ab);
+        if (s & 1) {
+            const uint4 bb = make_uint4(ea0, ea, eb0, eb);
+            cq[s / 2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, __builtin_bit_cast(lin_half8, bb),
+                                                              cq[s / 2], 0, 0, 0);
+        } else {
+            ea0 = ea;
+            eb0 = eb;
+        }
+        Pa += Da;
+        Pb += Db;
+    }
+}
+
+/* the pair MFMA's A operand: lanes 20q + r (q, r = 0..3) hold g_a at element r and g_b at 4 + r,
+   every other lane zeros; sel0 / sel1 (per lane, from lin_pair_sel) mask the f16 half of
+   elements 0..3 (dword 0, 1) that is this lane's element r */
+__device__ __forceinline__ lin_half8 lin_pair_gains(uint32_t ga2, uint32_t gb2, uint32_t sel0,
+                                                    uint32_t sel1)
+{
+    const uint4 v = make_uint4(ga2 & sel0, ga2 & sel1, gb2 & sel0, gb2 & sel1);
+    return __builtin_bit_cast(lin_half8, v);
+}
+
+__device__ __forceinline__ void lin_pair_sel(int lane, uint32_t &sel0, uint32_t &sel1)
+{
+    const int q = lane >> 4, r = lane & 3;
+    const bool act = ((lane & 15) >> 2) == q;
+    const uint32_t half = (r & 1) ? 0xFFFF0000u : 0x0000FFFFu;
+    sel0 = act && r < 2 ? half : 0u;
+    sel1 = act && r >= 2 ? half : 0u;
 }
 
 /* the MFMA gain operand of this lane (g at slot lane mod 4, f16 bits gh) */
@@ -1004,6 +1075,10 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
     __syncthreads();
     uint32_t M = (LIN_ABLATE & 128) ? 0x7FCu : 0xFFCu;   /* LUT address mask, in a VGPR */
     asm volatile("" : "+v"(M));
+#if LIN_MFMA == 2
+    uint32_t psel0, psel1;                                /* the pair MFMA's A-operand masks */
+    lin_pair_sel(lane, psel0, psel1);
+#endif
     const int sg = w * LIN_WAVES + wave;
     const int n0 = sg * (64 * LIN_STEPS);
     if (n0 >= n_per_blk)
@@ -1018,6 +1093,7 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
         if (nb0 >= n_per_blk)
             break;
         /* ---- the chunk's parameters, lane k for channel k ---- */
+        uint32_t my_flags = 0;
         if (lane < nc) {
             const lin_chan ck = CH[lane];
             const lin_seg sk = S[(size_t)lane * nseg];
@@ -1034,6 +1110,7 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
             t.gd = g1 - g0;
             t.pos1 = sk.pos1;
             t.flags = (chg && sk.pos1 > nb0 ? 1u : 0u) | (sk.npatch != 0 ? 2u : 0u);
+            my_flags = t.flags;
             /* 1/16 chip below lane 0's first chip, plus CBW_PRE chips */
             t.q0 = (uint32_t)(zb >> 46) + (16 * CBW_PRE - 1);
             t.dq = ck.dq;
@@ -1044,8 +1121,11 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
             t.A[1][0] = gh << 16;   t.A[1][1] = 0;
             t.A[2][0] = 0;          t.A[2][1] = gh;
             t.A[3][0] = 0;          t.A[3][1] = gh << 16;
+            t.g2 = gh | (gh << 16);
 #endif
         }
+        /* the channels with a gain change or patches in this chunk (wave-uniform) */
+        const uint64_t fmask = __builtin_amdgcn_ballot_w64(my_flags != 0);
         wave_sync_lds();
         /* ---- the chip windows, lane (k, s) ---- */
         for (int i = lane; i < nc * LIN_CH; i += 64) {
@@ -1073,13 +1153,31 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
             acc[s] = lin_f4{LIN_MAGF, LIN_MAGF, LIN_MAGF, LIN_MAGF};
             asm volatile("" : "+v"(acc[s]));
         }
-        for (int k = 0; k < nc; k++) {                    /* uniform channel loop */
+#if LIN_MFMA == 2
+        int k0 = 0;
+        for (; k0 + 1 < nc; k0 += 2) {                    /* uniform loop over channel pairs */
+            const lin_ct &ta = T[k0], &tb = T[k0 + 1];
+            lin_pair_chunk(acc, s_lane[k0 * 64 + lane] + ta.B, ta.D, ta.W,
+                           s_lane[(k0 + 1) * 64 + lane] + tb.B, tb.D, tb.W, M,
+                           lin_pair_gains(ta.g2, tb.g2, psel0, psel1), s_lut);
+        }
+#else
+        const int k0 = 0;
+#endif
+        for (int k = k0; k < nc; k++) {                   /* uniform channel loop (mode 1), or
+                                                             the lone last channel (mode 2) */
             const lin_ct &t = T[k];
             const uint64_t B = t.B, D = t.D;
-            const uint32_t fl = __builtin_amdgcn_readfirstlane(t.flags);
             const uint2 a2 = *(const uint2 *)t.A[lane & 3];
             lin_channel_chunk_m<false>(acc, s_lane[k * 64 + lane] + B, D, t.W, M,
                                        __builtin_bit_cast(lin_half4, a2), 0, 0, s_lut);
+        }
+        /* gain changes and patches (rare): only the channels whose flags are set */
+        for (uint64_t fm = fmask; fm; fm &= fm - 1) {
+            const int k = __builtin_amdgcn_readfirstlane((int)__builtin_ctzll(fm));
+            const lin_ct &t = T[k];
+            const uint64_t B = t.B, D = t.D;
+            const uint32_t fl = __builtin_amdgcn_readfirstlane(t.flags);
             if (__builtin_expect(fl & 1u, 0)) {
                 uint32_t l2 = (uint32_t)lane;
                 asm volatile("" : "+v"(l2));

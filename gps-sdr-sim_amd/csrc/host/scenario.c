@@ -67,12 +67,13 @@ struct gss_scn {
     uint32_t *nav_rows;
     int n_nav, cap_nav;
     double carr[K_MAX_CHAN];                /* planner: carrier at the next block start per slot */
+    int carr_known;                         /* 0 after gss_scn_seek until gss_scn_set_carrier */
     double plan_sec;
-    /* per-batch side info for the planner */
+    int64_t rows_out;                       /* blocks whose rows this handle has produced */
+    /* per-batch carrier-chain bookkeeping of gss_scn_next (gss_scn_next_deferred's is the
+       caller's) */
     int batch_cap;
-    int8_t *b_slot;                         /* [b][k] slot of entry k */
-    uint8_t *b_reset;                       /* [b][k] 1 if the slot's chain restarts here */
-    double *b_init;                         /* [b][k] restart value */
+    gss_chain_t *chain;                     /* [b][k] */
     /* ranges of the blocks up to the next 30 s update, computed in parallel (range_pass) */
     rng_t *rg;                              /* [j][slot] */
     int rg_cap;
@@ -347,6 +348,7 @@ int gss_scn_open(gss_scn **out, const gss_opts_t *opt)
 
     s->grx = gt_add(s->grx, 0.1);
     s->iumd = 1;
+    s->carr_known = 1;              /* every slot's chain starts with a reset at block 0 */
     *out = s;
     return 0;
 fail:
@@ -365,6 +367,9 @@ int gss_scn_info(const gss_scn *s, gss_scn_info_t *info)
     info->delt = s->delt;
     info->week = s->g0.week;
     info->sec = s->g0.sec;
+    info->next_block = s->iumd - 1;
+    info->rows_out = s->rows_out;
+    info->carrier_int = s->opt.carrier_int;
     return 0;
 }
 
@@ -386,46 +391,53 @@ static double carr_int_walk(double x, double step, int n, double *ck)
 }
 
 typedef struct {
-    gss_scn *s;
+    double *carr;
     gss_chan_blk_t *blk;
     const int32_t *nch;
+    const gss_chain_t *chain;
     double *ck;
-    int nblk, slot_lo, slot_hi;
+    int nblk, n_per_blk, carrier_int, slot_lo, slot_hi;
 } plan_job;
 
 static void *plan_slots(void *arg)
 {
     plan_job *j = arg;
-    gss_scn *s = j->s;
     for (int slot = j->slot_lo; slot < j->slot_hi; slot++) {
-        double x = s->carr[slot];
+        double x = j->carr[slot];
         for (int b = 0; b < j->nblk; b++) {
             for (int k = 0; k < j->nch[b]; k++) {
                 size_t e = (size_t)b * GSS_MAXCH + k;
-                if (s->b_slot[e] != slot)
+                if (j->chain[e].slot != slot)
                     continue;
-                if (s->b_reset[e])
-                    x = s->b_init[e];
+                if (j->chain[e].reset)
+                    x = j->chain[e].init;
                 j->blk[e].carr0 = x;
-                if (s->opt.carrier_int)    /* exact integer chain, checkpoints included */
-                    x = carr_int_walk(x, j->blk[e].carr_step, s->n_per_blk,
+                if (j->carrier_int)        /* exact integer chain, checkpoints included */
+                    x = carr_int_walk(x, j->blk[e].carr_step, j->n_per_blk,
                                       j->ck ? j->ck + e * GSS_NCK : NULL);
                 else if (j->ck) /* same walk, recording the sub-block checkpoints on the way */
-                    x = gss_carr_walk_ck(x, j->blk[e].carr_step, s->n_per_blk,
+                    x = gss_carr_walk_ck(x, j->blk[e].carr_step, j->n_per_blk,
                                          j->ck + e * GSS_NCK);
                 else
-                    x = gss_carr_walk_cc(x, j->blk[e].carr_step, s->n_per_blk);
+                    x = gss_carr_walk_cc(x, j->blk[e].carr_step, j->n_per_blk);
                 break;
             }
         }
-        s->carr[slot] = x;
+        j->carr[slot] = x;
     }
     return NULL;
 }
 
-static void plan_batch(gss_scn *s, gss_chan_blk_t *blk, const int32_t *nch, double *ck, int nblk,
-                       int threads)
+/* The carrier chain (gpssim.c:2245-2250, carried across blocks) over nblk consecutive blocks:
+   one chain per channel slot, restarted where allocateChannel re-initialised it; slots are
+   independent, so one slot per thread. */
+int gss_carr_chain(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
+                   const gss_chain_t *chain, int nblk, int n_per_blk, int carrier_int,
+                   double *carr_ck, int threads)
 {
+    if (carr == NULL || (nblk > 0 && (blk == NULL || nch == NULL || chain == NULL)) ||
+        nblk < 0 || n_per_blk <= 0)
+        return gss_fail(GSS_E_ARG, "invalid carrier-chain arguments");
     if (threads < 1)
         threads = 1;
     if (threads > K_MAX_CHAN)
@@ -435,7 +447,8 @@ static void plan_batch(gss_scn *s, gss_chan_blk_t *blk, const int32_t *nch, doub
     int per = (K_MAX_CHAN + threads - 1) / threads;
     int started = 0;
     for (int t = 0; t < threads; t++) {
-        job[t] = (plan_job){s, blk, nch, ck, nblk, t * per, (t + 1) * per};
+        job[t] = (plan_job){carr, blk, nch, chain, carr_ck, nblk, n_per_blk, carrier_int,
+                            t * per, (t + 1) * per};
         if (job[t].slot_hi > K_MAX_CHAN)
             job[t].slot_hi = K_MAX_CHAN;
         if (job[t].slot_lo >= job[t].slot_hi)
@@ -444,11 +457,11 @@ static void plan_batch(gss_scn *s, gss_chan_blk_t *blk, const int32_t *nch, doub
             plan_slots(&job[t]);
         else
             started |= 1 << t;
-        (void)0;
     }
     for (int t = 0; t < threads; t++)
         if (started & (1 << t))
             pthread_join(tid[t], NULL);
+    return 0;
 }
 
 /* ---- per-block ranges in parallel --------------------------------------------------------------
@@ -525,24 +538,49 @@ static int range_pass(gss_scn *s, int max_j, int threads)
     return nj;
 }
 
-int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, double *carr_ck,
-                 int *n_out, int threads)
+/* The 30 s update after the block at s->grx (gpssim.c:2294-2345): nav message, ephemeris set,
+   allocation.  push_nav: append the new dwrd to the nav table (not while seeking). */
+static int update_30s(gss_scn *s, const double *xyz, int push_nav)
 {
-    *n_out = 0;
-    if (s == NULL || blk == NULL || nch == NULL || max_blocks <= 0)
-        return gss_fail(GSS_E_ARG, "invalid argument");
-    double t_start = wall_now();
-    if (max_blocks > s->batch_cap) {
-        free(s->b_slot); free(s->b_reset); free(s->b_init);
-        size_t n = (size_t)max_blocks * GSS_MAXCH;
-        s->b_slot = malloc(n);
-        s->b_reset = malloc(n);
-        s->b_init = malloc(n * sizeof(double));
-        if (!s->b_slot || !s->b_reset || !s->b_init)
-            return gss_fail(GSS_E_NOMEM, "out of memory");
-        s->batch_cap = max_blocks;
+    for (int i = 0; i < K_MAX_CHAN; i++)
+        if (s->chan[i].prn > 0) {
+            nav_frame(s->grx, &s->chan[i], 0);
+            if (push_nav) {
+                int rc = nav_push(s, &s->chan[i]);
+                if (rc)
+                    return rc;
+            }
+        }
+    /* step to the next ephemeris set when its TOC is < 1 h away; only the first valid SV of that
+       set is tested (gpssim.c:2307-2326).  New subframes reach dwrd at the next 30 s update. */
+    for (int sv = 0; sv < K_MAX_SAT; sv++) {
+        if (s->eph[s->ieph + 1][sv].vflg == 1) {
+            double dt = gt_diff(s->eph[s->ieph + 1][sv].toc, s->grx);
+            if (dt < K_SEC_HOUR) {
+                s->ieph++;
+                for (int i = 0; i < K_MAX_CHAN; i++)
+                    if (s->chan[i].prn != 0)
+                        nav_subframes(&s->eph[s->ieph][s->chan[i].prn - 1], &s->io,
+                                      s->chan[i].sbf);
+            }
+            break;
+        }
     }
+    int rc = allocate_channels(s, s->eph[s->ieph], s->grx, xyz);
+    if (rc < 0)
+        return rc;
+    if (push_nav && s->opt.verbose) {
+        msg(s, "\n");
+        print_channels(s);
+    }
+    return 0;
+}
 
+/* Rows of the next blocks without their carrier phase (carr0 = 0): the per-block refresh and the
+   30 s updates of gpssim.c:2154-2352; chain[] records which slot chain each row continues. */
+static int next_rows(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch,
+                     gss_chain_t *chain, double *carr_ck, int *n_out, int threads)
+{
     int nb = 0, jr = 0, nr = 0;                /* block jr of a range pass of nr blocks */
     while (nb < max_blocks && s->iumd < s->numd) {
         const double *xyz = s->static_mode ? s->xyz[0] : s->xyz[s->iumd];
@@ -586,7 +624,7 @@ int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, 
             int gain = (int)(path_loss * ant_gain * 128.0);
 
             gss_chan_blk_t *p = &row[k];
-            p->carr0 = 0.0;                        /* filled by the planner */
+            p->carr0 = 0.0;                        /* filled by the carrier chain */
             p->carr_step = ch->f_carr * s->delt;
             if (s->opt.carrier_int)       /* carr_phasestep (gpssim.c:2175-2177) */
                 p->carr_step = (double)(int)round(512.0 * 65536.0 * ch->f_carr * s->delt) /
@@ -599,15 +637,19 @@ int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, 
             p->gain = gain;
             p->ca_tbl = ch->prn - 1;
             p->nav_tbl = ch->nav_row;
-            size_t e = (size_t)nb * GSS_MAXCH + k;
-            s->b_slot[e] = (int8_t)i;
-            s->b_reset[e] = (uint8_t)ch->carr_fresh;
-            s->b_init[e] = ch->carr_phase;
+            gss_chain_t *c = &chain[(size_t)nb * GSS_MAXCH + k];
+            memset(c, 0, sizeof *c);
+            c->slot = (int8_t)i;
+            c->reset = (uint8_t)ch->carr_fresh;
+            c->init = ch->carr_phase;
             ch->carr_fresh = 0;
             k++;
         }
-        for (int r = k; r < GSS_MAXCH; r++)
+        for (int r = k; r < GSS_MAXCH; r++) {
             memset(&row[r], 0, sizeof row[r]);
+            memset(&chain[(size_t)nb * GSS_MAXCH + r], 0, sizeof chain[0]);
+            chain[(size_t)nb * GSS_MAXCH + r].slot = -1;
+        }
         if (carr_ck)             /* padding rows: defined (zero) checkpoints */
             memset(carr_ck + ((size_t)nb * GSS_MAXCH + k) * GSS_NCK, 0,
                    sizeof(double) * GSS_NCK * (GSS_MAXCH - k));
@@ -617,46 +659,129 @@ int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, 
         /* ---- 30 s update: nav message, ephemeris set, allocation (gpssim.c:2294-2345) ---- */
         int igrx = (int)(s->grx.sec * 10.0 + 0.5);
         if (igrx % 300 == 0) {
-            for (int i = 0; i < K_MAX_CHAN; i++)
-                if (s->chan[i].prn > 0) {
-                    nav_frame(s->grx, &s->chan[i], 0);
-                    int rc = nav_push(s, &s->chan[i]);
-                    if (rc)
-                        return rc;
-                }
-            /* step to the next ephemeris set when its TOC is < 1 h away; only the first valid
-               SV of that set is tested (gpssim.c:2307-2326).  New subframes reach dwrd at the
-               next 30 s update. */
-            for (int sv = 0; sv < K_MAX_SAT; sv++) {
-                if (s->eph[s->ieph + 1][sv].vflg == 1) {
-                    double dt = gt_diff(s->eph[s->ieph + 1][sv].toc, s->grx);
-                    if (dt < K_SEC_HOUR) {
-                        s->ieph++;
-                        for (int i = 0; i < K_MAX_CHAN; i++)
-                            if (s->chan[i].prn != 0)
-                                nav_subframes(&s->eph[s->ieph][s->chan[i].prn - 1], &s->io,
-                                              s->chan[i].sbf);
-                    }
-                    break;
-                }
-            }
-            int rc = allocate_channels(s, s->eph[s->ieph], s->grx, xyz);
-            if (rc < 0)
+            int rc = update_30s(s, xyz, 1);
+            if (rc)
                 return rc;
-            if (s->opt.verbose) {
-                msg(s, "\n");
-                print_channels(s);
-            }
         }
 
         s->grx = gt_add(s->grx, 0.1);
         msg(s, "\rTime into run = %4.1f", gt_diff(s->grx, s->g0));
         s->iumd++;
     }
-
-    plan_batch(s, blk, nch, carr_ck, nb, threads);
-    s->plan_sec += wall_now() - t_start;
+    s->rows_out += nb;
     *n_out = nb;
+    return 0;
+}
+
+int gss_scn_next_deferred(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch,
+                          gss_chain_t *chain, int *n_out, int threads)
+{
+    *n_out = 0;
+    if (s == NULL || blk == NULL || nch == NULL || chain == NULL || max_blocks <= 0)
+        return gss_fail(GSS_E_ARG, "invalid argument");
+    double t_start = wall_now();
+    int rc = next_rows(s, max_blocks, blk, nch, chain, NULL, n_out, threads);
+    s->plan_sec += wall_now() - t_start;
+    return rc;
+}
+
+int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, double *carr_ck,
+                 int *n_out, int threads)
+{
+    *n_out = 0;
+    if (s == NULL || blk == NULL || nch == NULL || max_blocks <= 0)
+        return gss_fail(GSS_E_ARG, "invalid argument");
+    if (!s->carr_known)
+        return gss_fail(GSS_E_STATE, "carrier phases unknown after gss_scn_seek: "
+                        "gss_scn_set_carrier first, or use gss_scn_next_deferred");
+    double t_start = wall_now();
+    if (max_blocks > s->batch_cap) {
+        free(s->chain);
+        s->chain = malloc((size_t)max_blocks * GSS_MAXCH * sizeof(gss_chain_t));
+        if (!s->chain) {
+            s->batch_cap = 0;
+            return gss_fail(GSS_E_NOMEM, "out of memory");
+        }
+        s->batch_cap = max_blocks;
+    }
+    int nb = 0;
+    int rc = next_rows(s, max_blocks, blk, nch, s->chain, carr_ck, &nb, threads);
+    if (rc == 0)
+        rc = gss_carr_chain(s->carr, blk, nch, s->chain, nb, s->n_per_blk, s->opt.carrier_int,
+                            carr_ck, threads);
+    s->plan_sec += wall_now() - t_start;
+    *n_out = rc ? 0 : nb;
+    return rc;
+}
+
+/* Jump to run block `block` without producing the blocks before it: only the 30 s updates are
+   replayed (nav frames, ephemeris steps, allocation: all independent of the per-block refresh),
+   plus, for the block just before the target, the ranges that computeCodePhase of the target
+   block needs as rho0 (gpssim.c:1324-1348).  The slots' carrier phases are then unknown. */
+int gss_scn_seek(gss_scn *s, int64_t block, int threads)
+{
+    (void)threads;
+    if (s == NULL || block < 0)
+        return gss_fail(GSS_E_ARG, "invalid seek");
+    const int64_t target = block + 1;                 /* iumd of the first block to produce */
+    if (target < s->iumd)
+        return gss_fail(GSS_E_STATE, "seek backwards (at block %d, asked %lld)", s->iumd - 1,
+                        (long long)block);
+    if (target > s->numd)
+        return gss_fail(GSS_E_ARG, "seek past the end (%d blocks)", s->numd - 1);
+    if (target == s->iumd)
+        return 0;
+    double t_start = wall_now();
+    while (s->iumd < target) {
+        const double *xyz = s->static_mode ? s->xyz[0] : s->xyz[s->iumd];
+        for (int i = 0; i < K_MAX_CHAN; i++) {
+            chan_t *ch = &s->chan[i];
+            if (ch->prn <= 0)
+                continue;
+            ch->carr_fresh = 0;              /* the chain started in a skipped block */
+            if (s->iumd == target - 1) {     /* rho0 of the target block: this block's range */
+                rng_t rho;
+                sv_range(&rho, &s->eph[s->ieph][ch->prn - 1], &s->io, s->grx, xyz);
+                ch->rho0 = rho;
+                ch->azel[0] = rho.azel[0];
+                ch->azel[1] = rho.azel[1];
+            }
+        }
+        int igrx = (int)(s->grx.sec * 10.0 + 0.5);
+        if (igrx % 300 == 0) {
+            int rc = update_30s(s, xyz, 0);
+            if (rc)
+                return rc;
+        }
+        s->grx = gt_add(s->grx, 0.1);
+        s->iumd++;
+    }
+    /* the active channels' current words as rows of this handle's nav table */
+    for (int i = 0; i < K_MAX_CHAN; i++)
+        if (s->chan[i].prn > 0) {
+            int rc = nav_push(s, &s->chan[i]);
+            if (rc)
+                return rc;
+        }
+    s->carr_known = 0;
+    s->plan_sec += wall_now() - t_start;
+    return 0;
+}
+
+int gss_scn_carrier(const gss_scn *s, double *carr)
+{
+    if (s == NULL || carr == NULL)
+        return gss_fail(GSS_E_ARG, "null argument");
+    memcpy(carr, s->carr, sizeof s->carr);
+    return 0;
+}
+
+int gss_scn_set_carrier(gss_scn *s, const double *carr)
+{
+    if (s == NULL || carr == NULL)
+        return gss_fail(GSS_E_ARG, "null argument");
+    memcpy(s->carr, carr, sizeof s->carr);
+    s->carr_known = 1;
     return 0;
 }
 
@@ -677,9 +802,7 @@ int gss_scn_close(gss_scn *s)
         return 0;
     free(s->xyz);
     free(s->nav_rows);
-    free(s->b_slot);
-    free(s->b_reset);
-    free(s->b_init);
+    free(s->chain);
     free(s->rg);
     free(s);
     return 0;

@@ -48,6 +48,10 @@ LIN_DTYPE = np.dtype([
 ])
 assert LIN_DTYPE.itemsize == 192
 
+# gss_chain_t (16 bytes): the carrier chain a (block, channel) row continues, gpssim_amd.h
+CHAIN_DTYPE = np.dtype([("slot", "i1"), ("reset", "u1"), ("pad", "u1", (6,)), ("init", "<f8")])
+assert CHAIN_DTYPE.itemsize == 16
+
 
 class GssError(RuntimeError):
     def __init__(self, code, msg):
@@ -75,7 +79,8 @@ class _Cli(C.Structure):
 class _Info(C.Structure):
     _fields_ = [("n_per_blk", C.c_int), ("n_blocks", C.c_int), ("data_format", C.c_int),
                 ("samp_freq", C.c_double), ("delt", C.c_double), ("week", C.c_int),
-                ("sec", C.c_double)]
+                ("sec", C.c_double), ("next_block", C.c_int64), ("rows_out", C.c_int64),
+                ("carrier_int", C.c_int)]
 
 
 _lib = None
@@ -86,6 +91,7 @@ _P = C.c_void_p
 SINK_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int64, C.c_int)
 _SIGS = {
     "gss_run": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.c_int, C.c_int, SINK_FN, _P]),
+    "gss_run_ex": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.c_int, C.c_int, SINK_FN, _P, _P]),
     "gss_dev_open": (C.c_int, [C.POINTER(_P), C.c_int]),
     "gss_dev_close": (C.c_int, [_P]),
     "gss_dev_reserve": (C.c_int, [_P, C.c_int, C.c_int]),
@@ -111,6 +117,11 @@ _SIGS = {
     "gss_scn_open": (C.c_int, [C.POINTER(_P), C.POINTER(_Opts)]),
     "gss_scn_info": (C.c_int, [_P, C.POINTER(_Info)]),
     "gss_scn_next": (C.c_int, [_P, C.c_int, _P, _P, _P, C.POINTER(C.c_int), C.c_int]),
+    "gss_scn_next_deferred": (C.c_int, [_P, C.c_int, _P, _P, _P, C.POINTER(C.c_int), C.c_int]),
+    "gss_carr_chain": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int]),
+    "gss_scn_seek": (C.c_int, [_P, C.c_int64, C.c_int]),
+    "gss_scn_carrier": (C.c_int, [_P, _P]),
+    "gss_scn_set_carrier": (C.c_int, [_P, _P]),
     "gss_scn_nav_table": (C.c_int, [_P, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_int)]),
     "gss_ca_table": (C.c_int, [_P]),
     "gss_scn_plan_seconds": (C.c_double, [_P]),
@@ -260,6 +271,7 @@ class Scenario:
         o.user_motion_size = int(user_motion_size)
         o.quiet = int(bool(quiet))
         o.carrier_int = int(carrier == "int")      # FLOAT_CARR_PHASE off (gpssim.h:4)
+        self._carrier_int = o.carrier_int
         self._h = C.c_void_p()
         _check(lib().gss_scn_open(C.byref(self._h), C.byref(o)))
         self._init_info()
@@ -276,6 +288,7 @@ class Scenario:
             raise SystemExit(1)
         self = cls.__new__(cls)
         self._keep = [cli]
+        self._carrier_int = cli.opt.carrier_int
         self._h = C.c_void_p()
         _check(lib().gss_scn_open(C.byref(self._h), C.byref(cli.opt)))
         self._init_info()
@@ -287,6 +300,44 @@ class Scenario:
         self.n_per_blk, self.n_blocks = inf.n_per_blk, inf.n_blocks
         self.data_format, self.samp_freq, self.delt = inf.data_format, inf.samp_freq, inf.delt
         self.start_week, self.start_sec = inf.week, inf.sec
+
+    def position(self):
+        """(next run block this handle produces, blocks whose rows it has produced)"""
+        inf = _Info()
+        _check(lib().gss_scn_info(self._h, C.byref(inf)))
+        return inf.next_block, inf.rows_out
+
+    def seek(self, block, threads=8):
+        """Skip to run block `block` without producing the blocks before it (gss_scn_seek): only
+        the 30 s updates are replayed.  The slot carriers are unknown until set_carrier()."""
+        _check(lib().gss_scn_seek(self._h, int(block), threads))
+
+    def carrier(self):
+        """The planner's carrier phase per channel slot at the next block ([16] float64)."""
+        c = np.zeros(MAXCH, np.float64)
+        _check(lib().gss_scn_carrier(self._h, _ptr(c)))
+        return c
+
+    def set_carrier(self, carr):
+        c = np.ascontiguousarray(carr, np.float64)
+        assert c.shape == (MAXCH,)
+        _check(lib().gss_scn_set_carrier(self._h, _ptr(c)))
+
+    def next_deferred(self, max_blocks, threads=8):
+        """Next batch without its carrier phases: (blk, nch, chain[nb, 16] CHAIN_DTYPE);
+        carr_chain() fills blk["carr0"] once the slot carriers at the first block are known."""
+        blk = np.zeros((max_blocks, MAXCH), CHAN_DTYPE)
+        nch = np.zeros(max_blocks, np.int32)
+        chain = np.zeros((max_blocks, MAXCH), CHAIN_DTYPE)
+        nb = C.c_int(0)
+        _check(lib().gss_scn_next_deferred(self._h, max_blocks, _ptr(blk), _ptr(nch),
+                                           _ptr(chain), C.byref(nb), threads))
+        n = nb.value
+        return blk[:n].copy(), nch[:n].copy(), chain[:n].copy()
+
+    @property
+    def carrier_int(self):
+        return bool(self._carrier_int)
 
     def _s(self, v):
         b = str(v).encode()
@@ -340,6 +391,21 @@ class Scenario:
             self.close()
         except Exception:
             pass
+
+
+def carr_chain(carr, blk, nch, chain, n_per_blk, carrier_int=False, with_ck=True, threads=8):
+    """The carrier chain over deferred rows (gss_carr_chain): fills blk["carr0"] in place from
+    carr[16] = the slot carriers at the first block; returns (carrier after the last block,
+    checkpoints [nb, 16, NCK] or None)."""
+    c = np.array(carr, np.float64, copy=True)
+    assert c.shape == (MAXCH,) and blk.flags.c_contiguous and blk.dtype == CHAN_DTYPE
+    nch = np.ascontiguousarray(nch, np.int32)
+    chain = np.ascontiguousarray(chain, CHAIN_DTYPE)
+    nb = len(nch)
+    ck = np.zeros((nb, MAXCH, NCK), np.float64) if with_ck else None
+    _check(lib().gss_carr_chain(_ptr(c), _ptr(blk), _ptr(nch), _ptr(chain), nb, int(n_per_blk),
+                                int(bool(carrier_int)), _ptr(ck), threads))
+    return c, ck
 
 
 class Device:

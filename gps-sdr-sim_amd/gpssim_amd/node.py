@@ -2,7 +2,9 @@
 options>` under torchrun, one process per GPU.
 
 Every rank renders its contiguous block range of the run on its own GPU into HBM (the time-window
-shard: [B r/N, B (r+1)/N), the partition the C CLI's pwrite path uses, gps_sdr_sim.c).  Rank 0
+shard: [B r/N, B (r+1)/N), the partition the C CLI's pwrite path uses, gps_sdr_sim.c).  Each rank
+plans only its own window (gpssim_amd.shard.plan_window: seek, deferred rows, the slot carriers
+handed on from the rank before).  Rank 0
 then writes the whole run to the reference's sink -- a file, or stdout with `-o -`
 (gpssim.c:2101-2111, 2276-2287) -- in run order: its own chunks straight from HBM, every other
 rank's chunks received point to point over RCCL (xGMI) into two alternating receive buffers, the
@@ -97,7 +99,8 @@ def run_node(argv, rank, world, local, backend="nccl", chunk_blocks=None, thread
     """The whole-node run of one gps-sdr-sim command line; returns rank 0's byte count."""
     import torch
     import torch.distributed as dist
-    from .render import DeviceWindow, plan_range
+    from .render import DeviceWindow
+    from .shard import Baton, plan_window
 
     chunk_blocks = chunk_blocks or int(os.environ.get("GSS_CHUNK_BLOCKS", "256"))
     scn, out_file = Scenario.from_cli(argv)
@@ -107,7 +110,8 @@ def run_node(argv, rank, world, local, backend="nccl", chunk_blocks=None, thread
     dev_t = torch.device("cuda", local)
     dev = Device(local)
     b0, b1 = rank_blocks(n_blocks, rank, world)
-    blk, nch, ck = plan_range(scn, b0, b1 - b0, threads=threads, with_ck=True)
+    baton = Baton(dist, rank, world, device=dev_t if backend == "nccl" else "cpu")
+    blk, nch, ck, _ = plan_window(scn, b0, b1 - b0, baton=baton, threads=threads)
     win = DeviceWindow(torch, dev, dev_t, blk, nch, scn.nav_table(), npb, fmt, ck=ck,
                        threads=threads)
     win.step(torch.cuda.current_stream(dev_t).cuda_stream)

@@ -2,38 +2,14 @@
 (gss_linearize) and gss_synth_lin_device in batches, output left in HBM (a torch uint8 tensor).
 
 Used by bench.py (timed steps over a resident window) and gpssim_amd.node (each rank renders its
-time-window shard before the ordered gather to rank 0).  torch is only the allocator and stream
+time-window shard before the ordered gather to rank 0); the rows come from gpssim_amd.shard.  torch is only the allocator and stream
 here; the kernels run through the C ABI.
 """
 import time
 
 import numpy as np
 
-from . import (CHAN_DTYPE, LIN_DTYPE, MAXCH, NCK, block_bytes, ca_table, linearize)
-
-
-def plan_range(scn, first, count, threads=8, batch=2000, with_ck=False):
-    """Blocks [first, first + count) of Scenario scn (count < 0: to the end): blk, nch (and the
-    carrier checkpoints when with_ck).  Blocks before `first` are planned and dropped: the
-    carrier chain is serial (gpssim.c:2245-2250 carries carr_phase across blocks)."""
-    done, parts = 0, []
-    want = None if count < 0 else first + count
-    while want is None or done < want:
-        ask = batch if want is None else min(batch, want - done)
-        r = scn.next(ask, threads=threads, with_ck=with_ck)
-        nb = len(r[1])
-        if nb == 0:
-            break
-        lo = max(0, first - done)
-        if lo < nb:
-            parts.append(tuple(a[lo:] for a in r))
-        done += nb
-    if not parts:
-        empty = [np.zeros((0, MAXCH), CHAN_DTYPE), np.zeros(0, np.int32)]
-        if with_ck:
-            empty.append(np.zeros((0, MAXCH, NCK)))
-        return tuple(empty)
-    return tuple(np.concatenate([p[i] for p in parts]) for i in range(len(parts[0])))
+from . import CHAN_DTYPE, LIN_DTYPE, MAXCH, NCK, block_bytes, ca_table, linearize
 
 
 class DeviceWindow:

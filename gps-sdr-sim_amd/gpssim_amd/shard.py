@@ -1,18 +1,30 @@
-"""Time-window sharding of one run across ranks.
+"""Time-window sharding of one run across ranks, planned once per node.
 
 Blocks are independent given their per-block parameters: the code state is recomputed every
-block (gpssim.c:1331-1345) and the host planner supplies each block's exact carrier start
-(gss_carr_advance), so rank r can synthesise any contiguous block range on its own.  There is no
-data-path collective; a whole-run file is rank slices at byte offset first_block * block_bytes.
+block (gpssim.c:1331-1345), and the only state the sample loop carries across blocks is the
+carrier phase (gpssim.c:2245-2250), one chain per channel slot, restarted where allocateChannel
+re-initialises the slot (gpssim.c:1615-1626).  So every rank plans its own window in parallel:
+
+  1. gss_scn_seek to its first block: only the 30 s updates before it are replayed (nav frames,
+     ephemeris steps, allocation), never the per-block refresh of earlier blocks;
+  2. gss_scn_next_deferred over its window: every row except the carrier phases, plus the slot
+     chain each row continues;
+  3. the 16 slot carriers at its first block arrive from rank r-1 (the baton: 128 bytes, point to
+     point over torch.distributed); gss_carr_chain walks the carrier over its window, filling
+     carr0 and the checkpoints, and the end state goes on to rank r+1.
+
+Steps 1-2 cost the same on every rank; step 3 is the carrier-only walk, the one serial piece, and
+each rank walks only its own window.  There is no data-path collective; a whole-run file is rank
+slices at byte offset first_block * block_bytes.
 
 Weak scaling (bench.py): every rank owns `window_s` seconds, i.e. blocks_per = window_s*10 - 1
-blocks starting at r * blocks_per, of one run of world * window_s seconds.  The host plane is
-serial in the carrier chain, so each rank plans up to its own window (the carrier at a block
-start depends on every earlier block).
+blocks starting at r * blocks_per, of one run of world * window_s seconds.
 """
+import time
+
 import numpy as np
 
-from . import Scenario
+from . import MAXCH, Scenario, carr_chain
 
 
 def blocks_per_rank(window_s):
@@ -27,34 +39,87 @@ def rank_range(rank, world, window_s):
     return rank * n, n
 
 
-def plan_rank(nav_file, rank, world, window_s, *, llh, samp_freq=2.6e6, data_format=16,
-              threads=8, batch=1000):
-    """Host plane for one rank: (blk[n, 16], nch[n], ck[n, 16, NCK], nav rows, n_per_blk) of its
-    block range (ck: the planner's carrier checkpoints)."""
-    first, count = rank_range(rank, world, window_s)
-    scn = Scenario(nav_file, llh=llh, duration=window_s * world if world > 1 else window_s,
-                   samp_freq=samp_freq, data_format=data_format)
-    done, keep_b, keep_n, keep_c = 0, [], [], []
-    while done < first + count:
-        if done < first:             # before the window only the carrier chain matters
-            ask = min(batch, first - done)
-            b, n = scn.next(ask, threads=threads)
+class Baton:
+    """The slot carriers at a rank's first block, handed from rank r-1 to rank r (point to point
+    over torch.distributed; `device` "cuda" for RCCL, "cpu" for gloo)."""
+
+    def __init__(self, dist, rank, world, device="cpu"):
+        import torch
+        self.torch, self.dist, self.rank, self.world, self.device = torch, dist, rank, world, device
+
+    def recv(self):
+        t = self.torch.empty(MAXCH, dtype=self.torch.float64, device=self.device)
+        self.dist.recv(t, src=self.rank - 1)
+        return t.cpu().numpy()
+
+    def send(self, carr):
+        if self.rank + 1 < self.world:
+            t = self.torch.from_numpy(np.ascontiguousarray(carr, np.float64)).to(self.device)
+            self.dist.send(t, dst=self.rank + 1)
+
+
+def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=True):
+    """Rows of blocks [first, first + count) of Scenario scn (count < 0: to the end), planned
+    without the blocks before `first` when a baton supplies the carriers there (rank > 0).
+    Returns (blk, nch, ck or None, timings {seek_s, rows_s, wait_s, chain_s}).  Without a baton
+    and first > 0 the prefix's carrier chain is planned here (a lone process)."""
+    t = {}
+    t0 = time.perf_counter()
+    carr = None
+    if first > 0 and baton is None:          # no rank before us: walk the prefix ourselves
+        done = scn.position()[0]
+        while done < first:
+            b, n = scn.next(min(batch, first - done), threads=threads)
             if len(n) == 0:
                 break
             done += len(n)
-            continue
-        b, n, c = scn.next(min(batch, first + count - done), threads=threads, with_ck=True)
+        carr = scn.carrier()
+    else:
+        scn.seek(first, threads=threads)
+    t["seek_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    parts = []
+    done = 0
+    while count < 0 or done < count:
+        ask = batch if count < 0 else min(batch, count - done)
+        b, n, c = scn.next_deferred(ask, threads=threads)
         if len(n) == 0:
             break
-        lo = max(0, first - done)
-        if lo < len(n):
-            keep_b.append(b[lo:])
-            keep_n.append(n[lo:])
-            keep_c.append(c[lo:])
+        parts.append((b, n, c))
         done += len(n)
-    blk = np.concatenate(keep_b)[:count]
-    nch = np.concatenate(keep_n)[:count]
-    ck = np.concatenate(keep_c)[:count]
+    t["rows_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    if carr is None:
+        carr = baton.recv() if (baton is not None and baton.rank > 0) else scn.carrier()
+    t["wait_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    if parts:
+        blk = np.concatenate([p[0] for p in parts])
+        nch = np.concatenate([p[1] for p in parts])
+        chain = np.concatenate([p[2] for p in parts])
+    else:
+        from . import CHAIN_DTYPE, CHAN_DTYPE
+        blk = np.zeros((0, MAXCH), CHAN_DTYPE)
+        nch = np.zeros(0, np.int32)
+        chain = np.zeros((0, MAXCH), CHAIN_DTYPE)
+    end, ck = carr_chain(carr, blk, nch, chain, scn.n_per_blk, carrier_int=scn.carrier_int,
+                         with_ck=with_ck, threads=threads)
+    t["chain_s"] = time.perf_counter() - t0
+    if baton is not None:
+        baton.send(end)
+    return blk, nch, ck, t
+
+
+def plan_rank(nav_file, rank, world, window_s, *, llh, samp_freq=2.6e6, data_format=16,
+              threads=8, batch=2000, baton=None):
+    """Host plane for one rank: (blk[n, 16], nch[n], ck[n, 16, NCK], nav rows, n_per_blk,
+    timings) of its block range (ck: the carrier checkpoints).  With world > 1 pass a Baton: the
+    rank then plans only its own window (module docstring)."""
+    first, count = rank_range(rank, world, window_s)
+    scn = Scenario(nav_file, llh=llh, duration=window_s * world if world > 1 else window_s,
+                   samp_freq=samp_freq, data_format=data_format)
+    blk, nch, ck, t = plan_window(scn, first, count, baton=baton, threads=threads, batch=batch)
     if len(nch) != count:
         raise RuntimeError(f"rank {rank}: planned {len(nch)} of {count} blocks")
-    return blk, nch, ck, scn.nav_table(), scn.n_per_blk
+    t["rows_out"] = int(scn.position()[1])
+    return blk, nch, ck, scn.nav_table(), scn.n_per_blk, t

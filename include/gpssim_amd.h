@@ -233,6 +233,10 @@ typedef struct gss_scn_info {
     double samp_freq;           /* after rounding to a multiple of 10 Hz                       */
     double delt;                /* 1/samp_freq (gpssim.c:1881)                                 */
     int    week;  double sec;   /* g0 (start time)                                             */
+    int64_t next_block;         /* run index of the next block gss_scn_next* produces          */
+    int64_t rows_out;           /* blocks whose rows this handle produced (gss_scn_seek skips
+                                   blocks without producing them)                              */
+    int    carrier_int;         /* gss_opts_t.carrier_int                                      */
 } gss_scn_info_t;
 
 typedef struct gss_scn gss_scn;
@@ -248,6 +252,40 @@ int gss_scn_info(const gss_scn *s, gss_scn_info_t *info);
    [max_blocks][GSS_MAXCH][GSS_NCK] carrier checkpoints.  *n_out = blocks produced (0 at end). */
 int gss_scn_next(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch, double *carr_ck,
                  int *n_out, int threads);
+
+/* ---- planning a time window without its prefix (multi-GPU: plan once, scatter) ----------------
+   The carrier phase is the only state the sample loop carries across blocks (gpssim.c:2245-2250;
+   the code state is recomputed every block, gpssim.c:1331-1345), and it is one chain per channel
+   slot, restarted where allocateChannel re-initialises the slot (gpssim.c:1615-1626).  So a rank
+   can produce its window's rows by itself (gss_scn_seek + gss_scn_next_deferred) and receive only
+   the 16 slot carriers at its first block from the rank before it, which runs the chain over its
+   own window (gss_carr_chain) and hands the end state on.                                     */
+typedef struct gss_chain {       /* per (block, channel row): the carrier chain it continues     */
+    int8_t  slot;                /* chan[] slot 0..15; -1 for padding rows                        */
+    uint8_t reset;               /* 1: the slot's chain restarts at this block with `init`        */
+    uint8_t pad[6];
+    double  init;                /* carr_phase set by allocateChannel (valid when reset)          */
+} gss_chain_t;                   /* 16 bytes, laid out [nblk][GSS_MAXCH] like the rows             */
+
+/* gss_scn_next without the carrier chain: blk[].carr0 is left 0 and chain[] says which slot's
+   chain each row continues; gss_carr_chain fills carr0 (and checkpoints) afterwards.           */
+int gss_scn_next_deferred(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch,
+                          gss_chain_t *chain, int *n_out, int threads);
+/* The carrier chain over nblk consecutive blocks of deferred rows: carr[GSS_MAXCH] holds each
+   slot's carrier phase at the first block's start on entry and after the last block on return;
+   fills blk[].carr0 and, if carr_ck != NULL, the [nblk][GSS_MAXCH][GSS_NCK] checkpoints.
+   carrier_int: the integer-carrier chain of gss_opts_t.carrier_int.  One slot per thread.    */
+int gss_carr_chain(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
+                   const gss_chain_t *chain, int nblk, int n_per_blk, int carrier_int,
+                   double *carr_ck, int threads);
+/* Move to run block `block` (>= the next block) without producing the blocks in between: only the
+   30 s updates are replayed (nav frames, ephemeris steps, allocation), and the ranges of the
+   block before the target (rho0 of computeCodePhase).  The slot carriers are unknown afterwards:
+   gss_scn_next fails until gss_scn_set_carrier; gss_scn_next_deferred works.                */
+int gss_scn_seek(gss_scn *s, int64_t block, int threads);
+/* The planner's carrier per slot at the next block (get) / set it (after a seek).             */
+int gss_scn_carrier(const gss_scn *s, double *carr);
+int gss_scn_set_carrier(gss_scn *s, const double *carr);
 
 /* Nav-word table rows produced so far ([n][GSS_NAV_WORDS]); valid until the next gss_scn_next. */
 int gss_scn_nav_table(const gss_scn *s, const uint32_t **rows, int *n_rows);
@@ -277,6 +315,21 @@ typedef int (*gss_sink_fn)(void *user, const void *bytes, size_t n, int64_t firs
    multi-GPU run passes its own range and writes at first_block * gss_block_bytes().           */
 int gss_run(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_blocks, int batch,
             int threads, gss_sink_fn sink, void *user);
+
+/* gss_run for one process of a multi-process run, planned once per node (no process plans another
+   process's blocks): with carr_in set, the planner thread seeks to first_block (gss_scn_seek),
+   produces the range's rows (gss_scn_next_deferred), calls carr_in for the 16 slot carriers at
+   first_block (it may block until the process before has them), walks the carrier chain over
+   the range (gss_carr_chain) and hands the end state to carr_out (if set) -- before the first
+   batch renders.  Both callbacks return 0, or non-zero to abort the run (GSS_E_IO).
+   opts == NULL or carr_in == NULL: gss_run (blocks before first_block planned and dropped).  */
+typedef struct gss_run_opts {
+    int (*carr_in)(void *user, double *carr);             /* [GSS_MAXCH], out                  */
+    int (*carr_out)(void *user, const double *carr);      /* [GSS_MAXCH]                       */
+    void *carr_user;
+} gss_run_opts_t;
+int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_blocks, int batch,
+               int threads, gss_sink_fn sink, void *user, const gss_run_opts_t *opts);
 
 
 /* Exact carrier-chain helpers (exported for tests): advance the reference recurrence

@@ -1,9 +1,9 @@
 """The N>1 path on CPU: time-window shards (gpssim_amd.shard, the decomposition bench.py runs under
-torchrun) planned independently by two gloo ranks, synthesised per rank (CPU oracle as the
-byte producer; no GPU here), gathered over torch.distributed, and compared block by block with
-the reference's golden hashes of one single-process run.  Covers the rank partition, each rank's
-independent host planning (the exact carrier chain up to its window) and the byte layout of the
-concatenated slices."""
+torchrun) planned once per node by two gloo ranks -- each seeks to its own window, produces its
+rows, and receives the 16 slot carriers at its first block from the rank before (the baton) --
+synthesised per rank (CPU oracle as the byte producer; no GPU here), gathered over
+torch.distributed, and compared block by block with the reference's golden hashes of one
+single-process run.  Rank 1 must never produce a row of a block before its window."""
 import hashlib
 import json
 import os
@@ -24,18 +24,21 @@ def _paths():
             sys.path.insert(0, p)
 
 
-def _worker(rank, world, port, result_path):
+def _worker(rank, world, port, result_path, window_s=WINDOW_S):
     _paths()
     import numpy as np
     import torch
     import torch.distributed as dist
     import gpssim_amd as G
     import oracle
-    from gpssim_amd.shard import plan_rank, rank_range
+    from gpssim_amd.shard import Baton, plan_rank, rank_range
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    blk, nch, ck, nav, npb = plan_rank(NAV, rank, world, WINDOW_S, llh=LOC, threads=2)
+    blk, nch, ck, nav, npb, t = plan_rank(NAV, rank, world, window_s, llh=LOC, threads=2,
+                                          baton=Baton(dist, rank, world))
+    # the rank produced rows for its own window only (rank 1 seeked past rank 0's blocks)
+    assert t["rows_out"] == len(nch) == rank_range(rank, world, window_s)[1]
     out, rc = oracle.synth(blk, nch, G.ca_table(), nav, npb, 16)
     assert rc == 0
     t = torch.from_numpy(np.ascontiguousarray(out))
@@ -46,7 +49,7 @@ def _worker(rank, world, port, result_path):
         whole = torch.cat(parts).numpy().tobytes()
         hashes = [hashlib.sha256(whole[i * bb:(i + 1) * bb]).hexdigest()[:16]
                   for i in range(len(whole) // bb)]
-        firsts = [rank_range(r, world, WINDOW_S)[0] for r in range(world)]
+        firsts = [rank_range(r, world, window_s)[0] for r in range(world)]
         json.dump({"hashes": hashes, "firsts": firsts}, open(result_path, "w"))
     dist.barrier()
     dist.destroy_process_group()
@@ -60,12 +63,19 @@ def _free_port():
     return p
 
 
-def test_two_rank_time_window_shards(tmp_path, golden):
+@pytest.mark.parametrize("window_s,gold", [
+    (WINDOW_S, "static_d30_b16"),
+    # rank 1 starts at block 309: its seek replays the 30 s nav/allocation update after block
+    # 299 (gpssim.c:2294-2345) and its own window crosses the one after block 599
+    (31.0, "static_d300_b16"),
+])
+def test_two_rank_time_window_shards(tmp_path, golden, window_s, gold):
     import torch.multiprocessing as mp
     world = 2
     res = tmp_path / "r.json"
-    mp.spawn(_worker, args=(world, _free_port(), str(res)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(res), window_s), nprocs=world, join=True)
     r = json.load(open(res))
-    assert r["firsts"] == [0, 4]
-    want = golden["static_d30_b16"]["block_sha16"][: 4 * world]
+    n = int(round(window_s * 10)) - 1
+    assert r["firsts"] == [0, n]
+    want = golden[gold]["block_sha16"][: n * world]
     assert r["hashes"] == want
