@@ -687,6 +687,7 @@ typedef struct gss_cyc {
                              w - w0 is exact (same coarse lattice) and so is the sum (the result
                              is representable).  A stored difference v0 - w0 would round.      */
     int64_t L;            /* steps                                                              */
+    int succ;             /* the entry the cycle after this one used last time (-1: none)       */
 } gss_cyc;
 
 #define GSS_CC_N 16
@@ -694,6 +695,7 @@ typedef struct gss_cyc_cache {
     gss_cyc e[GSS_CC_N];
     int n, next;
     int enabled;
+    int last;             /* entry of the previous cycle (-1: none / not cached) */
 } gss_cyc_cache;
 
 /* exponent of a positive normal double: v in [2^e, 2^(e+1)) */
@@ -819,19 +821,33 @@ GSS_HD int64_t gss_desc_head(double *x, double s, double T, int64_t n, int *stop
 
 #define GSS_BIG 1.0e300
 
-GSS_HD const gss_cyc *gss_cc_find(const gss_cyc_cache *cc, double w, int64_t nmax)
+/* The orbit of cycle starts visits the entries in a nearly fixed order (the cycle map is a
+   translation per entry), so the successor of the previous cycle's entry is tried first. */
+GSS_HD const gss_cyc *gss_cc_find(gss_cyc_cache *cc, double w, int64_t nmax)
 {
-    for (int i = 0; i < cc->n; i++)
-        if (w >= cc->e[i].lo && w <= cc->e[i].hi && cc->e[i].L <= nmax)
-            return &cc->e[i];
-    return 0;
+    const int p = cc->last >= 0 ? cc->e[cc->last].succ : -1;
+    int hit = -1;
+    if (p >= 0 && w >= cc->e[p].lo && w <= cc->e[p].hi && cc->e[p].L <= nmax) {
+        hit = p;
+    } else {
+        for (int i = 0; i < cc->n; i++)
+            if (w >= cc->e[i].lo && w <= cc->e[i].hi && cc->e[i].L <= nmax) {
+                hit = i;
+                break;
+            }
+    }
+    if (hit >= 0 && cc->last >= 0)
+        cc->e[cc->last].succ = hit;
+    cc->last = hit;
+    return hit >= 0 ? &cc->e[hit] : 0;
 }
 
 GSS_HD void gss_cc_put(gss_cyc_cache *cc, double w, double dlo, double dhi, double safe,
                        double v_end, int64_t L)
 {
     if (!(dlo <= 0.0 && dhi >= 0.0)) return;
-    gss_cyc *e = &cc->e[cc->next];
+    const int i = cc->next;
+    gss_cyc *e = &cc->e[i];
     e->lo = w + dlo + safe;
     e->hi = w + dhi - safe;
     if (e->lo > w) e->lo = w;                  /* the walked start itself is always valid */
@@ -839,6 +855,10 @@ GSS_HD void gss_cc_put(gss_cyc_cache *cc, double w, double dlo, double dhi, doub
     e->w0 = w;
     e->v0 = v_end;
     e->L = L;
+    e->succ = -1;
+    if (cc->last >= 0 && cc->last != i)
+        cc->e[cc->last].succ = i;
+    cc->last = i;
     cc->next = (cc->next + 1) % GSS_CC_N;
     if (cc->n < GSS_CC_N) cc->n++;
 }
@@ -860,6 +880,7 @@ GSS_HD void gss_carr_it_init(gss_carr_it *it, double x, double s, int64_t n)
     it->mid = 1;
     it->cc.n = 0;
     it->cc.next = 0;
+    it->cc.last = -1;
     it->cc.enabled = (s != 0.0);
     double as = s < 0.0 ? -s : s;
     it->T = as > 0.0 ? gss_pow2(gss_exp2i(as) + 2) : 0.0;
@@ -977,6 +998,7 @@ GSS_HD void gss_code_it_init(gss_code_it *it, gss_code_state c, double cs, int64
     it->mid = 1;
     it->cc.n = 0;
     it->cc.next = 0;
+    it->cc.last = -1;
     it->cc.enabled = (cs > 0.0);
 }
 

@@ -742,8 +742,13 @@ __device__ __forceinline__ void lin_pair_chunk(lin_f4 (&cq)[LIN_CH / 2], uint64_
 #pragma unroll
     for (int s = 0; s < LIN_CH; s++) {
         if (s % 4 == 0) {
-            wa4 = ((const uint4 *)Wa)[s / 4];
-            wb4 = ((const uint4 *)Wb)[s / 4];
+            if (LIN_ABLATE & 64) {
+                wa4 = make_uint4(M * (s + 1), M * (s + 3), M * (s + 5), M * (s + 7));
+                wb4 = make_uint4(M * (s + 2), M * (s + 4), M * (s + 6), M * (s + 8));
+            } else {
+                wa4 = ((const uint4 *)Wa)[s / 4];
+                wb4 = ((const uint4 *)Wb)[s / 4];
+            }
         }
         const uint32_t wa = s % 4 == 0 ? wa4.x : s % 4 == 1 ? wa4.y : s % 4 == 2 ? wa4.z : wa4.w;
         const uint32_t wb = s % 4 == 0 ? wb4.x : s % 4 == 1 ? wb4.y : s % 4 == 2 ? wb4.z : wb4.w;

@@ -278,7 +278,14 @@ def test_streaming_run_bit_exact(dev, golden):
     assert [x for _, x in blocks] == g["block_sha16"][123:184]
 
 
-def test_cli_two_ranks_one_file(golden):
+@pytest.mark.parametrize("handoff,gold,args", [
+    # every rank plans the blocks before its range itself (no run id)
+    (False, "static_d30_b16", ["-l", ",".join(map(str, LOC)), "-d", "30", "-b", "16"]),
+    # planned once per node: rank 1 seeks to block 324, past the 30 s update after block 299,
+    # and takes the slot carriers there from rank 0's hand-off file (gss_run_ex)
+    (True, "static_d65_b8_noiono", ["-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8", "-i"]),
+])
+def test_cli_two_ranks_one_file(golden, handoff, gold, args):
     """The CLI as two ranks (RANK/WORLD_SIZE, both on GPU 0 here): each pwrite()s its block
     range into the same file, which equals the single-process reference output."""
     with tempfile.TemporaryDirectory() as td:
@@ -286,14 +293,20 @@ def test_cli_two_ranks_one_file(golden):
         procs = []
         for r in range(2):
             env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK="0")
+            env.pop("TORCHELASTIC_RUN_ID", None)
+            env.pop("GSS_RUN_ID", None)
+            if handoff:
+                env["GSS_RUN_ID"] = "t%d" % os.getpid()
             procs.append(subprocess.Popen(
-                [G.CLI_PATH, "-e", NAV, "-l", ",".join(map(str, LOC)), "-d", "30", "-b", "16",
-                 "-o", out], env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
+                [G.CLI_PATH, "-e", NAV] + args + ["-o", out], env=env,
+                stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
         for p in procs:
             _, err = p.communicate(timeout=300)
             assert p.returncode == 0, err[-2000:]
         h = hashlib.sha256(open(out, "rb").read()).hexdigest()
-    assert h == golden["static_d30_b16"]["sha256"]
+        left = [f for f in os.listdir(td) if f != "gpssim.bin"]
+    assert h == golden[gold]["sha256"]
+    assert left == [], left                      # the hand-off file was consumed
 
 
 def test_streaming_run_walk_path(dev, golden, monkeypatch):

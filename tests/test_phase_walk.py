@@ -237,3 +237,31 @@ def test_stationary_and_single_steps():
             assert W.wc_carr_f(x, s, n, C.byref(nw)) == want
             assert W.wc_carr_bf(x, s, n, C.byref(nw)) == want
             assert W.wc_carr_trip(x, s, n) == want
+
+
+@pytest.mark.parametrize("seed", [40, 41])
+def test_long_walks_multi_cycle(seed):
+    """Long walks (a 20 MS/s block and 10^8 samples): the cycle-cached walk takes many cached
+    cycles at once (gss_carr_next_wrap with `multi`), stopping at every checkpoint; the end value
+    and all checkpoints equal brute force, including steps whose cycle drifts across a cache
+    entry's [lo, hi] (near-integer 1/s), ties and zero phase."""
+    W = walk_lib()
+    rng = random.Random(seed)
+    for i in range(10):
+        n = [2_000_000, 100_000_000][i % 2] if i < 8 else rng.randint(1, 5_000_000)
+        f = rng.uniform(-6000, 6000)
+        s = f / 2.6e6
+        if i == 2:                            # 1/s within 1e-9 of an integer: slow drift
+            L = rng.randint(300, 3000)
+            s = 1.0 / L + rng.choice([-1, 1]) * 1e-12
+        if i == 3:
+            s = (math.floor(abs(s) / 2.0 ** -53) + 0.5) * 2.0 ** -53
+        x0 = rng.random() if i != 4 else 0.0
+        want = oracle.carr_brute(x0, s, n)
+        assert W.wc_carr_cached(x0, s, n) == want, (i, x0, s, n)
+        if n < 1 << 31:
+            nck = W.wc_nck()
+            ck = np.zeros(nck)
+            assert W.wc_carr_walk_ck(x0, s, n, ck.ctypes.data) == want, i
+            at = [j * n // nck for j in range(nck)]
+            assert np.array_equal(ck, oracle.carr_brute_trace(x0, s, at)), i
