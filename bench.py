@@ -131,6 +131,11 @@ def cpu_baseline(seconds=30):
                       f"{avail[-1]}): wall {wn:.2f} s"}
 
 
+def progress(msg):
+    """a progress line on stderr (the JSON result is the last stdout line)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def lib_sha16(path):
     import hashlib
     with open(path, "rb") as f:
@@ -154,7 +159,8 @@ def load_traffic(workload, kernel, kern_ms, lib_sha):
         return None, "profile of another workload"
     if d.get("lib_sha16") != lib_sha:
         return None, "profile of another build"
-    prof_ms = (d.get("kernel_warm_avg_ns") or d.get("kernel_avg_ns") or 0) / 1e6
+    prof_ms = (d.get("kernel_timed_avg_ns") or d.get("kernel_warm_avg_ns") or
+               d.get("kernel_avg_ns") or 0) / 1e6
     if kern_ms <= 0 or abs(prof_ms - kern_ms) > PROFILE_TOL * kern_ms:
         return None, (f"committed profile kernel time {prof_ms:.3f} ms vs {kern_ms:.3f} ms of "
                       "this un-profiled run")
@@ -210,7 +216,8 @@ def live_traffic(fmt, window, threads, kern_ms, steps, warmup, timeout=150):
         k = next((n for n in cs if n.startswith("gss_lin_kernel")), None)
         if k is None or "WRITE_SIZE" not in cs[k] or "FETCH_SIZE" not in cs[k] or k not in ks:
             return None, "rocprofv3 passes gave no gss_lin_kernel counters", None
-        prof_ms = (PS.warm_avg_ns(kd[k]) if kd.get(k) else ks[k]["avg_ns"]) / 1e6
+        # the same launches as the timed region: the last `steps` dispatches (PS.timed_avg_ns)
+        prof_ms = (PS.timed_avg_ns(kd[k], steps) if kd.get(k) else ks[k]["avg_ns"]) / 1e6
         try:
             line = [l for l in open(os.path.join(top, "kt.log")) if l.startswith("{")][-1]
             child_ms = json.loads(line)["stages_ms"]["fast_path"]
@@ -218,7 +225,8 @@ def live_traffic(fmt, window, threads, kern_ms, steps, warmup, timeout=150):
             child_ms = None
         traffic = round((cs[k]["WRITE_SIZE"] + 2 * cs[k]["FETCH_SIZE"]) * 1024)
         summary = {"kernel": k, "calls": ks[k]["calls"], "avg_ns": ks[k]["avg_ns"],
-                   "warm_avg_ns": prof_ms * 1e6, "min_ns": ks[k]["min_ns"],
+                   "warm_avg_ns": PS.warm_avg_ns(kd[k]) if kd.get(k) else None,
+                   "timed_avg_ns": prof_ms * 1e6, "min_ns": ks[k]["min_ns"],
                    "max_ns": ks[k]["max_ns"], "profiled_run_event_ms": child_ms,
                    "unprofiled_event_ms": kern_ms, "steps": steps, "warmup": warmup,
                    "hbm_write_bytes": cs[k]["WRITE_SIZE"] * 1024,
@@ -234,9 +242,9 @@ def live_traffic(fmt, window, threads, kern_ms, steps, warmup, timeout=150):
                          f"warm-up as this run ({k}: write "
                          f"{cs[k]['WRITE_SIZE'] * 1024 / 1e9:.3f} GB + read "
                          f"{2 * cs[k]['FETCH_SIZE'] * 1024 / 1e9:.3f} GB per launch; profiled "
-                         f"kernel {prof_ms:.3f} ms over its warm launches, "
-                         f"{ks[k]['avg_ns'] / 1e6:.3f} ms over all {ks[k]['calls']}; this run "
-                         f"without the profiler {kern_ms:.3f} ms)"), summary
+                         f"kernel {prof_ms:.3f} ms over its {steps} timed launches, "
+                         f"{ks[k]['avg_ns'] / 1e6:.3f} ms over all {ks[k]['calls']} with the "
+                         f"warm-up; this run without the profiler {kern_ms:.3f} ms)"), summary
     finally:
         if not save:
             shutil.rmtree(top, ignore_errors=True)
@@ -256,7 +264,7 @@ def time_steps(torch, dev, dev_t, res, steps, warmup, stream):
     return el, n_lin, lin_ms
 
 
-def per_config(G, torch, dev, dev_t, stream, steps, warmup, threads):
+def per_config(G, torch, dev, dev_t, stream, steps, warmup, threads, e2e=True):
     from gpssim_amd.render import DeviceWindow
     from gpssim_amd.shard import blocks_per_rank
     out = []
@@ -289,6 +297,11 @@ def per_config(G, torch, dev, dev_t, stream, steps, warmup, threads):
             "host_plan_s": round(plan_s, 3), "host_linearize_s": round(res.lin_s, 3)})
         res.free()
         del blk, nch, s
+        progress(f"{c['name']}: {out[-1]['value']} MS/s")
+        if e2e:
+            # the same run end to end through gss_run (the CLI's path), one pass
+            out[-1]["e2e"] = e2e_run(G, dev, threads, c["window"], fs=c["fs"], fmt=c["fmt"],
+                                     kw=c["kw"], slope=False, desc=c["desc"])
     return out
 
 
@@ -308,14 +321,22 @@ def d2h_ceiling(nbytes, reps=8):
     return round(rate, 2)
 
 
-def e2e_run(G, dev, threads, window=1800.0, batch=128):
-    """gss_run over the whole static run into a discarding sink, wall-clocked (planner, proofs,
-    uploads, kernels, D2H into pinned buffers and the sink, overlapped).  A second run of a third
-    of the length gives the steady-state rate (the slope; the rest is the fixed start-up), to be
-    read against d2h_ceiling_GBps, the measured device -> pinned host copy rate."""
+E2E_SLOT_BYTES = 128 * 1040000  # gss_run slot size: 128 blocks at 2.6 MS/s -b 16 (133 MB)
+
+
+def e2e_run(G, dev, threads, window=1800.0, batch=None, fs=FS, fmt=16, kw=None, slope=True,
+            desc=None):
+    """gss_run over a whole run into a discarding sink, wall-clocked (planner, proofs, uploads,
+    kernels, D2H into pinned buffers and the sink, overlapped).  With `slope` a second run of a
+    third of the length gives the steady-state rate (the slope; the rest is the fixed start-up).
+    Read against d2h_ceiling_GBps, the measured device -> pinned host copy rate of one slot."""
+    kw = kw if kw is not None else {"llh": LOC}
+    bb = G.block_bytes(int(round(fs / 10)), fmt)
+    if batch is None:
+        batch = max(1, E2E_SLOT_BYTES // bb)
 
     def one(w):
-        s = G.Scenario(NAV, llh=LOC, duration=w, samp_freq=FS, data_format=16)
+        s = G.Scenario(NAV, duration=w, samp_freq=fs, data_format=fmt, **kw)
         got = {"bytes": 0, "blocks": 0}
 
         def sink(mv, first, nb):
@@ -326,19 +347,24 @@ def e2e_run(G, dev, threads, window=1800.0, batch=128):
         dev.run(s, sink, batch=batch, threads=threads)
         return time.perf_counter() - t0, got["blocks"], got["bytes"], s.n_per_blk
 
-    ws, bs, _, _ = one(window / 3)
+    if slope:
+        ws, bs, _, _ = one(window / 3)
     wall, blocks, nbytes, n_per_blk = one(window)
     samples = blocks * n_per_blk
-    slope = (blocks - bs) / (wall - ws)
-    return {"value": round(samples / wall / 1e6, 2), "unit": "MS/s",
-            "x_realtime": round(samples / wall / FS, 1), "wall_s": round(wall, 3),
-            "blocks": blocks, "d2h_GBps": round(nbytes / wall / 1e9, 2),
-            "steady_MSps": round(slope * n_per_blk / 1e6, 1),
-            "steady_d2h_GBps": round(slope * nbytes / blocks / 1e9, 2),
-            "startup_s": round(wall - blocks / slope, 3),
-            "d2h_ceiling_GBps": d2h_ceiling(batch * n_per_blk * 4),
-            "workload": f"static -b 16, {window:g} s through gss_run (batch {batch} blocks), "
-                        "discarding sink"}
+    ceiling = d2h_ceiling(batch * bb)
+    out = {"value": round(samples / wall / 1e6, 2), "unit": "MS/s",
+           "x_realtime": round(samples / wall / fs, 1), "wall_s": round(wall, 3),
+           "blocks": blocks, "batch_blocks": batch, "threads": threads,
+           "d2h_GBps": round(nbytes / wall / 1e9, 2), "d2h_ceiling_GBps": ceiling,
+           "frac_of_d2h_ceiling": round(nbytes / wall / 1e9 / ceiling, 3) if ceiling else None,
+           "workload": (desc or f"static -b {fmt}, {window:g} s") +
+                       f" through gss_run (batch {batch} blocks), discarding sink"}
+    if slope:
+        sl = (blocks - bs) / (wall - ws)
+        out.update({"steady_MSps": round(sl * n_per_blk / 1e6, 1),
+                    "steady_d2h_GBps": round(sl * nbytes / blocks / 1e9, 2),
+                    "startup_s": round(wall - blocks / sl, 3)})
+    return out
 
 def main():
     ap = argparse.ArgumentParser()
@@ -367,6 +393,7 @@ def main():
     cpu = None
     if single and not args.no_cpu_baseline:
         cpu = cpu_baseline()
+        progress(f"cpu baseline: {cpu and cpu['value']} MS/s")
 
     import torch                      # loads the HIP runtime our library then shares
     import gpssim_amd as G
@@ -389,6 +416,7 @@ def main():
                                                samp_freq=FS, data_format=args.fmt,
                                                threads=args.threads, baton=baton)
     host_plan_s = time.perf_counter() - t_plan0
+    progress(f"planned {len(nch)} blocks in {host_plan_s:.2f} s")
 
     dev = G.Device(local)
     stream = torch.cuda.current_stream(dev_t).cuda_stream
@@ -453,6 +481,7 @@ def main():
         exact = {"value": round(samples_rank * args.steps / el / 1e6, 2),
                  "ms_per_step": round(el / args.steps * 1e3, 3)}
     ms_per_step = elapsed / args.steps * 1e3
+    progress(f"timed {args.steps} steps: {ms_per_step:.3f} ms/step, kernel {lin_ms:.3f} ms")
     value = world * samples_rank * args.steps / elapsed / 1e6          # MS/s, whole job
     # the dominant kernel is gss_lin_kernel; its algorithmic bytes are the certified blocks'
     bytes_launch = res.n_fast * res.bb
@@ -473,11 +502,14 @@ def main():
         else:
             traffic_src = f"{traffic_src}; committed profile: {s2}"
 
+    progress(f"traffic: {traffic_src[:120]}")
     configs = e2e = None
     if single and not args.no_configs:
-        configs = per_config(G, torch, dev, dev_t, stream, min(args.steps, 3), 1, args.threads)
+        configs = per_config(G, torch, dev, dev_t, stream, min(args.steps, 3), 1, args.threads,
+                             e2e=not args.no_e2e)
     if single and not args.no_e2e:
-        e2e = e2e_run(G, dev, args.threads, args.e2e_window)
+        e2e = e2e_run(G, dev, args.threads, args.e2e_window, batch=128)
+        progress(f"e2e: {e2e['value']} MS/s")
 
     out = {
         "metric": METRIC,

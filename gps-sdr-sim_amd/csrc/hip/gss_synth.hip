@@ -529,6 +529,20 @@ static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole ch
 #ifndef LIN_ABLATE
 #define LIN_ABLATE 0
 #endif
+/* LIN_SWIN 1: the steps' chip windows come from a static table in global memory -- row = C/A
+   table row, entry j = the 32 chips from extended chip j - 32 on, rotated left by j mod 32
+   (gss_tw_kernel; the same word the LDS window pass builds) -- read with wave-uniform addresses,
+   i.e. scalar loads into SGPRs that the shift takes directly.  No window pass, no LDS window
+   reads, no per-workgroup bit-stream copy. */
+#ifndef LIN_SWIN
+#define LIN_SWIN 0
+#endif
+#define LIN_TW_W   (32 * CAB_W - 32)       /* table entries per row (j <= 32 CAB_W - 64 used)    */
+#if LIN_SWIN
+#define LIN_WCON "s"                       /* the shift takes the window from an SGPR            */
+#else
+#define LIN_WCON "v"
+#endif
 /* LIN_MFMA 1: the gain x LUT accumulation runs on the matrix cores instead of v_mad_i64_i32.
    The LUT holds (cos, sin) as an f16 pair (exact integers, |v| <= 250); per channel and pair of
    steps one v_mfma_f32_4x4x4_16b_f16 takes B = the lane's two LUT words (K = cos_s, sin_s,
@@ -571,7 +585,9 @@ struct lin_ct {
     int32_t pos1;
     uint32_t flags;              /* 1: a gain change inside the chunk, 2: patched samples       */
     uint32_t q0, dq, tab, pad;   /* first window offset (1/16 chip), its step, the row          */
+#if !LIN_SWIN
     uint32_t W[LIN_CH];          /* the steps' chip windows                                     */
+#endif
 #if LIN_MFMA
     uint32_t A[4][2];            /* the MFMA gain operand of lane 4b + i: g (f16) at slot i      */
     uint32_t g2, pad2[3];        /* g as an f16 pair (both halves), the pair MFMA's gain         */
@@ -661,6 +677,89 @@ __global__ void gss_cab_kernel(const uint32_t *__restrict__ ca_bits, int n_ca,
     cab[i] = w;
 }
 
+/* the window table of LIN_SWIN: row r, entry j = extended chips j - 32 .. j - 1 of row r's
+   bit-stream, rotated left by j mod 32 (bit (E mod 32) = chip E's sign, E = j - 32 + bit) */
+__global__ void gss_tw_kernel(const uint32_t *__restrict__ cab, int n_ca, uint32_t *__restrict__ tw)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_ca * LIN_TW_W)
+        return;
+    const int row = i / LIN_TW_W;
+    const uint32_t j = (uint32_t)(i - row * LIN_TW_W);
+    if (j > (uint32_t)(32 * CAB_W - 64)) {
+        tw[i] = 0u;
+        return;
+    }
+    const uint32_t *c = cab + (size_t)row * CAB_W;
+    const uint32_t lin = __builtin_amdgcn_alignbit(c[(j >> 5) + 1], c[j >> 5], j & 31);
+    tw[i] = __builtin_amdgcn_alignbit(lin, lin, (32u - j) & 31u);
+}
+
+/* where a channel's chunk windows come from: the wave's LDS record (W = its W[]) or, with
+   LIN_SWIN, the window table (W = the channel's row; q0, dq as in lin_ct, wave-uniform) */
+struct lin_wsrc {
+    const uint32_t *W;
+    uint32_t q0, dq;
+};
+
+/* step s's window; w4 caches four LDS windows (one broadcast read per four steps) */
+__device__ __forceinline__ uint32_t lin_wget(const lin_wsrc &w, int s, uint4 &w4, uint32_t M,
+                                             int salt)
+{
+#if LIN_SWIN
+    (void)w4; (void)M; (void)salt;
+    const uint32_t j = min(((w.q0 + (uint32_t)s * w.dq) >> 4) + (32 - CBW_PRE),
+                           (uint32_t)(32 * CAB_W - 64));
+    return w.W[j];
+#else
+    if (s % 4 == 0) {                                     /* four windows per broadcast read */
+        if (LIN_ABLATE & 64)
+            w4 = make_uint4(M * (s + 1 + salt), M * (s + 3 + salt), M * (s + 5 + salt),
+                            M * (s + 7 + salt));
+        else
+            w4 = ((const uint4 *)w.W)[s / 4];
+    }
+    return s % 4 == 0 ? w4.x : s % 4 == 1 ? w4.y : s % 4 == 2 ? w4.z : w4.w;
+#endif
+}
+
+/* LIN_SWIN: all LIN_CH windows of a chunk as scalar loads issued together and waited for once
+   (the scalar and LDS loads share one counter, so a window load left in flight would turn every
+   LUT read's wait into a full drain) */
+__device__ __forceinline__ void lin_wissue(const lin_wsrc &w, uint32_t (&ws)[LIN_CH])
+{
+#pragma unroll
+    for (int s = 0; s < LIN_CH; s++) {
+        uint4 unused;
+        ws[s] = lin_wget(w, s, unused, 0u, 0);
+    }
+}
+
+/* ... and the fence that needs them all (one wait, after every load of the chunk is issued) */
+__device__ __forceinline__ void lin_wfence(const uint32_t (&ws)[LIN_CH])
+{
+#if LIN_SWIN
+    static_assert(LIN_CH == 16, "the fence below names 16 windows");
+    asm volatile("" :: "s"(ws[0]), "s"(ws[1]), "s"(ws[2]), "s"(ws[3]), "s"(ws[4]), "s"(ws[5]),
+                 "s"(ws[6]), "s"(ws[7]), "s"(ws[8]), "s"(ws[9]), "s"(ws[10]), "s"(ws[11]),
+                 "s"(ws[12]), "s"(ws[13]), "s"(ws[14]), "s"(ws[15]));
+#else
+    (void)ws;
+#endif
+}
+
+__device__ __forceinline__ lin_wsrc lin_wsrc_of(const lin_ct &t, const uint32_t *__restrict__ tw)
+{
+#if LIN_SWIN
+    const uint32_t row = __builtin_amdgcn_readfirstlane(t.tab);
+    return lin_wsrc{tw + (size_t)row * LIN_TW_W, (uint32_t)__builtin_amdgcn_readfirstlane(t.q0),
+                    (uint32_t)__builtin_amdgcn_readfirstlane(t.dq)};
+#else
+    (void)tw;
+    return lin_wsrc{t.W, 0u, 0u};
+#endif
+}
+
 /* one channel's contribution to the chunk's LIN_CH steps: the lane's anchor P (carrier : code,
    high : low word, gss_lin.h) and its 64-sample step D, the steps' chip windows (LDS, the same for every lane),
    the LUT mask M, the signed gain (with LANE_GAIN: the gain difference, applied from sample
@@ -669,22 +768,16 @@ __global__ void gss_cab_kernel(const uint32_t *__restrict__ ca_bits, int n_ca,
 
 template <bool LANE_GAIN>
 __device__ __forceinline__ void lin_channel_chunk(int64_t (&acc)[LIN_CH], uint64_t P, uint64_t D,
-                                                  const uint32_t *W, uint32_t M, int g, int pos1,
+                                                  lin_wsrc W, uint32_t M, int g, int pos1,
                                                   int p0, const int32_t *__restrict__ s_lut)
 {
     uint4 w4;
 #pragma unroll
     for (int s = 0; s < LIN_CH; s++) {
-        if (s % 4 == 0) {                                 /* four windows per broadcast read */
-            if (LIN_ABLATE & 64)
-                w4 = make_uint4(M * (s + 1), M * (s + 3), M * (s + 5), M * (s + 7));
-            else
-                w4 = ((const uint4 *)W)[s / 4];
-        }
-        const uint32_t ws = s % 4 == 0 ? w4.x : s % 4 == 1 ? w4.y : s % 4 == 2 ? w4.z : w4.w;
+        const uint32_t ws = lin_wget(W, s, w4, M, 0);
         uint32_t t;
         asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
-            "src1_sel:DWORD" : "=v"(t) : "v"((uint32_t)P), "v"(ws));             /* bit 0: sign */
+            "src1_sel:DWORD" : "=v"(t) : "v"((uint32_t)P), LIN_WCON(ws));             /* bit 0: sign */
         const uint32_t a = ((LIN_ABLATE & 32) ? t : __builtin_amdgcn_alignbit(t, (uint32_t)(P >> 32), 21)) & M;
         const int32_t e = (LIN_ABLATE & 4) ? (int32_t)a : *(const int32_t *)((const char *)s_lut + a);
         const int gg = LANE_GAIN ? (p0 + s * 64 >= pos1 ? g : 0) : g;
@@ -697,24 +790,27 @@ __device__ __forceinline__ void lin_channel_chunk(int64_t (&acc)[LIN_CH], uint64
    LANE_GAIN the LUT words of samples before pos1 are zeroed and A carries the gain difference) */
 template <bool LANE_GAIN>
 __device__ __forceinline__ void lin_channel_chunk_m(lin_f4 (&cq)[LIN_CH / 2], uint64_t P,
-                                                    uint64_t D, const uint32_t *W, uint32_t M,
+                                                    uint64_t D, lin_wsrc W, uint32_t M,
                                                     lin_half4 A, int pos1, int p0,
                                                     const int32_t *__restrict__ s_lut)
 {
     uint4 w4;
     uint32_t e0 = 0;
+#if LIN_SWIN
+    uint32_t sw[LIN_CH];
+    lin_wissue(W, sw);
+    lin_wfence(sw);
+#endif
 #pragma unroll
     for (int s = 0; s < LIN_CH; s++) {
-        if (s % 4 == 0) {
-            if (LIN_ABLATE & 64)
-                w4 = make_uint4(M * (s + 1), M * (s + 3), M * (s + 5), M * (s + 7));
-            else
-                w4 = ((const uint4 *)W)[s / 4];
-        }
-        const uint32_t ws = s % 4 == 0 ? w4.x : s % 4 == 1 ? w4.y : s % 4 == 2 ? w4.z : w4.w;
+#if LIN_SWIN
+        const uint32_t ws = sw[s];
+#else
+        const uint32_t ws = lin_wget(W, s, w4, M, 0);
+#endif
         uint32_t t;
         asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
-            "src1_sel:DWORD" : "=v"(t) : "v"((uint32_t)P), "v"(ws));             /* bit 0: sign */
+            "src1_sel:DWORD" : "=v"(t) : "v"((uint32_t)P), LIN_WCON(ws));             /* bit 0: sign */
         const uint32_t a = __builtin_amdgcn_alignbit(t, (uint32_t)(P >> 32), 21) & M;
         uint32_t e = *(const uint32_t *)((const char *)s_lut + a);
         if (LANE_GAIN)
@@ -731,32 +827,37 @@ __device__ __forceinline__ void lin_channel_chunk_m(lin_f4 (&cq)[LIN_CH / 2], ui
 }
 
 /* LIN_MFMA 2: two channels' steps, one v_mfma_f32_16x16x32_f16 per two steps (B = channel a's
-   words of steps s, s+1 and channel b's; A = the pair's gains, lin_pair_gains) */
-__device__ __forceinline__ void lin_pair_chunk(lin_f4 (&cq)[LIN_CH / 2], uint64_t Pa, uint64_t Da,
-                                               const uint32_t *Wa, uint64_t Pb, uint64_t Db,
-                                               const uint32_t *Wb, uint32_t M, lin_half8 A,
+   words of steps s, s+1 and channel b's; A = the pair's gains, lin_pair_gains).  FIRST: the
+   chunk's first pair, whose MFMAs take C = the bias c0 instead of the accumulators (no
+   per-chunk initialisation) */
+template <bool FIRST>
+__device__ __forceinline__ void lin_pair_chunk(lin_f4 (&cq)[LIN_CH / 2], lin_f4 c0, uint64_t Pa, uint64_t Da,
+                                               lin_wsrc Wa, uint64_t Pb, uint64_t Db,
+                                               lin_wsrc Wb, uint32_t M, lin_half8 A,
                                                const int32_t *__restrict__ s_lut)
 {
     uint4 wa4, wb4;
     uint32_t ea0 = 0, eb0 = 0;
+#if LIN_SWIN
+    uint32_t swa[LIN_CH], swb[LIN_CH];
+    lin_wissue(Wa, swa);
+    lin_wissue(Wb, swb);
+    lin_wfence(swa);
+    lin_wfence(swb);
+#endif
 #pragma unroll
     for (int s = 0; s < LIN_CH; s++) {
-        if (s % 4 == 0) {
-            if (LIN_ABLATE & 64) {
-                wa4 = make_uint4(M * (s + 1), M * (s + 3), M * (s + 5), M * (s + 7));
-                wb4 = make_uint4(M * (s + 2), M * (s + 4), M * (s + 6), M * (s + 8));
-            } else {
-                wa4 = ((const uint4 *)Wa)[s / 4];
-                wb4 = ((const uint4 *)Wb)[s / 4];
-            }
-        }
-        const uint32_t wa = s % 4 == 0 ? wa4.x : s % 4 == 1 ? wa4.y : s % 4 == 2 ? wa4.z : wa4.w;
-        const uint32_t wb = s % 4 == 0 ? wb4.x : s % 4 == 1 ? wb4.y : s % 4 == 2 ? wb4.z : wb4.w;
+#if LIN_SWIN
+        const uint32_t wa = swa[s], wb = swb[s];
+#else
+        const uint32_t wa = lin_wget(Wa, s, wa4, M, 0);
+        const uint32_t wb = lin_wget(Wb, s, wb4, M, 1);
+#endif
         uint32_t ta, tb;
         asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
-            "src1_sel:DWORD" : "=v"(ta) : "v"((uint32_t)Pa), "v"(wa));
+            "src1_sel:DWORD" : "=v"(ta) : "v"((uint32_t)Pa), LIN_WCON(wa));
         asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
-            "src1_sel:DWORD" : "=v"(tb) : "v"((uint32_t)Pb), "v"(wb));
+            "src1_sel:DWORD" : "=v"(tb) : "v"((uint32_t)Pb), LIN_WCON(wb));
         const uint32_t aa = __builtin_amdgcn_alignbit(ta, (uint32_t)(Pa >> 32), 21) & M;
         const uint32_t ab = __builtin_amdgcn_alignbit(tb, (uint32_t)(Pb >> 32), 21) & M;
         const uint32_t ea = *(const uint32_t *)((const char *)s_lut + aa);
@@ -764,7 +865,7 @@ __device__ __forceinline__ void lin_pair_chunk(lin_f4 (&cq)[LIN_CH / 2], uint64_
         if (s & 1) {
             const uint4 bb = make_uint4(ea0, ea, eb0, eb);
             cq[s / 2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, __builtin_bit_cast(lin_half8, bb),
-                                                              cq[s / 2], 0, 0, 0);
+                                                              FIRST ? c0 : cq[s / 2], 0, 0, 0);
         } else {
             ea0 = ea;
             eb0 = eb;
@@ -1043,13 +1144,16 @@ template <int FMT>
 __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
     const gss_lin_t *__restrict__ lin, const lin_seg *__restrict__ segs,
     const lin_chan *__restrict__ chans, const int32_t *__restrict__ nch,
-    const int32_t *__restrict__ fast, const uint32_t *__restrict__ cab, lut_arg lut,
-    int n_per_blk, int nseg, int wg_per_blk, uint8_t *__restrict__ out, size_t block_bytes)
+    const int32_t *__restrict__ fast, const uint32_t *__restrict__ cab,
+    const uint32_t *__restrict__ tw, lut_arg lut, int n_per_blk, int nseg, int wg_per_blk,
+    uint8_t *__restrict__ out, size_t block_bytes)
 {
     __shared__ int32_t s_lut[1024];                       /* cos + 2^22 sin; [512+i] = -[i] */
     __shared__ uint64_t s_lane[GSS_MAXCH * 64];           /* lane offsets L(l) per channel    */
     __shared__ lin_ct s_ct[LIN_WAVES][GSS_MAXCH];         /* the current chunk, per wave      */
+#if !LIN_SWIN
     __shared__ uint32_t s_cab[GSS_MAXCH][CAB_W];          /* the channels' sign bit-streams   */
+#endif
 #ifdef LIN_LDS_PAD                                        /* occupancy measurements only      */
     __shared__ uint32_t s_pad[LIN_LDS_PAD];
     if (threadIdx.x == 1023) s_pad[blockIdx.x % LIN_LDS_PAD] = 0;
@@ -1075,14 +1179,21 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
     const int nc = nch[b];
     for (int i = tid; i < nc * 64; i += LIN_THREADS)
         s_lane[i] = gss_lin_lane(CH[i >> 6].xs, CH[i >> 6].zs, (uint32_t)(i & 63));
+#if LIN_SWIN
+    (void)cab;
+#else
+    (void)tw;
     for (int i = tid; i < nc * CAB_W; i += LIN_THREADS)
         s_cab[i / CAB_W][i % CAB_W] = cab[(size_t)CH[i / CAB_W].tab * CAB_W + i % CAB_W];
+#endif
     __syncthreads();
     uint32_t M = (LIN_ABLATE & 128) ? 0x7FCu : 0xFFCu;   /* LUT address mask, in a VGPR */
     asm volatile("" : "+v"(M));
 #if LIN_MFMA == 2
     uint32_t psel0, psel1;                                /* the pair MFMA's A-operand masks */
     lin_pair_sel(lane, psel0, psel1);
+    lin_f4 c0 = lin_f4{LIN_MAGF, LIN_MAGF, LIN_MAGF, LIN_MAGF};   /* the accumulators' bias */
+    asm volatile("" : "+v"(c0));
 #endif
     const int sg = w * LIN_WAVES + wave;
     const int n0 = sg * (64 * LIN_STEPS);
@@ -1132,6 +1243,7 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
         /* the channels with a gain change or patches in this chunk (wave-uniform) */
         const uint64_t fmask = __builtin_amdgcn_ballot_w64(my_flags != 0);
         wave_sync_lds();
+#if !LIN_SWIN
         /* ---- the chip windows, lane (k, s) ---- */
         for (int i = lane; i < nc * LIN_CH; i += 64) {
             const int k = i / LIN_CH;
@@ -1151,22 +1263,38 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
             T[k].W[i % LIN_CH] = wv;
         }
         wave_sync_lds();
+#endif
 #if LIN_MFMA
         lin_f4 acc[LIN_CH / 2];
+#if LIN_MFMA == 2
+#ifndef LIN_C0
+#define LIN_C0 1        /* the first pair's MFMAs take the bias as C (no init moves); 0: moves */
+#endif
+        int k0 = 0;
+        if (LIN_C0 && nc >= 2) {                          /* the first pair sets acc = bias + ... */
+            const lin_ct &ta = T[0], &tb = T[1];
+            lin_pair_chunk<true>(acc, c0, s_lane[lane] + ta.B, ta.D, lin_wsrc_of(ta, tw),
+                                 s_lane[64 + lane] + tb.B, tb.D, lin_wsrc_of(tb, tw), M,
+                                 lin_pair_gains(ta.g2, tb.g2, psel0, psel1), s_lut);
+            k0 = 2;
+        } else {
+#pragma unroll
+            for (int s = 0; s < LIN_CH / 2; s++)
+                acc[s] = c0;
+        }
+        for (; k0 + 1 < nc; k0 += 2) {                    /* uniform loop over channel pairs */
+            const lin_ct &ta = T[k0], &tb = T[k0 + 1];
+            lin_pair_chunk<false>(acc, c0, s_lane[k0 * 64 + lane] + ta.B, ta.D,
+                                  lin_wsrc_of(ta, tw), s_lane[(k0 + 1) * 64 + lane] + tb.B, tb.D,
+                                  lin_wsrc_of(tb, tw), M,
+                                  lin_pair_gains(ta.g2, tb.g2, psel0, psel1), s_lut);
+        }
+#else
 #pragma unroll
         for (int s = 0; s < LIN_CH / 2; s++) {
             acc[s] = lin_f4{LIN_MAGF, LIN_MAGF, LIN_MAGF, LIN_MAGF};
             asm volatile("" : "+v"(acc[s]));
         }
-#if LIN_MFMA == 2
-        int k0 = 0;
-        for (; k0 + 1 < nc; k0 += 2) {                    /* uniform loop over channel pairs */
-            const lin_ct &ta = T[k0], &tb = T[k0 + 1];
-            lin_pair_chunk(acc, s_lane[k0 * 64 + lane] + ta.B, ta.D, ta.W,
-                           s_lane[(k0 + 1) * 64 + lane] + tb.B, tb.D, tb.W, M,
-                           lin_pair_gains(ta.g2, tb.g2, psel0, psel1), s_lut);
-        }
-#else
         const int k0 = 0;
 #endif
         for (int k = k0; k < nc; k++) {                   /* uniform channel loop (mode 1), or
@@ -1174,7 +1302,7 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
             const lin_ct &t = T[k];
             const uint64_t B = t.B, D = t.D;
             const uint2 a2 = *(const uint2 *)t.A[lane & 3];
-            lin_channel_chunk_m<false>(acc, s_lane[k * 64 + lane] + B, D, t.W, M,
+            lin_channel_chunk_m<false>(acc, s_lane[k * 64 + lane] + B, D, lin_wsrc_of(t, tw), M,
                                        __builtin_bit_cast(lin_half4, a2), 0, 0, s_lut);
         }
         /* gain changes and patches (rare): only the channels whose flags are set */
@@ -1186,7 +1314,7 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
             if (__builtin_expect(fl & 1u, 0)) {
                 uint32_t l2 = (uint32_t)lane;
                 asm volatile("" : "+v"(l2));
-                lin_channel_chunk_m<true>(acc, s_lane[k * 64 + l2] + B, D, t.W, M,
+                lin_channel_chunk_m<true>(acc, s_lane[k * 64 + l2] + B, D, lin_wsrc_of(t, tw), M,
                                           lin_gain_operand(lin_f16_bits(t.gd), (int)l2), t.pos1,
                                           nb0 + (int)l2, s_lut);
             }
@@ -1204,12 +1332,14 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
             const lin_ct &t = T[k];                       /* broadcast LDS reads */
             const uint64_t B = t.B, D = t.D;
             const uint32_t fl = __builtin_amdgcn_readfirstlane(t.flags);
-            lin_channel_chunk<false>(acc, s_lane[k * 64 + lane] + B, D, t.W, M, t.g, 0, 0, s_lut);
+            lin_channel_chunk<false>(acc, s_lane[k * 64 + lane] + B, D, lin_wsrc_of(t, tw), M, t.g,
+                                     0, 0, s_lut);
             /* ... inside it: add (g1 - g0) e from sample pos1 on */
             if (__builtin_expect(fl & 1u, 0)) {
                 uint32_t l2 = (uint32_t)lane;
                 asm volatile("" : "+v"(l2));               /* recomputed: nothing stays live */
-                lin_channel_chunk<true>(acc, s_lane[k * 64 + l2] + B, D, t.W, M, t.gd, t.pos1,
+                lin_channel_chunk<true>(acc, s_lane[k * 64 + l2] + B, D, lin_wsrc_of(t, tw), M, t.gd,
+                                        t.pos1,
                                         nb0 + (int)l2, s_lut);
             }
             if (__builtin_expect(fl & 2u, 0))
@@ -1496,8 +1626,8 @@ extern "C" int gss_render_device(gss_dev *d, int set, const gss_chan_blk_t *blk,
 
 /* ---- fast path -------------------------------------------------------------------------- */
 typedef void (*lin_fn)(const gss_lin_t *, const lin_seg *, const lin_chan *, const int32_t *,
-                       const int32_t *, const uint32_t *, lut_arg, int, int, int, uint8_t *,
-                       size_t);
+                       const int32_t *, const uint32_t *, const uint32_t *, lut_arg, int, int,
+                       int, uint8_t *, size_t);
 
 static lin_fn pick_lin(int fmt)
 {
@@ -1531,18 +1661,25 @@ extern "C" int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const
         return gss_fail(GSS_E_ARG, "no fast kernel for fmt=%d nch=%d", fmt, nchp);
     HIP_TRY(hipSetDevice(d->ordinal));
     hipStream_t st = (hipStream_t)stream;
-    /* chip-sign bit-streams of every C/A table row (32 x 99 x 4 B; rebuilt per call: ~µs) */
-    const size_t ncbw = (size_t)n_ca * CAB_W;
-    if (ncbw * sizeof(uint32_t) > d->d_cbw_cap) {
+    /* chip-sign bit-streams of every C/A table row (32 x 99 x 4 B) and, after them, the window
+       table of LIN_SWIN (32 x 3136 x 4 B); rebuilt per call: ~µs */
+    const size_t ncbw = (size_t)n_ca * CAB_W, ntw = LIN_SWIN ? (size_t)n_ca * LIN_TW_W : 0;
+    const size_t tw_off = (ncbw + 63) & ~(size_t)63;
+    if ((tw_off + ntw) * sizeof(uint32_t) > d->d_cbw_cap) {
         (void)hipFree(d->d_cbw);
         d->d_cbw = nullptr;
         d->d_cbw_cap = 0;
-        HIP_TRY(hipMalloc(&d->d_cbw, ncbw * sizeof(uint32_t)));
-        d->d_cbw_cap = ncbw * sizeof(uint32_t);
+        HIP_TRY(hipMalloc(&d->d_cbw, (tw_off + ntw) * sizeof(uint32_t)));
+        d->d_cbw_cap = (tw_off + ntw) * sizeof(uint32_t);
     }
     hipLaunchKernelGGL(gss_cab_kernel, dim3((unsigned)((ncbw + 255) / 256)), dim3(256), 0, st,
                        ca_bits, n_ca, d->d_cbw);
     HIP_TRY(hipGetLastError());
+    if (ntw) {
+        hipLaunchKernelGGL(gss_tw_kernel, dim3((unsigned)((ntw + 255) / 256)), dim3(256), 0, st,
+                           (const uint32_t *)d->d_cbw, n_ca, d->d_cbw + tw_off);
+        HIP_TRY(hipGetLastError());
+    }
     const int segs = (n_per_blk + 64 * LIN_STEPS - 1) / (64 * LIN_STEPS);
     const int wg_per_blk = (segs + LIN_WAVES - 1) / LIN_WAVES;
     const size_t nsegrows = (size_t)nblk * GSS_MAXCH * segs;
@@ -1578,7 +1715,7 @@ extern "C" int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const
     HIP_TRY(hipEventRecord(ev[0], st));
     hipLaunchKernelGGL(fn, dim3((unsigned)nblk * wg_per_blk), dim3(LIN_THREADS), 0, st, lin,
                        (const lin_seg *)d_segs, (const lin_chan *)d_chans, nch, fast, d->d_cbw,
-                       d->lut, n_per_blk, segs, wg_per_blk, (uint8_t *)out, bb);
+                       d->d_cbw + tw_off, d->lut, n_per_blk, segs, wg_per_blk, (uint8_t *)out, bb);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], st));
     if (n_fb > 0)                                 /* the call completes when both are done */

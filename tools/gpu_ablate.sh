@@ -15,7 +15,7 @@ for lib in gps-sdr-sim_amd/lib/libgpssim_amd.so _var/*/libgpssim_amd.so; do
         echo "$lib $(echo "$r" | python3 -c 'import json,sys; d=json.load(sys.stdin)["e2e"]; print(d["value"], d["d2h_GBps"], d["wall_s"], d.get("d2h_ceiling_GBps"))')" >> $out
         continue
     fi
-    r=$(GSS_ALLOW_LIB_OVERRIDE=1 GSS_LIB_PATH=$lib timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-configs --no-e2e \
+    r=$(GSS_ALLOW_LIB_OVERRIDE=1 GSS_LIB_PATH=$lib timeout -k 10 200 python bench.py --steps ${STEPS:-10} --warmup ${WARMUP:-2} --no-configs --no-e2e \
         --no-cpu-baseline --no-exact --no-pmc 2>/dev/null | tail -1) || exit $?
     echo "$lib $(echo "$r" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["stages_ms"]["fast_path"], d["value"])')" >> $out
 done

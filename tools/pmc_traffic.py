@@ -17,8 +17,14 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     d = sys.argv[1]
     out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "profiles", "pmc_traffic.json")
+    live = {}
+    try:
+        live = json.load(open(os.path.join(d, "live_summary.json")))
+    except OSError:
+        pass
     summ = json.loads(subprocess.check_output([sys.executable,
-                                               os.path.join(REPO, "tools", "prof_summary.py"), d]))
+                                               os.path.join(REPO, "tools", "prof_summary.py"), d,
+                                               str(live.get("steps") or 0)]))
     bench = None
     for name in ("bench", "kt", "pmc_write", "pmc_fetch"):
         try:
@@ -27,11 +33,6 @@ def main():
                     bench = bench or json.loads(line)
         except OSError:
             pass
-    live = {}
-    try:
-        live = json.load(open(os.path.join(d, "live_summary.json")))
-    except OSError:
-        pass
     k = next(n for n in summ if n.startswith("gss_lin_kernel"))
     e = summ[k]
     w, r = e["hbm_write_bytes"], e["hbm_read_bytes_corrected"]
@@ -43,6 +44,7 @@ def main():
            "hbm_bytes_per_launch": round(w + r), "hbm_write_bytes_per_launch": round(w),
            "hbm_read_bytes_per_launch": round(r), "algorithmic_bytes_per_launch": alg,
            "kernel_avg_ns": e.get("avg_ns"), "kernel_warm_avg_ns": e.get("warm_avg_ns"),
+           "kernel_timed_avg_ns": e.get("timed_avg_ns"), "timed_launches": e.get("timed_launches"),
            "profiled_run_event_ms": live.get("profiled_run_event_ms"),
            "unprofiled_event_ms": (bench or {}).get("stages_ms", {}).get("fast_path"),
            "steps": live.get("steps"), "warmup": live.get("warmup"),
@@ -50,7 +52,8 @@ def main():
            "method": "rocprofv3 --kernel-trace --stats; --pmc WRITE_SIZE / --pmc FETCH_SIZE in "
                      "separate passes (--kernel-trace only), KiB x1024, FETCH_SIZE x2 (gfx950 "
                      "correction); the same bench command, steps and warm-up as the un-profiled "
-                     "run",
+                     "run; kernel_timed_avg_ns = the last `steps` dispatches, the launches the "
+                     "bench times",
            "source": os.path.relpath(d, REPO)}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))

@@ -44,6 +44,15 @@ def warm_avg_ns(durs):
     return sum(w) / len(w) if w else 0.0
 
 
+def timed_avg_ns(durs, steps):
+    """mean duration of the last `steps` dispatches: the launches a bench run times after its
+    warm-up (one launch per step).  Under sustained load the shader clock ramps up over the
+    first ~20 launches (GRBM_GUI_ACTIVE per dispatch: 1.7 -> 2.3 GHz), so an average over all
+    dispatches, warm-up included, is longer than the timed region's."""
+    w = durs[-steps:] if steps and len(durs) >= steps else durs
+    return sum(w) / len(w) if w else 0.0
+
+
 def counters(d):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     meta = {}
@@ -63,6 +72,7 @@ def counters(d):
 
 def main():
     d = sys.argv[1]
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 0     # timed launches (bench --steps)
     ks = kernel_stats(d)
     kd = kernel_durations(d)
     cs = counters(d)
@@ -71,6 +81,9 @@ def main():
         e = dict(ks.get(k, {}))
         if k in kd:
             e["warm_avg_ns"] = warm_avg_ns(kd[k])
+            if steps:
+                e["timed_avg_ns"] = timed_avg_ns(kd[k], steps)
+                e["timed_launches"] = min(steps, len(kd[k]))
         c = cs.get(k, {})
         e.update({"meta": c.get("_meta")})
         e["counters"] = {n: v for n, v in c.items() if n != "_meta"}
