@@ -73,6 +73,48 @@ constexpr size_t SLOT_OUT_MAX = (size_t)256 << 20;     /* pinned output bytes pe
 
 enum { FREE, PLANNED };
 
+/* The slots' output buffers (pinned host + device, ~133 MB each at the defaults) outlive a run:
+   page-locking them costs tens of ms, so a later gss_run in the same process (a service, or a
+   rank's next window) takes them from this pool instead.  Bounded by POOL_MAX_BYTES; a buffer is
+   reused only for a request of at least half its size. */
+struct PoolBuf { void *p; size_t n; int dev; bool host; };
+std::mutex pool_mu;
+std::vector<PoolBuf> pool;
+size_t pool_bytes = 0;
+constexpr size_t POOL_MAX_BYTES = (size_t)2 << 30;
+
+static hipError_t pool_get(void **p, size_t n, bool host, int dev)
+{
+    {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        for (size_t i = 0; i < pool.size(); i++) {
+            const PoolBuf &b = pool[i];
+            if (b.host == host && b.dev == dev && b.n >= n && b.n <= 2 * n) {
+                *p = b.p;
+                pool_bytes -= b.n;
+                pool.erase(pool.begin() + (long)i);
+                return hipSuccess;
+            }
+        }
+    }
+    return host ? hipHostMalloc(p, n, hipHostMallocDefault) : hipMalloc(p, n);
+}
+
+static void pool_put(void *p, size_t n, bool host, int dev)
+{
+    if (!p)
+        return;
+    {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        if (pool_bytes + n <= POOL_MAX_BYTES) {
+            pool.push_back({p, n, dev, host});
+            pool_bytes += n;
+            return;
+        }
+    }
+    (void)(host ? hipHostFree(p) : hipFree(p));
+}
+
 struct Slot {
     /* planner side (pinned host memory) */
     gss_chan_blk_t *blk = nullptr;
@@ -91,6 +133,7 @@ struct Slot {
     uint8_t *d_in = nullptr;
     size_t d_in_cap = 0;
     uint8_t *d_out = nullptr, *h_out = nullptr;
+    size_t out_bytes = 0;            /* their size (pool_get / pool_put)                  */
     int32_t *d_status = nullptr, *h_status = nullptr;
     hipEvent_t rendered = nullptr;   /* compute stream: the slot's kernels are done      */
     hipEvent_t done = nullptr;       /* copy stream: the slot's bytes are in h_out        */
@@ -99,6 +142,8 @@ struct Slot {
 struct Run {
     gss_scn *scn;
     int batch, threads, n_per_blk, use_lin, carrier_int;
+    int force_exact;                 /* GSS_RUN_FORCE_EXACT=k: every k-th block to the exact
+                                        path (tests of the mixed batch), 0 = off */
     int64_t first, last;             /* [first, last) block range of the run */
     const gss_run_opts_t *opts;      /* carrier hand-off (gss_run_ex), or null */
     /* with opts->carr_in: the whole range planned up front (rows, carriers, checkpoints) */
@@ -114,6 +159,37 @@ struct Run {
 };
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+/* The carrier checkpoints feed only the exact path's Stage A, i.e. the blocks the proofs do not
+   certify (none of the 2,999 of the bench run).  With the fast path the chain is therefore
+   walked without them (a third cheaper: no partial-cycle walks to the 8 checkpoint positions)
+   and they are computed afterwards for the uncertified blocks only, from each row's carr0 by
+   the same exact walk.  The integer-carrier chain records them for free and keeps doing so. */
+static bool lazy_ck(const Run &r) { return r.use_lin && !r.carrier_int; }
+
+static void fill_fb_ck(const Run &r, Slot &sl)
+{
+    if (r.force_exact > 0) {
+        for (int i = 0; i < sl.nb; i++)
+            if ((sl.first + i) % r.force_exact == 0)
+                sl.fast[i] = 0;
+        int nf = 0;
+        for (int i = 0; i < sl.nb; i++)
+            if (!sl.fast[i])
+                sl.fast[sl.nb + nf++] = i;
+        sl.n_fb = nf;
+    }
+    if (!lazy_ck(r))
+        return;
+    for (int i = 0; i < sl.n_fb; i++) {
+        const int b = sl.fast[sl.nb + i];
+        for (int k = 0; k < sl.nch[b]; k++) {
+            const size_t e = (size_t)b * GSS_MAXCH + k;
+            (void)gss_carr_advance_ck(sl.blk[e].carr0, sl.blk[e].carr_step, r.n_per_blk,
+                                      sl.ck + e * GSS_NCK);
+        }
+    }
+}
 
 /* gss_run_ex with a carrier hand-off: seek to the range, produce its rows, take the slot
    carriers at its first block from carr_in, walk the chain, give the end state to carr_out. */
@@ -146,9 +222,11 @@ int plan_range_upfront(Run &r)
     if (r.opts->carr_in(r.opts->carr_user, carr))
         return gss_fail(GSS_E_IO, "carrier hand-off (in) failed at block %lld",
                         (long long)r.first);
-    r.pre_ck.resize((size_t)r.pre_n * GSS_MAXCH * GSS_NCK);
+    if (!lazy_ck(r))
+        r.pre_ck.resize((size_t)r.pre_n * GSS_MAXCH * GSS_NCK);
     rc = gss_carr_chain(carr, r.pre_blk.data(), r.pre_nch.data(), chain.data(), (int)r.pre_n,
-                        r.n_per_blk, r.carrier_int, r.pre_ck.data(), r.threads);
+                        r.n_per_blk, r.carrier_int, lazy_ck(r) ? nullptr : r.pre_ck.data(),
+                        r.threads);
     if (rc)
         return rc;
     if (r.opts->carr_out && r.opts->carr_out(r.opts->carr_user, carr))
@@ -169,8 +247,9 @@ int take_upfront(Run &r, Slot &sl, int *nb_out)
     const size_t rows = (size_t)nb * GSS_MAXCH;
     memcpy(sl.blk, &r.pre_blk[(size_t)r.pre_at * GSS_MAXCH], rows * sizeof(gss_chan_blk_t));
     memcpy(sl.nch, &r.pre_nch[(size_t)r.pre_at], (size_t)nb * sizeof(int32_t));
-    memcpy(sl.ck, &r.pre_ck[(size_t)r.pre_at * GSS_MAXCH * GSS_NCK],
-           rows * GSS_NCK * sizeof(double));
+    if (!lazy_ck(r))
+        memcpy(sl.ck, &r.pre_ck[(size_t)r.pre_at * GSS_MAXCH * GSS_NCK],
+               rows * GSS_NCK * sizeof(double));
     int lo = INT32_MAX, hi = -1;
     for (int b = 0; b < nb; b++)
         for (int k = 0; k < sl.nch[b]; k++) {
@@ -235,6 +314,7 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
                 if (!sl.fast[i])
                     sl.fast[nb + nf++] = i;
             sl.n_fb = nf;
+            fill_fb_ck(r, sl);
         }
         return 0;
     }
@@ -250,8 +330,8 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
             ask = (int)(r.first - *cursor);            /* stop exactly at the range start */
         int nb = 0;
         /* before the range only the carrier chain matters: no checkpoints recorded */
-        int rc = gss_scn_next(r.scn, ask, sl.blk, sl.nch, *cursor < r.first ? nullptr : sl.ck,
-                              &nb, r.threads);
+        int rc = gss_scn_next(r.scn, ask, sl.blk, sl.nch,
+                              (*cursor < r.first || lazy_ck(r)) ? nullptr : sl.ck, &nb, r.threads);
         if (rc)
             return rc;
         if (nb == 0) {
@@ -297,6 +377,7 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
                 if (!sl.fast[i])
                     sl.fast[nb + nf++] = i;
             sl.n_fb = nf;
+            fill_fb_ck(r, sl);
         }
         return 0;
     }
@@ -482,6 +563,8 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
     {
         const char *path = getenv("GSS_PATH");        /* "walk": the exact path for every block */
         r.use_lin = !(path && strcmp(path, "walk") == 0);
+        const char *fe = getenv("GSS_RUN_FORCE_EXACT");
+        r.force_exact = fe && *fe ? atoi(fe) : 0;
     }
     r.batch = batch > 0 ? batch : 100;
     if ((size_t)r.batch * bb > SLOT_OUT_MAX)
@@ -500,9 +583,11 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             if (c) (void)hipStreamSynchronize(c);
         for (Slot &sl : r.slot) {
             (void)hipHostFree(sl.blk); (void)hipHostFree(sl.nch); (void)hipHostFree(sl.ck);
-            (void)hipHostFree(sl.nav); (void)hipHostFree(sl.h_out); (void)hipHostFree(sl.h_status);
+            (void)hipHostFree(sl.nav); (void)hipHostFree(sl.h_status);
+            pool_put(sl.h_out, sl.out_bytes, true, ordinal);
+            pool_put(sl.d_out, sl.out_bytes, false, ordinal);
             (void)hipHostFree(sl.lin); (void)hipHostFree(sl.fast);
-            (void)hipFree(sl.d_in); (void)hipFree(sl.d_out); (void)hipFree(sl.d_status);
+            (void)hipFree(sl.d_in); (void)hipFree(sl.d_status);
             if (sl.done) (void)hipEventDestroy(sl.done);
             if (sl.rendered) (void)hipEventDestroy(sl.rendered);
         }
@@ -528,10 +613,11 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                     hipSuccess ||
                 hipHostMalloc((void **)&sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * nb,
                               hipHostMallocDefault) != hipSuccess ||
-                hipHostMalloc((void **)&sl.h_out, bb * nb, hipHostMallocDefault) != hipSuccess ||
+                (sl.out_bytes = bb * nb,
+                 pool_get((void **)&sl.h_out, bb * nb, true, ordinal) != hipSuccess) ||
                 hipHostMalloc((void **)&sl.h_status, sizeof(int32_t), hipHostMallocDefault) !=
                     hipSuccess ||
-                hipMalloc((void **)&sl.d_out, bb * nb) != hipSuccess ||
+                pool_get((void **)&sl.d_out, bb * nb, false, ordinal) != hipSuccess ||
                 hipMalloc((void **)&sl.d_status, sizeof(int32_t)) != hipSuccess ||
                 hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&sl.rendered, hipEventDisableTiming) != hipSuccess)

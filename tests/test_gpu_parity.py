@@ -278,6 +278,30 @@ def test_streaming_run_bit_exact(dev, golden):
     assert [x for _, x in blocks] == g["block_sha16"][123:184]
 
 
+@pytest.mark.parametrize("fmt,every", [(16, 5), (8, 7)])
+def test_streaming_run_mixed_exact(dev, golden, monkeypatch, fmt, every):
+    """gss_run with every k-th block sent to the exact path (GSS_RUN_FORCE_EXACT, a test hook):
+    the planner walks the chain without checkpoints and computes them afterwards for those
+    blocks only (fill_fb_ck); whole run and a mid-run range against the golden hashes."""
+    monkeypatch.setenv("GSS_RUN_FORCE_EXACT", str(every))
+    g = golden[f"static_d30_b{fmt}"]
+    s = G.Scenario(NAV, llh=LOC, duration=30.0, data_format=fmt)
+    bb = G.block_bytes(s.n_per_blk, fmt)
+    blocks = []
+
+    def sink(buf, first, nb):
+        for i in range(nb):
+            blocks.append((first + i, hashlib.sha256(buf[i * bb:(i + 1) * bb]).hexdigest()[:16]))
+
+    dev.run(s, sink, batch=40, threads=4)
+    assert [x for _, x in blocks] == g["block_sha16"]
+    blocks.clear()
+    s = G.Scenario(NAV, llh=LOC, duration=30.0, data_format=fmt)
+    dev.run(s, sink, first_block=101, n_blocks=77, batch=30)
+    assert [b for b, _ in blocks] == list(range(101, 178))
+    assert [x for _, x in blocks] == g["block_sha16"][101:178]
+
+
 @pytest.mark.parametrize("handoff,gold,args", [
     # every rank plans the blocks before its range itself (no run id)
     (False, "static_d30_b16", ["-l", ",".join(map(str, LOC)), "-d", "30", "-b", "16"]),
@@ -297,6 +321,7 @@ def test_cli_two_ranks_one_file(golden, handoff, gold, args):
             env.pop("GSS_RUN_ID", None)
             if handoff:
                 env["GSS_RUN_ID"] = "t%d" % os.getpid()
+                env["GSS_RUN_FORCE_EXACT"] = "9"     # + the hand-off path's lazy checkpoints
             procs.append(subprocess.Popen(
                 [G.CLI_PATH, "-e", NAV] + args + ["-o", out], env=env,
                 stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
