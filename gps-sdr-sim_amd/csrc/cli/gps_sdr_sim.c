@@ -15,7 +15,8 @@
  * and removed by its reader.  The run id is torchrun's TORCHELASTIC_RUN_ID (or GSS_RUN_ID);
  * without one every rank plans the blocks before its range itself.
  * Env: GSS_DEVICE (ordinal; default LOCAL_RANK or 0), GSS_BATCH (blocks per launch, default
- *      128), GSS_THREADS (planner threads, default 8), GSS_HANDOFF_TIMEOUT (seconds a rank waits
+ *      128), GSS_THREADS (planner threads, default the CPU share: cgroup cpu.max, else the online
+ *      CPUs, at most 16), GSS_HANDOFF_TIMEOUT (seconds a rank waits
  *      for its carriers, default 3600).
  */
 #include <fcntl.h>
@@ -56,6 +57,22 @@ static int env_int(const char *name, int dflt)
 {
     const char *v = getenv(name);
     return v && *v ? atoi(v) : dflt;
+}
+
+/* planner threads: the CPUs' worth of time this process may use (cgroup v2 cpu.max quota, else
+   the online CPUs), 1..16 (16 channel slots; more buys the chain nothing) */
+static int default_threads(void)
+{
+    long n = sysconf(_SC_NPROCESSORS_ONLN);
+    FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r");
+    if (f) {
+        char q[32] = {0};
+        long period = 0;
+        if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0)
+            n = atol(q) / period;
+        fclose(f);
+    }
+    return n < 1 ? 1 : n > 16 ? 16 : (int)n;
 }
 
 /* The carrier hand-off between ranks (plan once per node): a 16-double file per boundary. */
@@ -148,7 +165,7 @@ static int run_rank(const gss_cli_t *cli, gss_scn *scn, const gss_scn_info_t *in
                      run_id, (long long)last);
     }
     if (gss_run_ex(dev, scn, first, last - first, env_int("GSS_BATCH", 128),
-                   env_int("GSS_THREADS", 8), pwrite_sink, &c,
+                   env_int("GSS_THREADS", default_threads()), pwrite_sink, &c,
                    run_id && *run_id ? &ro : NULL)) {
         fprintf(stderr, "\nERROR: rank %d: %s\n", rank, gss_last_error());
         return 1;
@@ -200,7 +217,7 @@ int main(int argc, char **argv)
         }
     }
     int batch = env_int("GSS_BATCH", 128);
-    int threads = env_int("GSS_THREADS", 8);
+    int threads = env_int("GSS_THREADS", default_threads());
     if (batch < 1) batch = 1;
     clock_t t0 = clock();
     /* planning, upload, both kernel stages, download and fwrite overlap inside gss_run; the
