@@ -788,8 +788,8 @@ __device__ __forceinline__ void lin_channel_chunk(int64_t (&acc)[LIN_CH], uint64
 
 /* LIN_MFMA: the same steps, the accumulation on the matrix cores (one MFMA per two steps; with
    LANE_GAIN the LUT words of samples before pos1 are zeroed and A carries the gain difference) */
-template <bool LANE_GAIN>
-__device__ __forceinline__ void lin_channel_chunk_m(lin_f4 (&cq)[LIN_CH / 2], uint64_t P,
+template <bool LANE_GAIN, bool FIRST = false>
+__device__ __forceinline__ void lin_channel_chunk_m(lin_f4 (&cq)[LIN_CH / 2], lin_f4 c0, uint64_t P,
                                                     uint64_t D, lin_wsrc W, uint32_t M,
                                                     lin_half4 A, int pos1, int p0,
                                                     const int32_t *__restrict__ s_lut)
@@ -818,7 +818,7 @@ __device__ __forceinline__ void lin_channel_chunk_m(lin_f4 (&cq)[LIN_CH / 2], ui
         if (s & 1) {
             const uint2 bb = make_uint2(e0, e);
             cq[s / 2] = __builtin_amdgcn_mfma_f32_4x4x4f16(A, __builtin_bit_cast(lin_half4, bb),
-                                                          cq[s / 2], 0, 0, 0);
+                                                          FIRST ? c0 : cq[s / 2], 0, 0, 0);
         } else {
             e0 = e;
         }
@@ -1192,6 +1192,8 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
 #if LIN_MFMA == 2
     uint32_t psel0, psel1;                                /* the pair MFMA's A-operand masks */
     lin_pair_sel(lane, psel0, psel1);
+#endif
+#if LIN_MFMA
     lin_f4 c0 = lin_f4{LIN_MAGF, LIN_MAGF, LIN_MAGF, LIN_MAGF};   /* the accumulators' bias */
     asm volatile("" : "+v"(c0));
 #endif
@@ -1266,10 +1268,10 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
 #endif
 #if LIN_MFMA
         lin_f4 acc[LIN_CH / 2];
-#if LIN_MFMA == 2
 #ifndef LIN_C0
-#define LIN_C0 1        /* the first pair's MFMAs take the bias as C (no init moves); 0: moves */
+#define LIN_C0 1        /* the first channel (pair)'s MFMAs take the bias as C, no init moves */
 #endif
+#if LIN_MFMA == 2
         int k0 = 0;
         if (LIN_C0 && nc >= 2) {                          /* the first pair sets acc = bias + ... */
             const lin_ct &ta = T[0], &tb = T[1];
@@ -1290,19 +1292,25 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
                                   lin_pair_gains(ta.g2, tb.g2, psel0, psel1), s_lut);
         }
 #else
+        int k0 = 0;
+        if (LIN_C0 && nc >= 1) {                          /* the first channel sets acc = bias + ... */
+            const lin_ct &t = T[0];
+            const uint2 a2 = *(const uint2 *)t.A[lane & 3];
+            lin_channel_chunk_m<false, true>(acc, c0, s_lane[lane] + t.B, t.D, lin_wsrc_of(t, tw), M,
+                                             __builtin_bit_cast(lin_half4, a2), 0, 0, s_lut);
+            k0 = 1;
+        } else {
 #pragma unroll
-        for (int s = 0; s < LIN_CH / 2; s++) {
-            acc[s] = lin_f4{LIN_MAGF, LIN_MAGF, LIN_MAGF, LIN_MAGF};
-            asm volatile("" : "+v"(acc[s]));
+            for (int s = 0; s < LIN_CH / 2; s++)
+                acc[s] = c0;
         }
-        const int k0 = 0;
 #endif
         for (int k = k0; k < nc; k++) {                   /* uniform channel loop (mode 1), or
                                                              the lone last channel (mode 2) */
             const lin_ct &t = T[k];
             const uint64_t B = t.B, D = t.D;
             const uint2 a2 = *(const uint2 *)t.A[lane & 3];
-            lin_channel_chunk_m<false>(acc, s_lane[k * 64 + lane] + B, D, lin_wsrc_of(t, tw), M,
+            lin_channel_chunk_m<false>(acc, c0, s_lane[k * 64 + lane] + B, D, lin_wsrc_of(t, tw), M,
                                        __builtin_bit_cast(lin_half4, a2), 0, 0, s_lut);
         }
         /* gain changes and patches (rare): only the channels whose flags are set */
@@ -1314,7 +1322,7 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
             if (__builtin_expect(fl & 1u, 0)) {
                 uint32_t l2 = (uint32_t)lane;
                 asm volatile("" : "+v"(l2));
-                lin_channel_chunk_m<true>(acc, s_lane[k * 64 + l2] + B, D, lin_wsrc_of(t, tw), M,
+                lin_channel_chunk_m<true>(acc, c0, s_lane[k * 64 + l2] + B, D, lin_wsrc_of(t, tw), M,
                                           lin_gain_operand(lin_f16_bits(t.gd), (int)l2), t.pos1,
                                           nb0 + (int)l2, s_lut);
             }

@@ -129,6 +129,10 @@ int    rinex_read(eph_t eph[][K_MAX_SAT], iono_t *io, const char *fname);
 int    motion_read_csv(double (*xyz)[3], int cap, const char *fname);
 int    motion_read_nmea(double (*xyz)[3], int cap, const char *fname);
 
+/* ---- pool.c ------------------------------------------------------------------------------- */
+typedef void (*gss_task_fn)(void *arg, int part);
+int    gss_pool_run(int nthreads, int nparts, gss_task_fn fn, void *arg);
+
 /* ---- errors ------------------------------------------------------------------------------- */
 int    gss_fail(int code, const char *fmt, ...);
 extern double gss_ant_pat_db[37];

@@ -419,6 +419,14 @@ static void *lin_run(void *arg)
     return NULL;
 }
 
+static void lin_part(void *arg, int b)
+{
+    lin_job j = *(const lin_job *)arg;
+    j.b_lo = b;
+    j.b_hi = b + 1;
+    (void)lin_run(&j);
+}
+
 int gss_linearize(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
                   const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
                   gss_lin_t *lin, int32_t *fast, int threads)
@@ -429,25 +437,8 @@ int gss_linearize(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n
     if (nblk == 0)
         return 0;
     pthread_once(&lut_once, lut_fill);                /* before any worker thread starts */
-    if (threads < 1) threads = 1;
-    if (threads > 64) threads = 64;
-    if (threads > nblk) threads = nblk;
-    pthread_t tid[64];
-    lin_job job[64];
-    int started[64] = {0};
-    const int per = (nblk + threads - 1) / threads;
-    for (int t = 0; t < threads; t++) {
-        int lo = t * per, hi = lo + per > nblk ? nblk : lo + per;
-        job[t] = (lin_job){blk, nch, nav, ca_bits, n_nav, n_ca, n_per_blk, lo, hi, lin, fast};
-        if (lo >= hi)
-            continue;
-        if (threads == 1 || pthread_create(&tid[t], NULL, lin_run, &job[t]) != 0)
-            lin_run(&job[t]);
-        else
-            started[t] = 1;
-    }
-    for (int t = 0; t < threads; t++)
-        if (started[t])
-            pthread_join(tid[t], NULL);
+    const lin_job all = {blk, nch, nav, ca_bits, n_nav, n_ca, n_per_blk, 0, nblk, lin, fast};
+    /* one part per block on the pooled workers (blocks differ in their ambiguous samples) */
+    gss_pool_run(threads, nblk, lin_part, (void *)&all);
     return 0;
 }

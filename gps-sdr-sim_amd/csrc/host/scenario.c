@@ -428,6 +428,14 @@ static void *plan_slots(void *arg)
     return NULL;
 }
 
+static void plan_slot_part(void *arg, int slot)
+{
+    plan_job j = *(const plan_job *)arg;
+    j.slot_lo = slot;
+    j.slot_hi = slot + 1;
+    (void)plan_slots(&j);
+}
+
 /* The carrier chain (gpssim.c:2245-2250, carried across blocks) over nblk consecutive blocks:
    one chain per channel slot, restarted where allocateChannel re-initialised it; slots are
    independent, so one slot per thread. */
@@ -438,29 +446,9 @@ int gss_carr_chain(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
     if (carr == NULL || (nblk > 0 && (blk == NULL || nch == NULL || chain == NULL)) ||
         nblk < 0 || n_per_blk <= 0)
         return gss_fail(GSS_E_ARG, "invalid carrier-chain arguments");
-    if (threads < 1)
-        threads = 1;
-    if (threads > K_MAX_CHAN)
-        threads = K_MAX_CHAN;
-    pthread_t tid[K_MAX_CHAN];
-    plan_job job[K_MAX_CHAN];
-    int per = (K_MAX_CHAN + threads - 1) / threads;
-    int started = 0;
-    for (int t = 0; t < threads; t++) {
-        job[t] = (plan_job){carr, blk, nch, chain, carr_ck, nblk, n_per_blk, carrier_int,
-                            t * per, (t + 1) * per};
-        if (job[t].slot_hi > K_MAX_CHAN)
-            job[t].slot_hi = K_MAX_CHAN;
-        if (job[t].slot_lo >= job[t].slot_hi)
-            break;
-        if (threads == 1 || pthread_create(&tid[t], NULL, plan_slots, &job[t]) != 0)
-            plan_slots(&job[t]);
-        else
-            started |= 1 << t;
-    }
-    for (int t = 0; t < threads; t++)
-        if (started & (1 << t))
-            pthread_join(tid[t], NULL);
+    const plan_job all = {carr, blk, nch, chain, carr_ck, nblk, n_per_blk, carrier_int, 0,
+                          K_MAX_CHAN};
+    gss_pool_run(threads, K_MAX_CHAN, plan_slot_part, (void *)&all);   /* one part per slot */
     return 0;
 }
 
@@ -493,6 +481,14 @@ static void *range_worker(void *arg)
     return NULL;
 }
 
+static void range_part(void *arg, int j)
+{
+    range_job r = *(const range_job *)arg;
+    r.j0 = j;
+    r.nj = j + 1;
+    (void)range_worker(&r);
+}
+
 /* blocks of the run from the current one that share its channel set (the last is the one after
    which the 30 s update runs), at most max_j; their ranges into s->rg */
 static int range_pass(gss_scn *s, int max_j, int threads)
@@ -515,26 +511,8 @@ static int range_pass(gss_scn *s, int max_j, int threads)
         }
         s->rg_cap = nj;
     }
-    if (threads < 1)
-        threads = 1;
-    if (threads > 32)
-        threads = 32;
-    if (threads > nj)
-        threads = nj;
-    pthread_t tid[32];
-    range_job job[32];
-    int started = 0;
-    for (int t = 0; t < threads; t++) {
-        job[t] = (range_job){s, gbuf, t, nj, threads, s->iumd};
-        if (t > 0 && pthread_create(&tid[t], NULL, range_worker, &job[t]) == 0)
-            started |= 1u << t;
-        else if (t > 0)
-            range_worker(&job[t]);
-    }
-    range_worker(&job[0]);
-    for (int t = 1; t < threads; t++)
-        if (started & (1u << t))
-            pthread_join(tid[t], NULL);
+    const range_job all = {s, gbuf, 0, nj, 1, s->iumd};
+    gss_pool_run(threads, nj, range_part, (void *)&all);      /* one part per block */
     return nj;
 }
 
