@@ -1,0 +1,77 @@
+/*
+ * gss_producers.hip — the 30 s producers on the GPU: the C/A chip table
+ * (codegen, gpssim.c:132-171) and the LNAV frame rows with parity (generateNavMsg,
+ * gpssim.c:1467-1547; computeChecksum 693-756) that the render kernels read, built on the device
+ * from the host plane's compact sources (gss_nav_src_t).  The arithmetic is gss_nav.h, shared
+ * with the host checker gss_nav_rows_host.  gss_run builds its device nav table with them.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "gpssim_amd.h"
+#include "../common/gss_nav.h"
+
+extern "C" int gss_fail(int code, const char *fmt, ...);
+extern "C" int gss_dev_ordinal(const gss_dev *d);
+
+/* one workgroup of 64 lanes: lane 0 runs the two 10-stage registers (1023 steps), then the wave
+   forms each PRN's chips 64 at a time and packs them with a ballot */
+__global__ __launch_bounds__(64) void gss_ca_kernel(uint32_t *__restrict__ out)
+{
+    __shared__ uint32_t g1[GSS_CA_WORDS], g2[GSS_CA_WORDS];
+    const int lane = threadIdx.x;
+    if (lane == 0)
+        gss_g1g2(g1, g2);
+    __syncthreads();
+    for (int prn = 1; prn <= 32; prn++)
+        for (int c0 = 0; c0 < 32 * GSS_CA_WORDS; c0 += 64) {
+            const int i = c0 + lane;
+            const uint32_t bit = i < GSS_CA_LEN ? gss_ca_chip(g1, g2, prn, i) : 0u;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(bit != 0);
+            if (lane < 2)
+                out[(size_t)(prn - 1) * GSS_CA_WORDS + c0 / 32 + lane] =
+                    (uint32_t)(m >> (32 * lane));
+        }
+}
+
+/* rows [first, first + n): a lane per row whose predecessor is not among them (a chain head)
+   builds its row and then the rows that continue it, in order */
+__global__ void gss_nav_kernel(const gss_nav_src_t *__restrict__ src, int first, int n,
+                               uint32_t *__restrict__ rows)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    if (src[i].prev >= first)
+        return;                                   /* built by its chain's head */
+    for (int r = first + i, guard = 0; r >= first && r < first + n && guard < n; guard++) {
+        const gss_nav_src_t *q = &src[r - first];
+        gss_nav_frame(q, gss_nav_head(q, rows), rows + (size_t)r * GSS_NAV_WORDS);
+        r = q->next;
+    }
+}
+
+extern "C" int gss_ca_table_device(gss_dev *d, uint32_t *out, void *stream)
+{
+    if (!d || !out)
+        return gss_fail(GSS_E_ARG, "invalid C/A table arguments");
+    if (hipSetDevice(gss_dev_ordinal(d)) != hipSuccess)
+        return gss_fail(GSS_E_HIP, "hipSetDevice failed");
+    hipLaunchKernelGGL(gss_ca_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "C/A kernel: %s", hipGetErrorString(e));
+}
+
+extern "C" int gss_nav_rows_device(gss_dev *d, const gss_nav_src_t *src, int first, int n,
+                                   uint32_t *rows, void *stream)
+{
+    if (!d || (n > 0 && (!src || !rows)) || first < 0 || n < 0)
+        return gss_fail(GSS_E_ARG, "invalid nav-row arguments");
+    if (n == 0)
+        return 0;
+    if (hipSetDevice(gss_dev_ordinal(d)) != hipSuccess)
+        return gss_fail(GSS_E_HIP, "hipSetDevice failed");
+    hipLaunchKernelGGL(gss_nav_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
+                       (hipStream_t)stream, src, first, n, rows);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "nav kernel: %s", hipGetErrorString(e));
+}

@@ -3,9 +3,12 @@
  * plane to the caller's byte sink, every stage overlapped.  Replaces the reference's block loop
  * (gpssim.c:2154-2353: refresh, sample loop, fwrite at 2276/2283/2287, 30 s updates).
  *
- *   planner thread   gss_scn_next into pinned slot buffers (+ a snapshot of the nav table),
- *                    then gss_linearize: the fast path's certified lines and patches
- *   main thread      per slot: async H2D and gss_synth_lin_device on the compute stream
+ *   planner thread   gss_scn_next into pinned slot buffers (+ the sources of the nav rows new
+ *                    since the previous slot), then gss_linearize: the fast path's certified
+ *                    lines and patches
+ *   main thread      per slot: async H2D; the 30 s producer builds the new nav rows of the
+ *                    run's device nav table (gss_nav_rows_device; the C/A table likewise, once
+ *                    per run: gss_ca_table_device); gss_synth_lin_device on the compute stream
  *                    (certified blocks on the integer fast path, the rest on Stage A + B; with
  *                    GSS_PATH=walk gss_synth_device renders every block), then async D2H into a
  *                    pinned output buffer on the copy stream (after an event); while the next
@@ -120,8 +123,9 @@ struct Slot {
     gss_chan_blk_t *blk = nullptr;
     int32_t *nch = nullptr;
     double *ck = nullptr;
-    uint32_t *nav = nullptr;
-    int nav_cap = 0, n_nav = 0;
+    gss_nav_src_t *nav = nullptr;    /* sources of the nav rows new with this slot (pinned)  */
+    int nav_cap = 0, n_nav = 0;      /* ... capacity, count                                   */
+    int nav_first = 0;               /* global row index of the first of them                 */
     gss_lin_t *lin = nullptr;        /* certified lines [nb][GSS_MAXCH] (fast path)      */
     int32_t *fast = nullptr;         /* fast[nb], then the exact-path block list [n_fb] */
     int n_fb = 0;
@@ -155,6 +159,9 @@ struct Run {
     std::condition_variable cv;
     int abort = 0;
     uint32_t ca[32 * GSS_CA_WORDS];  /* C/A chips (gss_ca_table) for the proofs' patch terms */
+    int nav_planned = 0;             /* nav rows whose sources a slot has taken (planner)      */
+    uint32_t *d_nav = nullptr;       /* the run's nav table on the device, built by the GPU   */
+    size_t d_nav_cap = 0;            /* producer (gss_nav_rows_device); rows                   */
     Slot slot[NSLOT];
 };
 
@@ -235,8 +242,35 @@ int plan_range_upfront(Run &r)
     return 0;
 }
 
-/* the slot's batch from the up-front plan; its nav rows are the contiguous table range its rows
-   reference (rows are appended in run order), renumbered from 0 */
+/* The nav rows new since the previous slot, as sources for the GPU producer: rows
+   [r.nav_planned, upto) of the scenario's table (rows are appended in run order). */
+int take_nav_sources(Run &r, Slot &sl, int upto)
+{
+    const gss_nav_src_t *src = nullptr;
+    int n_all = 0;
+    gss_scn_nav_sources(r.scn, &src, &n_all);
+    if (upto > n_all)
+        upto = n_all;
+    const int n = upto > r.nav_planned ? upto - r.nav_planned : 0;
+    if (n > sl.nav_cap) {
+        (void)hipHostFree(sl.nav);
+        sl.nav = nullptr;
+        sl.nav_cap = 0;
+        const int cap = n * 2 + 16;
+        if (hipHostMalloc((void **)&sl.nav, sizeof(gss_nav_src_t) * (size_t)cap,
+                          hipHostMallocDefault) != hipSuccess)
+            return gss_fail(GSS_E_NOMEM, "pinned nav sources");
+        sl.nav_cap = cap;
+    }
+    if (n > 0)
+        memcpy(sl.nav, src + r.nav_planned, sizeof(gss_nav_src_t) * (size_t)n);
+    sl.nav_first = r.nav_planned;
+    sl.n_nav = n;
+    r.nav_planned += n;
+    return 0;
+}
+
+/* the slot's batch from the up-front plan (rows keep their global nav indices) */
 int take_upfront(Run &r, Slot &sl, int *nb_out)
 {
     const int64_t left = r.pre_n - r.pre_at;
@@ -250,36 +284,15 @@ int take_upfront(Run &r, Slot &sl, int *nb_out)
     if (!lazy_ck(r))
         memcpy(sl.ck, &r.pre_ck[(size_t)r.pre_at * GSS_MAXCH * GSS_NCK],
                rows * GSS_NCK * sizeof(double));
-    int lo = INT32_MAX, hi = -1;
+    int hi = -1;
     for (int b = 0; b < nb; b++)
         for (int k = 0; k < sl.nch[b]; k++) {
             const int t = sl.blk[(size_t)b * GSS_MAXCH + k].nav_tbl;
-            lo = t < lo ? t : lo;
             hi = t > hi ? t : hi;
         }
-    if (hi < lo)
-        lo = hi = 0;
-    for (int b = 0; b < nb; b++)
-        for (int k = 0; k < sl.nch[b]; k++)
-            sl.blk[(size_t)b * GSS_MAXCH + k].nav_tbl -= lo;
-    const uint32_t *all = nullptr;
-    int n_all = 0;
-    gss_scn_nav_table(r.scn, &all, &n_all);
-    const int n_rows = n_all > 0 ? hi - lo + 1 : 0;
-    if (n_rows > sl.nav_cap) {
-        (void)hipHostFree(sl.nav);
-        sl.nav = nullptr;
-        sl.nav_cap = 0;
-        const int cap = n_rows * 2 + 16;
-        if (hipHostMalloc((void **)&sl.nav, sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)cap,
-                          hipHostMallocDefault) != hipSuccess)
-            return gss_fail(GSS_E_NOMEM, "pinned nav table");
-        sl.nav_cap = cap;
-    }
-    if (n_rows > 0)
-        memcpy(sl.nav, all + (size_t)lo * GSS_NAV_WORDS,
-               sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)n_rows);
-    sl.n_nav = n_rows;
+    const int rc = take_nav_sources(r, sl, hi + 1);
+    if (rc)
+        return rc;
     sl.first = r.first + r.pre_at;
     r.pre_at += nb;
     return 0;
@@ -305,7 +318,10 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
             m = sl.nch[i] > m ? sl.nch[i] : m;
         sl.nch_max = m;
         if (r.use_lin) {
-            rc = gss_linearize(sl.blk, sl.nch, nb, r.n_per_blk, r.ca, 32, sl.nav, sl.n_nav,
+            const uint32_t *rows = nullptr;
+            int n_rows = 0;
+            gss_scn_nav_table(r.scn, &rows, &n_rows);
+            rc = gss_linearize(sl.blk, sl.nch, nb, r.n_per_blk, r.ca, 32, rows, n_rows,
                                sl.lin, sl.fast, r.threads);
             if (rc)
                 return rc;
@@ -352,23 +368,13 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
         const uint32_t *rows = nullptr;
         int n_rows = 0;
         gss_scn_nav_table(r.scn, &rows, &n_rows);
-        if (n_rows > sl.nav_cap) {                     /* snapshot: the table grows later */
-            (void)hipHostFree(sl.nav);
-            sl.nav = nullptr;
-            sl.nav_cap = 0;
-            int cap = n_rows * 2 + 16;
-            if (hipHostMalloc((void **)&sl.nav, sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)cap,
-                              hipHostMallocDefault) != hipSuccess)
-                return gss_fail(GSS_E_NOMEM, "pinned nav table");
-            sl.nav_cap = cap;
-        }
-        if (n_rows > 0)
-            memcpy(sl.nav, rows, sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)n_rows);
-        sl.n_nav = n_rows;
+        rc = take_nav_sources(r, sl, n_rows);          /* the GPU builds the new rows */
+        if (rc)
+            return rc;
         if (r.use_lin) {                               /* the proofs, on the planner thread */
             if (trace_on())
                 fprintf(stderr, "trace scn_done %.6f\n", tnow());
-            rc = gss_linearize(sl.blk, sl.nch, nb, r.n_per_blk, r.ca, 32, sl.nav, n_rows, sl.lin,
+            rc = gss_linearize(sl.blk, sl.nch, nb, r.n_per_blk, r.ca, 32, rows, n_rows, sl.lin,
                                sl.fast, r.threads);
             if (rc)
                 return rc;
@@ -413,15 +419,36 @@ void planner(Run *r)
     }
 }
 
-int submit(gss_dev *d, Slot &sl, const uint32_t *d_ca, int n_per_blk, int fmt, size_t bb,
-           hipStream_t st, hipStream_t cp)
+/* the device nav table holds at least `rows` rows (grown on the compute stream's order) */
+int nav_reserve(Run &r, size_t rows, hipStream_t st)
+{
+    if (rows <= r.d_nav_cap)
+        return 0;
+    size_t cap = r.d_nav_cap ? 2 * r.d_nav_cap : 4096;
+    while (cap < rows)
+        cap *= 2;
+    uint32_t *p = nullptr;
+    RUN_TRY(hipMalloc((void **)&p, sizeof(uint32_t) * GSS_NAV_WORDS * cap));
+    if (r.d_nav) {
+        RUN_TRY(hipStreamSynchronize(st));             /* earlier slots' kernels read it */
+        RUN_TRY(hipMemcpy(p, r.d_nav, sizeof(uint32_t) * GSS_NAV_WORDS * r.d_nav_cap,
+                          hipMemcpyDeviceToDevice));
+        RUN_TRY(hipFree(r.d_nav));
+    }
+    r.d_nav = p;
+    r.d_nav_cap = cap;
+    return 0;
+}
+
+int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, int fmt,
+           size_t bb, hipStream_t st, hipStream_t cp)
 {
     /* the slot's previous D2H must have read d_out before the kernels rewrite it */
     RUN_TRY(hipStreamWaitEvent(st, sl.done, 0));
     const size_t s_blk = sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)sl.nb;
     const size_t s_nch = sizeof(int32_t) * (size_t)sl.nb;
     const size_t s_ck = sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb;
-    const size_t s_nav = sizeof(uint32_t) * GSS_NAV_WORDS * (size_t)(sl.n_nav > 0 ? sl.n_nav : 1);
+    const size_t s_nav = sizeof(gss_nav_src_t) * (size_t)(sl.n_nav > 0 ? sl.n_nav : 1);
     const size_t s_lin = sl.lin ? sizeof(gss_lin_t) * GSS_MAXCH * (size_t)sl.nb : 0;
     const size_t s_fast = sl.lin ? sizeof(int32_t) * 2 * (size_t)sl.nb : 0;
     const size_t need = al256(s_blk) + al256(s_nch) + al256(s_ck) + al256(s_nav) + al256(s_lin) +
@@ -438,27 +465,34 @@ int submit(gss_dev *d, Slot &sl, const uint32_t *d_ca, int n_per_blk, int fmt, s
     gss_chan_blk_t *d_blk = (gss_chan_blk_t *)p;
     int32_t *d_nch = (int32_t *)(p + al256(s_blk));
     double *d_ck = (double *)(p + al256(s_blk) + al256(s_nch));
-    uint32_t *d_nav = (uint32_t *)(p + al256(s_blk) + al256(s_nch) + al256(s_ck));
-    gss_lin_t *d_lin = (gss_lin_t *)((uint8_t *)d_nav + al256(s_nav));
+    gss_nav_src_t *d_src = (gss_nav_src_t *)(p + al256(s_blk) + al256(s_nch) + al256(s_ck));
+    gss_lin_t *d_lin = (gss_lin_t *)((uint8_t *)d_src + al256(s_nav));
     int32_t *d_fast = (int32_t *)((uint8_t *)d_lin + al256(s_lin));
     RUN_TRY(hipMemcpyAsync(d_blk, sl.blk, s_blk, hipMemcpyHostToDevice, st));
     RUN_TRY(hipMemcpyAsync(d_nch, sl.nch, s_nch, hipMemcpyHostToDevice, st));
     RUN_TRY(hipMemcpyAsync(d_ck, sl.ck, s_ck, hipMemcpyHostToDevice, st));
-    if (sl.n_nav > 0)
-        RUN_TRY(hipMemcpyAsync(d_nav, sl.nav, s_nav, hipMemcpyHostToDevice, st));
-    else
-        RUN_TRY(hipMemsetAsync(d_nav, 0, s_nav, st));
+    /* the 30 s producer: this slot's new nav rows built on the device (gss_producers.hip) */
+    const int n_rows = sl.nav_first + sl.n_nav;
+    int rc = nav_reserve(r, (size_t)(n_rows > 0 ? n_rows : 1), st);
+    if (rc)
+        return rc;
+    if (sl.n_nav > 0) {
+        RUN_TRY(hipMemcpyAsync(d_src, sl.nav, s_nav, hipMemcpyHostToDevice, st));
+        rc = gss_nav_rows_device(d, d_src, sl.nav_first, sl.n_nav, r.d_nav, st);
+        if (rc)
+            return rc;
+    }
+    const uint32_t *d_nav = r.d_nav;
     RUN_TRY(hipMemsetAsync(sl.d_status, 0, sizeof(int32_t), st));
-    int rc;
     if (sl.lin) {
         RUN_TRY(hipMemcpyAsync(d_lin, sl.lin, s_lin, hipMemcpyHostToDevice, st));
         RUN_TRY(hipMemcpyAsync(d_fast, sl.fast, sizeof(int32_t) * (size_t)(sl.nb + sl.n_fb),
                                hipMemcpyHostToDevice, st));
         rc = gss_synth_lin_device(d, d_blk, d_nch, sl.nch_max, d_lin, d_fast, d_fast + sl.nb,
-                                  sl.n_fb, d_ck, d_ca, 32, d_nav, sl.n_nav, sl.nb, n_per_blk,
+                                  sl.n_fb, d_ck, d_ca, 32, d_nav, n_rows, sl.nb, n_per_blk,
                                   fmt, sl.d_out, sl.d_status, st);
     } else {
-        rc = gss_synth_device(d, d_blk, d_nch, sl.nch_max, d_ck, d_ca, 32, d_nav, sl.n_nav,
+        rc = gss_synth_device(d, d_blk, d_nch, sl.nch_max, d_ck, d_ca, 32, d_nav, n_rows,
                               sl.nb, n_per_blk, fmt, sl.d_out, nullptr, sl.d_status, st);
     }
     if (rc)
@@ -523,7 +557,7 @@ int run_main(gss_dev *d, Run &r, int n_per_blk, int fmt, size_t bb, gss_sink_fn 
             np--;
         }
         const double ts0 = trace_on() ? tnow() : 0.0;
-        int rc = submit(d, sl, d_ca, n_per_blk, fmt, bb, st, cp[i % NCOPY]);
+        int rc = submit(d, r, sl, d_ca, n_per_blk, fmt, bb, st, cp[i % NCOPY]);
         if (trace_on())
             fprintf(stderr, "trace submit slot %d %.6f %.6f\n", i % NSLOT, ts0, tnow());
         if (rc)
@@ -592,18 +626,21 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             if (sl.rendered) (void)hipEventDestroy(sl.rendered);
         }
         (void)hipFree(d_ca);
+        (void)hipFree(r.d_nav);
         if (st) (void)hipStreamDestroy(st);
         for (hipStream_t c : cp)
             if (c) (void)hipStreamDestroy(c);
     };
     /* buffers */
     {
-        gss_ca_table(r.ca);
+        gss_ca_table(r.ca);                            /* the proofs' copy, on the host */
         if (hipMalloc((void **)&d_ca, sizeof r.ca) != hipSuccess ||
-            hipMemcpy(d_ca, r.ca, sizeof r.ca, hipMemcpyHostToDevice) != hipSuccess ||
             hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
             !make_streams(cp))
             err = gss_fail(GSS_E_HIP, "run setup failed");
+        /* the kernels' copy built on the device by the 30 s producer (gss_producers.hip) */
+        if (!err)
+            err = gss_ca_table_device(d, d_ca, st);
         const size_t nb = (size_t)r.batch;
         for (Slot &sl : r.slot) {
             if (err) break;

@@ -1409,6 +1409,9 @@ extern "C" int gss_fail(int code, const char *fmt, ...);
 
 #define GSS_STR2(x) #x
 #define GSS_STR(x) GSS_STR2(x)
+/* the device ordinal of an open handle (gss_producers.hip, gss_run.hip) */
+extern "C" int gss_dev_ordinal(const gss_dev *d) { return d->ordinal; }
+
 extern "C" const char *gss_build_info(void)
 {
     return "lin_mfma=" GSS_STR(LIN_MFMA) " lin_ch=" GSS_STR(LIN_CH) " arch=gfx950";

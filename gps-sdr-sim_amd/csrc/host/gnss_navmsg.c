@@ -204,6 +204,12 @@ void nav_frame(gtime_t g, chan_t *ch, int init)
     uint32_t wn = (uint32_t)(g0.week % 1024);
     uint32_t tow = (uint32_t)(((unsigned long)g0.sec) / 6UL);
     uint32_t prev = 0;
+    /* the frame as a source for the GPU producer (gss_nav.h): the same data words, TOW, week */
+    memcpy(ch->fsrc.sbf, ch->sbf, sizeof ch->fsrc.sbf);
+    ch->fsrc.tow = tow;
+    ch->fsrc.wn = wn;
+    ch->frame_init = init == 1;
+    ch->frame_seq++;
 
     if (init == 1) {
         for (int i = 0; i < K_N_DWRD_SBF; i++) {

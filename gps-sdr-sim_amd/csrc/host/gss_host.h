@@ -93,6 +93,10 @@ typedef struct {                     /* the fields of channel_t (gpssim.h:160-18
     double azel[2];
     rng_t rho0;
     int nav_row;                     /* row of the nav table holding the current dwrd          */
+    gss_nav_src_t fsrc;              /* the current frame as a GPU producer source (nav_frame)  */
+    int frame_init;                  /* the current frame was built from sbf[4] (allocation)    */
+    int frame_seq;                   /* frames built so far on this channel                      */
+    int last_row, last_row_seq;      /* the channel's last pushed row and its frame_seq          */
     int carr_fresh;                  /* carr_phase was (re)initialised since the last block     */
 } chan_t;
 

@@ -18,6 +18,7 @@
 #include <string.h>
 #include <time.h>
 #include "gss_host.h"
+#include "../common/gss_nav.h"
 #include "../common/gss_phase.h"
 
 /* Receiver antenna attenuation [dB] vs boresight angle 0:5:180 deg (gpssim.c:86-91). */
@@ -65,6 +66,7 @@ struct gss_scn {
     double ant_pat[37];
     int iumd;                               /* next block index, 1..numd-1 (gpssim.c:2154) */
     uint32_t *nav_rows;
+    gss_nav_src_t *nav_src;          /* row r's source for the GPU producer (gss_nav.h)         */
     int n_nav, cap_nav;
     double carr[K_MAX_CHAN];                /* planner: carrier at the next block start per slot */
     int carr_known;                         /* 0 after gss_scn_seek until gss_scn_set_carrier */
@@ -89,7 +91,10 @@ static void msg(const gss_scn *s, const char *fmt, ...)
     va_end(ap);
 }
 
-/* Append a copy of ch->dwrd to the nav table and point the channel at it. */
+/* Append a copy of ch->dwrd to the nav table and point the channel at it.  The row's source
+   (gss_nav_src_t) continues the channel's previous row when that row holds the frame before this
+   one, is rebuilt from sbf[4] for a fresh allocation, and carries its first ten words otherwise
+   (frames built during a seek are not rows). */
 static int nav_push(gss_scn *s, chan_t *ch)
 {
     if (s->n_nav == s->cap_nav) {
@@ -98,9 +103,29 @@ static int nav_push(gss_scn *s, chan_t *ch)
         if (p == NULL)
             return gss_fail(GSS_E_NOMEM, "out of memory (nav table)");
         s->nav_rows = p;
+        gss_nav_src_t *q = realloc(s->nav_src, (size_t)cap * sizeof(gss_nav_src_t));
+        if (q == NULL)
+            return gss_fail(GSS_E_NOMEM, "out of memory (nav sources)");
+        s->nav_src = q;
         s->cap_nav = cap;
     }
-    memcpy(s->nav_rows + (size_t)s->n_nav * GSS_NAV_WORDS, ch->dwrd, sizeof ch->dwrd);
+    const int r = s->n_nav;
+    memcpy(s->nav_rows + (size_t)r * GSS_NAV_WORDS, ch->dwrd, sizeof ch->dwrd);
+    gss_nav_src_t *src = &s->nav_src[r];
+    *src = ch->fsrc;
+    src->next = -1;
+    memset(src->head, 0, sizeof src->head);
+    if (ch->frame_init) {
+        src->prev = GSS_NAV_HEAD_INIT;
+    } else if (ch->last_row >= 0 && ch->last_row_seq == ch->frame_seq - 1) {
+        src->prev = ch->last_row;
+        s->nav_src[ch->last_row].next = r;
+    } else {
+        src->prev = GSS_NAV_HEAD_GIVEN;
+        memcpy(src->head, ch->dwrd, sizeof src->head);
+    }
+    ch->last_row = r;
+    ch->last_row_seq = ch->frame_seq;
     ch->nav_row = s->n_nav++;
     return 0;
 }
@@ -334,8 +359,10 @@ int gss_scn_open(gss_scn **out, const gss_opts_t *opt)
     }
 
     /* ---- channels (gpssim.c:2117-2143) ---- */
-    for (int i = 0; i < K_MAX_CHAN; i++)
+    for (int i = 0; i < K_MAX_CHAN; i++) {
         s->chan[i].prn = 0;
+        s->chan[i].last_row = -1;
+    }
     for (int sv = 0; sv < K_MAX_SAT; sv++)
         s->alloc_sat[sv] = -1;
     s->grx = gt_add(g0, 0.0);
@@ -763,6 +790,28 @@ int gss_scn_set_carrier(gss_scn *s, const double *carr)
     return 0;
 }
 
+int gss_scn_nav_sources(const gss_scn *s, const gss_nav_src_t **src, int *n_rows)
+{
+    if (s == NULL || src == NULL || n_rows == NULL)
+        return gss_fail(GSS_E_ARG, "invalid nav-source query");
+    *src = s->nav_src;
+    *n_rows = s->n_nav;
+    return 0;
+}
+
+int gss_nav_rows_host(const gss_nav_src_t *src, int first, int n, uint32_t *rows)
+{
+    if ((n > 0 && (src == NULL || rows == NULL)) || first < 0 || n < 0)
+        return gss_fail(GSS_E_ARG, "invalid nav-row arguments");
+    for (int i = 0; i < n; i++) {
+        const gss_nav_src_t *q = &src[i];
+        if (q->prev >= first + i || q->prev < GSS_NAV_HEAD_GIVEN)
+            return gss_fail(GSS_E_ARG, "nav source %d: prev %d out of order", first + i, q->prev);
+        gss_nav_frame(q, gss_nav_head(q, rows), rows + (size_t)(first + i) * GSS_NAV_WORDS);
+    }
+    return 0;
+}
+
 int gss_scn_nav_table(const gss_scn *s, const uint32_t **rows, int *n_rows)
 {
     if (s == NULL)
@@ -780,6 +829,7 @@ int gss_scn_close(gss_scn *s)
         return 0;
     free(s->xyz);
     free(s->nav_rows);
+    free(s->nav_src);
     free(s->chain);
     free(s->rg);
     free(s);

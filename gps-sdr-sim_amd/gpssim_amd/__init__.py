@@ -51,6 +51,11 @@ assert LIN_DTYPE.itemsize == 192
 # gss_chain_t (16 bytes): the carrier chain a (block, channel) row continues, gpssim_amd.h
 CHAIN_DTYPE = np.dtype([("slot", "i1"), ("reset", "u1"), ("pad", "u1", (6,)), ("init", "<f8")])
 assert CHAIN_DTYPE.itemsize == 16
+# gss_nav_src_t: one nav-table row's source for the GPU producer (include/gpssim_amd.h)
+NAV_SRC_DTYPE = np.dtype([("sbf", "<u4", (5, 10)), ("tow", "<u4"), ("wn", "<u4"), ("prev", "<i4"),
+                          ("next", "<i4"), ("head", "<u4", (10,))])
+assert NAV_SRC_DTYPE.itemsize == 256
+NAV_HEAD_INIT, NAV_HEAD_GIVEN = -1, -2
 
 
 class GssError(RuntimeError):
@@ -124,6 +129,10 @@ _SIGS = {
     "gss_scn_set_carrier": (C.c_int, [_P, _P]),
     "gss_scn_nav_table": (C.c_int, [_P, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_int)]),
     "gss_ca_table": (C.c_int, [_P]),
+    "gss_scn_nav_sources": (C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_int)]),
+    "gss_nav_rows_host": (C.c_int, [_P, C.c_int, C.c_int, _P]),
+    "gss_nav_rows_device": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, _P]),
+    "gss_ca_table_device": (C.c_int, [_P, _P, _P]),
     "gss_scn_plan_seconds": (C.c_double, [_P]),
     "gss_scn_close": (C.c_int, [_P]),
     "gss_carr_advance": (C.c_double, [C.c_double, C.c_double, C.c_int64]),
@@ -189,6 +198,17 @@ def block_bytes(n_per_blk, fmt):
 def ca_table():
     out = np.zeros((32, CA_WORDS), np.uint32)
     _check(lib().gss_ca_table(_ptr(out)))
+    return out
+
+
+def nav_rows_host(src, first=0, rows=None):
+    """rows [first, first + len(src)) from their sources (gss_nav_rows_host); rows: the table so
+    far (>= first rows), extended and returned"""
+    src = np.ascontiguousarray(src, NAV_SRC_DTYPE)
+    out = np.zeros((first + len(src), NAV_WORDS), np.uint32)
+    if first:
+        out[:first] = rows[:first]
+    _check(lib().gss_nav_rows_host(_ptr(src), first, len(src), _ptr(out)))
     return out
 
 
@@ -378,6 +398,16 @@ class Scenario:
             return np.zeros((1, NAV_WORDS), np.uint32)
         return np.ctypeslib.as_array(rows, shape=(n.value, NAV_WORDS)).copy()
 
+    def nav_sources(self):
+        """the rows' GPU-producer sources (NAV_SRC_DTYPE [n]), same order as nav_table()"""
+        src = _P()
+        n = C.c_int(0)
+        _check(lib().gss_scn_nav_sources(self._h, C.byref(src), C.byref(n)))
+        if n.value == 0:
+            return np.zeros(0, NAV_SRC_DTYPE)
+        buf = (C.c_uint8 * (n.value * NAV_SRC_DTYPE.itemsize)).from_address(src.value)
+        return np.frombuffer(buf, NAV_SRC_DTYPE).copy()
+
     def plan_seconds(self):
         return lib().gss_scn_plan_seconds(self._h)
 
@@ -442,6 +472,14 @@ class Device:
                                       n_ca, nav_ptr,
                                       n_nav, nblk, n_per_blk, fmt, out_ptr,
                                       carr_end_ptr or None, status_ptr or None, stream or None))
+
+    def ca_table_device(self, out_ptr, stream=0):
+        """the C/A table built on the device (gss_ca_table_device) into out_ptr [32][CA_WORDS]"""
+        _check(lib().gss_ca_table_device(self._h, out_ptr, stream or None))
+
+    def nav_rows_device(self, src_ptr, first, n, rows_ptr, stream=0):
+        """nav rows [first, first + n) from device sources (gss_nav_rows_device)"""
+        _check(lib().gss_nav_rows_device(self._h, src_ptr, first, n, rows_ptr, stream or None))
 
     def synth_lin_device(self, blk_ptr, nch_ptr, nch_max, lin_ptr, fast_ptr, fb_ptr, n_fb, ca_ptr,
                          n_ca, nav_ptr, n_nav, nblk, n_per_blk, fmt, out_ptr, status_ptr=0,

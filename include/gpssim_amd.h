@@ -293,6 +293,37 @@ int gss_scn_nav_table(const gss_scn *s, const uint32_t **rows, int *n_rows);
 /* Packed C/A codes for PRN 1..32 into out[32][GSS_CA_WORDS] (row prn-1).                      */
 int gss_ca_table(uint32_t *out);
 
+/* ---- the 30 s producers on the GPU ---------------------------------------------
+   What the 30 s cadence produces for the sample loop -- the C/A chips (codegen, gpssim.c:132-171)
+   and each channel's LNAV frame words with parity (generateNavMsg, gpssim.c:1467-1547) -- built
+   on the device.  The host keeps what needs libm-exact doubles: ephemeris-to-subframe packing
+   (eph2sbf, gpssim.c:490-665), allocation and ranges.  A nav-table row is described by its
+   source: the frame's subframe data words, TOW count and week, and where its first ten words
+   (the previous frame's subframe 5) come from.                                                */
+#define GSS_NAV_HEAD_INIT   (-1)   /* rebuilt from sbf[4] with tow (a newly allocated channel) */
+#define GSS_NAV_HEAD_GIVEN  (-2)   /* in head[] (the first row after a seek)                    */
+typedef struct {
+    uint32_t sbf[5][10];     /* subframe data words (no TOW/WN/parity) at the frame's update   */
+    uint32_t tow;            /* g0.sec / 6: the TOW count before the first subframe            */
+    uint32_t wn;             /* g0.week % 1024                                                  */
+    int32_t  prev;           /* >= 0: row whose words 50..59 are this row's words 0..9, else
+                                GSS_NAV_HEAD_INIT / GSS_NAV_HEAD_GIVEN                          */
+    int32_t  next;           /* row continuing this one (its prev), or -1                       */
+    uint32_t head[10];       /* words 0..9 for GSS_NAV_HEAD_GIVEN                               */
+} gss_nav_src_t;             /* 256 bytes; row r of gss_scn_nav_table is built from source r   */
+
+/* The sources of the rows of gss_scn_nav_table ([n], same order); next links within the table. */
+int gss_scn_nav_sources(const gss_scn *s, const gss_nav_src_t **src, int *n_rows);
+/* Rows [first, first + n) of a nav table from their sources src[0 .. n) (host: the producers'
+   reference); rows before `first` must already be in rows (a source's prev may point there). */
+int gss_nav_rows_host(const gss_nav_src_t *src, int first, int n, uint32_t *rows);
+/* The same on the device (asynchronous on `stream`): src, rows are device pointers, src holds
+   the sources of rows [first, first + n) at src[0 .. n); one lane per chain of rows.          */
+int gss_nav_rows_device(gss_dev *d, const gss_nav_src_t *src, int first, int n, uint32_t *rows,
+                        void *stream);
+/* The packed C/A table of gss_ca_table built on the device into out[32][GSS_CA_WORDS].        */
+int gss_ca_table_device(gss_dev *d, uint32_t *out, void *stream);
+
 /* Wall time [s] the host planner spent so far (control plane + carrier chain).                */
 double gss_scn_plan_seconds(const gss_scn *s);
 

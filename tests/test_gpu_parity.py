@@ -371,3 +371,25 @@ def test_integration_patch_bit_exact(golden, exe, name, args):
                        timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
     assert hashlib.sha256(p.stdout).hexdigest() == golden[name]["sha256"]
+
+
+def test_producers_on_device(dev, golden):
+    """The 30 s producers on the GPU: the C/A table and a whole run's nav rows, in
+    two launches as gss_run builds them, equal the host plane's table word for word."""
+    import torch
+    ca = torch.zeros((32, G.CA_WORDS), dtype=torch.int32, device="cuda")
+    dev.ca_table_device(ca.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(ca.cpu().numpy().view(np.uint32), G.ca_table())
+    for kw in (dict(llh=LOC, duration=300.0), dict(motion_file=CIRCLE, data_format=8)):
+        s = G.Scenario(NAV, **kw)
+        s.all_blocks(batch=500, threads=4)
+        src, want = s.nav_sources(), s.nav_table()
+        d_src = torch.from_numpy(src.view(np.uint8).copy()).cuda()
+        rows = torch.zeros(want.shape, dtype=torch.int32, device="cuda")
+        cut = len(src) // 2
+        dev.nav_rows_device(d_src.data_ptr(), 0, cut, rows.data_ptr())
+        dev.nav_rows_device(d_src.data_ptr() + cut * G.NAV_SRC_DTYPE.itemsize, cut,
+                            len(src) - cut, rows.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(rows.cpu().numpy().view(np.uint32), want), kw

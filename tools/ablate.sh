@@ -10,6 +10,7 @@ HIPCC=/opt/rocm/bin/hipcc
 F="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Iinclude -Wno-unused-result -mllvm -amdgpu-mfma-vgpr-form=1 $flags"
 $HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_synth.hip -o _var/$name/obj/gss_synth.o
 $HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_run.hip -o _var/$name/obj/gss_run.o
+$HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_producers.hip -o _var/$name/obj/gss_producers.o
 HOSTOBJ=gps-sdr-sim_amd/obj/host/*.o
 if [ -n "$HOSTFLAGS" ]; then          # the host proof must agree with the kernel (e.g. GSS_LIN_CH)
     mkdir -p _var/$name/obj/host
@@ -20,4 +21,4 @@ if [ -n "$HOSTFLAGS" ]; then          # the host proof must agree with the kerne
     HOSTOBJ=_var/$name/obj/host/*.o
 fi
 $HIPCC -shared -fPIC --offload-arch=gfx950 -o _var/$name/libgpssim_amd.so $HOSTOBJ \
-    _var/$name/obj/gss_synth.o _var/$name/obj/gss_run.o -lm -lpthread
+    _var/$name/obj/gss_synth.o _var/$name/obj/gss_run.o _var/$name/obj/gss_producers.o -lm -lpthread
