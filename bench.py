@@ -400,17 +400,23 @@ def main():
     from gpssim_amd.render import DeviceWindow
 
     dist = world > 1
+    # GSS_BENCH_REHEARSE=1 (multi-rank rehearsal on a one-GPU box): every rank on GPU 0, gloo
+    # collectives on host tensors; the data path is the same, the driver's runs use RCCL
+    rehearse = dist and os.environ.get("GSS_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if dist:
         import torch.distributed as td
         torch.cuda.set_device(local)
-        td.init_process_group("nccl")
+        td.init_process_group("gloo" if rehearse else "nccl")
     dev_t = torch.device("cuda", local)
+    coll_t = torch.device("cpu") if rehearse else dev_t     # where collective tensors live
 
     # ---- host control plane for this rank's window (untimed setup) ----
     # planned once per node: each rank seeks to its window, produces its rows, and receives the
     # 16 slot carriers at its first block from rank r-1 (gpssim_amd.shard)
     from gpssim_amd.shard import Baton, plan_rank
-    baton = Baton(td, rank, world, device=dev_t) if dist else None
+    baton = Baton(td, rank, world, device=coll_t) if dist else None
     t_plan0 = time.perf_counter()
     blk, nch, ck, nav, npb, plan_t = plan_rank(NAV, rank, world, args.window, llh=LOC,
                                                samp_freq=FS, data_format=args.fmt,
@@ -464,10 +470,10 @@ def main():
     per_rank = [mine]
     if dist:
         t = torch.tensor([elapsed, ck_ms, syn_ms, host_plan_s, lin_ms, host_lin_s],
-                         dtype=torch.float64, device=dev_t)
+                         dtype=torch.float64, device=coll_t)
         td.all_reduce(t, op=td.ReduceOp.MAX)
         elapsed, ck_ms, syn_ms, host_plan_s, lin_ms, host_lin_s = t.tolist()
-        mt = torch.tensor(mine, dtype=torch.float64, device=dev_t)
+        mt = torch.tensor(mine, dtype=torch.float64, device=coll_t)
         parts = [torch.empty_like(mt) for _ in range(world)]
         td.all_gather(parts, mt)
         per_rank = [p.tolist() for p in parts]
