@@ -542,6 +542,7 @@ def main():
         "vs_baseline": None,
         "dtype": ("int64 phases + f16 x f16 -> f32 MFMA accumulate (exact integer sums)"
                   if G.lib_mfma() else "int64 phases + int64 accumulate"),
+        "build": G.build_info(),
         "data": "synthetic: deterministic static-receiver scenario (brdc3540.14n), no dataset",
         "config": {"workload": workload, "samples_per_gpu": samples_rank, "path": "lin",
                    "channels_max": res.nch_max, "parallelism": f"time-window shards x{world}"},

@@ -15,11 +15,12 @@
  *                    slot renders, hands the previous slot's bytes to the sink in run order
  *
  * Slots cycle planner -> main -> sink -> planner; a slot's buffers belong to exactly one side at
- * a time (state under a mutex).  Shipped defaults (GSS_RUN_NCOPY = 1, GSS_RUN_DEPTH = 1): one
- * compute stream and one copy stream, NSLOT = DEPTH + 2 = 3 slots; the D2H of slot i overlaps
- * the kernels of slot i+1 and the planning of slot i+2; DEPTH slots are submitted before the
- * oldest is handed to the sink.  NCOPY = 2 alternates slots over two copy streams (two DMA
- * engines on the link; measured no faster, profiles/round2/ablate_e2e*.log).  A slot's device
+ * a time (state under a mutex).  Shipped defaults (GSS_RUN_NCOPY = 1, GSS_RUN_DEPTH = 2): one
+ * compute stream and one copy stream, NSLOT = DEPTH + 2 = 4 slots; DEPTH slots are submitted
+ * before the oldest is handed to the sink, so the copy engine always has the next slot's D2H
+ * queued behind the current one (DEPTH 1 left it idle while the next slot uploaded and
+ * rendered: 12.5 vs 13.4 GS/s, profiles/round3/ablate_r3n.log).  NCOPY = 2 alternates slots over
+ * two copy streams (two DMA engines on the link; measured slower, same log).  A slot's device
  * output buffer is rewritten only after its own D2H (event).
  */
 #include <hip/hip_runtime.h>
@@ -67,7 +68,7 @@ static int trace_on()
 #define GSS_RUN_NCOPY 1
 #endif
 #ifndef GSS_RUN_DEPTH
-#define GSS_RUN_DEPTH 1
+#define GSS_RUN_DEPTH 2                                /* profiles/round3/ablate_r3n.log */
 #endif
 constexpr int NCOPY = GSS_RUN_NCOPY;                   /* copy streams (DMA engines) */
 constexpr int DEPTH = GSS_RUN_DEPTH;                   /* slots submitted, not yet drained */

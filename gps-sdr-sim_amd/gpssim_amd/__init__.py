@@ -179,7 +179,7 @@ def build_info():
 
 def lib_mfma():
     """True when the fast path accumulates on the matrix cores (LIN_MFMA build)."""
-    return build_info().get("lin_mfma") == "1"
+    return build_info().get("lin_mfma", "0") != "0"
 
 
 def _check(rc):

@@ -49,3 +49,13 @@ def test_cpu_baseline_short_sample():
     r = bench.cpu_baseline(seconds=1)
     assert r is not None and r["cores"] == len(os.sched_getaffinity(0)) and r["value"] > 0
     assert r["single_core"]["cores"] == 1 and r["kind"] in ("reference", "port")
+
+
+def test_dtype_label_follows_the_build():
+    """bench's dtype names the accumulation the loaded build uses (LIN_MFMA 1 or 2: matrix cores)"""
+    sys.path.insert(0, os.path.join(REPO, "gps-sdr-sim_amd"))
+    import gpssim_amd as G
+    info = G.build_info()
+    assert info["lin_mfma"] in ("0", "1", "2")
+    assert G.lib_mfma() == (info["lin_mfma"] != "0")
+    assert info["lin_mfma"] == "2"                 # the shipped build: channel pairs on MFMA
