@@ -735,6 +735,23 @@ GSS_HD void gss_margin_step(double v, double s, double dunit, double *dlo, doubl
     if (hi < *dhi) *dhi = hi;
 }
 
+/* A conservative gss_margin_step for the steps inside a carrier jump (W = 1: v and fl(v + s) in
+   the same binade [2^e, 2^(e+1)), e <= -1).  The exact sum t = v + s lies within half an ulp of
+   r = fl(v + s), so the distances of r to the binade's ends less one ulp bound t's from inside;
+   no tie rule is needed there (a translation by 2^-52 is an even multiple of the lattice
+   2^(e-52), so round-half-even sees the same parity).  Narrower than the exact interval by at
+   most two ulps. */
+GSS_HD void gss_margin_step_carr(double v, double s, double *dlo, double *dhi)
+{
+    const double r = v + s;
+    const int e = gss_exp2i(r);
+    const double p = gss_pow2(e), ulp = gss_pow2(e - 52);
+    const double lo = ulp - (r - p);                   /* -(t - 2^e), rounded outward */
+    const double hi = (2.0 * p - r) - ulp;             /* 2^(e+1) - t, rounded inward */
+    if (lo > *dlo) *dlo = lo;
+    if (hi < *dhi) *dhi = hi;
+}
+
 /* Walk ascending (s > 0) from w until the first wrap at threshold W (carrier W=1, code 1023)
    or n steps.  Returns steps taken; *x = value reached (post-wrap if *wrapped).  If margins is
    non-NULL, accumulates the admissible translation interval [*dlo, *dhi] of w. */
@@ -751,7 +768,13 @@ GSS_HD int64_t gss_asc_to_wrap(double *x, double s, double W, int64_t n, int *wr
         if (J > 0) {
             if (J == INT64_MAX) { if (dlo) { *dlo = 0.0; *dhi = 0.0; } taken = n; break; }
             if (J > n - taken) J = n - taken;
-            if (dlo) {
+            if (dlo && W == 1.0) {                       /* carrier: the cheap bound */
+                gss_margin_step_carr(v, s, dlo, dhi);
+                gss_margin_step_carr(v + (double)(J - 1) * D, s, dlo, dhi);
+                double top = v + (double)J * D;
+                double lim = (W - top) - 2.0 * gss_pow2(gss_exp2i(W) - 52);
+                if (lim < *dhi) *dhi = lim;
+            } else if (dlo) {
                 gss_margin_step(v, s, dunit, dlo, dhi);
                 double vl = v + (double)(J - 1) * D;
                 gss_margin_step(vl, s, dunit, dlo, dhi);
@@ -763,8 +786,15 @@ GSS_HD int64_t gss_asc_to_wrap(double *x, double s, double W, int64_t n, int *wr
             taken += J;
             if (taken == n) break;
         }
-        if (dlo) gss_margin_step(v, s, dunit, dlo, dhi);
         double r = v + s;
+        if (dlo) {                /* the carrier's non-wrapping steps take the cheap bound too:
+                                     a binade crossing below 1 rounds to a lattice that 2^-52
+                                     still divides evenly; the wrap step keeps the exact rule */
+            if (W == 1.0 && r < 1.0)
+                gss_margin_step_carr(v, s, dlo, dhi);
+            else
+                gss_margin_step(v, s, dunit, dlo, dhi);
+        }
         taken++;
         if (r >= W) {                                    /* wrap step: r + δ >= W */
             if (dlo) {
