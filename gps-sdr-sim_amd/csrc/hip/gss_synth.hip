@@ -533,12 +533,14 @@ static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole ch
    table row, entry j = the 32 chips from extended chip j - 32 on, rotated left by j mod 32
    (gss_tw_kernel; the same word the LDS window pass builds) -- read with wave-uniform addresses,
    i.e. scalar loads into SGPRs that the shift takes directly.  No window pass, no LDS window
-   reads, no per-workgroup bit-stream copy. */
+   reads, no per-workgroup bit-stream copy.  LIN_SWIN 2: the same table read by vector buffer
+   loads at a wave-uniform offset (one cache line for the wave, into VGPRs), which wait on
+   vmcnt, in order, instead of the counter the LDS reads use. */
 #ifndef LIN_SWIN
 #define LIN_SWIN 0
 #endif
 #define LIN_TW_W   (32 * CAB_W - 32)       /* table entries per row (j <= 32 CAB_W - 64 used)    */
-#if LIN_SWIN
+#if LIN_SWIN == 1
 #define LIN_WCON "s"                       /* the shift takes the window from an SGPR            */
 #else
 #define LIN_WCON "v"
@@ -710,7 +712,13 @@ __device__ __forceinline__ uint32_t lin_wget(const lin_wsrc &w, int s, uint4 &w4
     (void)w4; (void)M; (void)salt;
     const uint32_t j = min(((w.q0 + (uint32_t)s * w.dq) >> 4) + (32 - CBW_PRE),
                            (uint32_t)(32 * CAB_W - 64));
+#if LIN_SWIN == 2
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)w.W, (short)0, (int)(LIN_TW_W * sizeof(uint32_t)), 0x00020000);
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, 0, (int)(j * 4u), 0);
+#else
     return w.W[j];
+#endif
 #else
     if (s % 4 == 0) {                                     /* four windows per broadcast read */
         if (LIN_ABLATE & 64)
@@ -738,7 +746,7 @@ __device__ __forceinline__ void lin_wissue(const lin_wsrc &w, uint32_t (&ws)[LIN
 /* ... and the fence that needs them all (one wait, after every load of the chunk is issued) */
 __device__ __forceinline__ void lin_wfence(const uint32_t (&ws)[LIN_CH])
 {
-#if LIN_SWIN
+#if LIN_SWIN == 1
     static_assert(LIN_CH == 16, "the fence below names 16 windows");
     asm volatile("" :: "s"(ws[0]), "s"(ws[1]), "s"(ws[2]), "s"(ws[3]), "s"(ws[4]), "s"(ws[5]),
                  "s"(ws[6]), "s"(ws[7]), "s"(ws[8]), "s"(ws[9]), "s"(ws[10]), "s"(ws[11]),

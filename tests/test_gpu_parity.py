@@ -302,21 +302,23 @@ def test_streaming_run_mixed_exact(dev, golden, monkeypatch, fmt, every):
     assert [x for _, x in blocks] == g["block_sha16"][101:178]
 
 
-@pytest.mark.parametrize("handoff,gold,args", [
+@pytest.mark.parametrize("world,handoff,gold,args", [
     # every rank plans the blocks before its range itself (no run id)
-    (False, "static_d30_b16", ["-l", ",".join(map(str, LOC)), "-d", "30", "-b", "16"]),
+    (2, False, "static_d30_b16", ["-l", ",".join(map(str, LOC)), "-d", "30", "-b", "16"]),
     # planned once per node: rank 1 seeks to block 324, past the 30 s update after block 299,
     # and takes the slot carriers there from rank 0's hand-off file (gss_run_ex)
-    (True, "static_d65_b8_noiono", ["-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8", "-i"]),
+    (2, True, "static_d65_b8_noiono", ["-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8", "-i"]),
+    # three ranks: rank 1 both receives (block 216) and hands on (block 432)
+    (3, True, "static_d65_b8_noiono", ["-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8", "-i"]),
 ])
-def test_cli_two_ranks_one_file(golden, handoff, gold, args):
-    """The CLI as two ranks (RANK/WORLD_SIZE, both on GPU 0 here): each pwrite()s its block
+def test_cli_two_ranks_one_file(golden, world, handoff, gold, args):
+    """The CLI as several ranks (RANK/WORLD_SIZE, all on GPU 0 here): each pwrite()s its block
     range into the same file, which equals the single-process reference output."""
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "gpssim.bin")
         procs = []
-        for r in range(2):
-            env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK="0")
+        for r in range(world):
+            env = dict(os.environ, WORLD_SIZE=str(world), RANK=str(r), LOCAL_RANK="0")
             env.pop("TORCHELASTIC_RUN_ID", None)
             env.pop("GSS_RUN_ID", None)
             if handoff:

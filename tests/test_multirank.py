@@ -63,19 +63,20 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("window_s,gold", [
-    (WINDOW_S, "static_d30_b16"),
+@pytest.mark.parametrize("world,window_s,gold", [
+    (2, WINDOW_S, "static_d30_b16"),
     # rank 1 starts at block 309: its seek replays the 30 s nav/allocation update after block
     # 299 (gpssim.c:2294-2345) and its own window crosses the one after block 599
-    (31.0, "static_d300_b16"),
+    (2, 31.0, "static_d300_b16"),
+    # three ranks: the middle one both receives and hands on the baton
+    (3, WINDOW_S, "static_d30_b16"),
 ])
-def test_two_rank_time_window_shards(tmp_path, golden, window_s, gold):
+def test_two_rank_time_window_shards(tmp_path, golden, world, window_s, gold):
     import torch.multiprocessing as mp
-    world = 2
     res = tmp_path / "r.json"
     mp.spawn(_worker, args=(world, _free_port(), str(res), window_s), nprocs=world, join=True)
     r = json.load(open(res))
     n = int(round(window_s * 10)) - 1
-    assert r["firsts"] == [0, n]
+    assert r["firsts"] == [k * n for k in range(world)]
     want = golden[gold]["block_sha16"][: n * world]
     assert r["hashes"] == want
