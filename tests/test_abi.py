@@ -59,3 +59,21 @@ def test_integration_patch_compiles_and_links():
     subprocess.check_call([sys.executable, os.path.join(REPO, "tools", "integration",
                                                         "build_integ.py")])
     assert os.path.exists(os.path.join(REPO, "oracle", "_ref", "gps-sdr-sim-integ"))
+
+
+def test_struct_sizes_match_the_c_header(tmp_path):
+    """the numpy views of the public structs have the C compiler's sizes (include/gpssim_amd.h)"""
+    import subprocess
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include "gpssim_amd.h"\n'
+                   'int main(void){printf("%zu %zu %zu %zu\\n", sizeof(gss_chan_blk_t), '
+                   'sizeof(gss_chain_t), sizeof(gss_nav_src_t), sizeof(gss_lin_t));return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    chan, chain, nav, lin = map(int, subprocess.run([str(exe)], capture_output=True, text=True,
+                                                    check=True).stdout.split())
+    assert chan == G.CHAN_DTYPE.itemsize
+    assert chain == G.CHAIN_DTYPE.itemsize
+    assert nav == G.NAV_SRC_DTYPE.itemsize == 256
+    assert lin == G.LIN_DTYPE.itemsize == 192
