@@ -189,7 +189,8 @@ def live_traffic(fmt, window, threads, kern_ms, steps, warmup, timeout=150):
     os.makedirs(top, exist_ok=True)
     child = [sys.executable, os.path.abspath(__file__), "--steps", str(steps), "--warmup",
              str(warmup), "--fmt", str(fmt), "--window", str(window), "--threads", str(threads),
-             "--no-cpu-baseline", "--no-exact", "--no-configs", "--no-e2e", "--no-pmc"]
+             "--no-cpu-baseline", "--no-exact", "--no-configs", "--no-e2e", "--no-pmc",
+             "--no-sustained"]
     env = dict(os.environ, TMPDIR="/tmp")
     env.pop("GSS_PROF_SAVE", None)
     passes = [("kt", ["--kernel-trace", "--stats"]),
@@ -216,8 +217,8 @@ def live_traffic(fmt, window, threads, kern_ms, steps, warmup, timeout=150):
         k = next((n for n in cs if n.startswith("gss_lin_kernel")), None)
         if k is None or "WRITE_SIZE" not in cs[k] or "FETCH_SIZE" not in cs[k] or k not in ks:
             return None, "rocprofv3 passes gave no gss_lin_kernel counters", None
-        # the same launches as the timed region: the last `steps` dispatches (PS.timed_avg_ns)
-        prof_ms = (PS.timed_avg_ns(kd[k], steps) if kd.get(k) else ks[k]["avg_ns"]) / 1e6
+        # the same launches as the timed region: dispatches warmup .. warmup + steps - 1
+        prof_ms = (PS.timed_avg_ns(kd[k], steps, warmup) if kd.get(k) else ks[k]["avg_ns"]) / 1e6
         try:
             line = [l for l in open(os.path.join(top, "kt.log")) if l.startswith("{")][-1]
             child_ms = json.loads(line)["stages_ms"]["fast_path"]
@@ -242,7 +243,8 @@ def live_traffic(fmt, window, threads, kern_ms, steps, warmup, timeout=150):
                          f"warm-up as this run ({k}: write "
                          f"{cs[k]['WRITE_SIZE'] * 1024 / 1e9:.3f} GB + read "
                          f"{2 * cs[k]['FETCH_SIZE'] * 1024 / 1e9:.3f} GB per launch; profiled "
-                         f"kernel {prof_ms:.3f} ms over its {steps} timed launches, "
+                         f"kernel {prof_ms:.3f} ms over its {steps} timed launches (after "
+                         f"{warmup} warm-up), "
                          f"{ks[k]['avg_ns'] / 1e6:.3f} ms over all {ks[k]['calls']} with the "
                          f"warm-up; this run without the profiler {kern_ms:.3f} ms)"), summary
     finally:
@@ -379,6 +381,8 @@ def main():
     ap.add_argument("--no-configs", action="store_true", help="skip per_config")
     ap.add_argument("--no-e2e", action="store_true", help="skip the gss_run end-to-end run")
     ap.add_argument("--e2e-window", type=float, default=1800.0)
+    ap.add_argument("--no-sustained", action="store_true",
+                    help="skip the sustained-clock launches after the timed region")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the live rocprofv3 traffic passes (roofline.traffic)")
     ap.add_argument("--threads", type=int, default=BOX_CORES)
@@ -456,7 +460,7 @@ def main():
     # informational, after the timed region: the same launches continued until the shader clock
     # has finished ramping (clock ramp), i.e. the rate of a long run
     sustained_ms = None
-    if single and args.steps >= 5:
+    if single and args.steps >= 5 and not args.no_sustained:
         for _ in range(20):
             res.step(stream)
         torch.cuda.synchronize(dev_t)

@@ -24,7 +24,8 @@ def main():
         pass
     summ = json.loads(subprocess.check_output([sys.executable,
                                                os.path.join(REPO, "tools", "prof_summary.py"), d,
-                                               str(live.get("steps") or 0)]))
+                                               str(live.get("steps") or 0),
+                                               str(live.get("warmup") or 0)]))
     bench = None
     for name in ("bench", "kt", "pmc_write", "pmc_fetch"):
         try:
@@ -52,8 +53,8 @@ def main():
            "method": "rocprofv3 --kernel-trace --stats; --pmc WRITE_SIZE / --pmc FETCH_SIZE in "
                      "separate passes (--kernel-trace only), KiB x1024, FETCH_SIZE x2 (gfx950 "
                      "correction); the same bench command, steps and warm-up as the un-profiled "
-                     "run; kernel_timed_avg_ns = the last `steps` dispatches, the launches the "
-                     "bench times",
+                     "run; kernel_timed_avg_ns = dispatches warmup .. warmup + steps - 1, "
+                     "the launches the bench times",
            "source": os.path.relpath(d, REPO)}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))

@@ -44,12 +44,12 @@ def warm_avg_ns(durs):
     return sum(w) / len(w) if w else 0.0
 
 
-def timed_avg_ns(durs, steps):
-    """mean duration of the last `steps` dispatches: the launches a bench run times after its
-    warm-up (one launch per step).  Under sustained load the shader clock ramps up over the
-    first ~20 launches (GRBM_GUI_ACTIVE per dispatch: 1.7 -> 2.3 GHz), so an average over all
+def timed_avg_ns(durs, steps, warmup=0):
+    """mean duration of dispatches warmup .. warmup + steps - 1: the launches a bench run times
+    after its warm-up (one launch per step).  Under sustained load the shader clock ramps up over
+    the first ~25 launches (GRBM_GUI_ACTIVE per dispatch: 1.7 -> 2.3 GHz), so an average over all
     dispatches, warm-up included, is longer than the timed region's."""
-    w = durs[-steps:] if steps and len(durs) >= steps else durs
+    w = durs[warmup:warmup + steps] if steps and len(durs) >= warmup + steps else durs
     return sum(w) / len(w) if w else 0.0
 
 
@@ -73,6 +73,7 @@ def counters(d):
 def main():
     d = sys.argv[1]
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 0     # timed launches (bench --steps)
+    warmup = int(sys.argv[3]) if len(sys.argv) > 3 else 0    # launches before them (--warmup)
     ks = kernel_stats(d)
     kd = kernel_durations(d)
     cs = counters(d)
@@ -82,7 +83,7 @@ def main():
         if k in kd:
             e["warm_avg_ns"] = warm_avg_ns(kd[k])
             if steps:
-                e["timed_avg_ns"] = timed_avg_ns(kd[k], steps)
+                e["timed_avg_ns"] = timed_avg_ns(kd[k], steps, warmup)
                 e["timed_launches"] = min(steps, len(kd[k]))
         c = cs.get(k, {})
         e.update({"meta": c.get("_meta")})
