@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build measurement variants of the library into _var/<name>/ (ablations of the fast-path kernel,
 # or other LIN_CH): usage  [HOSTFLAGS="-D..."] bash tools/ablate.sh name "EXTRA_HIPFLAGS"
+# SYNTH_SRC=<file> builds another version of gss_synth.hip (e.g. a previous commit's, next to it).
 # The variant is loaded by bench.py through GSS_LIB_PATH=_var/<name>/libgpssim_amd.so.
 set -e
 cd "$(dirname "$0")/.."
@@ -8,7 +9,7 @@ name=$1; flags=$2
 mkdir -p _var/$name/obj
 HIPCC=/opt/rocm/bin/hipcc
 F="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Iinclude -Wno-unused-result -mllvm -amdgpu-mfma-vgpr-form=1 $flags"
-$HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_synth.hip -o _var/$name/obj/gss_synth.o
+$HIPCC $F -c ${SYNTH_SRC:-gps-sdr-sim_amd/csrc/hip/gss_synth.hip} -o _var/$name/obj/gss_synth.o
 $HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_run.hip -o _var/$name/obj/gss_run.o
 $HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_producers.hip -o _var/$name/obj/gss_producers.o
 HOSTOBJ=gps-sdr-sim_amd/obj/host/*.o
