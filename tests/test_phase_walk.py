@@ -265,3 +265,26 @@ def test_long_walks_multi_cycle(seed):
             assert W.wc_carr_walk_ck(x0, s, n, ck.ctypes.data) == want, i
             at = [j * n // nck for j in range(nck)]
             assert np.array_equal(ck, oracle.carr_brute_trace(x0, s, at)), i
+
+
+@pytest.mark.parametrize("seed", [50, 51])
+def test_block_chains_successor_fast_path(seed):
+    """The planner's chain as it runs: 0.1 s blocks at 2.6 MS/s chained end to start, with the
+    step drifting a little per block, for Dopplers across +-5 kHz and near zero: every block end
+    and every checkpoint of the cycle-cached walks equals brute force."""
+    W = walk_lib()
+    rng = random.Random(seed)
+    n = 260_000
+    nck = W.wc_nck()
+    at = [j * n // nck for j in range(nck)]
+    for i in range(8):
+        f = rng.uniform(-5000, 5000) if i % 4 else rng.uniform(-80, 80)
+        s = f / 2.6e6
+        x = rng.random()
+        for b in range(3):
+            want = oracle.carr_brute(x, s, n)
+            assert W.wc_carr_cached(x, s, n) == want, (seed, i, b, x, s)
+            ck = np.zeros(nck)
+            assert W.wc_carr_walk_ck(x, s, n, ck.ctypes.data) == want, (seed, i, b, x, s)
+            assert np.array_equal(ck, oracle.carr_brute_trace(x, s, at)), (seed, i, b, x, s)
+            x, s = want, s * (1.0 + rng.uniform(-2e-7, 2e-7))
