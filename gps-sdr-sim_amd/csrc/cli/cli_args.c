@@ -81,7 +81,10 @@ int gss_cli_parse(int argc, char **argv, gss_cli_t *c)
         return 1;
     }
     int r, has_d = 0;
-    optind = 1;
+    /* 0, not 1: glibc then re-initialises all of getopt's state.  With 1 it keeps its pointer
+       into the previous call's argv, which a library caller (the Python binding) has freed, and
+       reads it as more options. */
+    optind = 0;
     while ((r = getopt(argc, argv, "e:u:g:c:l:o:s:b:T:t:d:iv")) != -1) {
         switch (r) {
         case 'e':

@@ -1010,6 +1010,193 @@ GSS_HD double gss_carr_walk_cc(double x, double s, int64_t n)
     return it.x;
 }
 
+/* ---- speculative block walk: the planner's carrier chain off the serial path -------------------
+ * The chain (gpssim.c:2245-2250, carried across blocks) is serial: a block's start is the previous
+ * block's exact end.  But every cycle after a wrap starts on the post-wrap lattice (2^-52
+ * ascending, 2^-53 descending), and a walk from there is a translation of the walk from a nearby
+ * lattice point, exactly, inside an interval the margins give (the cycle cache's argument,
+ * applied to whole stretches of cycles).  So a block's walk can run ahead of the chain, in
+ * parallel over blocks and over GSS_SPEC_K segments of each block (on the GPU: gss_run), from
+ * guesses: the start from the slot's line (accurate to ~1e-12 per block), and the segment starts
+ * at wraps the line predicts (position P[j] and post-wrap value W[j], gss_carr_chain_guess):
+ *   gss_spec_seg_walk  segment 0: the guess g -> its first wrap (p1, w1) exactly, then on to P[1]
+ *                      with margins; segment j: from W[j] at P[j] to P[j+1] (the block end for the
+ *                      last) with margins: end(start + d) = end + d for every lattice multiple d
+ *                      in [dlo, dhi], and whether the segment ended on a wrap
+ *   gss_spec_fix       the true start x -> its first wrap exactly (one partial cycle); if that wrap
+ *                      is at p1, d = w1(x) - w1 is carried through the segments while it stays in
+ *                      their intervals; where a check fails (or with no wrap in the block) the
+ *                      cycle-cached walk goes on from the last exact value.
+ * Exact in every case; tests/test_phase_walk.py and test_host_plane.py check against brute force
+ * and the serial chain. */
+#ifndef GSS_SPEC_T_DEFINED             /* = include/gpssim_amd.h */
+#define GSS_SPEC_T_DEFINED
+#define GSS_SPEC_K 8                   /* segments per block */
+typedef struct gss_spec_in {           /* a row's guesses (host, gss_carr_chain_guess)          */
+    double g, s;                       /* start guess, carr_step (0: padding row)               */
+    int32_t k, pad;                    /* segments (1..GSS_SPEC_K)                              */
+    int64_t P[GSS_SPEC_K];             /* segment j >= 1 starts at sample P[j], a predicted wrap */
+    double W[GSS_SPEC_K];              /* ... with post-wrap value W[j]                         */
+} gss_spec_in_t;                       /* 152 bytes */
+typedef struct gss_spec_seg {
+    double end, dlo, dhi;              /* end value, admissible translations of the start       */
+    int64_t wrap_end;                  /* 1: the segment's last step wrapped                    */
+} gss_spec_seg_t;
+typedef struct gss_spec {              /* a row's speculative walk (GPU or host)                */
+    int64_t p1;                        /* samples to the guess's first wrap (n: none)           */
+    double w1;                         /* its post-wrap value                                   */
+    gss_spec_seg_t seg[GSS_SPEC_K];
+} gss_spec_t;                          /* 272 bytes */
+#endif
+
+/* Exactly to the first wrap or n steps (the reference's order: ">= 1" before "< 0"). */
+GSS_HD int64_t gss_carr_to_wrap(double *x, double s, int64_t n, int *wr)
+{
+    if (s > 0.0)
+        return gss_asc_to_wrap(x, s, 1.0, n, wr, 0, 0);
+    double v = *x;
+    int64_t taken = 0;
+    *wr = 0;
+    while (taken < n) {
+        double D;
+        int64_t J = gss_jump(v, s, 1.0, &D);
+        if (J > 0) {
+            if (J == INT64_MAX) { taken = n; break; }
+            if (J > n - taken) J = n - taken;
+            v = v + (double)J * D;
+            taken += J;
+            if (taken == n) break;
+        }
+        const double r = v + s;
+        taken++;
+        if (r >= 1.0) { v = r - 1.0; *wr = 1; break; }
+        if (r < 0.0) { v = r + 1.0; *wr = 1; break; }
+        v = r;
+    }
+    *x = v;
+    return taken;
+}
+
+/* From a post-wrap value, n steps recording the admissible translations of the start; *wrap_end
+   = the last step wrapped.  Ascending: gss_asc_to_wrap's margins.  Descending: the head down to T
+   by gss_desc_head, then every real step below T, the wrap add and the wrap decisions with their
+   own margins. */
+GSS_HD double gss_walk_margins(double x, double s, int64_t n, double *dlo, double *dhi,
+                               int *wrap_end)
+{
+    int64_t left = n;
+    int last = 0;
+    if (s > 0.0) {
+        while (left > 0) {
+            int wr = 0;
+            left -= gss_asc_to_wrap(&x, s, 1.0, left, &wr, dlo, dhi);
+            last = wr;
+        }
+        *wrap_end = last;
+        return x;
+    }
+    const double T = gss_pow2(gss_exp2i(-s) + 2);
+    const double dunit = gss_pow2(-53);
+    while (left > 0) {
+        int st = 0;
+        last = 0;
+        left -= gss_desc_head(&x, s, T, left, &st, dlo, dhi);
+        if (!st || left <= 0)
+            break;
+        while (left > 0) {                      /* below T: real steps to the wrap */
+            gss_margin_step(x, s, dunit, dlo, dhi);
+            const double r = x + s;
+            left--;
+            if (r < 0.0) {                      /* r + d < 0 as well, and the rounded r + 1 */
+                const double lim = -r - 2.0 * dunit;
+                if (lim < *dhi) *dhi = lim;
+                gss_margin_step(r, 1.0, dunit, dlo, dhi);
+                x = r + 1.0;
+                last = 1;
+                break;
+            }
+            if (-r > *dlo) *dlo = -r;           /* r + d >= 0: no wrap under translation */
+            x = r;
+        }
+    }
+    *wrap_end = last;
+    return x;
+}
+
+/* Segment j of a row's walk (n samples per block). */
+GSS_HD void gss_spec_seg_walk(const gss_spec_in_t *in, int j, int64_t n, gss_spec_t *o)
+{
+    const double s = in->s;
+    const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
+    gss_spec_seg_t *sg = &o->seg[j];
+    const int64_t stop = j + 1 < k ? in->P[j + 1] : n;
+    double x;
+    int64_t pos;
+    sg->dlo = 1.0;                              /* an empty interval until walked */
+    sg->dhi = 0.0;
+    sg->wrap_end = 0;
+    if (j == 0) {
+        x = in->g;
+        int wr = 0;
+        const int64_t t = s != 0.0 ? gss_carr_to_wrap(&x, s, stop, &wr) : stop;
+        o->p1 = wr ? t : n;
+        o->w1 = x;
+        sg->end = x;
+        if (!wr || t >= stop)
+            return;                             /* no wrap before the segment's end */
+        pos = t;
+    } else {
+        x = in->W[j];
+        pos = in->P[j];
+        sg->end = x;
+        if (s == 0.0 || pos >= stop)
+            return;
+    }
+    double dlo = -GSS_BIG, dhi = GSS_BIG;
+    int we = 0;
+    x = gss_walk_margins(x, s, stop - pos, &dlo, &dhi, &we);
+    sg->end = x;
+    sg->dlo = dlo;
+    sg->dhi = dhi;
+    sg->wrap_end = we;
+}
+
+/* The block's exact end from its true start x and the row's speculative walk (*hit = 1 where the
+   translation carried through every segment). */
+GSS_HD double gss_spec_fix(double x, int64_t n, const gss_spec_in_t *in, const gss_spec_t *o,
+                           int *hit)
+{
+    const double s = in->s;
+    const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
+    *hit = 0;
+    double v = x;
+    int wr = 0;
+    const int64_t t = gss_carr_to_wrap(&v, s, n, &wr);
+    if (!wr || t >= n)
+        return v;                               /* no wrap: v is the end, walked exactly */
+    int64_t pos = t;
+    if (t == o->p1) {
+        double d = v - o->w1;                   /* exact: both on the post-wrap lattice */
+        int j = 0;
+        for (; j < k; j++) {
+            const gss_spec_seg_t *sg = &o->seg[j];
+            if (!(d >= sg->dlo && d <= sg->dhi))
+                break;                          /* v is still the exact value at pos */
+            v = sg->end + d;
+            pos = j + 1 < k ? in->P[j + 1] : n;
+            if (j + 1 < k) {
+                if (!sg->wrap_end) { j++; break; }   /* exact at pos, but not post-wrap */
+                d = v - in->W[j + 1];
+            }
+        }
+        if (j == k && pos == n) {
+            *hit = 1;
+            return v;
+        }
+    }
+    return gss_carr_walk_cc(v, s, n - pos);
+}
+
 /* ---- code iterator ---------------------------------------------------------------------- */
 typedef struct gss_code_it {
     gss_code_state c;

@@ -4,11 +4,15 @@
  * gpssim.c:1467-1547; computeChecksum 693-756) that the render kernels read, built on the device
  * from the host plane's compact sources (gss_nav_src_t).  The arithmetic is gss_nav.h, shared
  * with the host checker gss_nav_rows_host.  gss_run builds its device nav table with them.
+ * Also the planner's carrier chain walked ahead: gss_spec_kernel runs each
+ * block's walk from a guess of its start (gss_phase.h, speculative block walk), one lane per row,
+ * so that the serial chain on the host (gss_carr_chain_spec) takes one partial cycle per block.
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "gpssim_amd.h"
 #include "../common/gss_nav.h"
+#include "../common/gss_phase.h"
 
 extern "C" int gss_fail(int code, const char *fmt, ...);
 extern "C" int gss_dev_ordinal(const gss_dev *d);
@@ -74,4 +78,38 @@ extern "C" int gss_nav_rows_device(gss_dev *d, const gss_nav_src_t *src, int fir
                        (hipStream_t)stream, src, first, n, rows);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "nav kernel: %s", hipGetErrorString(e));
+}
+
+/* one lane per segment of a row (gss_spec_seg_walk).  Rows laid out [nblk][GSS_MAXCH] are taken
+   channel-major, so that a wave's lanes walk the segments of consecutive blocks of one channel:
+   close steps, nearly the same cycles and binades (uniform control flow) instead of 16 different
+   Dopplers per wave. */
+__global__ void gss_spec_kernel(const gss_spec_in_t *__restrict__ in, int nrow, int n,
+                                gss_spec_t *__restrict__ spec)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nrow * GSS_SPEC_K)
+        return;
+    const int u = t / GSS_SPEC_K, j = t % GSS_SPEC_K;
+    const int nb = nrow / GSS_MAXCH;
+    const int i = nrow % GSS_MAXCH ? u : (u % nb) * GSS_MAXCH + u / nb;
+    if (j >= in[i].k)
+        return;
+    gss_spec_seg_walk(&in[i], j, n, &spec[i]);
+}
+
+extern "C" int gss_spec_device(gss_dev *d, const gss_spec_in_t *in, int nrow, int n_per_blk,
+                               gss_spec_t *spec, void *stream)
+{
+    if (!d || nrow < 0 || n_per_blk <= 0 || (nrow > 0 && (!in || !spec)))
+        return gss_fail(GSS_E_ARG, "invalid speculative-walk arguments");
+    if (nrow == 0)
+        return 0;
+    if (hipSetDevice(gss_dev_ordinal(d)) != hipSuccess)
+        return gss_fail(GSS_E_HIP, "hipSetDevice failed");
+    const long long lanes = (long long)nrow * GSS_SPEC_K;
+    hipLaunchKernelGGL(gss_spec_kernel, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0,
+                       (hipStream_t)stream, in, nrow, n_per_blk, spec);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "spec kernel: %s", hipGetErrorString(e));
 }

@@ -5,7 +5,12 @@
  *
  *   planner thread   gss_scn_next into pinned slot buffers (+ the sources of the nav rows new
  *                    since the previous slot), then gss_linearize: the fast path's certified
- *                    lines and patches
+ *                    lines and patches.  With the fast path (float carrier) the carrier chain
+ *                    is run ahead on the GPU: the rows come without carriers
+ *                    (gss_scn_next_deferred), every block's walk runs from a guess of its start
+ *                    on the planner's own stream (gss_spec_device), and the serial chain on the
+ *                    host takes one partial cycle per block (gss_carr_chain_spec; exact either
+ *                    way, gss_phase.h).  GSS_RUN_SPEC=0: the host walks every block (gss_scn_next)
  *   main thread      per slot: async H2D; the 30 s producer builds the new nav rows of the
  *                    run's device nav table (gss_nav_rows_device; the C/A table likewise, once
  *                    per run: gss_ca_table_device); gss_synth_lin_device on the compute stream
@@ -163,6 +168,14 @@ struct Run {
     int nav_planned = 0;             /* nav rows whose sources a slot has taken (planner)      */
     uint32_t *d_nav = nullptr;       /* the run's nav table on the device, built by the GPU   */
     size_t d_nav_cap = 0;            /* producer (gss_nav_rows_device); rows                   */
+    /* the carrier chain run ahead (planner thread): rows' guesses and walks, pinned + device */
+    gss_dev *dev = nullptr;
+    int spec = 0;
+    hipStream_t spec_st = nullptr;
+    std::vector<gss_chain_t> spec_chain;
+    gss_spec_in_t *h_in = nullptr, *d_in = nullptr;
+    gss_spec_t *h_spec = nullptr, *d_spec = nullptr;
+    int64_t spec_rows = 0, spec_hits = 0;
     Slot slot[NSLOT];
 };
 
@@ -299,6 +312,54 @@ int take_upfront(Run &r, Slot &sl, int *nb_out)
     return 0;
 }
 
+/* The next batch's rows with the carrier chain run ahead on the GPU (see the header).  The
+   buffers hold r.batch blocks of rows. */
+int spec_next(Run &r, int ask, gss_chan_blk_t *blk, int32_t *nch, int *nb_out)
+{
+    *nb_out = 0;
+    double carr[GSS_MAXCH];
+    int rc = gss_scn_carrier(r.scn, carr);            /* exact, at the batch's first block */
+    if (rc)
+        return rc;
+    int nb = 0;
+    rc = gss_scn_next_deferred(r.scn, ask, blk, nch, r.spec_chain.data(), &nb, r.threads);
+    if (rc || nb == 0)
+        return rc;
+    const int nrow = nb * GSS_MAXCH;
+    const double tg = trace_on() ? tnow() : 0.0;
+    rc = gss_carr_chain_guess(carr, blk, nch, r.spec_chain.data(), nb, r.n_per_blk, r.h_in);
+    if (rc)
+        return rc;
+    RUN_TRY(hipMemcpyAsync(r.d_in, r.h_in, sizeof(gss_spec_in_t) * (size_t)nrow,
+                           hipMemcpyHostToDevice, r.spec_st));
+    rc = gss_spec_device(r.dev, r.d_in, nrow, r.n_per_blk, r.d_spec, r.spec_st);
+    if (rc)
+        return rc;
+    RUN_TRY(hipMemcpyAsync(r.h_spec, r.d_spec, sizeof(gss_spec_t) * (size_t)nrow,
+                           hipMemcpyDeviceToHost, r.spec_st));
+    const double tk = trace_on() ? tnow() : 0.0;
+    RUN_TRY(hipStreamSynchronize(r.spec_st));
+    const double t0 = trace_on() ? tnow() : 0.0;
+    int hit = 0;
+    rc = gss_carr_chain_spec(carr, blk, nch, r.spec_chain.data(), nb, r.n_per_blk, r.h_in,
+                             r.h_spec, r.threads, &hit);
+    if (rc)
+        return rc;
+    rc = gss_scn_set_carrier(r.scn, carr);
+    if (rc)
+        return rc;
+    int rows = 0;
+    for (int b = 0; b < nb; b++)
+        rows += nch[b];
+    r.spec_rows += rows;
+    r.spec_hits += hit;
+    if (trace_on())
+        fprintf(stderr, "trace spec nb %d rows %d hits %d guess %.6f gpu %.6f chain %.6f\n", nb,
+                rows, hit, tk - tg, t0 - tk, tnow() - t0);
+    *nb_out = nb;
+    return 0;
+}
+
 /* Fill slot k's pinned buffers with the next batch inside [first, last); without a carrier
    hand-off, blocks before `first` are planned (the carrier chain is serial) and dropped. */
 int plan_into(Run &r, Slot &sl, int64_t *cursor)
@@ -347,8 +408,10 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
             ask = (int)(r.first - *cursor);            /* stop exactly at the range start */
         int nb = 0;
         /* before the range only the carrier chain matters: no checkpoints recorded */
-        int rc = gss_scn_next(r.scn, ask, sl.blk, sl.nch,
-                              (*cursor < r.first || lazy_ck(r)) ? nullptr : sl.ck, &nb, r.threads);
+        int rc = r.spec ? spec_next(r, ask, sl.blk, sl.nch, &nb)
+                        : gss_scn_next(r.scn, ask, sl.blk, sl.nch,
+                                       (*cursor < r.first || lazy_ck(r)) ? nullptr : sl.ck, &nb,
+                                       r.threads);
         if (rc)
             return rc;
         if (nb == 0) {
@@ -628,6 +691,12 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         }
         (void)hipFree(d_ca);
         (void)hipFree(r.d_nav);
+        (void)hipHostFree(r.h_in); (void)hipHostFree(r.h_spec);
+        (void)hipFree(r.d_in); (void)hipFree(r.d_spec);
+        if (r.spec_st) (void)hipStreamDestroy(r.spec_st);
+        if (trace_on() && r.spec_rows)
+            fprintf(stderr, "trace spec total rows %lld hits %lld\n", (long long)r.spec_rows,
+                    (long long)r.spec_hits);
         if (st) (void)hipStreamDestroy(st);
         for (hipStream_t c : cp)
             if (c) (void)hipStreamDestroy(c);
@@ -667,6 +736,28 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                                hipHostMallocDefault) != hipSuccess))
                 err = gss_fail(GSS_E_NOMEM, "run lines (%zu B per slot)",
                                sizeof(gss_lin_t) * GSS_MAXCH * nb);
+        }
+        /* the chain run ahead: fast path, float carrier, no hand-off (which plans up front) */
+        {
+            const char *e = getenv("GSS_RUN_SPEC");
+            r.spec = lazy_ck(r) && !(opts && opts->carr_in) && !(e && e[0] == '0');
+        }
+        if (!err && r.spec) {
+            const size_t rows = nb * GSS_MAXCH;
+            r.dev = d;
+            r.spec_chain.resize(rows);
+            /* high priority: the walks wait for free CUs behind the render kernels otherwise */
+            int lo_pri = 0, hi_pri = 0;
+            (void)hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri);
+            if (hipStreamCreateWithPriority(&r.spec_st, hipStreamNonBlocking, hi_pri) !=
+                    hipSuccess ||
+                hipHostMalloc((void **)&r.h_in, sizeof(gss_spec_in_t) * rows,
+                              hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void **)&r.h_spec, sizeof(gss_spec_t) * rows,
+                              hipHostMallocDefault) != hipSuccess ||
+                hipMalloc((void **)&r.d_in, sizeof(gss_spec_in_t) * rows) != hipSuccess ||
+                hipMalloc((void **)&r.d_spec, sizeof(gss_spec_t) * rows) != hipSuccess)
+                err = gss_fail(GSS_E_NOMEM, "run carrier-chain buffers (%zu rows)", rows);
         }
         if (!err)
             err = gss_dev_reserve(d, r.batch, info.n_per_blk);

@@ -479,6 +479,175 @@ int gss_carr_chain(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
     return 0;
 }
 
+/* ---- the chain with the block walks run ahead (gss_phase.h, speculative block walk) ---------- */
+/* The line of a slot predicts where a block's walk wraps: ascending, wrap q at step
+   ceil((q - g)/s) with post-wrap value g + p s - q; descending, wrap q at step
+   floor((g + q - 1)/|s|) + 1 with value g + p s + q.  Segment starts: GSS_SPEC_K - 1 wraps spread
+   over the block's wraps after its first.  Doubles suffice (errors ~1e-13 against translation
+   intervals ~1e-8; guesses only: any mismatch is caught by the fix-up). */
+static void spec_guess_row(double g, double s, int n, gss_spec_in_t *in)
+{
+    const double g0 = g;
+    in->g = g0;
+    in->s = s;
+    in->k = 1;
+    in->pad = 0;
+    if (s == 0.0)
+        return;
+    const double as = s > 0.0 ? s : -s;
+    const double e = g0 + (double)n * s;                 /* the line at the block end */
+    const double mw = s > 0.0 ? floor(e) : floor(1.0 - e);   /* wraps in the block */
+    if (!(mw >= 2.0))
+        return;
+    const int64_t m = mw > 1e9 ? (int64_t)1e9 : (int64_t)mw;
+    const int64_t kk = m < GSS_SPEC_K ? m : GSS_SPEC_K;
+    const double unit = s > 0.0 ? 0x1p-52 : 0x1p-53;
+    int k = 1;
+    int64_t prev = 0;
+    for (int64_t j = 1; j < kk; j++) {
+        const int64_t q = 1 + (j * (m - 1) + kk - 1) / kk;          /* wrap index, >= 2 */
+        const int64_t p = s > 0.0 ? (int64_t)ceil(((double)q - g0) / as)
+                                  : (int64_t)floor((g0 + (double)q - 1.0) / as) + 1;
+        if (p <= prev || p >= n)
+            break;
+        const double v = (g0 + (double)p * s) + (s > 0.0 ? -(double)q : (double)q);
+        const double w = rint(v / unit) * unit;
+        if (!(w >= 0.0 && w < 1.0))
+            break;
+        in->P[k] = p;
+        in->W[k] = w;
+        prev = p;
+        k++;
+    }
+    in->k = k;
+}
+
+typedef struct {
+    const gss_chan_blk_t *blk;
+    int n_per_blk;
+    gss_spec_in_t *in;
+} guess_job;
+
+static void guess_part(void *arg, int b)
+{
+    const guess_job *j = arg;
+    for (int k = 0; k < GSS_MAXCH; k++) {
+        gss_spec_in_t *r = &j->in[(size_t)b * GSS_MAXCH + k];
+        if (r->s != 0.0)
+            spec_guess_row(r->g, r->s, j->n_per_blk, r);
+    }
+}
+
+int gss_carr_chain_guess(const double *carr, const gss_chan_blk_t *blk, const int32_t *nch,
+                         const gss_chain_t *chain, int nblk, int n_per_blk, gss_spec_in_t *in)
+{
+    if (carr == NULL || in == NULL || nblk < 0 || n_per_blk <= 0 ||
+        (nblk > 0 && (blk == NULL || nch == NULL || chain == NULL)))
+        return gss_fail(GSS_E_ARG, "invalid carrier-guess arguments");
+    /* the starts, serially: the line of each slot from its exact start (in double: the drift
+       over a batch, ~1e-13 per block, stays far inside the translation intervals) */
+    double run[K_MAX_CHAN];
+    for (int i = 0; i < K_MAX_CHAN; i++)
+        run[i] = carr[i];
+    for (int b = 0; b < nblk; b++)
+        for (int k = 0; k < GSS_MAXCH; k++) {
+            const size_t e = (size_t)b * GSS_MAXCH + k;
+            const int slot = k < nch[b] ? chain[e].slot : -1;
+            in[e].k = 1;
+            in[e].s = 0.0;
+            in[e].g = 0.0;
+            if (slot < 0 || slot >= K_MAX_CHAN)
+                continue;
+            if (chain[e].reset)
+                run[slot] = chain[e].init;
+            const double g = run[slot];
+            in[e].g = g >= 0.0 && g < 1.0 ? g : 0.0;
+            in[e].s = blk[e].carr_step;
+            const double v = g + (double)n_per_blk * blk[e].carr_step;
+            run[slot] = v - floor(v);
+        }
+    /* the segment starts, in parallel over blocks */
+    const guess_job j = {blk, n_per_blk, in};
+    gss_pool_run(8, nblk, guess_part, (void *)&j);
+    return 0;
+}
+
+typedef struct {
+    const gss_spec_in_t *in;
+    int nrow, n_per_blk;
+    gss_spec_t *spec;
+} spec_host_job;
+
+static void spec_host_part(void *arg, int part)
+{
+    const spec_host_job *j = arg;
+    for (int i = part * 16; i < j->nrow && i < part * 16 + 16; i++)
+        for (int g = 0; g < j->in[i].k && g < GSS_SPEC_K; g++)
+            gss_spec_seg_walk(&j->in[i], g, j->n_per_blk, &j->spec[i]);
+}
+
+int gss_spec_host(const gss_spec_in_t *in, int nrow, int n_per_blk, gss_spec_t *spec,
+                  int threads)
+{
+    if (nrow < 0 || n_per_blk <= 0 || (nrow > 0 && (in == NULL || spec == NULL)))
+        return gss_fail(GSS_E_ARG, "invalid speculative-walk arguments");
+    const spec_host_job j = {in, nrow, n_per_blk, spec};
+    gss_pool_run(threads, (nrow + 15) / 16, spec_host_part, (void *)&j);
+    return 0;
+}
+
+typedef struct {
+    double *carr;
+    gss_chan_blk_t *blk;
+    const int32_t *nch;
+    const gss_chain_t *chain;
+    const gss_spec_in_t *in;
+    const gss_spec_t *spec;
+    int nblk, n_per_blk;
+    int hits[K_MAX_CHAN];
+} spec_chain_job;
+
+static void spec_slot_part(void *arg, int slot)
+{
+    spec_chain_job *j = arg;
+    double x = j->carr[slot];
+    int hits = 0;
+    for (int b = 0; b < j->nblk; b++)
+        for (int k = 0; k < j->nch[b]; k++) {
+            const size_t e = (size_t)b * GSS_MAXCH + k;
+            if (j->chain[e].slot != slot)
+                continue;
+            if (j->chain[e].reset)
+                x = j->chain[e].init;
+            j->blk[e].carr0 = x;
+            int hit = 0;
+            x = gss_spec_fix(x, j->n_per_blk, &j->in[e], &j->spec[e], &hit);
+            hits += hit;
+            break;
+        }
+    j->carr[slot] = x;
+    j->hits[slot] = hits;
+}
+
+int gss_carr_chain_spec(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
+                        const gss_chain_t *chain, int nblk, int n_per_blk,
+                        const gss_spec_in_t *in, const gss_spec_t *spec, int threads,
+                        int *n_hit)
+{
+    if (carr == NULL || nblk < 0 || n_per_blk <= 0 ||
+        (nblk > 0 && (blk == NULL || nch == NULL || chain == NULL || in == NULL || spec == NULL)))
+        return gss_fail(GSS_E_ARG, "invalid carrier-chain arguments");
+    spec_chain_job j = {carr, blk, nch, chain, in, spec, nblk, n_per_blk, {0}};
+    gss_pool_run(threads, K_MAX_CHAN, spec_slot_part, (void *)&j);   /* one part per slot */
+    if (n_hit) {
+        int h = 0;
+        for (int i = 0; i < K_MAX_CHAN; i++)
+            h += j.hits[i];
+        *n_hit = h;
+    }
+    return 0;
+}
+
 /* ---- per-block ranges in parallel --------------------------------------------------------------
  * The per-block refresh (gpssim.c:2156-2188) needs computeRange for every active channel of
  * every block, and block b only uses its own range and block b-1's.  Between two 30 s updates the

@@ -51,6 +51,14 @@ assert LIN_DTYPE.itemsize == 192
 # gss_chain_t (16 bytes): the carrier chain a (block, channel) row continues, gpssim_amd.h
 CHAIN_DTYPE = np.dtype([("slot", "i1"), ("reset", "u1"), ("pad", "u1", (6,)), ("init", "<f8")])
 assert CHAIN_DTYPE.itemsize == 16
+# the carrier chain run ahead (gss_carr_chain_guess / gss_spec_* / gss_carr_chain_spec)
+SPEC_K = 8
+SPEC_IN_DTYPE = np.dtype([("g", "<f8"), ("s", "<f8"), ("k", "<i4"), ("pad", "<i4"),
+                          ("P", "<i8", (SPEC_K,)), ("W", "<f8", (SPEC_K,))])
+assert SPEC_IN_DTYPE.itemsize == 152
+SPEC_SEG_DTYPE = np.dtype([("end", "<f8"), ("dlo", "<f8"), ("dhi", "<f8"), ("wrap_end", "<i8")])
+SPEC_DTYPE = np.dtype([("p1", "<i8"), ("w1", "<f8"), ("seg", SPEC_SEG_DTYPE, (SPEC_K,))])
+assert SPEC_DTYPE.itemsize == 272
 # gss_nav_src_t: one nav-table row's source for the GPU producer (include/gpssim_amd.h)
 NAV_SRC_DTYPE = np.dtype([("sbf", "<u4", (5, 10)), ("tow", "<u4"), ("wn", "<u4"), ("prev", "<i4"),
                           ("next", "<i4"), ("head", "<u4", (10,))])
@@ -124,6 +132,11 @@ _SIGS = {
     "gss_scn_next": (C.c_int, [_P, C.c_int, _P, _P, _P, C.POINTER(C.c_int), C.c_int]),
     "gss_scn_next_deferred": (C.c_int, [_P, C.c_int, _P, _P, _P, C.POINTER(C.c_int), C.c_int]),
     "gss_carr_chain": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int]),
+    "gss_carr_chain_guess": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P]),
+    "gss_spec_host": (C.c_int, [_P, C.c_int, C.c_int, _P, C.c_int]),
+    "gss_spec_device": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, _P]),
+    "gss_carr_chain_spec": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P, C.c_int,
+                                      C.POINTER(C.c_int)]),
     "gss_scn_seek": (C.c_int, [_P, C.c_int64, C.c_int]),
     "gss_scn_carrier": (C.c_int, [_P, _P]),
     "gss_scn_set_carrier": (C.c_int, [_P, _P]),
@@ -438,6 +451,43 @@ def carr_chain(carr, blk, nch, chain, n_per_blk, carrier_int=False, with_ck=True
     return c, ck
 
 
+def carr_chain_guess(carr, blk, nch, chain, n_per_blk):
+    """Each row's guesses (gss_carr_chain_guess): SPEC_IN_DTYPE [nb, 16]."""
+    c = np.ascontiguousarray(carr, np.float64)
+    nch = np.ascontiguousarray(nch, np.int32)
+    chain = np.ascontiguousarray(chain, CHAIN_DTYPE)
+    gi = np.zeros((len(nch), MAXCH), SPEC_IN_DTYPE)
+    _check(lib().gss_carr_chain_guess(_ptr(c), _ptr(np.ascontiguousarray(blk)), _ptr(nch),
+                                      _ptr(chain), len(nch), int(n_per_blk), _ptr(gi)))
+    return gi
+
+
+def spec_host(gi, n_per_blk, threads=8):
+    """The speculative walk of every row's segments (gss_spec_host): SPEC_DTYPE rows."""
+    gi = np.ascontiguousarray(gi, SPEC_IN_DTYPE).reshape(-1)
+    spec = np.zeros(len(gi), SPEC_DTYPE)
+    _check(lib().gss_spec_host(_ptr(gi), len(gi), int(n_per_blk), _ptr(spec), threads))
+    return spec
+
+
+def carr_chain_spec(carr, blk, nch, chain, n_per_blk, gi, spec, threads=8):
+    """The carrier chain from the rows' speculative walks (gss_carr_chain_spec): fills
+    blk["carr0"] in place; returns (carrier after the last block, blocks where the translation
+    carried through)."""
+    c = np.array(carr, np.float64, copy=True)
+    assert c.shape == (MAXCH,) and blk.flags.c_contiguous and blk.dtype == CHAN_DTYPE
+    nch = np.ascontiguousarray(nch, np.int32)
+    chain = np.ascontiguousarray(chain, CHAIN_DTYPE)
+    gi = np.ascontiguousarray(gi, SPEC_IN_DTYPE)
+    spec = np.ascontiguousarray(spec, SPEC_DTYPE)
+    assert spec.size == gi.size == len(nch) * MAXCH
+    hit = C.c_int(0)
+    _check(lib().gss_carr_chain_spec(_ptr(c), _ptr(blk), _ptr(nch), _ptr(chain), len(nch),
+                                     int(n_per_blk), _ptr(gi), _ptr(spec), threads,
+                                     C.byref(hit)))
+    return c, hit.value
+
+
 class Device:
     """One GPU (gss_dev_*).  synth_host() moves host arrays; synth_device() takes raw device
     pointers (e.g. torch tensors' data_ptr()) and is stream-ordered."""
@@ -538,6 +588,12 @@ class Device:
         n, a, b = C.c_int(), C.c_float(), C.c_float()
         _check(lib().gss_dev_timing(self._h, 0, C.byref(n), C.byref(a), C.byref(b)))
         return n.value, a.value, b.value
+
+    def spec_device(self, in_ptr, nrow, n_per_blk, spec_ptr, stream=0):
+        """gss_spec_device on raw device pointers (nrow SPEC_IN_DTYPE rows in, SPEC_DTYPE rows
+        out), async on stream."""
+        _check(lib().gss_spec_device(self._h, C.c_void_p(in_ptr), nrow, n_per_blk,
+                                     C.c_void_p(spec_ptr), C.c_void_p(stream)))
 
     def close(self):
         if self._h:

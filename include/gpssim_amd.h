@@ -278,6 +278,46 @@ int gss_scn_next_deferred(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32
 int gss_carr_chain(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
                    const gss_chain_t *chain, int nblk, int n_per_blk, int carrier_int,
                    double *carr_ck, int threads);
+/* The same chain with the blocks' walks run ahead of it, in parallel (the chain's serial part is
+   then one partial cycle per block; gss_phase.h, "speculative block walk").
+     gss_carr_chain_guess  each row's guesses: its start from the line of its slot (exact at the
+                           slot's first block and at a reset) and up to GSS_SPEC_K - 1 segment
+                           starts at wraps the line predicts, in[nblk][GSS_MAXCH] (padding: s 0)
+     gss_spec_host/device  the speculative walk of every row's segments: spec[nrow]; host
+                           threads, or the GPU (device pointers, async on stream; gss_run; one
+                           lane per segment, rows channel-major for a multiple of GSS_MAXCH)
+     gss_carr_chain_spec   the chain: as gss_carr_chain without checkpoints, each block's end from
+                           its true start and its speculative walk (exact whether or not the
+                           translation applies); *n_hit counts the blocks where it did.        */
+#ifndef GSS_SPEC_T_DEFINED
+#define GSS_SPEC_T_DEFINED
+#define GSS_SPEC_K 8                   /* segments per block */
+typedef struct gss_spec_in {           /* a row's guesses (host, gss_carr_chain_guess)          */
+    double g, s;                       /* start guess, carr_step (0: padding row)               */
+    int32_t k, pad;                    /* segments (1..GSS_SPEC_K)                              */
+    int64_t P[GSS_SPEC_K];             /* segment j >= 1 starts at sample P[j], a predicted wrap */
+    double W[GSS_SPEC_K];              /* ... with post-wrap value W[j]                         */
+} gss_spec_in_t;                       /* 152 bytes */
+typedef struct gss_spec_seg {
+    double end, dlo, dhi;              /* end value, admissible translations of the start       */
+    int64_t wrap_end;                  /* 1: the segment's last step wrapped                    */
+} gss_spec_seg_t;
+typedef struct gss_spec {              /* a row's speculative walk (GPU or host)                */
+    int64_t p1;                        /* samples to the guess's first wrap (n: none)           */
+    double w1;                         /* its post-wrap value                                   */
+    gss_spec_seg_t seg[GSS_SPEC_K];
+} gss_spec_t;                          /* 272 bytes */
+#endif
+int gss_carr_chain_guess(const double *carr, const gss_chan_blk_t *blk, const int32_t *nch,
+                         const gss_chain_t *chain, int nblk, int n_per_blk, gss_spec_in_t *in);
+int gss_spec_host(const gss_spec_in_t *in, int nrow, int n_per_blk, gss_spec_t *spec,
+                  int threads);
+int gss_spec_device(gss_dev *d, const gss_spec_in_t *in, int nrow, int n_per_blk,
+                    gss_spec_t *spec, void *stream);
+int gss_carr_chain_spec(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
+                        const gss_chain_t *chain, int nblk, int n_per_blk,
+                        const gss_spec_in_t *in, const gss_spec_t *spec, int threads,
+                        int *n_hit);
 /* Move to run block `block` (>= the next block) without producing the blocks in between: only the
    30 s updates are replayed (nav frames, ephemeris steps, allocation), and the ranges of the
    block before the target (rho0 of computeCodePhase).  The slot carriers are unknown afterwards:

@@ -395,3 +395,62 @@ def test_producers_on_device(dev, golden):
                             len(src) - cut, rows.data_ptr())
         torch.cuda.synchronize()
         assert np.array_equal(rows.cpu().numpy().view(np.uint32), want), kw
+
+
+def test_spec_walks_on_device(dev):
+    """The carrier chain run ahead: the GPU's speculative block walks
+    (gss_spec_device, a lane per segment, rows channel-major) equal the host's (gss_spec_host)
+    field for field, and
+    the chain from them equals the exact chain (gss_carr_chain), for a static run across 30 s
+    updates and the circle.csv run; nearly every block takes the translation."""
+    import torch
+    for kw in (dict(llh=LOC, duration=400.0), dict(motion_file=CIRCLE, data_format=8)):
+        s = G.Scenario(NAV, **kw)
+        carr = s.carrier()
+        n = s.n_per_blk
+        blk, nch, chain = s.next_deferred(300, threads=8)
+        gi = G.carr_chain_guess(carr, blk, nch, chain, n)
+        want = G.spec_host(gi, n, threads=8)
+        d_in = torch.from_numpy(gi.reshape(-1).view(np.uint8).copy()).cuda()
+        d_spec = torch.zeros(want.nbytes, dtype=torch.uint8, device="cuda")
+        dev.spec_device(d_in.data_ptr(), len(want), n, d_spec.data_ptr())
+        torch.cuda.synchronize()
+        got = d_spec.cpu().numpy().view(G.SPEC_DTYPE)
+        live = gi.reshape(-1)["s"] != 0                   # padding rows are not walked
+        assert np.array_equal(got["p1"][live], want["p1"][live]), kw
+        assert np.array_equal(got["w1"][live], want["w1"][live]), kw
+        for r in np.flatnonzero(live):
+            k = gi.reshape(-1)["k"][r]
+            assert got["seg"][r][:k].tobytes() == want["seg"][r][:k].tobytes(), (kw, r)
+        ref = blk.copy()
+        end_ref, _ = G.carr_chain(carr, ref, nch, chain, n, with_ck=False)
+        end, hit = G.carr_chain_spec(carr, blk, nch, chain, n, gi, got)
+        assert np.array_equal(blk["carr0"], ref["carr0"]) and np.array_equal(end, end_ref), kw
+        assert hit >= 0.95 * int(nch.sum()), (kw, hit)
+
+
+@pytest.mark.parametrize("spec", ["0", "1"])
+def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec):
+    """gss_run with the carrier chain walked on the host (GSS_RUN_SPEC=0) and run ahead on the
+    GPU (the default): a 65 s run across two 30 s updates, whole and from a mid-run block, against
+    the reference's golden hashes."""
+    monkeypatch.setenv("GSS_RUN_SPEC", spec)
+    g = golden["static_d65_b8_noiono"]
+    bb = None
+    blocks = []
+
+    def sink(buf, first, nb):
+        for i in range(nb):
+            blocks.append((first + i, hashlib.sha256(buf[i * bb:(i + 1) * bb]).hexdigest()[:16]))
+
+    s, _ = G.Scenario.from_cli(["-e", NAV, "-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8",
+                                "-i"])
+    bb = G.block_bytes(s.n_per_blk, 8)
+    dev.run(s, sink, batch=57, threads=4)
+    assert [x for _, x in blocks] == g["block_sha16"]
+    blocks.clear()
+    s, _ = G.Scenario.from_cli(["-e", NAV, "-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8",
+                                "-i"])
+    dev.run(s, sink, first_block=333, n_blocks=150, batch=64)
+    assert [b for b, _ in blocks] == list(range(333, 483))
+    assert [x for _, x in blocks] == g["block_sha16"][333:483]

@@ -107,3 +107,39 @@ def test_nav_table_rows():
             w = int(row[sf * 10])
             pre = (w >> 22) & 0xFF
             assert pre in (0x8B, 0x74)
+
+
+@pytest.mark.parametrize("kind,threads", [("static", 8), ("circle", 3), ("intcarr", 4)])
+def test_speculative_chain_equals_exact_chain(kind, threads):
+    """The planner's carrier chain with every block's walk run ahead from a guessed start
+    (gss_carr_chain_guess -> gss_spec_host -> gss_carr_chain_spec, the path gss_run takes with
+    the walks on the GPU) gives the same carr0 of every row and the same end carriers as the
+    exact chain (gss_carr_chain), over several batches across 30 s updates and re-allocations,
+    and nearly every block takes the translation (one partial cycle on the serial path)."""
+    if kind == "static":
+        s = G.Scenario(NAV, llh=LOC, duration=400.0)
+    elif kind == "circle":
+        s = G.Scenario(NAV, motion_file=CIRCLE, duration=300.0)
+    else:
+        s = G.Scenario(NAV, llh=LOC, duration=70.0, carrier="int")
+    carr = s.carrier()
+    n = s.n_per_blk
+    total = hit = 0
+    for _ in range(4):
+        blk, nch, chain = s.next_deferred(350, threads=threads)
+        if len(nch) == 0:
+            break
+        ref = blk.copy()
+        end_ref, _ = G.carr_chain(carr, ref, nch, chain, n, carrier_int=s.carrier_int,
+                                  with_ck=False, threads=threads)
+        gi = G.carr_chain_guess(carr, blk, nch, chain, n)
+        spec = G.spec_host(gi, n, threads=threads)
+        end, h = G.carr_chain_spec(carr, blk, nch, chain, n, gi, spec, threads=threads)
+        assert np.array_equal(blk["carr0"], ref["carr0"]), kind
+        assert np.array_equal(end, end_ref), kind
+        total += int(nch.sum())
+        hit += h
+        carr = end
+    assert total > 0
+    if kind != "intcarr":
+        assert hit >= 0.95 * total, (hit, total)
