@@ -168,18 +168,30 @@ struct Run {
     int nav_planned = 0;             /* nav rows whose sources a slot has taken (planner)      */
     uint32_t *d_nav = nullptr;       /* the run's nav table on the device, built by the GPU   */
     size_t d_nav_cap = 0;            /* producer (gss_nav_rows_device); rows                   */
-    /* the carrier chain run ahead (planner thread): rows' guesses and walks, pinned + device */
+    /* the carrier chain run ahead (planner thread): two batches, so that the GPU walks of the
+       next one run while this slot's proofs do */
+    struct SpecBatch {
+        std::vector<gss_chan_blk_t> blk;
+        std::vector<int32_t> nch;
+        std::vector<gss_chain_t> chain;
+        gss_spec_in_t *h_in = nullptr, *d_in = nullptr;       /* pinned host, device */
+        gss_spec_t *h_spec = nullptr, *d_spec = nullptr;
+        double carr[GSS_MAXCH];                              /* exact, at its first block */
+        int nb = 0, launched = 0;
+        double tg = 0.0, tk = 0.0;                           /* trace: guess start, launch end */
+    } sb[2];
+    int sb_cur = 0;
     gss_dev *dev = nullptr;
     int spec = 0;
     hipStream_t spec_st = nullptr;
-    std::vector<gss_chain_t> spec_chain;
-    gss_spec_in_t *h_in = nullptr, *d_in = nullptr;
-    gss_spec_t *h_spec = nullptr, *d_spec = nullptr;
+    uint64_t *spec_warm = nullptr;   /* device scratch of the walks' first launch (one row) */
     int64_t spec_rows = 0, spec_hits = 0;
     Slot slot[NSLOT];
 };
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+static_assert(sizeof(gss_spec_in_t) <= 256 && 256 + sizeof(gss_spec_t) <= 1024,
+              "one row in and out fit the walks' 1024-byte warm-up scratch");
 
 /* The carrier checkpoints feed only the exact path's Stage A, i.e. the blocks the proofs do not
    certify (none of the 2,999 of the bench run).  With the fast path the chain is therefore
@@ -312,52 +324,86 @@ int take_upfront(Run &r, Slot &sl, int *nb_out)
     return 0;
 }
 
-/* The next batch's rows with the carrier chain run ahead on the GPU (see the header).  The
-   buffers hold r.batch blocks of rows. */
-int spec_next(Run &r, int ask, gss_chan_blk_t *blk, int32_t *nch, int *nb_out)
+/* The carrier chain run ahead on the GPU (see the header), in two steps per batch:
+   spec_launch produces the batch's rows (carriers deferred) and its guesses and queues the GPU
+   walks; spec_finish waits for them, walks the chain (exact) and hands the rows over.  The
+   planner launches batch k+1 right after finishing batch k, so that k+1's walks run on the GPU
+   while k's proofs run on the host. */
+int spec_launch(Run &r, Run::SpecBatch &b, int ask)
 {
-    *nb_out = 0;
-    double carr[GSS_MAXCH];
-    int rc = gss_scn_carrier(r.scn, carr);            /* exact, at the batch's first block */
+    b.nb = 0;
+    b.launched = 1;
+    int rc = gss_scn_carrier(r.scn, b.carr);          /* exact: the previous batch is finished */
     if (rc)
         return rc;
     int nb = 0;
-    rc = gss_scn_next_deferred(r.scn, ask, blk, nch, r.spec_chain.data(), &nb, r.threads);
+    rc = gss_scn_next_deferred(r.scn, ask, b.blk.data(), b.nch.data(), b.chain.data(), &nb,
+                               r.threads);
     if (rc || nb == 0)
         return rc;
+    b.nb = nb;
     const int nrow = nb * GSS_MAXCH;
-    const double tg = trace_on() ? tnow() : 0.0;
-    rc = gss_carr_chain_guess(carr, blk, nch, r.spec_chain.data(), nb, r.n_per_blk, r.h_in);
+    b.tg = trace_on() ? tnow() : 0.0;
+    rc = gss_carr_chain_guess(b.carr, b.blk.data(), b.nch.data(), b.chain.data(), nb, r.n_per_blk,
+                              b.h_in);
     if (rc)
         return rc;
-    RUN_TRY(hipMemcpyAsync(r.d_in, r.h_in, sizeof(gss_spec_in_t) * (size_t)nrow,
+    RUN_TRY(hipMemcpyAsync(b.d_in, b.h_in, sizeof(gss_spec_in_t) * (size_t)nrow,
                            hipMemcpyHostToDevice, r.spec_st));
-    rc = gss_spec_device(r.dev, r.d_in, nrow, r.n_per_blk, r.d_spec, r.spec_st);
+    rc = gss_spec_device(r.dev, b.d_in, nrow, r.n_per_blk, b.d_spec, r.spec_st);
     if (rc)
         return rc;
-    RUN_TRY(hipMemcpyAsync(r.h_spec, r.d_spec, sizeof(gss_spec_t) * (size_t)nrow,
+    RUN_TRY(hipMemcpyAsync(b.h_spec, b.d_spec, sizeof(gss_spec_t) * (size_t)nrow,
                            hipMemcpyDeviceToHost, r.spec_st));
-    const double tk = trace_on() ? tnow() : 0.0;
+    b.tk = trace_on() ? tnow() : 0.0;
+    return 0;
+}
+
+int spec_finish(Run &r, Run::SpecBatch &b, gss_chan_blk_t *blk, int32_t *nch, int *nb_out)
+{
+    b.launched = 0;
+    *nb_out = 0;
+    const int nb = b.nb;
+    b.nb = 0;
+    if (nb == 0)
+        return 0;
+    const double tw = trace_on() ? tnow() : 0.0;
     RUN_TRY(hipStreamSynchronize(r.spec_st));
     const double t0 = trace_on() ? tnow() : 0.0;
+    double carr[GSS_MAXCH];
+    memcpy(carr, b.carr, sizeof carr);
     int hit = 0;
-    rc = gss_carr_chain_spec(carr, blk, nch, r.spec_chain.data(), nb, r.n_per_blk, r.h_in,
-                             r.h_spec, r.threads, &hit);
+    int rc = gss_carr_chain_spec(carr, b.blk.data(), b.nch.data(), b.chain.data(), nb,
+                                 r.n_per_blk, b.h_in, b.h_spec, r.threads, &hit);
     if (rc)
         return rc;
     rc = gss_scn_set_carrier(r.scn, carr);
     if (rc)
         return rc;
+    memcpy(blk, b.blk.data(), sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)nb);
+    memcpy(nch, b.nch.data(), sizeof(int32_t) * (size_t)nb);
     int rows = 0;
-    for (int b = 0; b < nb; b++)
-        rows += nch[b];
+    for (int i = 0; i < nb; i++)
+        rows += nch[i];
     r.spec_rows += rows;
     r.spec_hits += hit;
     if (trace_on())
-        fprintf(stderr, "trace spec nb %d rows %d hits %d guess %.6f gpu %.6f chain %.6f\n", nb,
-                rows, hit, tk - tg, t0 - tk, tnow() - t0);
+        fprintf(stderr, "trace spec nb %d rows %d hits %d guess %.6f gpu_wait %.6f chain %.6f\n",
+                nb, rows, hit, b.tk - b.tg, t0 - tw, tnow() - t0);
     *nb_out = nb;
     return 0;
+}
+
+/* the next batch's size from the cursor: stops exactly at the range start and at its end */
+int next_ask(const Run &r, int64_t cursor)
+{
+    const int64_t want = r.last - cursor;
+    if (want <= 0)
+        return 0;
+    int ask = want < r.batch ? (int)want : r.batch;
+    if (cursor < r.first && r.first - cursor < ask)
+        ask = (int)(r.first - cursor);
+    return ask;
 }
 
 /* Fill slot k's pinned buffers with the next batch inside [first, last); without a carrier
@@ -397,21 +443,26 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
         return 0;
     }
     for (;;) {
-        int64_t want = r.last - *cursor;
-        if (want <= 0) {
-            sl.nb = 0;
-            sl.end = 1;
-            return 0;
-        }
-        int ask = want < r.batch ? (int)want : r.batch;
-        if (*cursor < r.first && r.first - *cursor < ask)
-            ask = (int)(r.first - *cursor);            /* stop exactly at the range start */
+        const int ask = next_ask(r, *cursor);
         int nb = 0;
-        /* before the range only the carrier chain matters: no checkpoints recorded */
-        int rc = r.spec ? spec_next(r, ask, sl.blk, sl.nch, &nb)
-                        : gss_scn_next(r.scn, ask, sl.blk, sl.nch,
-                                       (*cursor < r.first || lazy_ck(r)) ? nullptr : sl.ck, &nb,
-                                       r.threads);
+        int rc = 0;
+        if (r.spec) {
+            Run::SpecBatch &b = r.sb[r.sb_cur];
+            if (!b.launched && ask > 0)
+                rc = spec_launch(r, b, ask);
+            if (!rc && b.launched)                     /* else the range is done: nb stays 0 */
+                rc = spec_finish(r, b, sl.blk, sl.nch, &nb);
+            if (!rc && nb > 0) {                       /* the next batch's walks, on the GPU now */
+                const int ask2 = next_ask(r, *cursor + nb);
+                r.sb_cur ^= 1;
+                if (ask2 > 0)
+                    rc = spec_launch(r, r.sb[r.sb_cur], ask2);
+            }
+        } else if (ask > 0) {
+            /* before the range only the carrier chain matters: no checkpoints recorded */
+            rc = gss_scn_next(r.scn, ask, sl.blk, sl.nch,
+                              (*cursor < r.first || lazy_ck(r)) ? nullptr : sl.ck, &nb, r.threads);
+        }
         if (rc)
             return rc;
         if (nb == 0) {
@@ -691,8 +742,12 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         }
         (void)hipFree(d_ca);
         (void)hipFree(r.d_nav);
-        (void)hipHostFree(r.h_in); (void)hipHostFree(r.h_spec);
-        (void)hipFree(r.d_in); (void)hipFree(r.d_spec);
+        if (r.spec_st) (void)hipStreamSynchronize(r.spec_st);
+        for (Run::SpecBatch &b : r.sb) {
+            (void)hipHostFree(b.h_in); (void)hipHostFree(b.h_spec);
+            (void)hipFree(b.d_in); (void)hipFree(b.d_spec);
+        }
+        (void)hipFree(r.spec_warm);
         if (r.spec_st) (void)hipStreamDestroy(r.spec_st);
         if (trace_on() && r.spec_rows)
             fprintf(stderr, "trace spec total rows %lld hits %lld\n", (long long)r.spec_rows,
@@ -745,19 +800,26 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         if (!err && r.spec) {
             const size_t rows = nb * GSS_MAXCH;
             r.dev = d;
-            r.spec_chain.resize(rows);
             /* high priority: the walks wait for free CUs behind the render kernels otherwise */
             int lo_pri = 0, hi_pri = 0;
             (void)hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri);
             if (hipStreamCreateWithPriority(&r.spec_st, hipStreamNonBlocking, hi_pri) !=
                     hipSuccess ||
-                hipHostMalloc((void **)&r.h_in, sizeof(gss_spec_in_t) * rows,
-                              hipHostMallocDefault) != hipSuccess ||
-                hipHostMalloc((void **)&r.h_spec, sizeof(gss_spec_t) * rows,
-                              hipHostMallocDefault) != hipSuccess ||
-                hipMalloc((void **)&r.d_in, sizeof(gss_spec_in_t) * rows) != hipSuccess ||
-                hipMalloc((void **)&r.d_spec, sizeof(gss_spec_t) * rows) != hipSuccess)
-                err = gss_fail(GSS_E_NOMEM, "run carrier-chain buffers (%zu rows)", rows);
+                hipMalloc((void **)&r.spec_warm, 1024) != hipSuccess)
+                err = gss_fail(GSS_E_HIP, "run carrier-chain stream");
+            for (Run::SpecBatch &b : r.sb) {
+                if (err) break;
+                b.blk.resize(rows);
+                b.nch.resize(nb);
+                b.chain.resize(rows);
+                if (hipHostMalloc((void **)&b.h_in, sizeof(gss_spec_in_t) * rows,
+                                  hipHostMallocDefault) != hipSuccess ||
+                    hipHostMalloc((void **)&b.h_spec, sizeof(gss_spec_t) * rows,
+                                  hipHostMallocDefault) != hipSuccess ||
+                    hipMalloc((void **)&b.d_in, sizeof(gss_spec_in_t) * rows) != hipSuccess ||
+                    hipMalloc((void **)&b.d_spec, sizeof(gss_spec_t) * rows) != hipSuccess)
+                    err = gss_fail(GSS_E_NOMEM, "run carrier-chain buffers (%zu rows)", rows);
+            }
         }
         if (!err)
             err = gss_dev_reserve(d, r.batch, info.n_per_blk);
@@ -770,6 +832,13 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         (void)hipSetDevice(ordinal);                   /* pinned reallocations */
         planner(&r);
     });
+    if (r.spec) {
+        /* the walks' first launch costs ~7 ms (the kernel's first use): here, on one zero row,
+           while the planner produces its first rows, instead of inside its first batch */
+        (void)hipMemsetAsync(r.spec_warm, 0, 1024, r.spec_st);
+        (void)gss_spec_device(d, (const gss_spec_in_t *)r.spec_warm, 1, info.n_per_blk,
+                              (gss_spec_t *)((uint8_t *)r.spec_warm + 256), r.spec_st);
+    }
     err = run_main(d, r, info.n_per_blk, info.data_format, bb, sink, user, st, cp, d_ca);
     {
         std::lock_guard<std::mutex> lk(r.mu);
