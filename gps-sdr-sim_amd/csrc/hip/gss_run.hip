@@ -10,7 +10,10 @@
  *                    (gss_scn_next_deferred), every block's walk runs from a guess of its start
  *                    on the planner's own stream (gss_spec_device), and the serial chain on the
  *                    host takes one partial cycle per block (gss_carr_chain_spec; exact either
- *                    way, gss_phase.h).  GSS_RUN_SPEC=0: the host walks every block (gss_scn_next)
+ *                    way, gss_phase.h); the next batch's walks run while this slot is proved.
+ *                    With a carrier hand-off (gss_run_ex) the whole range's chain is run ahead
+ *                    the same way, in chunks, once the carriers arrive.  GSS_RUN_SPEC=0: the
+ *                    host walks every block (gss_scn_next, gss_carr_chain)
  *   main thread      per slot: async H2D; the 30 s producer builds the new nav rows of the
  *                    run's device nav table (gss_nav_rows_device; the C/A table likewise, once
  *                    per run: gss_ca_table_device); gss_synth_lin_device on the compute stream
@@ -174,15 +177,15 @@ struct Run {
         std::vector<gss_chan_blk_t> blk;
         std::vector<int32_t> nch;
         std::vector<gss_chain_t> chain;
-        gss_spec_in_t *h_in = nullptr, *d_in = nullptr;       /* pinned host, device */
-        gss_spec_t *h_spec = nullptr, *d_spec = nullptr;
+        gss_spec_in_t *h_in = nullptr;        /* pinned host, read and written by the lanes */
+        gss_spec_t *h_spec = nullptr;
         double carr[GSS_MAXCH];                              /* exact, at its first block */
         int nb = 0, launched = 0;
         double tg = 0.0, tk = 0.0;                           /* trace: guess start, launch end */
     } sb[2];
     int sb_cur = 0;
     gss_dev *dev = nullptr;
-    int spec = 0;
+    int spec = 0;                    /* per batch (gss_run), or over the range (hand-off)      */
     hipStream_t spec_st = nullptr;
     uint64_t *spec_warm = nullptr;   /* device scratch of the walks' first launch (one row) */
     int64_t spec_rows = 0, spec_hits = 0;
@@ -224,6 +227,48 @@ static void fill_fb_ck(const Run &r, Slot &sl)
     }
 }
 
+/* The up-front range's chain run ahead on the GPU, in chunks of 4,096 blocks: each chunk's
+   guesses from the exact carriers at its start, its walks, then its chain (exact). */
+int chain_upfront_spec(Run &r, double *carr, const gss_chain_t *chain)
+{
+    constexpr int CH = 4096;
+    const size_t rows_max = (size_t)CH * GSS_MAXCH;
+    gss_spec_in_t *h_in = nullptr;                     /* pinned: the lanes use them directly */
+    gss_spec_t *h_spec = nullptr;
+    int rc = 0;
+    if (hipHostMalloc((void **)&h_in, sizeof(gss_spec_in_t) * rows_max, hipHostMallocDefault) !=
+            hipSuccess ||
+        hipHostMalloc((void **)&h_spec, sizeof(gss_spec_t) * rows_max, hipHostMallocDefault) !=
+            hipSuccess)
+        rc = gss_fail(GSS_E_NOMEM, "carrier-chain buffers (%zu rows)", rows_max);
+    int64_t hits = 0, n_rows = 0;
+    for (int64_t b0 = 0; !rc && b0 < r.pre_n; b0 += CH) {
+        const int nb = r.pre_n - b0 < CH ? (int)(r.pre_n - b0) : CH;
+        const int nrow = nb * GSS_MAXCH;
+        gss_chan_blk_t *blk = &r.pre_blk[(size_t)b0 * GSS_MAXCH];
+        const int32_t *nch = &r.pre_nch[(size_t)b0];
+        const gss_chain_t *ch = chain + (size_t)b0 * GSS_MAXCH;
+        rc = gss_carr_chain_guess(carr, blk, nch, ch, nb, r.n_per_blk, h_in);
+        if (rc) break;
+        if ((rc = gss_spec_device(r.dev, h_in, nrow, r.n_per_blk, h_spec, r.spec_st)) != 0 ||
+            hipStreamSynchronize(r.spec_st) != hipSuccess) {
+            if (!rc) rc = gss_fail(GSS_E_HIP, "carrier-chain walks");
+            break;
+        }
+        int hit = 0;
+        rc = gss_carr_chain_spec(carr, blk, nch, ch, nb, r.n_per_blk, h_in, h_spec, r.threads,
+                                 &hit);
+        hits += hit;
+        for (int i = 0; i < nb; i++)
+            n_rows += nch[i];
+    }
+    if (trace_on())
+        fprintf(stderr, "trace spec upfront rows %lld hits %lld\n", (long long)n_rows,
+                (long long)hits);
+    (void)hipHostFree(h_in); (void)hipHostFree(h_spec);
+    return rc;
+}
+
 /* gss_run_ex with a carrier hand-off: seek to the range, produce its rows, take the slot
    carriers at its first block from carr_in, walk the chain, give the end state to carr_out. */
 int plan_range_upfront(Run &r)
@@ -257,9 +302,12 @@ int plan_range_upfront(Run &r)
                         (long long)r.first);
     if (!lazy_ck(r))
         r.pre_ck.resize((size_t)r.pre_n * GSS_MAXCH * GSS_NCK);
-    rc = gss_carr_chain(carr, r.pre_blk.data(), r.pre_nch.data(), chain.data(), (int)r.pre_n,
-                        r.n_per_blk, r.carrier_int, lazy_ck(r) ? nullptr : r.pre_ck.data(),
-                        r.threads);
+    if (r.spec)                                        /* the chain run ahead on the GPU */
+        rc = chain_upfront_spec(r, carr, chain.data());
+    else
+        rc = gss_carr_chain(carr, r.pre_blk.data(), r.pre_nch.data(), chain.data(),
+                            (int)r.pre_n, r.n_per_blk, r.carrier_int,
+                            lazy_ck(r) ? nullptr : r.pre_ck.data(), r.threads);
     if (rc)
         return rc;
     if (r.opts->carr_out && r.opts->carr_out(r.opts->carr_user, carr))
@@ -348,13 +396,12 @@ int spec_launch(Run &r, Run::SpecBatch &b, int ask)
                               b.h_in);
     if (rc)
         return rc;
-    RUN_TRY(hipMemcpyAsync(b.d_in, b.h_in, sizeof(gss_spec_in_t) * (size_t)nrow,
-                           hipMemcpyHostToDevice, r.spec_st));
-    rc = gss_spec_device(r.dev, b.d_in, nrow, r.n_per_blk, b.d_spec, r.spec_st);
+    /* the lanes read their rows from, and write their walks to, the pinned host buffers
+       directly (a few hundred bytes each): no copy engine in the loop (the first copy on this
+       stream cost ~8 ms) */
+    rc = gss_spec_device(r.dev, b.h_in, nrow, r.n_per_blk, b.h_spec, r.spec_st);
     if (rc)
         return rc;
-    RUN_TRY(hipMemcpyAsync(b.h_spec, b.d_spec, sizeof(gss_spec_t) * (size_t)nrow,
-                           hipMemcpyDeviceToHost, r.spec_st));
     b.tk = trace_on() ? tnow() : 0.0;
     return 0;
 }
@@ -745,7 +792,6 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         if (r.spec_st) (void)hipStreamSynchronize(r.spec_st);
         for (Run::SpecBatch &b : r.sb) {
             (void)hipHostFree(b.h_in); (void)hipHostFree(b.h_spec);
-            (void)hipFree(b.d_in); (void)hipFree(b.d_spec);
         }
         (void)hipFree(r.spec_warm);
         if (r.spec_st) (void)hipStreamDestroy(r.spec_st);
@@ -792,10 +838,11 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                 err = gss_fail(GSS_E_NOMEM, "run lines (%zu B per slot)",
                                sizeof(gss_lin_t) * GSS_MAXCH * nb);
         }
-        /* the chain run ahead: fast path, float carrier, no hand-off (which plans up front) */
+        /* the chain run ahead: fast path, float carrier (per batch, or over the up-front range
+           of a hand-off) */
         {
             const char *e = getenv("GSS_RUN_SPEC");
-            r.spec = lazy_ck(r) && !(opts && opts->carr_in) && !(e && e[0] == '0');
+            r.spec = lazy_ck(r) && !(e && e[0] == '0');
         }
         if (!err && r.spec) {
             const size_t rows = nb * GSS_MAXCH;
@@ -815,9 +862,7 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                 if (hipHostMalloc((void **)&b.h_in, sizeof(gss_spec_in_t) * rows,
                                   hipHostMallocDefault) != hipSuccess ||
                     hipHostMalloc((void **)&b.h_spec, sizeof(gss_spec_t) * rows,
-                                  hipHostMallocDefault) != hipSuccess ||
-                    hipMalloc((void **)&b.d_in, sizeof(gss_spec_in_t) * rows) != hipSuccess ||
-                    hipMalloc((void **)&b.d_spec, sizeof(gss_spec_t) * rows) != hipSuccess)
+                                  hipHostMallocDefault) != hipSuccess)
                     err = gss_fail(GSS_E_NOMEM, "run carrier-chain buffers (%zu rows)", rows);
             }
         }
@@ -833,11 +878,12 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         planner(&r);
     });
     if (r.spec) {
-        /* the walks' first launch costs ~7 ms (the kernel's first use): here, on one zero row,
+        /* the walks' first launch costs ~1 ms (the kernel's first use): here, on one zero row,
            while the planner produces its first rows, instead of inside its first batch */
         (void)hipMemsetAsync(r.spec_warm, 0, 1024, r.spec_st);
         (void)gss_spec_device(d, (const gss_spec_in_t *)r.spec_warm, 1, info.n_per_blk,
                               (gss_spec_t *)((uint8_t *)r.spec_warm + 256), r.spec_st);
+
     }
     err = run_main(d, r, info.n_per_blk, info.data_format, bb, sink, user, st, cp, d_ca);
     {

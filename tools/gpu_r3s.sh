@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${1:-r3s}
 [ -n "$SKIP_TESTS" ] || timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q -p no:cacheprovider \
-    -k "spec_walks or chain_modes or streaming_run or producers" --timeout 100 \
+    -k "spec_walks or chain_modes or streaming_run or producers or two_ranks" --timeout 100 \
     --timeout-method thread > gpurun_out/pytest_spec_$TAG.log 2>&1 || exit $?
 for spec in ${SPECS:-0 1}; do
     GSS_RUN_SPEC=$spec GSS_RUN_TRACE=1 timeout -k 10 120 python tools/e2e_cfg_probe.py 4 3600 \
