@@ -143,3 +143,35 @@ def test_speculative_chain_equals_exact_chain(kind, threads):
     assert total > 0
     if kind != "intcarr":
         assert hit >= 0.95 * total, (hit, total)
+
+
+def test_speculative_chain_exact_with_wrong_guesses():
+    """gss_carr_chain_spec is exact whatever the guesses: starts moved far outside every
+    translation interval, segment starts moved off their wraps or to wrong values, and segment
+    counts cut: the chain still equals the exact one, with (almost) no block taking the
+    translation."""
+    s = G.Scenario(NAV, llh=LOC, duration=120.0)
+    carr = s.carrier()
+    n = s.n_per_blk
+    blk, nch, chain = s.next_deferred(600, threads=8)
+    ref = blk.copy()
+    end_ref, _ = G.carr_chain(carr, ref, nch, chain, n, with_ck=False)
+    gi = G.carr_chain_guess(carr, blk, nch, chain, n)
+    rng = np.random.default_rng(7)
+    for mode in ("start", "segments", "counts"):
+        g = gi.copy().reshape(-1)
+        live = g["s"] != 0
+        if mode == "start":                   # the start guess 1e-4 cycle off: another p1/w1
+            g["g"][live] = np.mod(g["g"][live] + 1e-4, 1.0)
+        elif mode == "segments":              # segment starts one sample late, values shifted
+            g["P"][:, 1:] += (g["P"][:, 1:] > 0)
+            g["W"][:, 1:] = np.where(g["P"][:, 1:] > 0, np.mod(g["W"][:, 1:] + 3e-7, 1.0), 0.0)
+        else:                                 # fewer segments than walked, random cut
+            g["k"] = np.minimum(g["k"], rng.integers(1, 4, size=len(g)))
+        spec = G.spec_host(g.reshape(gi.shape), n, threads=8)
+        b = blk.copy()
+        end, hit = G.carr_chain_spec(carr, b, nch, chain, n, g.reshape(gi.shape), spec)
+        assert np.array_equal(b["carr0"], ref["carr0"]), mode
+        assert np.array_equal(end, end_ref), mode
+        if mode != "counts":
+            assert hit < 0.05 * int(nch.sum()), (mode, hit)
