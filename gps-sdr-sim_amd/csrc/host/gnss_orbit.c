@@ -119,10 +119,14 @@ double iono_delay(const iono_t *io, gtime_t g, const double *llh, const double *
     return F * 5.0e-9 * K_C;
 }
 
-/* computeRange: light-time + Sagnac corrected pseudorange, rate, az/el and iono delay. */
-void sv_range(rng_t *rho, const eph_t *e, const iono_t *io, gtime_t g, const double *xyz)
+/* computeRange: light-time + Sagnac corrected pseudorange, rate, az/el and iono delay.  llh and
+   tmat are the receiver's geodetic position and local frame (ecef_to_llh, enu_matrix of xyz): the
+   reference recomputes them per call (gpssim.c:1277-1279); they depend on xyz alone, so callers
+   with many satellites per receiver position pass them in (sv_range_at). */
+void sv_range_at(rng_t *rho, const eph_t *e, const iono_t *io, gtime_t g, const double *xyz,
+                 const double *llh, double tmat[3][3])
 {
-    double pos[3], vel[3], clk[2], los[3], llh[3], neu[3], tmat[3][3];
+    double pos[3], vel[3], clk[2], los[3], neu[3];
 
     sv_state(e, g, pos, vel, clk);
     for (int i = 0; i < 3; i++)
@@ -144,13 +148,19 @@ void sv_range(rng_t *rho, const eph_t *e, const iono_t *io, gtime_t g, const dou
     rho->rate = vdot3(vel, los) / range;
     rho->g = g;
 
-    ecef_to_llh(xyz, llh);
-    enu_matrix(llh, tmat);
     ecef_to_neu(los, tmat, neu);
     neu_to_azel(rho->azel, neu);
 
     rho->iono_delay = iono_delay(io, g, llh, rho->azel);
     rho->range += rho->iono_delay;
+}
+
+void sv_range(rng_t *rho, const eph_t *e, const iono_t *io, gtime_t g, const double *xyz)
+{
+    double llh[3], tmat[3][3];
+    ecef_to_llh(xyz, llh);
+    enu_matrix(llh, tmat);
+    sv_range_at(rho, e, io, g, xyz, llh, tmat);
 }
 
 /* checkSatVisibility: 1 visible, 0 below mask, -1 no valid ephemeris. */

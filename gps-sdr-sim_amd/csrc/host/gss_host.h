@@ -119,6 +119,8 @@ double vdot3(const double *a, const double *b);
 void   sv_state(const eph_t *eph, gtime_t g, double *pos, double *vel, double *clk); /* satpos */
 double iono_delay(const iono_t *io, gtime_t g, const double *llh, const double *azel);
 void   sv_range(rng_t *rho, const eph_t *eph, const iono_t *io, gtime_t g, const double *xyz);
+void   sv_range_at(rng_t *rho, const eph_t *eph, const iono_t *io, gtime_t g, const double *xyz,
+                   const double *llh, double tmat[3][3]);   /* llh, tmat of xyz given */
 int    sv_visible(const eph_t *eph, gtime_t g, const double *xyz, double elv_mask, double *azel);
 
 /* ---- gnss_navmsg.c ------------------------------------------------------------------------ */

@@ -26,9 +26,9 @@
  *      (GSS_LIN_KDEV_*: about 2^-30 cycle and 2^-21 chip).
  *   2. The exact value, the line and the kernel can fall into different cells only where the line
  *      lies within D = D1 + D2 of a cell boundary (a multiple of B = 2^55, resp. 2^50):
- *      (line(p) + D) mod B < 2 D.  These samples are enumerated exactly: gss_minmod computes the
- *      min over p of (a + p s) mod m in O(log m) steps (a Euclid-like reduction of the sawtooth),
- *      inside a binary search over prefixes.  At 2.6 MS/s about one carrier chain in two has one.
+ *      (line(p) + D) mod B < 2 D.  These samples are enumerated exactly, each as the first p after
+ *      the previous one whose residue falls below 2 D: first_below, a Euclid-like descent in
+ *      O(log B) steps.  At 2.6 MS/s about one carrier chain in two has one.
  *   3. The exact value at each of them comes from the cycle-cached walks of gss_phase.h, the
  *      kernel's from gss_lin.h; where the signed LUT term differs it becomes a patch.
  *   4. Code wraps are chip boundaries too: the k-th wrap falls where the line crosses
@@ -88,7 +88,48 @@ u128 gss_maxmod(u128 n, u128 m, u128 a, u128 s)
     return m - 1 - gss_minmod(n, m, m - 1 - a, (m - s) % m);
 }
 
-/* exported for tests (64-bit operands): min and max of (a + p s) mod m over [0, n) */
+/* ---- exact first hit ------------------------------------------------------------------------- */
+/* Smallest x >= 0 with lo <= (s x) mod m <= hi, for 1 <= lo <= hi < m < 2^62 and s < m; UINT64_MAX if
+ * there is none below 2^64.  If s x reaches [lo, hi] before its first wrap, that is x = ceil(lo/s).
+ * Otherwise [lo, hi] holds no multiple of s (so hi - lo < s), and x exists for wrap count y iff some
+ * multiple of s lies in [lo + m y, hi + m y], i.e. (m y) mod s lies in [s - hi mod s, s - lo mod s]:
+ * the same question for (m mod s, s), Euclid's descent; x = ceil((lo + m y) / s) of the least y. */
+static uint64_t first_in(uint64_t s, uint64_t m, uint64_t lo, uint64_t hi)
+{
+    if (s == 0)
+        return UINT64_MAX;
+    const uint64_t x = (lo + s - 1) / s;
+    if (s * x <= hi)                                 /* s x <= lo + s - 1 < 2^63 */
+        return x;
+    const uint64_t lr = lo % s, hr = hi % s;         /* 1 <= lr <= hr < s (no multiple inside) */
+    const uint64_t y = first_in(m % s, s, s - hr, s - lr);
+    if (y == UINT64_MAX)
+        return UINT64_MAX;
+    const u128 v = ((u128)lo + (u128)m * y + s - 1) / s;
+    return v >> 64 ? UINT64_MAX : (uint64_t)v;
+}
+
+/* Smallest p in [0, n) with (a + p s) mod m < w (0 <= a, s < m < 2^62, 0 < w <= m), or n. */
+static uint64_t first_below(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint64_t w)
+{
+    if (n == 0)
+        return 0;
+    if (a < w)
+        return 0;
+    /* (a + p s) mod m < w  <=>  (s p) mod m in [m - a, m - a + w - 1], a range below m as a >= w */
+    const uint64_t p = first_in(s, m, m - a, m - a + w - 1);
+    return p < n ? p : n;
+}
+
+/* exported for tests: first_below, and min and max of (a + p s) mod m over [0, n) */
+uint64_t gss_first_below(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint64_t w)
+{
+    if (m == 0 || m >= ((uint64_t)1 << 62) || w == 0 || w > m)
+        return UINT64_MAX;
+    return first_below(n, m, a % m, s % m, w);
+}
+
+/* (64-bit operands) */
 void gss_minmax_mod(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint64_t *mn, uint64_t *mx)
 {
     *mn = (uint64_t)gss_minmod(n, m, a % m, s % m);
@@ -123,33 +164,31 @@ static i128 to_fix(double x, int k, int *inexact)
 
 /* Step 2: the samples p in [1, n) where the line L0 + p S comes within delta of a cell boundary
    (a multiple of 2^lgB).  Writes up to cap of them in ascending order to hit[]; returns their
-   number, or -1 if there are more (or delta is not small against B).  Binary search over prefix
-   minima. */
+   number, or -1 if there are more (or delta is not small against B).  Each hit is the next
+   sample whose residue falls below 2 delta (first_below: O(log B) per hit). */
 static int ambiguous(i128 L0, i128 S, i128 delta, int lgB, int64_t n, int64_t *hit, int cap)
 {
-    const u128 B = (u128)1 << lgB;
+    const uint64_t B = (uint64_t)1 << lgB;           /* lgB <= 55 */
     if (delta >= (i128)(B / 4))
         return -1;
-    const u128 st = (u128)(((S % (i128)B) + (i128)B) % (i128)B);
+    if (delta <= 0)
+        return 0;                                    /* nothing within a zero distance */
+    const uint64_t st = (uint64_t)(((S % (i128)B) + (i128)B) % (i128)B);
     /* r(p) in [0, delta) or [B - delta, B)  <=>  (r(p) + delta) mod B < 2 delta */
-    const u128 a0 = ((u128)(((L0 % (i128)B) + (i128)B) % (i128)B) + (u128)delta) % B;
-    const u128 w = 2 * (u128)delta;
+    const uint64_t a0 = (uint64_t)((((L0 % (i128)B) + (i128)B) % (i128)B + delta) % (i128)B);
+    const uint64_t w = 2 * (uint64_t)delta;
     int nh = 0;
     int64_t p0 = 1;
     while (p0 < n) {
-        const u128 a = (a0 + (u128)p0 % B * st) % B;
-        const u128 m = (u128)(n - p0);
-        if (gss_minmod(m, B, a, st) >= w)
+        const uint64_t a = (uint64_t)(((u128)a0 + (u128)p0 * st) % B);
+        const uint64_t m = (uint64_t)(n - p0);
+        const uint64_t i = first_below(m, B, a, st, w);
+        if (i >= m)
             break;
-        u128 lo = 1, hi = m;                         /* smallest prefix length with a hit */
-        while (lo < hi) {
-            const u128 mid = (lo + hi) / 2;
-            if (gss_minmod(mid, B, a, st) < w) hi = mid; else lo = mid + 1;
-        }
         if (nh == cap)
             return -1;
-        hit[nh++] = p0 + (int64_t)lo - 1;
-        p0 += (int64_t)lo;
+        hit[nh++] = p0 + (int64_t)i;
+        p0 += (int64_t)i + 1;
     }
     return nh;
 }
@@ -282,12 +321,13 @@ static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
     lin->gpos[ng] = 0;
     lin->gval[ng++] = g;
     gss_code_state cnt = {0.0, p->icode, p->ibit, p->iword};
-    /* the line's k-th wrap is the first q with Z0 + q ZS >= k per:  q = u + (v > 0) where
-       k per - Z0 = u ZS + v, 0 <= v < ZS; k -> k + 1 adds per = Q ZS + R */
-    const int64_t Q = per / ZS, R = per % ZS;
-    int64_t u = (per - Z0) / ZS, v = (per - Z0) % ZS;
-    for (int64_t k = 1;; k++) {
-        int64_t q = u + (v > 0);
+    /* the line's k-th wrap is the first q with Z0 + q ZS >= k per: q = ceil((k per - Z0) / ZS). */
+    /* Only the wraps that start a data bit matter: wrap 20 - icode, then every 20th (icode counts
+       0..19, gss_code_count_wrap).  The ones between decide nothing, and a later wrap lies >= 1023
+       samples further on (code_step < 1), so the loop ends where the per-wrap loop would. */
+    for (int64_t k = 20 - p->icode;; k += 20) {
+        const i128 num = (i128)k * per - Z0;             /* > 0: k >= 1, Z0 < per */
+        int64_t q = (int64_t)(num / ZS) + (num % ZS > 0);
         if (q - 1 >= n)
             break;
         int j = find_hit(hz, nhz, q - 1);
@@ -297,27 +337,19 @@ static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
             q++;                                 /* ... or one sample later */
         if (q >= n)
             break;
-        const int pb = cnt.ibit, pw = cnt.iword;
-        gss_code_count_wrap(&cnt);
-        if (cnt.ibit != pb || cnt.iword != pw) {            /* a new data bit */
-            if (cnt.iword >= GSS_NAV_WORDS)
-                return 0;                        /* dwrd[60]: the exact path reports it */
-            const int g2 = signed_gain(p->gain, nav, cnt.iword, cnt.ibit);
-            if (g2 != g) {
-                /* the kernel takes at most one change per 4096-sample wave segment (they are
-                   >= 20 code periods = 20 ms apart in any real run) */
-                if (ng == GSS_NGC || (ng > 1 && q - lin->gpos[ng - 1] < 4096))
-                    return 0;
-                lin->gpos[ng] = (int32_t)q;
-                lin->gval[ng++] = g2;
-                g = g2;
-            }
-        }
-        u += Q;
-        v += R;
-        if (v >= ZS) {
-            v -= ZS;
-            u++;
+        cnt.icode = 19;                          /* the 19 wraps since the last data bit */
+        gss_code_count_wrap(&cnt);               /* a new data bit */
+        if (cnt.iword >= GSS_NAV_WORDS)
+            return 0;                            /* dwrd[60]: the exact path reports it */
+        const int g2 = signed_gain(p->gain, nav, cnt.iword, cnt.ibit);
+        if (g2 != g) {
+            /* the kernel takes at most one change per 4096-sample wave segment (they are
+               >= 20 code periods = 20 ms apart in any real run) */
+            if (ng == GSS_NGC || (ng > 1 && q - lin->gpos[ng - 1] < 4096))
+                return 0;
+            lin->gpos[ng] = (int32_t)q;
+            lin->gval[ng++] = g2;
+            g = g2;
         }
     }
     for (int i = ng; i < GSS_NGC; i++) {

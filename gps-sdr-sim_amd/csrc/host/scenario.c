@@ -667,11 +667,14 @@ static void *range_worker(void *arg)
     const gss_scn *s = r->s;
     for (int j = r->j0; j < r->nj; j += r->jstep) {
         const double *xyz = s->static_mode ? s->xyz[0] : s->xyz[r->iumd0 + j];
+        double llh[3], tmat[3][3];                   /* the receiver's frame, once per block */
+        ecef_to_llh(xyz, llh);
+        enu_matrix(llh, tmat);
         for (int i = 0; i < K_MAX_CHAN; i++) {
             const chan_t *ch = &s->chan[i];
             if (ch->prn > 0)
-                sv_range(&s->rg[(size_t)j * K_MAX_CHAN + i], &s->eph[s->ieph][ch->prn - 1],
-                         &s->io, r->g[j], xyz);
+                sv_range_at(&s->rg[(size_t)j * K_MAX_CHAN + i], &s->eph[s->ieph][ch->prn - 1],
+                            &s->io, r->g[j], xyz, llh, tmat);
         }
     }
     return NULL;

@@ -124,6 +124,7 @@ _SIGS = {
                                        _P]),
     "gss_minmax_mod": (None, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
                               C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "gss_first_below": (C.c_uint64, [C.c_uint64] * 5),
     "gss_dev_timing": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_float),
                                  C.POINTER(C.c_float)]),
     "gss_dev_timing_lin": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_float)]),
@@ -252,6 +253,11 @@ def minmax_mod(n, m, a, s):
     mn, mx = C.c_uint64(), C.c_uint64()
     lib().gss_minmax_mod(n, m, a, s, C.byref(mn), C.byref(mx))
     return mn.value, mx.value
+
+
+def first_below(n, m, a, s, w):
+    """least p in [0, n) with (a + p s) mod m < w, or n (the proof's ambiguous-sample search)"""
+    return lib().gss_first_below(n, m, a, s, w)
 
 
 def carr_advance(carr, step, n):

@@ -165,6 +165,9 @@ int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *n
 /* min and max of (a + p*s) mod m over 0 <= p < n, exactly (the certificate's core; exported for
    tests).                                                                                      */
 void gss_minmax_mod(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint64_t *mn, uint64_t *mx);
+/* tests: the least p in [0, n) with (a + p s) mod m < w (n if none; UINT64_MAX for m = 0 or
+   m >= 2^62, w = 0 or w > m) -- the proof's enumeration of ambiguous samples */
+uint64_t gss_first_below(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint64_t w);
 
 /* Same, from host buffers: uploads inputs, runs, downloads `out` (and carr_end if non-NULL),
    synchronises.  Convenience for the CLI and tests; the bench uses gss_synth_device().

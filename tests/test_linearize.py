@@ -97,6 +97,53 @@ def test_minmax_mod_pow2_vs_numpy(lgm):
         assert G.minmax_mod(n, m, a, s) == (int(v.min()), int(v.max())), (n, a, s)
 
 
+def brute_first_below(n, m, a, s, w):
+    for p in range(n):
+        if (a + p * s) % m < w:
+            return p
+    return n
+
+
+def test_first_below_small_vs_brute():
+    """The proof's ambiguous-sample search (first_below) against a scan."""
+    rng = np.random.default_rng(7)
+    for _ in range(4000):
+        m = int(rng.integers(1, 3000))
+        n = int(rng.integers(0, 2000))
+        a, s = int(rng.integers(0, m)), int(rng.integers(0, m))
+        w = int(rng.integers(1, m + 1)) if rng.random() < 0.3 else int(rng.integers(1, max(2, m // 50)))
+        assert G.first_below(n, m, a, s, w) == brute_first_below(n, m, a, s, w), (n, m, a, s, w)
+
+
+@pytest.mark.parametrize("lgm", [50, 55])
+def test_first_below_pow2_vs_numpy(lgm):
+    """The proof's moduli and window widths (2 D of 2^-34 cycle / 2^-25 chip and wider), runs of a
+    whole block, steps near small rationals, vs numpy; and the hits enumerated one after another."""
+    rng = np.random.default_rng(100 + lgm)
+    m = 1 << lgm
+    for _ in range(60):
+        n = int(rng.integers(1, 300000))
+        a = int(rng.integers(0, m, dtype=np.uint64))
+        s = int(rng.integers(0, m, dtype=np.uint64))
+        if rng.random() < 0.5:
+            q = int(rng.integers(1, 40))
+            s = (m * int(rng.integers(0, q)) // q + int(rng.integers(-1000, 1000))) % m
+        w = 1 << int(rng.integers(lgm - 40, lgm - 8))
+        p = np.arange(n, dtype=np.uint64)
+        v = (np.uint64(a) + p * np.uint64(s)) & np.uint64(m - 1)
+        hits = np.flatnonzero(v < np.uint64(w))[:8]
+        got, p0 = [], 0
+        while len(got) < len(hits) + 1 and p0 < n:
+            i = G.first_below(n - p0, m, (a + p0 * s) % m, s, w)
+            if i >= n - p0:
+                break
+            got.append(p0 + i)
+            p0 += i + 1
+        assert got[:len(hits)] == [int(h) for h in hits], (n, a, s, w)
+        if len(hits) < 8:
+            assert len(got) == len(hits), (n, a, s, w)
+
+
 # ---------------------------------------------------------------------------------------------
 def synth_params(rng, nblk, nch_list, n_per_blk, ties=False, tiny=False, fs=2.6e6):
     """random blocks of n_per_blk samples at sample rate fs (realistic Doppler and code rate)"""
