@@ -44,6 +44,7 @@
 #include "gpssim_amd.h"
 
 extern "C" int gss_fail(int code, const char *fmt, ...);
+extern "C" void gss_pool_select(int id);             /* pool.c */
 
 #define RUN_TRY(x)                                                                           \
     do {                                                                                     \
@@ -184,6 +185,24 @@ struct Run {
         double tg = 0.0, tk = 0.0;                           /* trace: guess start, launch end */
     } sb[2];
     int sb_cur = 0;
+    /* the rows produced ahead on their own thread (chain run ahead, no hand-off): during the run
+       the scenario belongs to that thread; it hands over each batch's rows with the nav rows and
+       sources new with it, and the planner keeps the slot carriers and host copies of the nav
+       table (the proofs read it) */
+    struct RowBatch {
+        std::vector<gss_chan_blk_t> blk;
+        std::vector<int32_t> nch;
+        std::vector<gss_chain_t> chain;
+        std::vector<gss_nav_src_t> nav_src;
+        std::vector<uint32_t> nav_rows;
+        int64_t first = 0;
+        int nb = 0, end = 0, err = 0, ready = 0;
+        double t0 = 0.0, t1 = 0.0;                           /* trace: production start, end */
+    } rb[2];
+    int rows_ahead = 0, rb_take = 0, rows_done = 0;
+    double carr[GSS_MAXCH];          /* rows_ahead: the slot carriers at the planner's next batch */
+    std::vector<gss_nav_src_t> nav_src_h;
+    std::vector<uint32_t> nav_rows_h;
     gss_dev *dev = nullptr;
     int spec = 0;                    /* per batch (gss_run), or over the range (hand-off)      */
     hipStream_t spec_st = nullptr;
@@ -322,7 +341,12 @@ int take_nav_sources(Run &r, Slot &sl, int upto)
 {
     const gss_nav_src_t *src = nullptr;
     int n_all = 0;
-    gss_scn_nav_sources(r.scn, &src, &n_all);
+    if (r.rows_ahead) {
+        src = r.nav_src_h.data();
+        n_all = (int)r.nav_src_h.size();
+    } else {
+        gss_scn_nav_sources(r.scn, &src, &n_all);
+    }
     if (upto > n_all)
         upto = n_all;
     const int n = upto > r.nav_planned ? upto - r.nav_planned : 0;
@@ -377,16 +401,116 @@ int take_upfront(Run &r, Slot &sl, int *nb_out)
    walks; spec_finish waits for them, walks the chain (exact) and hands the rows over.  The
    planner launches batch k+1 right after finishing batch k, so that k+1's walks run on the GPU
    while k's proofs run on the host. */
+/* next_ask's batches in run order, produced ahead of the planner (rows_ahead): the scenario's
+   rows with their carriers deferred, and the nav rows and sources new with each batch */
+int next_ask(const Run &r, int64_t cursor);
+
+void rows_thread(Run *r)
+{
+    {
+        const char *e = getenv("GSS_RUN_ROWS_POOL");   /* 0: share the planner's workers */
+        gss_pool_select(e && e[0] == '0' ? 0 : 1);
+    }
+    int64_t cursor = 0;
+    int nav_done = 0;
+    for (int i = 0;; i++) {
+        Run::RowBatch &q = r->rb[i & 1];
+        {
+            std::unique_lock<std::mutex> lk(r->mu);
+            r->cv.wait(lk, [&] { return r->abort || !q.ready; });
+            if (r->abort)
+                break;
+        }
+        const int ask = next_ask(*r, cursor);
+        if (ask <= 0)
+            break;                                     /* the planner asks no further */
+        q.t0 = trace_on() ? tnow() : 0.0;
+        int nb = 0;
+        int rc = gss_scn_next_deferred(r->scn, ask, q.blk.data(), q.nch.data(), q.chain.data(),
+                                       &nb, r->threads);
+        const gss_nav_src_t *src = nullptr;
+        const uint32_t *rows = nullptr;
+        int n_src = 0, n_rows = 0;
+        if (!rc)
+            rc = gss_scn_nav_sources(r->scn, &src, &n_src);
+        if (!rc)
+            rc = gss_scn_nav_table(r->scn, &rows, &n_rows);
+        if (!rc && (n_src != n_rows || n_src < nav_done))
+            rc = gss_fail(GSS_E_STATE, "nav table and sources out of step");
+        if (!rc) {
+            q.nav_src.assign(src + nav_done, src + n_src);
+            q.nav_rows.assign(rows + (size_t)nav_done * GSS_NAV_WORDS,
+                              rows + (size_t)n_rows * GSS_NAV_WORDS);
+            nav_done = n_src;
+        }
+        q.first = cursor;
+        q.nb = nb;
+        q.err = rc;
+        q.end = rc || nb == 0;
+        cursor += nb;
+        q.t1 = trace_on() ? tnow() : 0.0;
+        {
+            std::lock_guard<std::mutex> lk(r->mu);
+            q.ready = 1;
+        }
+        r->cv.notify_all();
+        if (q.end)
+            break;
+    }
+    {
+        std::lock_guard<std::mutex> lk(r->mu);
+        r->rows_done = 1;
+    }
+    r->cv.notify_all();
+}
+
+/* the next batch of rows_ahead into b (vectors swapped, no copy); its nav rows and sources onto
+   the planner's copies */
+int take_rows(Run &r, Run::SpecBatch &b, int *nb_out)
+{
+    *nb_out = 0;
+    Run::RowBatch &q = r.rb[r.rb_take];
+    const double tw = trace_on() ? tnow() : 0.0;
+    {
+        std::unique_lock<std::mutex> lk(r.mu);
+        r.cv.wait(lk, [&] { return r.abort || q.ready || r.rows_done; });
+        if (!q.ready)
+            return gss_fail(GSS_E_STATE, r.abort ? "run aborted" : "rows ended before the run");
+    }
+    if (q.err)
+        return q.err;
+    std::swap(b.blk, q.blk);
+    std::swap(b.nch, q.nch);
+    std::swap(b.chain, q.chain);
+    r.nav_src_h.insert(r.nav_src_h.end(), q.nav_src.begin(), q.nav_src.end());
+    r.nav_rows_h.insert(r.nav_rows_h.end(), q.nav_rows.begin(), q.nav_rows.end());
+    *nb_out = q.nb;
+    if (trace_on())
+        fprintf(stderr, "trace rows nb %d produced %.6f %.6f wait %.6f\n", q.nb, q.t0, q.t1,
+                tnow() - tw);
+    {
+        std::lock_guard<std::mutex> lk(r.mu);
+        q.ready = 0;
+    }
+    r.cv.notify_all();
+    r.rb_take ^= 1;
+    return 0;
+}
+
 int spec_launch(Run &r, Run::SpecBatch &b, int ask)
 {
     b.nb = 0;
     b.launched = 1;
-    int rc = gss_scn_carrier(r.scn, b.carr);          /* exact: the previous batch is finished */
-    if (rc)
-        return rc;
-    int nb = 0;
-    rc = gss_scn_next_deferred(r.scn, ask, b.blk.data(), b.nch.data(), b.chain.data(), &nb,
-                               r.threads);
+    int rc = 0, nb = 0;
+    if (r.rows_ahead) {
+        memcpy(b.carr, r.carr, sizeof b.carr);         /* exact: the previous batch is finished */
+        rc = take_rows(r, b, &nb);
+    } else {
+        rc = gss_scn_carrier(r.scn, b.carr);
+        if (!rc)
+            rc = gss_scn_next_deferred(r.scn, ask, b.blk.data(), b.nch.data(), b.chain.data(),
+                                       &nb, r.threads);
+    }
     if (rc || nb == 0)
         return rc;
     b.nb = nb;
@@ -424,7 +548,10 @@ int spec_finish(Run &r, Run::SpecBatch &b, gss_chan_blk_t *blk, int32_t *nch, in
                                  r.n_per_blk, b.h_in, b.h_spec, r.threads, &hit);
     if (rc)
         return rc;
-    rc = gss_scn_set_carrier(r.scn, carr);
+    if (r.rows_ahead)
+        memcpy(r.carr, carr, sizeof carr);             /* the scenario is the rows thread's */
+    else
+        rc = gss_scn_set_carrier(r.scn, carr);
     if (rc)
         return rc;
     memcpy(blk, b.blk.data(), sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)nb);
@@ -529,7 +656,12 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
         sl.nch_max = m;
         const uint32_t *rows = nullptr;
         int n_rows = 0;
-        gss_scn_nav_table(r.scn, &rows, &n_rows);
+        if (r.rows_ahead) {
+            rows = r.nav_rows_h.data();
+            n_rows = (int)(r.nav_rows_h.size() / GSS_NAV_WORDS);
+        } else {
+            gss_scn_nav_table(r.scn, &rows, &n_rows);
+        }
         rc = take_nav_sources(r, sl, n_rows);          /* the GPU builds the new rows */
         if (rc)
             return rc;
@@ -866,6 +998,20 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                     err = gss_fail(GSS_E_NOMEM, "run carrier-chain buffers (%zu rows)", rows);
             }
         }
+        r.rows_ahead = r.spec && !(opts && opts->carr_in);
+        {
+            const char *e = getenv("GSS_RUN_ROWS_AHEAD");
+            if (e && e[0] == '0')
+                r.rows_ahead = 0;
+        }
+        if (!err && r.rows_ahead) {
+            for (Run::RowBatch &q : r.rb) {
+                q.blk.resize(nb * GSS_MAXCH);
+                q.nch.resize(nb);
+                q.chain.resize(nb * GSS_MAXCH);
+            }
+            err = gss_scn_carrier(s, r.carr);
+        }
         if (!err)
             err = gss_dev_reserve(d, r.batch, info.n_per_blk);
     }
@@ -877,6 +1023,9 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         (void)hipSetDevice(ordinal);                   /* pinned reallocations */
         planner(&r);
     });
+    std::thread th_rows;
+    if (r.rows_ahead)
+        th_rows = std::thread(rows_thread, &r);
     if (r.spec) {
         /* the walks' first launch costs ~1 ms (the kernel's first use): here, on one zero row,
            while the planner produces its first rows, instead of inside its first batch */
@@ -892,6 +1041,10 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
     }
     r.cv.notify_all();
     th.join();
+    if (th_rows.joinable())
+        th_rows.join();
+    if (r.rows_ahead && !err)                          /* the scenario's carriers: run's end */
+        err = gss_scn_set_carrier(s, r.carr);
     cleanup();
     return err;
 }

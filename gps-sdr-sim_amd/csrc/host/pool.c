@@ -5,31 +5,54 @@
  * sections per batch); creating and joining 16 threads for each costs 0.1-1.7 ms, a large share
  * of a 16-block batch at 20 MS/s.  gss_pool_run(nthreads, nparts, fn, arg) runs fn(arg, part)
  * for part = 0 .. nparts-1 on the caller plus up to nthreads-1 pooled workers, which take parts
- * dynamically (an atomic counter), so uneven parts balance themselves.  One job at a time: a
- * second caller waits for the first job to finish (jobs never nest).
+ * dynamically (an atomic counter), so uneven parts balance themselves.  One job at a time per
+ * pool: a second caller waits for the first job to finish (jobs never nest).  Two pools, chosen
+ * per calling thread (gss_pool_select): gss_run's rows thread has its own.
  */
 #include <pthread.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "gss_host.h"
 
 #define POOL_MAX 64
+#define POOL_N 2                         /* pool 0: the default; 1: gss_run's rows thread  */
 
-static pthread_mutex_t run_mu = PTHREAD_MUTEX_INITIALIZER;     /* one job at a time */
-static pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
-static pthread_cond_t go = PTHREAD_COND_INITIALIZER, done = PTHREAD_COND_INITIALIZER;
-static int n_workers;                    /* started (never exit)                        */
-static uint64_t generation;              /* bumped per job                              */
-static int job_workers;                  /* workers 0 .. job_workers-1 take part        */
-static int active;                       /* workers still in the current job            */
-static gss_task_fn job_fn;
-static void *job_arg;
-static int job_nparts;
-static int next_part;                    /* taken with __atomic_fetch_add               */
+typedef struct {
+    pthread_mutex_t run_mu;              /* one job at a time */
+    pthread_mutex_t mu;
+    pthread_cond_t go, done;
+    int n_workers;                       /* started (never exit)                        */
+    uint64_t generation;                 /* bumped per job                              */
+    int job_workers;                     /* workers 0 .. job_workers-1 take part        */
+    int active;                          /* workers still in the current job            */
+    gss_task_fn job_fn;
+    void *job_arg;
+    int job_nparts;
+    int next_part;                       /* taken with __atomic_fetch_add               */
+} pool_t;
 
-static void take_parts(gss_task_fn fn, void *arg, int nparts)
+#define POOL_INIT {PTHREAD_MUTEX_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, \
+                   PTHREAD_COND_INITIALIZER, 0, 0, 0, 0, NULL, NULL, 0, 0}
+static pool_t pools[POOL_N] = {POOL_INIT, POOL_INIT};
+static __thread int tl_pool;             /* the calling thread's pool (gss_pool_select) */
+
+/* Route this thread's gss_pool_run jobs to pool id (0 default): gss_run's rows thread takes its
+   own workers, so that its range passes run beside the planner's chain and proofs instead of
+   queueing behind them. */
+void gss_pool_select(int id)
+{
+    tl_pool = id >= 0 && id < POOL_N ? id : 0;
+}
+
+typedef struct {
+    pool_t *p;
+    int id;
+} worker_arg;
+
+static void take_parts(pool_t *P, gss_task_fn fn, void *arg, int nparts)
 {
     for (;;) {
-        const int p = __atomic_fetch_add(&next_part, 1, __ATOMIC_RELAXED);
+        const int p = __atomic_fetch_add(&P->next_part, 1, __ATOMIC_RELAXED);
         if (p >= nparts)
             return;
         fn(arg, p);
@@ -38,24 +61,26 @@ static void take_parts(gss_task_fn fn, void *arg, int nparts)
 
 static void *worker(void *arg)
 {
-    const int id = (int)(intptr_t)arg;
+    pool_t *P = ((worker_arg *)arg)->p;
+    const int id = ((worker_arg *)arg)->id;
+    free(arg);
     uint64_t seen = 0;
-    pthread_mutex_lock(&mu);
+    pthread_mutex_lock(&P->mu);
     for (;;) {
-        while (generation == seen || id >= job_workers) {
-            if (generation != seen)               /* a job this worker sits out */
-                seen = generation;
-            pthread_cond_wait(&go, &mu);
+        while (P->generation == seen || id >= P->job_workers) {
+            if (P->generation != seen)           /* a job this worker sits out */
+                seen = P->generation;
+            pthread_cond_wait(&P->go, &P->mu);
         }
-        seen = generation;
-        gss_task_fn fn = job_fn;
-        void *a = job_arg;
-        const int np = job_nparts;
-        pthread_mutex_unlock(&mu);
-        take_parts(fn, a, np);
-        pthread_mutex_lock(&mu);
-        if (--active == 0)
-            pthread_cond_signal(&done);
+        seen = P->generation;
+        gss_task_fn fn = P->job_fn;
+        void *a = P->job_arg;
+        const int np = P->job_nparts;
+        pthread_mutex_unlock(&P->mu);
+        take_parts(P, fn, a, np);
+        pthread_mutex_lock(&P->mu);
+        if (--P->active == 0)
+            pthread_cond_signal(&P->done);
     }
     return NULL;
 }
@@ -73,34 +98,42 @@ int gss_pool_run(int nthreads, int nparts, gss_task_fn fn, void *arg)
             fn(arg, p);
         return 0;
     }
-    pthread_mutex_lock(&run_mu);
-    pthread_mutex_lock(&mu);
-    while (n_workers < nthreads - 1) {        /* grow the pool on first use */
+    pool_t *P = &pools[tl_pool];
+    pthread_mutex_lock(&P->run_mu);
+    pthread_mutex_lock(&P->mu);
+    while (P->n_workers < nthreads - 1) {        /* grow the pool on first use */
         pthread_t t;
         pthread_attr_t at;
+        worker_arg *wa = malloc(sizeof *wa);
+        if (wa == NULL)
+            break;
+        wa->p = P;
+        wa->id = P->n_workers;
         pthread_attr_init(&at);
         pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
-        const int ok = pthread_create(&t, &at, worker, (void *)(intptr_t)n_workers) == 0;
+        const int ok = pthread_create(&t, &at, worker, wa) == 0;
         pthread_attr_destroy(&at);
-        if (!ok)
+        if (!ok) {
+            free(wa);
             break;
-        n_workers++;
+        }
+        P->n_workers++;
     }
-    const int w = nthreads - 1 < n_workers ? nthreads - 1 : n_workers;
-    job_fn = fn;
-    job_arg = arg;
-    job_nparts = nparts;
-    job_workers = w;
-    active = w;
-    __atomic_store_n(&next_part, 0, __ATOMIC_RELAXED);
-    generation++;
-    pthread_cond_broadcast(&go);
-    pthread_mutex_unlock(&mu);
-    take_parts(fn, arg, nparts);              /* the caller works too */
-    pthread_mutex_lock(&mu);
-    while (active > 0)
-        pthread_cond_wait(&done, &mu);
-    pthread_mutex_unlock(&mu);
-    pthread_mutex_unlock(&run_mu);
+    const int w = nthreads - 1 < P->n_workers ? nthreads - 1 : P->n_workers;
+    P->job_fn = fn;
+    P->job_arg = arg;
+    P->job_nparts = nparts;
+    P->job_workers = w;
+    P->active = w;
+    __atomic_store_n(&P->next_part, 0, __ATOMIC_RELAXED);
+    P->generation++;
+    pthread_cond_broadcast(&P->go);
+    pthread_mutex_unlock(&P->mu);
+    take_parts(P, fn, arg, nparts);              /* the caller works too */
+    pthread_mutex_lock(&P->mu);
+    while (P->active > 0)
+        pthread_cond_wait(&P->done, &P->mu);
+    pthread_mutex_unlock(&P->mu);
+    pthread_mutex_unlock(&P->run_mu);
     return 0;
 }

@@ -429,12 +429,43 @@ def test_spec_walks_on_device(dev):
         assert hit >= 0.95 * int(nch.sum()), (kw, hit)
 
 
-@pytest.mark.parametrize("spec", ["0", "1"])
-def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec):
+def test_streaming_run_sink_error_stops_cleanly(dev, golden):
+    """A sink that raises mid-run stops gss_run (planner, rows thread and GPU streams wound down),
+    the exception reaches the caller, and the next run on the same device is exact again."""
+    g = golden["static_d65_b8_noiono"]
+    args = ["-e", NAV, "-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8", "-i"]
+    calls = []
+
+    def bad(buf, first, nb):
+        calls.append(first)
+        if len(calls) == 3:
+            raise KeyError("stop")
+
+    s, _ = G.Scenario.from_cli(args)
+    with pytest.raises(KeyError):
+        dev.run(s, bad, batch=16, threads=4)
+    assert calls == [0, 16, 32]
+    blocks = []
+    bb = G.block_bytes(s.n_per_blk, 8)
+
+    def sink(buf, first, nb):
+        for i in range(nb):
+            blocks.append(hashlib.sha256(buf[i * bb:(i + 1) * bb]).hexdigest()[:16])
+
+    s, _ = G.Scenario.from_cli(args)
+    dev.run(s, sink, batch=40, threads=4)
+    assert blocks == g["block_sha16"]
+
+
+@pytest.mark.parametrize("spec,ahead,batch", [("0", "1", 57), ("1", "0", 57), ("1", "1", 57),
+                                               ("1", "1", 1)])
+def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec, ahead, batch):
     """gss_run with the carrier chain walked on the host (GSS_RUN_SPEC=0) and run ahead on the
-    GPU (the default): a 65 s run across two 30 s updates, whole and from a mid-run block, against
-    the reference's golden hashes."""
+    GPU (the default), with the rows produced on the planner thread (GSS_RUN_ROWS_AHEAD=0) or
+    ahead on their own (the default; one-block batches too): a 65 s run across two 30 s updates,
+    whole and from a mid-run block, against the reference's golden hashes."""
     monkeypatch.setenv("GSS_RUN_SPEC", spec)
+    monkeypatch.setenv("GSS_RUN_ROWS_AHEAD", ahead)
     g = golden["static_d65_b8_noiono"]
     bb = None
     blocks = []
@@ -446,11 +477,11 @@ def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec):
     s, _ = G.Scenario.from_cli(["-e", NAV, "-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8",
                                 "-i"])
     bb = G.block_bytes(s.n_per_blk, 8)
-    dev.run(s, sink, batch=57, threads=4)
+    dev.run(s, sink, batch=batch, threads=4)
     assert [x for _, x in blocks] == g["block_sha16"]
     blocks.clear()
     s, _ = G.Scenario.from_cli(["-e", NAV, "-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8",
                                 "-i"])
-    dev.run(s, sink, first_block=333, n_blocks=150, batch=64)
+    dev.run(s, sink, first_block=333, n_blocks=150, batch=64 if batch > 1 else 1)
     assert [b for b, _ in blocks] == list(range(333, 483))
     assert [x for _, x in blocks] == g["block_sha16"][333:483]
