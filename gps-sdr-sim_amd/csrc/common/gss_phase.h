@@ -1123,6 +1123,49 @@ GSS_HD double gss_walk_margins(double x, double s, int64_t n, double *dlo, doubl
     return x;
 }
 
+/* The line of a slot predicts where a block's walk wraps: ascending, wrap q at step
+   ceil((q - g)/s) with post-wrap value g + p s - q; descending, wrap q at step
+   floor((g + q - 1)/|s|) + 1 with value g + p s + q.  Segment starts: GSS_SPEC_K - 1 wraps spread
+   over the block's wraps after its first (gss_carr_chain_guess on the host, or the walkers
+   themselves for rows left with k = 0).  Doubles suffice (errors ~1e-13 against translation
+   intervals ~1e-8; guesses only: any mismatch is caught by the fix-up). */
+GSS_HD void gss_spec_guess_row(double g, double s, int64_t n, gss_spec_in_t *in)
+{
+    const double g0 = g;
+    in->g = g0;
+    in->s = s;
+    in->k = 1;
+    in->pad = 0;
+    if (s == 0.0)
+        return;
+    const double as = s > 0.0 ? s : -s;
+    const double e = g0 + (double)n * s;                 /* the line at the block end */
+    const double mw = s > 0.0 ? floor(e) : floor(1.0 - e);   /* wraps in the block */
+    if (!(mw >= 2.0))
+        return;
+    const int64_t m = mw > 1e9 ? (int64_t)1e9 : (int64_t)mw;
+    const int64_t kk = m < GSS_SPEC_K ? m : GSS_SPEC_K;
+    const double unit = s > 0.0 ? 0x1p-52 : 0x1p-53;
+    int k = 1;
+    int64_t prev = 0;
+    for (int64_t j = 1; j < kk; j++) {
+        const int64_t q = 1 + (j * (m - 1) + kk - 1) / kk;          /* wrap index, >= 2 */
+        const int64_t p = s > 0.0 ? (int64_t)ceil(((double)q - g0) / as)
+                                  : (int64_t)floor((g0 + (double)q - 1.0) / as) + 1;
+        if (p <= prev || p >= n)
+            break;
+        const double v = (g0 + (double)p * s) + (s > 0.0 ? -(double)q : (double)q);
+        const double w = rint(v / unit) * unit;
+        if (!(w >= 0.0 && w < 1.0))
+            break;
+        in->P[k] = p;
+        in->W[k] = w;
+        prev = p;
+        k++;
+    }
+    in->k = k;
+}
+
 /* Segment j of a row's walk (n samples per block). */
 GSS_HD void gss_spec_seg_walk(const gss_spec_in_t *in, int j, int64_t n, gss_spec_t *o)
 {

@@ -84,7 +84,7 @@ extern "C" int gss_nav_rows_device(gss_dev *d, const gss_nav_src_t *src, int fir
    channel-major, so that a wave's lanes walk the segments of consecutive blocks of one channel:
    close steps, nearly the same cycles and binades (uniform control flow) instead of 16 different
    Dopplers per wave. */
-__global__ void gss_spec_kernel(const gss_spec_in_t *__restrict__ in, int nrow, int n,
+__global__ void gss_spec_kernel(gss_spec_in_t *__restrict__ in, int nrow, int n,
                                 gss_spec_t *__restrict__ spec)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -93,12 +93,25 @@ __global__ void gss_spec_kernel(const gss_spec_in_t *__restrict__ in, int nrow, 
     const int u = t / GSS_SPEC_K, j = t % GSS_SPEC_K;
     const int nb = nrow / GSS_MAXCH;
     const int i = nrow % GSS_MAXCH ? u : (u % nb) * GSS_MAXCH + u / nb;
-    if (j >= in[i].k)
+    gss_spec_in_t row = in[i];
+    if (row.k == 0) {
+        /* segment starts not guessed yet (gss_carr_chain_starts): every lane of the row makes
+           the same guesses; its first lane writes them back for the host's chain */
+        gss_spec_guess_row(row.g, row.s, n, &row);
+        if (j == 0) {
+            in[i].k = row.k;
+            for (int q = 1; q < GSS_SPEC_K; q++) {
+                in[i].P[q] = row.P[q];
+                in[i].W[q] = row.W[q];
+            }
+        }
+    }
+    if (j >= row.k)
         return;
-    gss_spec_seg_walk(&in[i], j, n, &spec[i]);
+    gss_spec_seg_walk(&row, j, n, &spec[i]);
 }
 
-extern "C" int gss_spec_device(gss_dev *d, const gss_spec_in_t *in, int nrow, int n_per_blk,
+extern "C" int gss_spec_device(gss_dev *d, gss_spec_in_t *in, int nrow, int n_per_blk,
                                gss_spec_t *spec, void *stream)
 {
     if (!d || nrow < 0 || n_per_blk <= 0 || (nrow > 0 && (!in || !spec)))

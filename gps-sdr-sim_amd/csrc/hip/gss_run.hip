@@ -267,7 +267,7 @@ int chain_upfront_spec(Run &r, double *carr, const gss_chain_t *chain)
         gss_chan_blk_t *blk = &r.pre_blk[(size_t)b0 * GSS_MAXCH];
         const int32_t *nch = &r.pre_nch[(size_t)b0];
         const gss_chain_t *ch = chain + (size_t)b0 * GSS_MAXCH;
-        rc = gss_carr_chain_guess(carr, blk, nch, ch, nb, r.n_per_blk, h_in);
+        rc = gss_carr_chain_starts(carr, blk, nch, ch, nb, r.n_per_blk, h_in);
         if (rc) break;
         if ((rc = gss_spec_device(r.dev, h_in, nrow, r.n_per_blk, h_spec, r.spec_st)) != 0 ||
             hipStreamSynchronize(r.spec_st) != hipSuccess) {
@@ -516,8 +516,8 @@ int spec_launch(Run &r, Run::SpecBatch &b, int ask)
     b.nb = nb;
     const int nrow = nb * GSS_MAXCH;
     b.tg = trace_on() ? tnow() : 0.0;
-    rc = gss_carr_chain_guess(b.carr, b.blk.data(), b.nch.data(), b.chain.data(), nb, r.n_per_blk,
-                              b.h_in);
+    rc = gss_carr_chain_starts(b.carr, b.blk.data(), b.nch.data(), b.chain.data(), nb,
+                               r.n_per_blk, b.h_in);           /* the walkers guess the rest */
     if (rc)
         return rc;
     /* the lanes read their rows from, and write their walks to, the pinned host buffers
@@ -1030,7 +1030,7 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         /* the walks' first launch costs ~1 ms (the kernel's first use): here, on one zero row,
            while the planner produces its first rows, instead of inside its first batch */
         (void)hipMemsetAsync(r.spec_warm, 0, 1024, r.spec_st);
-        (void)gss_spec_device(d, (const gss_spec_in_t *)r.spec_warm, 1, info.n_per_blk,
+        (void)gss_spec_device(d, (gss_spec_in_t *)r.spec_warm, 1, info.n_per_blk,
                               (gss_spec_t *)((uint8_t *)r.spec_warm + 256), r.spec_st);
 
     }

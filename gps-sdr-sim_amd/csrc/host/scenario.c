@@ -480,48 +480,6 @@ int gss_carr_chain(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
 }
 
 /* ---- the chain with the block walks run ahead (gss_phase.h, speculative block walk) ---------- */
-/* The line of a slot predicts where a block's walk wraps: ascending, wrap q at step
-   ceil((q - g)/s) with post-wrap value g + p s - q; descending, wrap q at step
-   floor((g + q - 1)/|s|) + 1 with value g + p s + q.  Segment starts: GSS_SPEC_K - 1 wraps spread
-   over the block's wraps after its first.  Doubles suffice (errors ~1e-13 against translation
-   intervals ~1e-8; guesses only: any mismatch is caught by the fix-up). */
-static void spec_guess_row(double g, double s, int n, gss_spec_in_t *in)
-{
-    const double g0 = g;
-    in->g = g0;
-    in->s = s;
-    in->k = 1;
-    in->pad = 0;
-    if (s == 0.0)
-        return;
-    const double as = s > 0.0 ? s : -s;
-    const double e = g0 + (double)n * s;                 /* the line at the block end */
-    const double mw = s > 0.0 ? floor(e) : floor(1.0 - e);   /* wraps in the block */
-    if (!(mw >= 2.0))
-        return;
-    const int64_t m = mw > 1e9 ? (int64_t)1e9 : (int64_t)mw;
-    const int64_t kk = m < GSS_SPEC_K ? m : GSS_SPEC_K;
-    const double unit = s > 0.0 ? 0x1p-52 : 0x1p-53;
-    int k = 1;
-    int64_t prev = 0;
-    for (int64_t j = 1; j < kk; j++) {
-        const int64_t q = 1 + (j * (m - 1) + kk - 1) / kk;          /* wrap index, >= 2 */
-        const int64_t p = s > 0.0 ? (int64_t)ceil(((double)q - g0) / as)
-                                  : (int64_t)floor((g0 + (double)q - 1.0) / as) + 1;
-        if (p <= prev || p >= n)
-            break;
-        const double v = (g0 + (double)p * s) + (s > 0.0 ? -(double)q : (double)q);
-        const double w = rint(v / unit) * unit;
-        if (!(w >= 0.0 && w < 1.0))
-            break;
-        in->P[k] = p;
-        in->W[k] = w;
-        prev = p;
-        k++;
-    }
-    in->k = k;
-}
-
 typedef struct {
     const gss_chan_blk_t *blk;
     int n_per_blk;
@@ -533,19 +491,17 @@ static void guess_part(void *arg, int b)
     const guess_job *j = arg;
     for (int k = 0; k < GSS_MAXCH; k++) {
         gss_spec_in_t *r = &j->in[(size_t)b * GSS_MAXCH + k];
-        if (r->s != 0.0)
-            spec_guess_row(r->g, r->s, j->n_per_blk, r);
+        if (r->k == 0)
+            gss_spec_guess_row(r->g, r->s, j->n_per_blk, r);
     }
 }
 
-int gss_carr_chain_guess(const double *carr, const gss_chan_blk_t *blk, const int32_t *nch,
+/* the starts, serially: the line of each slot from its exact start (in double: the drift over a
+   batch, ~1e-13 per block, stays far inside the translation intervals); k = 0 on live rows (their
+   segment starts not guessed yet), 1 on padding rows */
+static void chain_starts(const double *carr, const gss_chan_blk_t *blk, const int32_t *nch,
                          const gss_chain_t *chain, int nblk, int n_per_blk, gss_spec_in_t *in)
 {
-    if (carr == NULL || in == NULL || nblk < 0 || n_per_blk <= 0 ||
-        (nblk > 0 && (blk == NULL || nch == NULL || chain == NULL)))
-        return gss_fail(GSS_E_ARG, "invalid carrier-guess arguments");
-    /* the starts, serially: the line of each slot from its exact start (in double: the drift
-       over a batch, ~1e-13 per block, stays far inside the translation intervals) */
     double run[K_MAX_CHAN];
     for (int i = 0; i < K_MAX_CHAN; i++)
         run[i] = carr[i];
@@ -563,9 +519,29 @@ int gss_carr_chain_guess(const double *carr, const gss_chan_blk_t *blk, const in
             const double g = run[slot];
             in[e].g = g >= 0.0 && g < 1.0 ? g : 0.0;
             in[e].s = blk[e].carr_step;
+            in[e].k = 0;
             const double v = g + (double)n_per_blk * blk[e].carr_step;
             run[slot] = v - floor(v);
         }
+}
+
+int gss_carr_chain_starts(const double *carr, const gss_chan_blk_t *blk, const int32_t *nch,
+                          const gss_chain_t *chain, int nblk, int n_per_blk, gss_spec_in_t *in)
+{
+    if (carr == NULL || in == NULL || nblk < 0 || n_per_blk <= 0 ||
+        (nblk > 0 && (blk == NULL || nch == NULL || chain == NULL)))
+        return gss_fail(GSS_E_ARG, "invalid carrier-guess arguments");
+    chain_starts(carr, blk, nch, chain, nblk, n_per_blk, in);
+    return 0;
+}
+
+int gss_carr_chain_guess(const double *carr, const gss_chan_blk_t *blk, const int32_t *nch,
+                         const gss_chain_t *chain, int nblk, int n_per_blk, gss_spec_in_t *in)
+{
+    if (carr == NULL || in == NULL || nblk < 0 || n_per_blk <= 0 ||
+        (nblk > 0 && (blk == NULL || nch == NULL || chain == NULL)))
+        return gss_fail(GSS_E_ARG, "invalid carrier-guess arguments");
+    chain_starts(carr, blk, nch, chain, nblk, n_per_blk, in);
     /* the segment starts, in parallel over blocks */
     const guess_job j = {blk, n_per_blk, in};
     gss_pool_run(8, nblk, guess_part, (void *)&j);
@@ -573,7 +549,7 @@ int gss_carr_chain_guess(const double *carr, const gss_chan_blk_t *blk, const in
 }
 
 typedef struct {
-    const gss_spec_in_t *in;
+    gss_spec_in_t *in;
     int nrow, n_per_blk;
     gss_spec_t *spec;
 } spec_host_job;
@@ -581,13 +557,15 @@ typedef struct {
 static void spec_host_part(void *arg, int part)
 {
     const spec_host_job *j = arg;
-    for (int i = part * 16; i < j->nrow && i < part * 16 + 16; i++)
+    for (int i = part * 16; i < j->nrow && i < part * 16 + 16; i++) {
+        if (j->in[i].k == 0)                     /* segment starts not guessed yet */
+            gss_spec_guess_row(j->in[i].g, j->in[i].s, j->n_per_blk, &j->in[i]);
         for (int g = 0; g < j->in[i].k && g < GSS_SPEC_K; g++)
             gss_spec_seg_walk(&j->in[i], g, j->n_per_blk, &j->spec[i]);
+    }
 }
 
-int gss_spec_host(const gss_spec_in_t *in, int nrow, int n_per_blk, gss_spec_t *spec,
-                  int threads)
+int gss_spec_host(gss_spec_in_t *in, int nrow, int n_per_blk, gss_spec_t *spec, int threads)
 {
     if (nrow < 0 || n_per_blk <= 0 || (nrow > 0 && (in == NULL || spec == NULL)))
         return gss_fail(GSS_E_ARG, "invalid speculative-walk arguments");

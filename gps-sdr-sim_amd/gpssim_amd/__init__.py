@@ -134,6 +134,7 @@ _SIGS = {
     "gss_scn_next_deferred": (C.c_int, [_P, C.c_int, _P, _P, _P, C.POINTER(C.c_int), C.c_int]),
     "gss_carr_chain": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int]),
     "gss_carr_chain_guess": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P]),
+    "gss_carr_chain_starts": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P]),
     "gss_spec_host": (C.c_int, [_P, C.c_int, C.c_int, _P, C.c_int]),
     "gss_spec_device": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, _P]),
     "gss_carr_chain_spec": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P, C.c_int,
@@ -457,19 +458,22 @@ def carr_chain(carr, blk, nch, chain, n_per_blk, carrier_int=False, with_ck=True
     return c, ck
 
 
-def carr_chain_guess(carr, blk, nch, chain, n_per_blk):
-    """Each row's guesses (gss_carr_chain_guess): SPEC_IN_DTYPE [nb, 16]."""
+def carr_chain_guess(carr, blk, nch, chain, n_per_blk, starts_only=False):
+    """Each row's guesses (gss_carr_chain_guess): SPEC_IN_DTYPE [nb, 16].  starts_only: the
+    starts alone (gss_carr_chain_starts), live rows with k = 0 for the walkers to complete."""
     c = np.ascontiguousarray(carr, np.float64)
     nch = np.ascontiguousarray(nch, np.int32)
     chain = np.ascontiguousarray(chain, CHAIN_DTYPE)
     gi = np.zeros((len(nch), MAXCH), SPEC_IN_DTYPE)
-    _check(lib().gss_carr_chain_guess(_ptr(c), _ptr(np.ascontiguousarray(blk)), _ptr(nch),
-                                      _ptr(chain), len(nch), int(n_per_blk), _ptr(gi)))
+    fn = lib().gss_carr_chain_starts if starts_only else lib().gss_carr_chain_guess
+    _check(fn(_ptr(c), _ptr(np.ascontiguousarray(blk)), _ptr(nch), _ptr(chain), len(nch),
+              int(n_per_blk), _ptr(gi)))
     return gi
 
 
 def spec_host(gi, n_per_blk, threads=8):
-    """The speculative walk of every row's segments (gss_spec_host): SPEC_DTYPE rows."""
+    """The speculative walk of every row's segments (gss_spec_host): SPEC_DTYPE rows.  Rows with
+    k = 0 get their segment guesses first, written back into gi (a contiguous array)."""
     gi = np.ascontiguousarray(gi, SPEC_IN_DTYPE).reshape(-1)
     spec = np.zeros(len(gi), SPEC_DTYPE)
     _check(lib().gss_spec_host(_ptr(gi), len(gi), int(n_per_blk), _ptr(spec), threads))

@@ -286,9 +286,11 @@ int gss_carr_chain(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
      gss_carr_chain_guess  each row's guesses: its start from the line of its slot (exact at the
                            slot's first block and at a reset) and up to GSS_SPEC_K - 1 segment
                            starts at wraps the line predicts, in[nblk][GSS_MAXCH] (padding: s 0)
+     gss_carr_chain_starts the starts only, live rows left with k = 0: the walkers guess their
+                           segment starts themselves and write them back into in[] (gss_run)
      gss_spec_host/device  the speculative walk of every row's segments: spec[nrow]; host
-                           threads, or the GPU (device pointers, async on stream; gss_run; one
-                           lane per segment, rows channel-major for a multiple of GSS_MAXCH)
+                           threads, or the GPU (device-visible pointers, async on stream; gss_run;
+                           one lane per segment, rows channel-major for a multiple of GSS_MAXCH)
      gss_carr_chain_spec   the chain: as gss_carr_chain without checkpoints, each block's end from
                            its true start and its speculative walk (exact whether or not the
                            translation applies); *n_hit counts the blocks where it did.        */
@@ -297,7 +299,7 @@ int gss_carr_chain(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
 #define GSS_SPEC_K 8                   /* segments per block */
 typedef struct gss_spec_in {           /* a row's guesses (host, gss_carr_chain_guess)          */
     double g, s;                       /* start guess, carr_step (0: padding row)               */
-    int32_t k, pad;                    /* segments (1..GSS_SPEC_K)                              */
+    int32_t k, pad;                    /* segments (1..GSS_SPEC_K; 0: not guessed yet)          */
     int64_t P[GSS_SPEC_K];             /* segment j >= 1 starts at sample P[j], a predicted wrap */
     double W[GSS_SPEC_K];              /* ... with post-wrap value W[j]                         */
 } gss_spec_in_t;                       /* 152 bytes */
@@ -313,10 +315,11 @@ typedef struct gss_spec {              /* a row's speculative walk (GPU or host)
 #endif
 int gss_carr_chain_guess(const double *carr, const gss_chan_blk_t *blk, const int32_t *nch,
                          const gss_chain_t *chain, int nblk, int n_per_blk, gss_spec_in_t *in);
-int gss_spec_host(const gss_spec_in_t *in, int nrow, int n_per_blk, gss_spec_t *spec,
-                  int threads);
-int gss_spec_device(gss_dev *d, const gss_spec_in_t *in, int nrow, int n_per_blk,
-                    gss_spec_t *spec, void *stream);
+int gss_carr_chain_starts(const double *carr, const gss_chan_blk_t *blk, const int32_t *nch,
+                          const gss_chain_t *chain, int nblk, int n_per_blk, gss_spec_in_t *in);
+int gss_spec_host(gss_spec_in_t *in, int nrow, int n_per_blk, gss_spec_t *spec, int threads);
+int gss_spec_device(gss_dev *d, gss_spec_in_t *in, int nrow, int n_per_blk, gss_spec_t *spec,
+                    void *stream);
 int gss_carr_chain_spec(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
                         const gss_chain_t *chain, int nblk, int n_per_blk,
                         const gss_spec_in_t *in, const gss_spec_t *spec, int threads,

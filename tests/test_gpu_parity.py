@@ -427,6 +427,19 @@ def test_spec_walks_on_device(dev):
         end, hit = G.carr_chain_spec(carr, blk, nch, chain, n, gi, got)
         assert np.array_equal(blk["carr0"], ref["carr0"]) and np.array_equal(end, end_ref), kw
         assert hit >= 0.95 * int(nch.sum()), (kw, hit)
+        # the starts alone (gss_run's path): the lanes guess the segment starts, write them back
+        # bit-equal to the host's guesses, and walk the same segments
+        g0 = G.carr_chain_guess(carr, blk, nch, chain, n, starts_only=True)
+        d_in = torch.from_numpy(g0.reshape(-1).view(np.uint8).copy()).cuda()
+        d_spec.zero_()
+        dev.spec_device(d_in.data_ptr(), len(want), n, d_spec.data_ptr())
+        torch.cuda.synchronize()
+        assert d_in.cpu().numpy().tobytes() == gi.reshape(-1).tobytes(), kw
+        got2 = d_spec.cpu().numpy().view(G.SPEC_DTYPE)
+        assert np.array_equal(got2["p1"][live], got["p1"][live]), kw
+        for r in np.flatnonzero(live):
+            k = gi.reshape(-1)["k"][r]
+            assert got2["seg"][r][:k].tobytes() == got["seg"][r][:k].tobytes(), (kw, r)
 
 
 def test_streaming_run_sink_error_stops_cleanly(dev, golden):

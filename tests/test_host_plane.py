@@ -109,13 +109,17 @@ def test_nav_table_rows():
             assert pre in (0x8B, 0x74)
 
 
-@pytest.mark.parametrize("kind,threads", [("static", 8), ("circle", 3), ("intcarr", 4)])
-def test_speculative_chain_equals_exact_chain(kind, threads):
+@pytest.mark.parametrize("kind,threads,starts_only", [("static", 8, False), ("circle", 3, False),
+                                                     ("intcarr", 4, False), ("static", 8, True),
+                                                     ("circle", 3, True)])
+def test_speculative_chain_equals_exact_chain(kind, threads, starts_only):
     """The planner's carrier chain with every block's walk run ahead from a guessed start
     (gss_carr_chain_guess -> gss_spec_host -> gss_carr_chain_spec, the path gss_run takes with
     the walks on the GPU) gives the same carr0 of every row and the same end carriers as the
     exact chain (gss_carr_chain), over several batches across 30 s updates and re-allocations,
-    and nearly every block takes the translation (one partial cycle on the serial path)."""
+    and nearly every block takes the translation (one partial cycle on the serial path).
+    starts_only: the starts alone (gss_carr_chain_starts, as gss_run), the walker guessing each
+    row's segment starts and writing back exactly the host's guesses."""
     if kind == "static":
         s = G.Scenario(NAV, llh=LOC, duration=400.0)
     elif kind == "circle":
@@ -132,8 +136,13 @@ def test_speculative_chain_equals_exact_chain(kind, threads):
         ref = blk.copy()
         end_ref, _ = G.carr_chain(carr, ref, nch, chain, n, carrier_int=s.carrier_int,
                                   with_ck=False, threads=threads)
-        gi = G.carr_chain_guess(carr, blk, nch, chain, n)
+        gi = G.carr_chain_guess(carr, blk, nch, chain, n, starts_only=starts_only)
+        full = G.carr_chain_guess(carr, blk, nch, chain, n)
+        assert np.array_equal(gi["g"], full["g"]) and np.array_equal(gi["s"], full["s"])
+        if starts_only:
+            assert (gi["k"][gi["s"] != 0] == 0).all()
         spec = G.spec_host(gi, n, threads=threads)
+        assert gi.tobytes() == full.tobytes(), kind          # the walker's guesses = the host's
         end, h = G.carr_chain_spec(carr, blk, nch, chain, n, gi, spec, threads=threads)
         assert np.array_equal(blk["carr0"], ref["carr0"]), kind
         assert np.array_equal(end, end_ref), kind
