@@ -89,24 +89,30 @@ u128 gss_maxmod(u128 n, u128 m, u128 a, u128 s)
 }
 
 /* ---- exact first hit ------------------------------------------------------------------------- */
-/* Smallest x >= 0 with lo <= (s x) mod m <= hi, for 1 <= lo <= hi < m < 2^62 and s < m; UINT64_MAX if
- * there is none below 2^64.  If s x reaches [lo, hi] before its first wrap, that is x = ceil(lo/s).
- * Otherwise [lo, hi] holds no multiple of s (so hi - lo < s), and x exists for wrap count y iff some
- * multiple of s lies in [lo + m y, hi + m y], i.e. (m y) mod s lies in [s - hi mod s, s - lo mod s]:
- * the same question for (m mod s, s), Euclid's descent; x = ceil((lo + m y) / s) of the least y. */
-static uint64_t first_in(uint64_t s, uint64_t m, uint64_t lo, uint64_t hi)
+/* Smallest x in [0, lim] with lo <= (s x) mod m <= hi, for 1 <= lo <= hi < m < 2^62 and s < m;
+ * UINT64_MAX if there is none.  Every candidate is >= ceil(lo/s); if s x reaches [lo, hi] before
+ * its first wrap, that is x.  Otherwise [lo, hi] holds no multiple of s (so hi - lo < s), and x
+ * exists for wrap count y iff some multiple of s lies in [lo + m y, hi + m y], i.e. (m y) mod s
+ * lies in [s - hi mod s, s - lo mod s]: the same question for (m mod s, s), Euclid's descent, with
+ * x = ceil((lo + m y) / s) of the least y.  x <= lim needs y <= lim s / m: the descent stops as
+ * soon as that bound (an overestimate in double, so nothing is cut wrongly) is out of reach. */
+static uint64_t first_in(uint64_t s, uint64_t m, uint64_t lo, uint64_t hi, uint64_t lim)
 {
     if (s == 0)
         return UINT64_MAX;
     const uint64_t x = (lo + s - 1) / s;
+    if (x > lim)
+        return UINT64_MAX;
     if (s * x <= hi)                                 /* s x <= lo + s - 1 < 2^63 */
         return x;
     const uint64_t lr = lo % s, hr = hi % s;         /* 1 <= lr <= hr < s (no multiple inside) */
-    const uint64_t y = first_in(m % s, s, s - hr, s - lr);
+    const double yd = (double)lim * (double)s / (double)m + 2.0;
+    const uint64_t ylim = yd < 0x1p52 ? (uint64_t)yd : UINT64_MAX;
+    const uint64_t y = first_in(m % s, s, s - hr, s - lr, ylim);
     if (y == UINT64_MAX)
         return UINT64_MAX;
     const u128 v = ((u128)lo + (u128)m * y + s - 1) / s;
-    return v >> 64 ? UINT64_MAX : (uint64_t)v;
+    return v <= lim ? (uint64_t)v : UINT64_MAX;
 }
 
 /* Smallest p in [0, n) with (a + p s) mod m < w (0 <= a, s < m < 2^62, 0 < w <= m), or n. */
@@ -117,7 +123,7 @@ static uint64_t first_below(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint
     if (a < w)
         return 0;
     /* (a + p s) mod m < w  <=>  (s p) mod m in [m - a, m - a + w - 1], a range below m as a >= w */
-    const uint64_t p = first_in(s, m, m - a, m - a + w - 1);
+    const uint64_t p = first_in(s, m, m - a, m - a + w - 1, n - 1);
     return p < n ? p : n;
 }
 
