@@ -84,7 +84,7 @@ constexpr int DEPTH = GSS_RUN_DEPTH;                   /* slots submitted, not y
 constexpr int NSLOT = DEPTH + 2;
 constexpr size_t SLOT_OUT_MAX = (size_t)256 << 20;     /* pinned output bytes per slot */
 
-enum { FREE, PLANNED };
+enum { FREE, PROVING, PLANNED };                  /* PROVING: rows planned, proofs pending */
 
 /* The slots' output buffers (pinned host + device, ~133 MB each at the defaults) outlive a run:
    page-locking them costs tens of ms, so a later gss_run in the same process (a service, or a
@@ -141,6 +141,8 @@ struct Slot {
     int n_fb = 0;
     int nb = 0, nch_max = 1;
     int64_t first = 0;               /* run index of the slot's first block */
+    const uint32_t *lin_nav = nullptr;   /* the nav table its proofs read (prover thread)  */
+    int lin_n_nav = 0;
     int end = 0, err = 0;            /* last slot / planner error code      */
     int state = FREE;
     /* main side */
@@ -200,6 +202,8 @@ struct Run {
         double t0 = 0.0, t1 = 0.0;                           /* trace: production start, end */
     } rb[2];
     int rows_ahead = 0, rb_take = 0, rows_done = 0;
+    int prover = 0;                  /* proofs on their own thread (rows_ahead, fast path): the
+                                        planner hands slots over PROVING */
     double carr[GSS_MAXCH];          /* rows_ahead: the slot carriers at the planner's next batch */
     std::vector<gss_nav_src_t> nav_src_h;
     std::vector<uint32_t> nav_rows_h;
@@ -482,6 +486,19 @@ int take_rows(Run &r, Run::SpecBatch &b, int *nb_out)
     std::swap(b.blk, q.blk);
     std::swap(b.nch, q.nch);
     std::swap(b.chain, q.chain);
+    if (r.nav_rows_h.size() + q.nav_rows.size() > r.nav_rows_h.capacity()) {
+        /* beyond the reservation (not expected): the prover reads the table, so grow it only
+           with no slot in its hands */
+        std::unique_lock<std::mutex> lk(r.mu);
+        r.cv.wait(lk, [&] {
+            for (const Slot &x : r.slot)
+                if (x.state == PROVING)
+                    return r.abort != 0;
+            return true;
+        });
+        if (r.abort)
+            return gss_fail(GSS_E_STATE, "run aborted");
+    }
     r.nav_src_h.insert(r.nav_src_h.end(), q.nav_src.begin(), q.nav_src.end());
     r.nav_rows_h.insert(r.nav_rows_h.end(), q.nav_rows.begin(), q.nav_rows.end());
     *nb_out = q.nb;
@@ -665,6 +682,11 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
         rc = take_nav_sources(r, sl, n_rows);          /* the GPU builds the new rows */
         if (rc)
             return rc;
+        if (r.prover) {                                /* the proofs, on the prover thread */
+            sl.lin_nav = rows;
+            sl.lin_n_nav = n_rows;
+            return 0;
+        }
         if (r.use_lin) {                               /* the proofs, on the planner thread */
             if (trace_on())
                 fprintf(stderr, "trace scn_done %.6f\n", tnow());
@@ -705,10 +727,52 @@ void planner(Run *r)
                 sl.err = rc;
                 sl.end = 1;
             }
-            sl.state = PLANNED;
+            sl.state = r->prover ? PROVING : PLANNED;
         }
         r->cv.notify_all();
         if (sl.end)
+            return;
+    }
+}
+
+/* The slots' proofs in slot order (r.prover): gss_linearize on this thread's own worker pool,
+   the exact-path block list and its checkpoints, then the slot goes to the main thread. */
+void prover(Run *r)
+{
+    gss_pool_select(2);
+    for (int i = 0;; i++) {
+        Slot &sl = r->slot[i % NSLOT];
+        {
+            std::unique_lock<std::mutex> lk(r->mu);
+            r->cv.wait(lk, [&] { return r->abort || sl.state == PROVING; });
+            if (r->abort)
+                return;
+        }
+        const double t0 = trace_on() ? tnow() : 0.0;
+        if (!sl.end && !sl.err) {
+            int rc = gss_linearize(sl.blk, sl.nch, sl.nb, r->n_per_blk, r->ca, 32, sl.lin_nav,
+                                   sl.lin_n_nav, sl.lin, sl.fast, r->threads);
+            if (rc) {
+                sl.err = rc;
+                sl.end = 1;
+            } else {
+                int nf = 0;
+                for (int b = 0; b < sl.nb; b++)
+                    if (!sl.fast[b])
+                        sl.fast[sl.nb + nf++] = b;
+                sl.n_fb = nf;
+                fill_fb_ck(*r, sl);
+            }
+        }
+        if (trace_on())
+            fprintf(stderr, "trace prove slot %d nb %d %.6f %.6f\n", i % NSLOT, sl.nb, t0, tnow());
+        const int end = sl.end;
+        {
+            std::lock_guard<std::mutex> lk(r->mu);
+            sl.state = PLANNED;
+        }
+        r->cv.notify_all();
+        if (end)
             return;
     }
 }
@@ -1004,7 +1068,16 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             if (e && e[0] == '0')
                 r.rows_ahead = 0;
         }
+        r.prover = r.rows_ahead && r.use_lin;
+        {
+            const char *e = getenv("GSS_RUN_PROVER");
+            if (e && e[0] == '0')
+                r.prover = 0;
+        }
         if (!err && r.rows_ahead) {
+            /* the nav table's host copy never moves while the prover reads it: room for the
+               allocation's rows and up to GSS_MAXCH new rows per 30 s update */
+            r.nav_rows_h.reserve(((size_t)info.n_blocks / 300 + 4) * GSS_MAXCH * GSS_NAV_WORDS);
             for (Run::RowBatch &q : r.rb) {
                 q.blk.resize(nb * GSS_MAXCH);
                 q.nch.resize(nb);
@@ -1023,9 +1096,11 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         (void)hipSetDevice(ordinal);                   /* pinned reallocations */
         planner(&r);
     });
-    std::thread th_rows;
+    std::thread th_rows, th_prove;
     if (r.rows_ahead)
         th_rows = std::thread(rows_thread, &r);
+    if (r.prover)
+        th_prove = std::thread(prover, &r);
     if (r.spec) {
         /* the walks' first launch costs ~1 ms (the kernel's first use): here, on one zero row,
            while the planner produces its first rows, instead of inside its first batch */
@@ -1043,6 +1118,8 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
     th.join();
     if (th_rows.joinable())
         th_rows.join();
+    if (th_prove.joinable())
+        th_prove.join();
     if (r.rows_ahead && !err)                          /* the scenario's carriers: run's end */
         err = gss_scn_set_carrier(s, r.carr);
     cleanup();

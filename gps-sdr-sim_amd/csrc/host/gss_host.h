@@ -138,7 +138,7 @@ int    motion_read_nmea(double (*xyz)[3], int cap, const char *fname);
 /* ---- pool.c ------------------------------------------------------------------------------- */
 typedef void (*gss_task_fn)(void *arg, int part);
 int    gss_pool_run(int nthreads, int nparts, gss_task_fn fn, void *arg);
-void   gss_pool_select(int id);     /* this thread's pool: 0 default, 1 gss_run's rows thread */
+void   gss_pool_select(int id);     /* this thread's pool: 0 default; 1, 2 gss_run's rows, proofs */
 
 /* ---- errors ------------------------------------------------------------------------------- */
 int    gss_fail(int code, const char *fmt, ...);

@@ -6,8 +6,8 @@
  * of a 16-block batch at 20 MS/s.  gss_pool_run(nthreads, nparts, fn, arg) runs fn(arg, part)
  * for part = 0 .. nparts-1 on the caller plus up to nthreads-1 pooled workers, which take parts
  * dynamically (an atomic counter), so uneven parts balance themselves.  One job at a time per
- * pool: a second caller waits for the first job to finish (jobs never nest).  Two pools, chosen
- * per calling thread (gss_pool_select): gss_run's rows thread has its own.
+ * pool: a second caller waits for the first job to finish (jobs never nest).  Three pools, chosen
+ * per calling thread (gss_pool_select): gss_run's rows and proof threads have their own.
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -15,7 +15,7 @@
 #include "gss_host.h"
 
 #define POOL_MAX 64
-#define POOL_N 2                         /* pool 0: the default; 1: gss_run's rows thread  */
+#define POOL_N 3                         /* 0: the default; 1, 2: gss_run's rows, proofs */
 
 typedef struct {
     pthread_mutex_t run_mu;              /* one job at a time */
@@ -33,12 +33,12 @@ typedef struct {
 
 #define POOL_INIT {PTHREAD_MUTEX_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, \
                    PTHREAD_COND_INITIALIZER, 0, 0, 0, 0, NULL, NULL, 0, 0}
-static pool_t pools[POOL_N] = {POOL_INIT, POOL_INIT};
+static pool_t pools[POOL_N] = {POOL_INIT, POOL_INIT, POOL_INIT};
 static __thread int tl_pool;             /* the calling thread's pool (gss_pool_select) */
 
-/* Route this thread's gss_pool_run jobs to pool id (0 default): gss_run's rows thread takes its
-   own workers, so that its range passes run beside the planner's chain and proofs instead of
-   queueing behind them. */
+/* Route this thread's gss_pool_run jobs to pool id (0 default): gss_run's rows and proof threads
+   take their own workers, so that their range passes and proofs run beside the planner's chain
+   instead of queueing behind it. */
 void gss_pool_select(int id)
 {
     tl_pool = id >= 0 && id < POOL_N ? id : 0;

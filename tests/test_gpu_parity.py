@@ -470,15 +470,18 @@ def test_streaming_run_sink_error_stops_cleanly(dev, golden):
     assert blocks == g["block_sha16"]
 
 
-@pytest.mark.parametrize("spec,ahead,batch", [("0", "1", 57), ("1", "0", 57), ("1", "1", 57),
-                                               ("1", "1", 1)])
-def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec, ahead, batch):
+@pytest.mark.parametrize("spec,ahead,prover,batch", [("0", "1", "1", 57), ("1", "0", "1", 57),
+                                                      ("1", "1", "0", 57), ("1", "1", "1", 57),
+                                                      ("1", "1", "1", 1)])
+def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec, ahead, prover, batch):
     """gss_run with the carrier chain walked on the host (GSS_RUN_SPEC=0) and run ahead on the
     GPU (the default), with the rows produced on the planner thread (GSS_RUN_ROWS_AHEAD=0) or
-    ahead on their own (the default; one-block batches too): a 65 s run across two 30 s updates,
-    whole and from a mid-run block, against the reference's golden hashes."""
+    ahead on their own (the default; one-block batches too), and the proofs on the planner thread
+    (GSS_RUN_PROVER=0) or their own (the default): a 65 s run across two 30 s updates, whole and
+    from a mid-run block, against the reference's golden hashes."""
     monkeypatch.setenv("GSS_RUN_SPEC", spec)
     monkeypatch.setenv("GSS_RUN_ROWS_AHEAD", ahead)
+    monkeypatch.setenv("GSS_RUN_PROVER", prover)
     g = golden["static_d65_b8_noiono"]
     bb = None
     blocks = []

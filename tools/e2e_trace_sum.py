@@ -5,7 +5,7 @@ wait for each slot's D2H; medians over the steady part of the run."""
 import statistics
 import sys
 
-plan, scn, drain = [], [], []
+plan, scn, drain, prove = [], [], [], []
 last_scn = None
 for line in open(sys.argv[1]):
     f = line.split()
@@ -18,6 +18,8 @@ for line in open(sys.argv[1]):
         if last_scn is not None and t0 <= last_scn <= t1:
             scn.append((last_scn - t0, t1 - last_scn))
         plan.append(t1 - t0)
+    elif f[1] == "prove":                        # proofs on the prover thread (gss_run)
+        prove.append(float(f[7]) - float(f[6]))
     elif f[1] == "drain":
         drain.append((float(f[6]) - float(f[5]), float(f[8]) - float(f[6])))
 steady = slice(2, -2)
@@ -25,5 +27,7 @@ med = lambda xs: statistics.median(xs) * 1e3 if xs else float("nan")
 print(f"slots {len(plan)}")
 print(f"planner per slot {med(plan[steady]):.2f} ms: host plane {med([a for a, _ in scn[steady]]):.2f} ms"
       f" + proofs {med([b for _, b in scn[steady]]):.2f} ms")
+if prove:
+    print(f"prover per slot {med(prove[steady]):.2f} ms")
 print(f"main thread: D2H wait per slot {med([a for a, _ in drain[steady]]):.2f} ms, sink "
       f"{med([b for _, b in drain[steady]]):.2f} ms")
