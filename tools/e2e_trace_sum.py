@@ -25,8 +25,11 @@ for line in open(sys.argv[1]):
 steady = slice(2, -2)
 med = lambda xs: statistics.median(xs) * 1e3 if xs else float("nan")
 print(f"slots {len(plan)}")
-print(f"planner per slot {med(plan[steady]):.2f} ms: host plane {med([a for a, _ in scn[steady]]):.2f} ms"
-      f" + proofs {med([b for _, b in scn[steady]]):.2f} ms")
+if scn:
+    print(f"planner per slot {med(plan[steady]):.2f} ms: host plane "
+          f"{med([a for a, _ in scn[steady]]):.2f} ms + proofs {med([b for _, b in scn[steady]]):.2f} ms")
+else:
+    print(f"planner per slot {med(plan[steady]):.2f} ms (rows, chain, walks; proofs on the prover)")
 if prove:
     print(f"prover per slot {med(prove[steady]):.2f} ms")
 print(f"main thread: D2H wait per slot {med([a for a, _ in drain[steady]]):.2f} ms, sink "
