@@ -1125,3 +1125,14 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
     cleanup();
     return err;
 }
+
+/* Threads besides the planner and main ones (round 3):
+ *   rows thread      (chain ahead, no hand-off) owns the scenario during the run: next_ask's
+ *                    batches (gss_scn_next_deferred) with the nav rows and sources new with each,
+ *                    a batch ahead of the planner, on its own worker pool; the planner then keeps
+ *                    the slot carriers and host copies of the nav table (GSS_RUN_ROWS_AHEAD=0:
+ *                    rows on the planner thread; GSS_RUN_ROWS_POOL=0: the planner's pool)
+ *   prover thread    (rows ahead, fast path) the slots' proofs in slot order on its own worker
+ *                    pool: the planner hands a slot over PROVING, the prover marks it PLANNED
+ *                    for the main thread (GSS_RUN_PROVER=0: proofs on the planner thread)
+ */
