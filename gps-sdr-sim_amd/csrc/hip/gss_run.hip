@@ -185,8 +185,10 @@ struct Run {
         double carr[GSS_MAXCH];                              /* exact, at its first block */
         int nb = 0, launched = 0;
         double tg = 0.0, tk = 0.0;                           /* trace: guess start, launch end */
-    } sb[2];
+    } sb[3];
     int sb_cur = 0;
+    int sb_head = 0, n_fly = 0, fly_end = 0;   /* rows_ahead: walks in flight (FIFO from
+                                                  sb_head), and whether the rows have ended */
     /* the rows produced ahead on their own thread (chain run ahead, no hand-off): during the run
        the scenario belongs to that thread; it hands over each batch's rows with the nav rows and
        sources new with it, and the planner keeps the slot carriers and host copies of the nav
@@ -520,7 +522,15 @@ int spec_launch(Run &r, Run::SpecBatch &b, int ask)
     b.launched = 1;
     int rc = 0, nb = 0;
     if (r.rows_ahead) {
-        memcpy(b.carr, r.carr, sizeof b.carr);         /* exact: the previous batch is finished */
+        /* the finished batches' exact carriers, carried by the lines through the batch still in
+           flight (if any): a prediction, ~3e-10 cycle off, which only the guesses use */
+        memcpy(b.carr, r.carr, sizeof b.carr);
+        for (int f = 0; f < r.n_fly; f++) {
+            const Run::SpecBatch &p = r.sb[(r.sb_head + f) % 3];
+            if (p.nb > 0)
+                (void)gss_carr_line_end(b.carr, p.blk.data(), p.nch.data(), p.chain.data(), p.nb,
+                                        r.n_per_blk, b.carr);
+        }
         rc = take_rows(r, b, &nb);
     } else {
         rc = gss_scn_carrier(r.scn, b.carr);
@@ -558,8 +568,8 @@ int spec_finish(Run &r, Run::SpecBatch &b, gss_chan_blk_t *blk, int32_t *nch, in
     const double tw = trace_on() ? tnow() : 0.0;
     RUN_TRY(hipStreamSynchronize(r.spec_st));
     const double t0 = trace_on() ? tnow() : 0.0;
-    double carr[GSS_MAXCH];
-    memcpy(carr, b.carr, sizeof carr);
+    double carr[GSS_MAXCH];                          /* exact: the batches before are done */
+    memcpy(carr, r.rows_ahead ? r.carr : b.carr, sizeof carr);
     int hit = 0;
     int rc = gss_carr_chain_spec(carr, b.blk.data(), b.nch.data(), b.chain.data(), nb,
                                  r.n_per_blk, b.h_in, b.h_spec, r.threads, &hit);
@@ -637,7 +647,28 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
         const int ask = next_ask(r, *cursor);
         int nb = 0;
         int rc = 0;
-        if (r.spec) {
+        if (r.rows_ahead) {
+            /* two batches' walks in flight: the oldest is finished (its chain, exact) while the
+               next one's walks run on the GPU; the batch after that is launched first */
+            while (!rc && r.n_fly < 2 && !r.fly_end) {
+                int64_t lc = *cursor;
+                for (int f = 0; f < r.n_fly; f++)
+                    lc += r.sb[(r.sb_head + f) % 3].nb;
+                const int a = next_ask(r, lc);
+                if (a <= 0)
+                    break;
+                Run::SpecBatch &b = r.sb[(r.sb_head + r.n_fly) % 3];
+                rc = spec_launch(r, b, a);
+                r.n_fly++;
+                if (!rc && b.nb == 0)
+                    r.fly_end = 1;                     /* the scenario's end */
+            }
+            if (!rc && r.n_fly > 0) {
+                rc = spec_finish(r, r.sb[r.sb_head], sl.blk, sl.nch, &nb);
+                r.sb_head = (r.sb_head + 1) % 3;
+                r.n_fly--;
+            }
+        } else if (r.spec) {
             Run::SpecBatch &b = r.sb[r.sb_cur];
             if (!b.launched && ask > 0)
                 rc = spec_launch(r, b, ask);

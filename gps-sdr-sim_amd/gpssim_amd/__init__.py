@@ -135,6 +135,7 @@ _SIGS = {
     "gss_carr_chain": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int]),
     "gss_carr_chain_guess": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P]),
     "gss_carr_chain_starts": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P]),
+    "gss_carr_line_end": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P]),
     "gss_spec_host": (C.c_int, [_P, C.c_int, C.c_int, _P, C.c_int]),
     "gss_spec_device": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, _P]),
     "gss_carr_chain_spec": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P, C.c_int,
@@ -469,6 +470,17 @@ def carr_chain_guess(carr, blk, nch, chain, n_per_blk, starts_only=False):
     _check(fn(_ptr(c), _ptr(np.ascontiguousarray(blk)), _ptr(nch), _ptr(chain), len(nch),
               int(n_per_blk), _ptr(gi)))
     return gi
+
+
+def carr_line_end(carr, blk, nch, chain, n_per_blk):
+    """The slots' carriers after the batch by the lines of gss_carr_chain_starts (a prediction)."""
+    c = np.ascontiguousarray(carr, np.float64)
+    out = np.zeros(MAXCH, np.float64)
+    nch = np.ascontiguousarray(nch, np.int32)
+    _check(lib().gss_carr_line_end(_ptr(c), _ptr(np.ascontiguousarray(blk)), _ptr(nch),
+                                   _ptr(np.ascontiguousarray(chain, CHAIN_DTYPE)), len(nch),
+                                   int(n_per_blk), _ptr(out)))
+    return out
 
 
 def spec_host(gi, n_per_blk, threads=8):

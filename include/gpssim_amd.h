@@ -317,6 +317,11 @@ int gss_carr_chain_guess(const double *carr, const gss_chan_blk_t *blk, const in
                          const gss_chain_t *chain, int nblk, int n_per_blk, gss_spec_in_t *in);
 int gss_carr_chain_starts(const double *carr, const gss_chan_blk_t *blk, const int32_t *nch,
                           const gss_chain_t *chain, int nblk, int n_per_blk, gss_spec_in_t *in);
+/* The slots' carriers after the nblk blocks by the same lines: a prediction, the start of the
+   next batch's guesses while this batch's chain is still pending (gss_run keeps two batches of
+   walks in flight). */
+int gss_carr_line_end(const double *carr, const gss_chan_blk_t *blk, const int32_t *nch,
+                      const gss_chain_t *chain, int nblk, int n_per_blk, double *carr_end);
 int gss_spec_host(gss_spec_in_t *in, int nrow, int n_per_blk, gss_spec_t *spec, int threads);
 int gss_spec_device(gss_dev *d, gss_spec_in_t *in, int nrow, int n_per_blk, gss_spec_t *spec,
                     void *stream);

@@ -154,6 +154,40 @@ def test_speculative_chain_equals_exact_chain(kind, threads, starts_only):
         assert hit >= 0.95 * total, (hit, total)
 
 
+def test_line_end_prediction_two_batches_ahead():
+    """gss_carr_line_end: the slots' carriers after a batch by the lines (what gss_run starts the
+    next batch's guesses from while this batch's chain is pending) equal a Python restatement
+    bit for bit, lie within 1e-8 cycle of the exact chain's end, and guesses started from them
+    keep nearly every block of the next batch on the translation; that chain stays exact."""
+    s = G.Scenario(NAV, llh=LOC, duration=90.0)
+    carr = s.carrier()
+    n = s.n_per_blk
+    b1, n1, c1 = s.next_deferred(300, threads=8)
+    b2, n2, c2 = s.next_deferred(300, threads=8)
+    pred = G.carr_line_end(carr, b1, n1, c1, n)
+    run = carr.copy()
+    for b in range(len(n1)):
+        for k in range(n1[b]):
+            sl = c1[b, k]["slot"]
+            if c1[b, k]["reset"]:
+                run[sl] = c1[b, k]["init"]
+            v = run[sl] + n * b1[b, k]["carr_step"]
+            run[sl] = v - np.floor(v)
+    assert pred.tobytes() == run.tobytes()
+    r1 = b1.copy()
+    end1, _ = G.carr_chain(carr, r1, n1, c1, n, with_ck=False)
+    live = sorted({int(c1[b, k]["slot"]) for b in range(len(n1)) for k in range(n1[b])})
+    d = np.abs(((pred[live] - end1[live]) + 0.5) % 1.0 - 0.5)
+    assert d.max() < 1e-8, d.max()
+    gi = G.carr_chain_guess(pred, b2, n2, c2, n)
+    spec = G.spec_host(gi, n, threads=8)
+    got, ref = b2.copy(), b2.copy()
+    end2_ref, _ = G.carr_chain(end1, ref, n2, c2, n, with_ck=False)
+    end2, hit = G.carr_chain_spec(end1, got, n2, c2, n, gi, spec, threads=8)
+    assert np.array_equal(got["carr0"], ref["carr0"]) and np.array_equal(end2, end2_ref)
+    assert hit >= 0.95 * int(n2.sum()), (hit, int(n2.sum()))
+
+
 def test_speculative_chain_exact_with_wrong_guesses():
     """gss_carr_chain_spec is exact whatever the guesses: starts moved far outside every
     translation interval, segment starts moved off their wraps or to wrong values, and segment
