@@ -185,6 +185,7 @@ struct Run {
         double carr[GSS_MAXCH];                              /* exact, at its first block */
         int nb = 0, launched = 0;
         double tg = 0.0, tk = 0.0;                           /* trace: guess start, launch end */
+        hipEvent_t walked = nullptr;          /* spec stream: this batch's walks are done      */
     } sb[3];
     int sb_cur = 0;
     int sb_head = 0, n_fly = 0, fly_end = 0;   /* rows_ahead: walks in flight (FIFO from
@@ -553,6 +554,7 @@ int spec_launch(Run &r, Run::SpecBatch &b, int ask)
     rc = gss_spec_device(r.dev, b.h_in, nrow, r.n_per_blk, b.h_spec, r.spec_st);
     if (rc)
         return rc;
+    RUN_TRY(hipEventRecord(b.walked, r.spec_st));    /* not the stream: later batches queue */
     b.tk = trace_on() ? tnow() : 0.0;
     return 0;
 }
@@ -566,7 +568,7 @@ int spec_finish(Run &r, Run::SpecBatch &b, gss_chan_blk_t *blk, int32_t *nch, in
     if (nb == 0)
         return 0;
     const double tw = trace_on() ? tnow() : 0.0;
-    RUN_TRY(hipStreamSynchronize(r.spec_st));
+    RUN_TRY(hipEventSynchronize(b.walked));
     const double t0 = trace_on() ? tnow() : 0.0;
     double carr[GSS_MAXCH];                          /* exact: the batches before are done */
     memcpy(carr, r.rows_ahead ? r.carr : b.carr, sizeof carr);
@@ -1019,6 +1021,7 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         if (r.spec_st) (void)hipStreamSynchronize(r.spec_st);
         for (Run::SpecBatch &b : r.sb) {
             (void)hipHostFree(b.h_in); (void)hipHostFree(b.h_spec);
+            if (b.walked) (void)hipEventDestroy(b.walked);
         }
         (void)hipFree(r.spec_warm);
         if (r.spec_st) (void)hipStreamDestroy(r.spec_st);
@@ -1086,7 +1089,8 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                 b.blk.resize(rows);
                 b.nch.resize(nb);
                 b.chain.resize(rows);
-                if (hipHostMalloc((void **)&b.h_in, sizeof(gss_spec_in_t) * rows,
+                if (hipEventCreateWithFlags(&b.walked, hipEventDisableTiming) != hipSuccess ||
+                    hipHostMalloc((void **)&b.h_in, sizeof(gss_spec_in_t) * rows,
                                   hipHostMallocDefault) != hipSuccess ||
                     hipHostMalloc((void **)&b.h_spec, sizeof(gss_spec_t) * rows,
                                   hipHostMallocDefault) != hipSuccess)
