@@ -1097,11 +1097,14 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                     err = gss_fail(GSS_E_NOMEM, "run carrier-chain buffers (%zu rows)", rows);
             }
         }
-        r.rows_ahead = r.spec && !(opts && opts->carr_in);
+        /* the rows and prover threads where the planner is the limit: slots of >= 1024 blocks
+           (-b 1 at 2.6 MS/s: 2,048).  The D2H-bound formats gain nothing from them, and inside
+           bench.py's process the extra threads cost the -b 16 leg a third of its download rate
+           (profiles/round3/e2e_planner/bench_*_r3af.log); GSS_RUN_ROWS_AHEAD=1 / 0 forces */
         {
             const char *e = getenv("GSS_RUN_ROWS_AHEAD");
-            if (e && e[0] == '0')
-                r.rows_ahead = 0;
+            const bool want = e && *e ? e[0] != '0' : r.batch >= 1024;
+            r.rows_ahead = r.spec && !(opts && opts->carr_in) && want;
         }
         r.prover = r.rows_ahead && r.use_lin;
         {
