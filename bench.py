@@ -526,12 +526,15 @@ def main():
 
     progress(f"traffic: {traffic_src[:120]}")
     configs = e2e = None
-    if single and not args.no_configs:
-        configs = per_config(G, torch, dev, dev_t, stream, min(args.steps, 3), 1, args.threads,
-                             e2e=not args.no_e2e)
+    # the headline's end-to-end leg before the per-config legs: after configs[4]'s -b 1 leg (rows
+    # and prover threads) this process's -b 16 downloads ran at ~39 instead of ~56 GB/s, which
+    # a fresh process does not show (cause not found)
     if single and not args.no_e2e:
         e2e = e2e_run(G, dev, args.threads, args.e2e_window, batch=128)
         progress(f"e2e: {e2e['value']} MS/s")
+    if single and not args.no_configs:
+        configs = per_config(G, torch, dev, dev_t, stream, min(args.steps, 3), 1, args.threads,
+                             e2e=not args.no_e2e)
 
     out = {
         "metric": METRIC,
