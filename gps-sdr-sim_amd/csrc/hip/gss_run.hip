@@ -1165,7 +1165,8 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
 }
 
 /* Threads besides the planner and main ones (round 3):
- *   rows thread      (chain ahead, no hand-off) owns the scenario during the run: next_ask's
+ *   rows thread      (chain ahead, no hand-off, slots of >= 1024 blocks unless GSS_RUN_ROWS_AHEAD
+ *                    says otherwise) owns the scenario during the run: next_ask's
  *                    batches (gss_scn_next_deferred) with the nav rows and sources new with each,
  *                    a batch ahead of the planner, on its own worker pool; the planner then keeps
  *                    the slot carriers and host copies of the nav table (GSS_RUN_ROWS_AHEAD=0:
