@@ -13,7 +13,11 @@
  * state the sample loop carries across blocks, gpssim.c:2245-2250) come from rank r-1 through a
  * hand-off file next to FILE, FILE.gss-carr-<run id>-<block>, written atomically (tmp + rename)
  * and removed by its reader.  The run id is torchrun's TORCHELASTIC_RUN_ID (or GSS_RUN_ID);
- * without one every rank plans the blocks before its range itself.
+ * without one every rank plans the blocks before its range itself.  torchrun's default run id
+ * is the same for every launch ("none"), so a file left by an interrupted earlier run can sit
+ * at the same path: the payload carries a fingerprint of everything the carriers depend on (the
+ * scenario options, the bytes of the navigation and motion files, the world size and the
+ * boundary block), and a reader ignores a file whose fingerprint differs and waits for its own.
  * Env: GSS_DEVICE (ordinal; default LOCAL_RANK or 0), GSS_BATCH (blocks per launch, default
  *      128), GSS_THREADS (planner threads, default the CPU share: cgroup cpu.max, else the online
  *      CPUs, at most 16), GSS_HANDOFF_TIMEOUT (seconds a rank waits
@@ -79,10 +83,51 @@ static int default_threads(void)
 typedef struct {
     gss_scn *scn;
     char in_path[600], out_path[600];      /* empty: none (rank 0 / last rank) */
+    uint64_t fp_in, fp_out;                /* fingerprints: scenario + boundary block */
     double timeout_s;
 } handoff_ctx;
 
-#define HANDOFF_MAGIC 0x67737363u          /* "gssc" */
+#define HANDOFF_MAGIC 0x67737364u          /* "gssd": magic, fingerprint, 16 carriers */
+
+/* FNV-1a 64 */
+static uint64_t fnv(uint64_t h, const void *p, size_t n)
+{
+    const unsigned char *b = (const unsigned char *)p;
+    for (size_t i = 0; i < n; i++)
+        h = (h ^ b[i]) * 0x100000001b3ull;
+    return h;
+}
+
+static uint64_t fnv_file(uint64_t h, const char *path)
+{
+    if (!path || !*path)
+        return fnv(h, "-", 1);
+    FILE *f = fopen(path, "rb");
+    if (!f)
+        return fnv(h, path, strlen(path));
+    unsigned char buf[65536];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof buf, f)) > 0)
+        h = fnv(h, buf, n);
+    fclose(f);
+    return h;
+}
+
+/* the scenario's identity: every option that shapes the carriers, and the input files' bytes */
+static uint64_t scenario_fingerprint(const gss_cli_t *cli, int world)
+{
+    const gss_opts_t *o = &cli->opt;
+    uint64_t h = 0xcbf29ce484222325ull;
+    h = fnv_file(h, cli->nav_file);
+    h = fnv_file(h, cli->motion_file[0] ? cli->motion_file : NULL);
+#define FP(x) h = fnv(h, &(x), sizeof(x))
+    FP(o->nmea); FP(o->has_xyz); FP(o->xyz); FP(o->has_llh); FP(o->llh); FP(o->samp_freq);
+    FP(o->data_format); FP(o->duration); FP(o->has_start); FP(o->time_overwrite); FP(o->start);
+    FP(o->start_sec); FP(o->iono_disable); FP(o->user_motion_size); FP(o->carrier_int);
+    FP(world);
+#undef FP
+    return h;
+}
 
 static int handoff_in(void *user, double *carr)
 {
@@ -95,13 +140,16 @@ static int handoff_in(void *user, double *carr)
         FILE *f = fopen(h->in_path, "rb");
         if (f) {
             uint32_t magic = 0;
-            size_t ok = fread(&magic, sizeof magic, 1, f) == 1 &&
-                        fread(carr, sizeof(double), GSS_MAXCH, f) == GSS_MAXCH;
+            uint64_t fp = 0;
+            const int ok = fread(&magic, sizeof magic, 1, f) == 1 &&
+                           fread(&fp, sizeof fp, 1, f) == 1 &&
+                           fread(carr, sizeof(double), GSS_MAXCH, f) == GSS_MAXCH;
             fclose(f);
-            if (!ok || magic != HANDOFF_MAGIC)
-                return 1;
-            unlink(h->in_path);
-            return 0;
+            if (ok && magic == HANDOFF_MAGIC && fp == h->fp_in) {
+                unlink(h->in_path);
+                return 0;
+            }
+            /* another run's (or a torn) file: not ours, wait for rank r-1 to replace it */
         }
         if (waited > h->timeout_s)
             return 1;
@@ -122,6 +170,7 @@ static int handoff_out(void *user, const double *carr)
         return 1;
     const uint32_t magic = HANDOFF_MAGIC;
     int ok = fwrite(&magic, sizeof magic, 1, f) == 1 &&
+             fwrite(&h->fp_out, sizeof h->fp_out, 1, f) == 1 &&
              fwrite(carr, sizeof(double), GSS_MAXCH, f) == GSS_MAXCH;
     ok = (fclose(f) == 0) && ok;
     return (ok && rename(tmp, h->out_path) == 0) ? 0 : 1;
@@ -155,6 +204,9 @@ static int run_rank(const gss_cli_t *cli, gss_scn *scn, const gss_scn_info_t *in
     memset(&h, 0, sizeof h);
     h.scn = scn;
     h.timeout_s = env_int("GSS_HANDOFF_TIMEOUT", 3600);
+    const uint64_t fp = scenario_fingerprint(cli, world);
+    h.fp_in = fnv(fp, &first, sizeof first);
+    h.fp_out = fnv(fp, &last, sizeof last);
     gss_run_opts_t ro = {handoff_in, handoff_out, &h};
     if (run_id && *run_id) {
         if (rank > 0)

@@ -89,6 +89,42 @@ GSS_LIN_FN uint32_t gss_lin_e0(uint64_t chips)
 /* the 32-chip step window holds every lane's chip (zs in 2^-50 chip per sample, < 1 chip) */
 #define GSS_LIN_WIN_OK(zs) ((zs) * 63u + (3ull << 50) <= (31ull << 50))
 
+/* The chunk window table (gss_tw16_kernel, gss_lin_kernel): row r (a C/A table row) and chunk
+   start chip E hold the 16 steps' 32-chip windows of a chunk whose code base zb has
+   zb >> 50 = E; step s's window starts at extended chip E + ((s w) >> 4) - GSS_LIN_CBW_PRE, w =
+   gss_lin_wstep16(n_per_blk) the nominal chip advance per 64-sample step in 1/16 chip (1.023 MHz
+   over the sample rate).  One table serves every channel of a launch: a channel's true advance
+   differs from w by its code Doppler (parts in 10^6) and the rounding of w, which
+   gss_lin_win16_ok checks against the window's slack, per channel and block. */
+#define GSS_LIN_TWE     2560                   /* chunk start chips per table row            */
+#define GSS_LIN_CBW_PRE 2                      /* a window starts this far below E + (s w>>4) */
+GSS_LIN_FN uint32_t gss_lin_wstep16(int n_per_blk)
+{
+    return (uint32_t)((104755200ull + (uint64_t)n_per_blk / 2) / (uint64_t)n_per_blk);
+}
+/* every lane's chip of every step lies in the step's table window, and every chunk's E is inside
+   the table, for a channel of code step zs (2^-50 chip per sample) whose code line is reduced to
+   at most chip 1024 at each wave segment start (gss_lin_e0) */
+GSS_LIN_FN int gss_lin_win16_ok(uint64_t zs, int n_per_blk)
+{
+    const int64_t U = (int64_t)1 << 50, z = (int64_t)zs;
+    /* the kernel's code within KDEV of its anchored line, plus the anchor's centring offset and
+       a margin (all below 2^-23 chip) */
+    const int64_t kd = (int64_t)GSS_LIN_KDEV_CODE + ((int64_t)1 << 27);
+    const uint32_t w = gss_lin_wstep16(n_per_blk);
+    if (zs == 0 || zs >= (uint64_t)U)
+        return 0;
+    for (int s = 0; s < GSS_LIN_CH; s++) {
+        const int64_t f = (int64_t)(((uint64_t)s * w) >> 4) - GSS_LIN_CBW_PRE;
+        if (64 * s * z - kd < f * U)                          /* lane 0 at or above the start */
+            return 0;
+        if (U + (64 * s + 63) * z + kd > (f + 32) * U)        /* lane 63 below the end        */
+            return 0;
+    }
+    /* the last chunk of a segment starts 3 chunks after a base at most 1024 chips */
+    return 1025 * U + (int64_t)(GSS_LIN_SEG - GSS_LIN_CHUNK) * z + kd < (int64_t)GSS_LIN_TWE * U;
+}
+
 /* the lane offset L(l) of gss_lin.h: carrier word (high) and code word (low) */
 GSS_LIN_FN uint64_t gss_lin_lane(uint64_t xs, uint64_t zs, uint32_t l)
 {

@@ -88,15 +88,19 @@ enum { FREE, PROVING, PLANNED };                  /* PROVING: rows planned, proo
 
 /* The slots' output buffers (pinned host + device, ~133 MB each at the defaults) outlive a run:
    page-locking them costs tens of ms, so a later gss_run in the same process (a service, or a
-   rank's next window) takes them from this pool instead.  Bounded by POOL_MAX_BYTES; a buffer is
-   reused only for a request of at least half its size. */
+   rank's next window) takes them from this pool instead.  Bounded by POOL_MAX_BYTES (the sizes
+   of the buffers themselves); a buffer is reused only for a request of at least half its size,
+   and gss_dev_close frees a device's buffers (gss_run_pool_drain). */
+namespace {
 struct PoolBuf { void *p; size_t n; int dev; bool host; };
 std::mutex pool_mu;
 std::vector<PoolBuf> pool;
 size_t pool_bytes = 0;
 constexpr size_t POOL_MAX_BYTES = (size_t)2 << 30;
+}  // namespace
 
-static hipError_t pool_get(void **p, size_t n, bool host, int dev)
+/* a buffer of at least n bytes; *got = its actual size, which pool_put must be given back */
+static hipError_t pool_get(void **p, size_t n, bool host, int dev, size_t *got)
 {
     {
         std::lock_guard<std::mutex> lk(pool_mu);
@@ -104,12 +108,14 @@ static hipError_t pool_get(void **p, size_t n, bool host, int dev)
             const PoolBuf &b = pool[i];
             if (b.host == host && b.dev == dev && b.n >= n && b.n <= 2 * n) {
                 *p = b.p;
+                *got = b.n;
                 pool_bytes -= b.n;
                 pool.erase(pool.begin() + (long)i);
                 return hipSuccess;
             }
         }
     }
+    *got = n;
     return host ? hipHostMalloc(p, n, hipHostMallocDefault) : hipMalloc(p, n);
 }
 
@@ -126,6 +132,26 @@ static void pool_put(void *p, size_t n, bool host, int dev)
         }
     }
     (void)(host ? hipHostFree(p) : hipFree(p));
+}
+
+/* free the pooled buffers of device `dev` (gss_dev_close; -1: every device) */
+extern "C" void gss_run_pool_drain(int dev)
+{
+    std::vector<PoolBuf> out;
+    {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        for (size_t i = 0; i < pool.size();) {
+            if (dev < 0 || pool[i].dev == dev) {
+                out.push_back(pool[i]);
+                pool_bytes -= pool[i].n;
+                pool.erase(pool.begin() + (long)i);
+            } else {
+                i++;
+            }
+        }
+    }
+    for (const PoolBuf &b : out)
+        (void)(b.host ? hipHostFree(b.p) : hipFree(b.p));
 }
 
 struct Slot {
@@ -149,7 +175,7 @@ struct Slot {
     uint8_t *d_in = nullptr;
     size_t d_in_cap = 0;
     uint8_t *d_out = nullptr, *h_out = nullptr;
-    size_t out_bytes = 0;            /* their size (pool_get / pool_put)                  */
+    size_t h_out_bytes = 0, d_out_bytes = 0;   /* their sizes (pool_get / pool_put)        */
     int32_t *d_status = nullptr, *h_status = nullptr;
     hipEvent_t rendered = nullptr;   /* compute stream: the slot's kernels are done      */
     hipEvent_t done = nullptr;       /* copy stream: the slot's bytes are in h_out        */
@@ -1009,8 +1035,8 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         for (Slot &sl : r.slot) {
             (void)hipHostFree(sl.blk); (void)hipHostFree(sl.nch); (void)hipHostFree(sl.ck);
             (void)hipHostFree(sl.nav); (void)hipHostFree(sl.h_status);
-            pool_put(sl.h_out, sl.out_bytes, true, ordinal);
-            pool_put(sl.d_out, sl.out_bytes, false, ordinal);
+            pool_put(sl.h_out, sl.h_out_bytes, true, ordinal);
+            pool_put(sl.d_out, sl.d_out_bytes, false, ordinal);
             (void)hipHostFree(sl.lin); (void)hipHostFree(sl.fast);
             (void)hipFree(sl.d_in); (void)hipFree(sl.d_status);
             if (sl.done) (void)hipEventDestroy(sl.done);
@@ -1051,11 +1077,12 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                     hipSuccess ||
                 hipHostMalloc((void **)&sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * nb,
                               hipHostMallocDefault) != hipSuccess ||
-                (sl.out_bytes = bb * nb,
-                 pool_get((void **)&sl.h_out, bb * nb, true, ordinal) != hipSuccess) ||
+                pool_get((void **)&sl.h_out, bb * nb, true, ordinal, &sl.h_out_bytes) !=
+                    hipSuccess ||
                 hipHostMalloc((void **)&sl.h_status, sizeof(int32_t), hipHostMallocDefault) !=
                     hipSuccess ||
-                pool_get((void **)&sl.d_out, bb * nb, false, ordinal) != hipSuccess ||
+                pool_get((void **)&sl.d_out, bb * nb, false, ordinal, &sl.d_out_bytes) !=
+                    hipSuccess ||
                 hipMalloc((void **)&sl.d_status, sizeof(int32_t)) != hipSuccess ||
                 hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&sl.rendered, hipEventDisableTiming) != hipSuccess)

@@ -525,22 +525,36 @@ static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole ch
 /* LIN_ABLATE (measurement builds only, tools/ablate.sh; wrong output): 1 no output stores,
    2 no chip-window loads, 4 no LUT reads, 8 every block stores into one of 8 blocks (L2),
    32 no alignbit (VALU work), 64 no window reads in the render loop (LDS work), 128 the LUT
-   address without the chip sign (no bank conflicts between a cell's two signs) */
+   address without the chip sign (no bank conflicts between a cell's two signs), 256 windows
+   made by the scalar unit in SGPRs (no window pass, no LDS window reads) */
 #ifndef LIN_ABLATE
 #define LIN_ABLATE 0
 #endif
-/* LIN_SWIN 1: the steps' chip windows come from a static table in global memory -- row = C/A
-   table row, entry j = the 32 chips from extended chip j - 32 on, rotated left by j mod 32
-   (gss_tw_kernel; the same word the LDS window pass builds) -- read with wave-uniform addresses,
-   i.e. scalar loads into SGPRs that the shift takes directly.  No window pass, no LDS window
-   reads, no per-workgroup bit-stream copy.  LIN_SWIN 2: the same table read by vector buffer
-   loads at a wave-uniform offset (one cache line for the wave, into VGPRs), which wait on
-   vmcnt, in order, instead of the counter the LDS reads use. */
-#ifndef LIN_SWIN
-#define LIN_SWIN 0
+/* LIN_STAMP (diagnostic builds only, tools/clock_stamp.py; MI355X_MICROARCH.md "DVFS give-back"
+   item 6): each wave of gss_lin_kernel reads the shader-clock counter (s_memtime) and the
+   constant 100 MHz counter (s_memrealtime) once before and once after its chunk loop and lane 0
+   writes the four values with a vector store into g_lin_stamp[wave of the launch], a buffer of
+   their own that nothing else reads.  Cycles per wave and the clock the launch held
+   (cycles / ticks x 100 MHz) then come apart; the product kernel executes no stamp. */
+#ifndef LIN_STAMP
+#define LIN_STAMP 0
 #endif
-#define LIN_TW_W   (32 * CAB_W - 32)       /* table entries per row (j <= 32 CAB_W - 64 used)    */
-#if LIN_SWIN == 1
+#if LIN_STAMP
+#define LIN_STAMP_WAVES (1 << 20)
+__device__ uint64_t g_lin_stamp[LIN_STAMP_WAVES][4];
+#endif
+/* LIN_SWIN 1 (the default): the steps' chip windows come from the chunk window table (gss_lin.h,
+   gss_tw16_kernel): per channel and chunk one 64-byte row -- the 16 windows of a chunk whose
+   code base has chip E, for the channel's C/A row -- at a wave-uniform address, read by one
+   s_load_dwordx16 into SGPRs that the chip-sign shift takes directly.  No window pass, no LDS
+   window reads, no per-workgroup copy of the bit-streams.  LIN_SWIN 0 (round 3): the lanes build
+   each chunk's windows from the bit-streams in LDS and the loop reads them back by broadcast LDS
+   reads.  In-kernel clock stamps (tools/clock_stamp.py, profiles/round4/): an ablation with the
+   windows made in SGPRs took the wave 20 % fewer cycles than the LDS windows. */
+#ifndef LIN_SWIN
+#define LIN_SWIN 1
+#endif
+#if LIN_SWIN || (LIN_ABLATE & 256)
 #define LIN_WCON "s"                       /* the shift takes the window from an SGPR            */
 #else
 #define LIN_WCON "v"
@@ -586,7 +600,8 @@ struct lin_ct {
     int32_t gd;                  /* gain change inside the chunk (g1 - g0), from sample pos1 on */
     int32_t pos1;
     uint32_t flags;              /* 1: a gain change inside the chunk, 2: patched samples       */
-    uint32_t q0, dq, tab, pad;   /* first window offset (1/16 chip), its step, the row          */
+    uint32_t q0, dq, tab;        /* first window offset (1/16 chip), its step, the row          */
+    uint32_t wa;                 /* LIN_SWIN: byte offset of the chunk's window-table row       */
 #if !LIN_SWIN
     uint32_t W[LIN_CH];          /* the steps' chip windows                                     */
 #endif
@@ -679,29 +694,29 @@ __global__ void gss_cab_kernel(const uint32_t *__restrict__ ca_bits, int n_ca,
     cab[i] = w;
 }
 
-/* the window table of LIN_SWIN: row r, entry j = extended chips j - 32 .. j - 1 of row r's
-   bit-stream, rotated left by j mod 32 (bit (E mod 32) = chip E's sign, E = j - 32 + bit) */
-__global__ void gss_tw_kernel(const uint32_t *__restrict__ cab, int n_ca, uint32_t *__restrict__ tw)
+/* the chunk window table (gss_lin.h): entry [row][E][s] = the 32 chips from extended chip
+   e = E + ((s w) >> 4) - GSS_LIN_CBW_PRE on of row's bit-stream, rotated left by e mod 32 (bit
+   (c mod 32) = chip c's sign), the word the LDS window pass builds; w = gss_lin_wstep16.  The
+   start is clamped to the bit-stream, which a certified channel never reaches. */
+__global__ void gss_tw16_kernel(const uint32_t *__restrict__ cab, int n_ca, uint32_t w,
+                                uint32_t *__restrict__ tw)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_ca * LIN_TW_W)
+    if (i >= n_ca * GSS_LIN_TWE * LIN_CH)
         return;
-    const int row = i / LIN_TW_W;
-    const uint32_t j = (uint32_t)(i - row * LIN_TW_W);
-    if (j > (uint32_t)(32 * CAB_W - 64)) {
-        tw[i] = 0u;
-        return;
-    }
+    const int row = i / (GSS_LIN_TWE * LIN_CH), r = i - row * (GSS_LIN_TWE * LIN_CH);
+    const int E = r / LIN_CH, st = r % LIN_CH;
+    const uint32_t j = min((uint32_t)(E + (int)(((uint32_t)st * w) >> 4) - GSS_LIN_CBW_PRE + 32),
+                           (uint32_t)(32 * CAB_W - 64));       /* bit index: chip j - 32 */
     const uint32_t *c = cab + (size_t)row * CAB_W;
     const uint32_t lin = __builtin_amdgcn_alignbit(c[(j >> 5) + 1], c[j >> 5], j & 31);
     tw[i] = __builtin_amdgcn_alignbit(lin, lin, (32u - j) & 31u);
 }
 
 /* where a channel's chunk windows come from: the wave's LDS record (W = its W[]) or, with
-   LIN_SWIN, the window table (W = the channel's row; q0, dq as in lin_ct, wave-uniform) */
+   LIN_SWIN, the chunk window table (W = the row of the channel's chunk, wave-uniform) */
 struct lin_wsrc {
     const uint32_t *W;
-    uint32_t q0, dq;
 };
 
 /* step s's window; w4 caches four LDS windows (one broadcast read per four steps) */
@@ -710,16 +725,10 @@ __device__ __forceinline__ uint32_t lin_wget(const lin_wsrc &w, int s, uint4 &w4
 {
 #if LIN_SWIN
     (void)w4; (void)M; (void)salt;
-    const uint32_t j = min(((w.q0 + (uint32_t)s * w.dq) >> 4) + (32 - CBW_PRE),
-                           (uint32_t)(32 * CAB_W - 64));
-#if LIN_SWIN == 2
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)w.W, (short)0, (int)(LIN_TW_W * sizeof(uint32_t)), 0x00020000);
-    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, 0, (int)(j * 4u), 0);
+    return w.W[s];                                  /* uniform: one s_load_dwordx16 for all 16 */
 #else
-    return w.W[j];
-#endif
-#else
+    if (LIN_ABLATE & 256)          /* measurement: SGPR windows, no LDS window reads or pass */
+        return __builtin_amdgcn_readfirstlane(M) * (uint32_t)(s + 1 + salt);
     if (s % 4 == 0) {                                     /* four windows per broadcast read */
         if (LIN_ABLATE & 64)
             w4 = make_uint4(M * (s + 1 + salt), M * (s + 3 + salt), M * (s + 5 + salt),
@@ -731,9 +740,9 @@ __device__ __forceinline__ uint32_t lin_wget(const lin_wsrc &w, int s, uint4 &w4
 #endif
 }
 
-/* LIN_SWIN: all LIN_CH windows of a chunk as scalar loads issued together and waited for once
-   (the scalar and LDS loads share one counter, so a window load left in flight would turn every
-   LUT read's wait into a full drain) */
+/* LIN_SWIN: all LIN_CH windows of a chunk as one scalar load, waited for before the steps (the
+   scalar and LDS loads share one counter, so a window load left in flight would turn every LUT
+   read's wait into a full drain) */
 __device__ __forceinline__ void lin_wissue(const lin_wsrc &w, uint32_t (&ws)[LIN_CH])
 {
 #pragma unroll
@@ -746,7 +755,7 @@ __device__ __forceinline__ void lin_wissue(const lin_wsrc &w, uint32_t (&ws)[LIN
 /* ... and the fence that needs them all (one wait, after every load of the chunk is issued) */
 __device__ __forceinline__ void lin_wfence(const uint32_t (&ws)[LIN_CH])
 {
-#if LIN_SWIN == 1
+#if LIN_SWIN
     static_assert(LIN_CH == 16, "the fence below names 16 windows");
     asm volatile("" :: "s"(ws[0]), "s"(ws[1]), "s"(ws[2]), "s"(ws[3]), "s"(ws[4]), "s"(ws[5]),
                  "s"(ws[6]), "s"(ws[7]), "s"(ws[8]), "s"(ws[9]), "s"(ws[10]), "s"(ws[11]),
@@ -759,12 +768,12 @@ __device__ __forceinline__ void lin_wfence(const uint32_t (&ws)[LIN_CH])
 __device__ __forceinline__ lin_wsrc lin_wsrc_of(const lin_ct &t, const uint32_t *__restrict__ tw)
 {
 #if LIN_SWIN
-    const uint32_t row = __builtin_amdgcn_readfirstlane(t.tab);
-    return lin_wsrc{tw + (size_t)row * LIN_TW_W, (uint32_t)__builtin_amdgcn_readfirstlane(t.q0),
-                    (uint32_t)__builtin_amdgcn_readfirstlane(t.dq)};
+    const uint32_t off = __builtin_amdgcn_readfirstlane(t.wa);
+    return lin_wsrc{(const uint32_t *)__builtin_assume_aligned(
+        (const char *)tw + off, 64)};
 #else
     (void)tw;
-    return lin_wsrc{t.W, 0u, 0u};
+    return lin_wsrc{t.W};
 #endif
 }
 
@@ -1213,6 +1222,9 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
     const lin_seg *S = segs + (size_t)b * GSS_MAXCH * nseg + sg;
     lin_ct *T = s_ct[wave];
     uint8_t *ob = out + ((LIN_ABLATE & 8) ? (size_t)(b & 7) : (size_t)b) * block_bytes;
+#if LIN_STAMP
+    const uint64_t st_t0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
     for (int c = 0; c < LIN_STEPS / LIN_CH; c++) {
         const int nb0 = n0 + c * (64 * LIN_CH);           /* first sample of the chunk */
@@ -1241,6 +1253,12 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
             t.q0 = (uint32_t)(zb >> 46) + (16 * CBW_PRE - 1);
             t.dq = ck.dq;
             t.tab = ck.tab;
+#if LIN_SWIN
+            /* the chunk's row of the window table: its C/A row and code base chip E (clamped to
+               the table; gss_lin_win16_ok keeps a certified channel inside it) */
+            t.wa = (ck.tab * GSS_LIN_TWE + min((uint32_t)(zb >> 50), (uint32_t)(GSS_LIN_TWE - 1))) *
+                   (uint32_t)(LIN_CH * sizeof(uint32_t));
+#endif
 #if LIN_MFMA
             const uint32_t gh = lin_f16_bits(t.g);        /* lane 4b + i's gain operand */
             t.A[0][0] = gh;         t.A[0][1] = 0;
@@ -1253,7 +1271,7 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
         /* the channels with a gain change or patches in this chunk (wave-uniform) */
         const uint64_t fmask = __builtin_amdgcn_ballot_w64(my_flags != 0);
         wave_sync_lds();
-#if !LIN_SWIN
+#if !LIN_SWIN && !(LIN_ABLATE & 256)
         /* ---- the chip windows, lane (k, s) ---- */
         for (int i = lane; i < nc * LIN_CH; i += 64) {
             const int k = i / LIN_CH;
@@ -1375,7 +1393,30 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
         else
             lin_store<FMT, true>(acc, ob, nb0, lane, n_per_blk);
     }
+#if LIN_STAMP
+    const uint64_t st_t1 = __builtin_amdgcn_s_memtime(), st_r1 = __builtin_amdgcn_s_memrealtime();
+    const size_t sw = (size_t)blockIdx.x * LIN_WAVES + wave;
+    if (lane == 0 && sw < LIN_STAMP_WAVES) {
+        uint64_t *d = g_lin_stamp[sw];
+        d[0] = st_t0;
+        d[1] = st_t1;
+        d[2] = st_r0;
+        d[3] = st_r1;
+    }
+#endif
 }
+
+#if LIN_STAMP
+/* the stamps of the last gss_lin_kernel launch: n waves x {memtime0, memtime1, realtime0,
+   realtime1} (diagnostic builds only; not in include/gpssim_amd.h) */
+extern "C" int gss_diag_lin_stamps(uint64_t *out, size_t n_waves)
+{
+    if (n_waves > LIN_STAMP_WAVES)
+        n_waves = LIN_STAMP_WAVES;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lin_stamp), n_waves * 4 * sizeof(uint64_t), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 /* ======================================================================================== */
 /* C ABI                                                                                    */
@@ -1472,10 +1513,13 @@ extern "C" int gss_dev_open(gss_dev **out, int ordinal)
     return 0;
 }
 
+extern "C" void gss_run_pool_drain(int dev);      /* gss_run.hip */
+
 extern "C" int gss_dev_close(gss_dev *d)
 {
     if (!d) return 0;
     (void)hipSetDevice(d->ordinal);
+    gss_run_pool_drain(d->ordinal);                  /* gss_run's pooled slot buffers */
     for (auto &a : d->set) {
         (void)hipFree(a.carr);
         (void)hipFree(a.code);
@@ -1680,9 +1724,11 @@ extern "C" int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const
         return gss_fail(GSS_E_ARG, "no fast kernel for fmt=%d nch=%d", fmt, nchp);
     HIP_TRY(hipSetDevice(d->ordinal));
     hipStream_t st = (hipStream_t)stream;
-    /* chip-sign bit-streams of every C/A table row (32 x 99 x 4 B) and, after them, the window
-       table of LIN_SWIN (32 x 3136 x 4 B); rebuilt per call: ~µs */
-    const size_t ncbw = (size_t)n_ca * CAB_W, ntw = LIN_SWIN ? (size_t)n_ca * LIN_TW_W : 0;
+    /* chip-sign bit-streams of every C/A table row (32 x 99 x 4 B) and, after them, the chunk
+       window table of LIN_SWIN (32 x 2560 x 64 B); rebuilt per call (the sample rate sets its
+       window advance): a few µs */
+    const size_t ncbw = (size_t)n_ca * CAB_W,
+                 ntw = LIN_SWIN ? (size_t)n_ca * GSS_LIN_TWE * LIN_CH : 0;
     const size_t tw_off = (ncbw + 63) & ~(size_t)63;
     if ((tw_off + ntw) * sizeof(uint32_t) > d->d_cbw_cap) {
         (void)hipFree(d->d_cbw);
@@ -1695,8 +1741,9 @@ extern "C" int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const
                        ca_bits, n_ca, d->d_cbw);
     HIP_TRY(hipGetLastError());
     if (ntw) {
-        hipLaunchKernelGGL(gss_tw_kernel, dim3((unsigned)((ntw + 255) / 256)), dim3(256), 0, st,
-                           (const uint32_t *)d->d_cbw, n_ca, d->d_cbw + tw_off);
+        hipLaunchKernelGGL(gss_tw16_kernel, dim3((unsigned)((ntw + 255) / 256)), dim3(256), 0,
+                           st, (const uint32_t *)d->d_cbw, n_ca, gss_lin_wstep16(n_per_blk),
+                           d->d_cbw + tw_off);
         HIP_TRY(hipGetLastError());
     }
     const int segs = (n_per_blk + 64 * LIN_STEPS - 1) / (64 * LIN_STEPS);

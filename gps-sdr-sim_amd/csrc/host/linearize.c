@@ -300,8 +300,10 @@ static int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
     const int64_t Z0 = (int64_t)to_fix(c0, 50, &inexact);
     const int64_t per = (int64_t)GSS_CA_LEN << LIN_CODE_LGB;
     /* the kernel reads one 32-chip window per 64-sample step, starting up to 2 chips below
-       lane 0's chip (gss_lin.h) */
-    if (ZS <= 0 || Z0 >= per || !GSS_LIN_WIN_OK((uint64_t)ZS))
+       lane 0's chip: from the LDS window pass (GSS_LIN_WIN_OK) or the chunk window table
+       (gss_lin_win16_ok); both hold, so that either build of the kernel may render the block */
+    if (ZS <= 0 || Z0 >= per || !GSS_LIN_WIN_OK((uint64_t)ZS) ||
+        !gss_lin_win16_ok((uint64_t)ZS, n))
         return 0;
     const int nhz = ambiguous(Z0, ZS, 2 + (i128)n * (LIN_CODE_ERR + 1) + GSS_LIN_KDEV_CODE,
                               LIN_CODE_LGB, n, hz, LIN_MAXHIT);

@@ -8,6 +8,9 @@
  * dynamically (an atomic counter), so uneven parts balance themselves.  One job at a time per
  * pool: a second caller waits for the first job to finish (jobs never nest).  Three pools, chosen
  * per calling thread (gss_pool_select): gss_run's rows and proof threads have their own.
+ * fork(): the workers do not exist in a child, so a pthread_atfork handler (registered at the
+ * first job) takes every pool's locks before the fork, releases them in the parent and resets
+ * the pools in the child (no workers, fresh locks): the child's first job grows its own.
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -35,6 +38,40 @@ typedef struct {
                    PTHREAD_COND_INITIALIZER, 0, 0, 0, 0, NULL, NULL, 0, 0}
 static pool_t pools[POOL_N] = {POOL_INIT, POOL_INIT, POOL_INIT};
 static __thread int tl_pool;             /* the calling thread's pool (gss_pool_select) */
+
+/* fork: no job runs across it (prepare takes each pool's job lock, then its state lock) */
+static void fork_prepare(void)
+{
+    for (int i = 0; i < POOL_N; i++) {
+        pthread_mutex_lock(&pools[i].run_mu);
+        pthread_mutex_lock(&pools[i].mu);
+    }
+}
+
+static void fork_parent(void)
+{
+    for (int i = POOL_N - 1; i >= 0; i--) {
+        pthread_mutex_unlock(&pools[i].mu);
+        pthread_mutex_unlock(&pools[i].run_mu);
+    }
+}
+
+static void fork_child(void)             /* only the forking thread exists here */
+{
+    for (int i = 0; i < POOL_N; i++) {
+        pool_t *P = &pools[i];
+        pthread_mutex_init(&P->run_mu, NULL);
+        pthread_mutex_init(&P->mu, NULL);
+        pthread_cond_init(&P->go, NULL);
+        pthread_cond_init(&P->done, NULL);
+        P->n_workers = 0;
+        P->job_workers = 0;
+        P->active = 0;
+    }
+}
+
+static pthread_once_t atfork_once = PTHREAD_ONCE_INIT;
+static void atfork_register(void) { pthread_atfork(fork_prepare, fork_parent, fork_child); }
 
 /* Route this thread's gss_pool_run jobs to pool id (0 default): gss_run's rows and proof threads
    take their own workers, so that their range passes and proofs run beside the planner's chain
@@ -98,6 +135,7 @@ int gss_pool_run(int nthreads, int nparts, gss_task_fn fn, void *arg)
             fn(arg, p);
         return 0;
     }
+    pthread_once(&atfork_once, atfork_register);
     pool_t *P = &pools[tl_pool];
     pthread_mutex_lock(&P->run_mu);
     pthread_mutex_lock(&P->mu);

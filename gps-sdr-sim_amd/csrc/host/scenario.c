@@ -69,7 +69,8 @@ struct gss_scn {
     gss_nav_src_t *nav_src;          /* row r's source for the GPU producer (gss_nav.h)         */
     int n_nav, cap_nav;
     double carr[K_MAX_CHAN];                /* planner: carrier at the next block start per slot */
-    int carr_known;                         /* 0 after gss_scn_seek until gss_scn_set_carrier */
+    int carr_known;                         /* 0 after gss_scn_seek or gss_scn_next_deferred
+                                               until gss_scn_set_carrier                      */
     double plan_sec;
     int64_t rows_out;                       /* blocks whose rows this handle has produced */
     /* per-batch carrier-chain bookkeeping of gss_scn_next (gss_scn_next_deferred's is the
@@ -865,6 +866,11 @@ int gss_scn_next_deferred(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32
     double t_start = wall_now();
     int rc = next_rows(s, max_blocks, blk, nch, chain, NULL, n_out, threads);
     s->plan_sec += wall_now() - t_start;
+    /* the slot carriers (s->carr) still belong to the first of these blocks: gss_scn_next
+       refuses to run on them until the chain's end arrives by gss_scn_set_carrier (a run that
+       stops early therefore leaves the handle marked, not silently stale) */
+    if (*n_out > 0)
+        s->carr_known = 0;
     return rc;
 }
 

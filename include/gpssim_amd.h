@@ -271,7 +271,9 @@ typedef struct gss_chain {       /* per (block, channel row): the carrier chain 
 } gss_chain_t;                   /* 16 bytes, laid out [nblk][GSS_MAXCH] like the rows             */
 
 /* gss_scn_next without the carrier chain: blk[].carr0 is left 0 and chain[] says which slot's
-   chain each row continues; gss_carr_chain fills carr0 (and checkpoints) afterwards.           */
+   chain each row continues; gss_carr_chain fills carr0 (and checkpoints) afterwards.  The
+   handle's slot carriers (gss_scn_carrier) stay those at the first produced block, and
+   gss_scn_next fails with GSS_E_STATE until gss_scn_set_carrier supplies the chain's end.       */
 int gss_scn_next_deferred(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch,
                           gss_chain_t *chain, int *n_out, int threads);
 /* The carrier chain over nblk consecutive blocks of deferred rows: carr[GSS_MAXCH] holds each

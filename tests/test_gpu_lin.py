@@ -29,10 +29,10 @@ def dev():
 
 
 @pytest.mark.parametrize("fmt", [16, 8, 1])
-@pytest.mark.parametrize("n", [26000, 26004, 260000])
+@pytest.mark.parametrize("n", [260000, 260004, 2000000])
 def test_lin_synthetic_vs_oracle(dev, fmt, n):
     rng = np.random.default_rng(n * 31 + fmt)
-    nch = [12, 0, 1, 7, 12, 16] if n < 100000 else [12, 11]
+    nch = [12, 0, 1, 7, 12, 16] if n < 1000000 else [12, 11]
     blk, nchv, nav = synth_params(rng, len(nch), nch, n)
     ca = G.ca_table()
     lin, fast = G.linearize(blk, nchv, nav, n)
@@ -52,7 +52,7 @@ def test_lin_mixed_batch_with_exact_leftovers(dev):
     and a start phase on a cell boundary forced uncertifiable) take the exact path inside the
     same call; all bytes equal the oracle's."""
     rng = np.random.default_rng(11)
-    n = 26000
+    n = 260000
     blk, nch, nav = synth_params(rng, 6, [12, 12, 5, 12, 3, 9], n)
     blk[1, 3]["code_step"] = 0.9                      # 127 * 0.9 chips > the 64-chip window
     blk[4, 0]["gain"] = 9000                          # > packed accumulator range
@@ -131,7 +131,7 @@ def test_lin_mfma_sum_extremes_vs_oracle(dev, fmt):
     sums from 1.5 2^23 + 64 stay exact integers and the packing from the f32 bits is the
     reference's (sum + 64) >> 7 (gpssim.c:2257-2287)."""
     rng = np.random.default_rng(1024 + fmt)
-    n = 26004
+    n = 260004
     blk, nch, nav = synth_params(rng, 4, [7, 7, 7, 12], n)
     blk[0, :7]["gain"] = 1024
     blk[1, :7]["gain"] = [1024, -1024, 1024, -1024, 1000, -999, 1]

@@ -336,6 +336,36 @@ def test_cli_two_ranks_one_file(golden, world, handoff, gold, args):
     assert left == [], left                      # the hand-off file was consumed
 
 
+def test_cli_handoff_ignores_a_stale_file(golden):
+    """torchrun's default run id is "none" for every launch: a hand-off file an interrupted
+    earlier run left at the same path (here: junk carriers, another scenario's fingerprint) is
+    not consumed; rank 1 waits for rank 0's own file and the output is the reference's."""
+    import struct
+    args = ["-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8", "-i"]
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "gpssim.bin")
+        first = (int(round(65 * 10)) - 1) // 2          # rank 1's first block
+        stale = f"{out}.gss-carr-none-{first}"
+        with open(stale, "wb") as f:
+            f.write(struct.pack("<IQ", 0x67737364, 0x0123456789ABCDEF) +
+                    struct.pack("<16d", *([0.25] * 16)))
+        procs = []
+        for r in range(2):
+            env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK="0",
+                       TORCHELASTIC_RUN_ID="none")
+            env.pop("GSS_RUN_ID", None)
+            procs.append(subprocess.Popen(
+                [G.CLI_PATH, "-e", NAV] + args + ["-o", out], env=env,
+                stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
+        for p in procs:
+            _, err = p.communicate(timeout=300)
+            assert p.returncode == 0, err[-2000:]
+        h = hashlib.sha256(open(out, "rb").read()).hexdigest()
+        left = [f for f in os.listdir(td) if f != "gpssim.bin"]
+    assert h == golden["static_d65_b8_noiono"]["sha256"]
+    assert left == [], left
+
+
 def test_streaming_run_walk_path(dev, golden, monkeypatch):
     """gss_run with GSS_PATH=walk (the exact path for every block): the same bytes."""
     monkeypatch.setenv("GSS_PATH", "walk")

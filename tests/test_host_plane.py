@@ -218,3 +218,35 @@ def test_speculative_chain_exact_with_wrong_guesses():
         assert np.array_equal(end, end_ref), mode
         if mode != "counts":
             assert hit < 0.05 * int(nch.sum()), (mode, hit)
+
+
+def test_worker_pool_after_fork():
+    """The host plane's persistent worker threads do not survive fork(): a child that plans
+    (gss_pool_run on 8 threads) after the parent has grown its pools must still finish, with the
+    parent's rows (pool.c's pthread_atfork reset)."""
+    import os
+    import signal
+    import time
+    s = G.Scenario(NAV, llh=LOC, duration=10.0)
+    want_blk, want_nch = s.next(40, threads=8)          # grows the default pool in the parent
+    s2 = G.Scenario(NAV, llh=LOC, duration=10.0)
+    pid = os.fork()
+    if pid == 0:                                         # child: plan again, exit 0 if equal
+        try:
+            blk, nch = s2.next(40, threads=8)
+            ok = np.array_equal(nch, want_nch) and \
+                np.array_equal(blk.view(np.uint8), want_blk.view(np.uint8))
+            os._exit(0 if ok else 3)
+        except BaseException:
+            os._exit(4)
+    t0 = time.time()
+    while True:
+        done, status = os.waitpid(pid, os.WNOHANG)
+        if done:
+            break
+        if time.time() - t0 > 60:
+            os.kill(pid, signal.SIGKILL)
+            os.waitpid(pid, 0)
+            pytest.fail("the child's planning hung (worker pool after fork)")
+        time.sleep(0.05)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status

@@ -145,11 +145,13 @@ def test_first_below_pow2_vs_numpy(lgm):
 
 
 # ---------------------------------------------------------------------------------------------
-def synth_params(rng, nblk, nch_list, n_per_blk, ties=False, tiny=False, fs=2.6e6):
-    """random blocks of n_per_blk samples at sample rate fs (realistic Doppler and code rate)"""
+def synth_params(rng, nblk, nch_list, n_per_blk, ties=False, tiny=False, fs=None):
+    """random blocks of n_per_blk samples at sample rate fs (realistic Doppler and code rate);
+    fs defaults to the reference's 10 n_per_blk (gpssim.c:1877-1881), whose nominal chip rate the
+    fast kernel's window table assumes (gss_lin.h, gss_lin_win16_ok)"""
     blk = np.zeros((nblk, G.MAXCH), G.CHAN_DTYPE)
     nch = np.array(nch_list, np.int32)
-    delt = 1.0 / fs
+    delt = 1.0 / (fs if fs is not None else 10.0 * n_per_blk)
     nav = rng.integers(0, 1 << 30, size=(8, 60), dtype=np.uint32)
     for b in range(nblk):
         for k in range(nch[b]):
@@ -177,7 +179,7 @@ def synth_params(rng, nblk, nch_list, n_per_blk, ties=False, tiny=False, fs=2.6e
 def test_lines_render_like_oracle(fmt, case):
     seed = zlib.crc32(f"{fmt}:{case}".encode())      # stable across processes (no hash())
     rng = np.random.default_rng(seed)
-    n = 26000
+    n = 260000
     nch = [12, 0, 1, 7, 12, 3, 16, 11]
     blk, nchv, nav = synth_params(rng, len(nch), nch, n, ties=case == "ties_tiny",
                                   tiny=case == "ties_tiny")
@@ -234,7 +236,7 @@ def test_certified_fraction(kw, min_frac):
 
 
 # ---------------------------------------------------------------------------------------------
-def boundary_params(nb=36, n=26000, fs=2.6e6, seed=11):
+def boundary_params(nb=36, n=260000, fs=2.6e6, seed=11):
     """One-channel blocks whose code reaches 1023 (a wrap that starts a new data bit) and whose
     carrier reaches a LUT cell boundary at one sample each, within about 1e-11 of the real line:
     there the exact values may fall on either side of the line's."""
@@ -316,7 +318,7 @@ def test_integer_carrier_on_cell_boundaries_like_oracle():
     large powers of two, starts on a boundary): every block certified, bytes equal the oracle's
     (patches come only from the code chain here)."""
     rng = np.random.default_rng(17)
-    n = 26000
+    n = 260000
     blk, nch, nav = synth_params(rng, 4, [12, 12, 12, 12], n)
     one = float(1 << 25)
     for b in range(4):
@@ -339,7 +341,7 @@ def test_gain_bound_of_the_mfma_operand():
     certifies a block only when every |gain| <= 1024, so that the gain and its doubled
     data-bit difference are exact f16 integers; larger gains go to the exact path."""
     rng = np.random.default_rng(7)
-    n = 26000
+    n = 260000
     blk, nch, nav = synth_params(rng, 4, [7, 7, 7, 3], n)
     blk[0, :7]["gain"] = 1024                          # sum 7168 <= 8000: certified
     blk[1, :7]["gain"] = -1024

@@ -6,6 +6,7 @@
 set -e
 cd "$(dirname "$0")/.."
 name=$1; flags=$2
+case "$flags" in *LIN_MFMA=*) ;; *) flags="-DLIN_MFMA=2 $flags" ;; esac   # the Makefile's default
 mkdir -p _var/$name/obj
 HIPCC=/opt/rocm/bin/hipcc
 F="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Iinclude -Wno-unused-result -mllvm -amdgpu-mfma-vgpr-form=1 $flags"
@@ -21,5 +22,6 @@ if [ -n "$HOSTFLAGS" ]; then          # the host proof must agree with the kerne
     done
     HOSTOBJ=_var/$name/obj/host/*.o
 fi
-$HIPCC -shared -fPIC --offload-arch=gfx950 -o _var/$name/libgpssim_amd.so $HOSTOBJ \
+$HIPCC -shared -fPIC --offload-arch=gfx950 -Wl,--version-script=gps-sdr-sim_amd/exports.map \
+    -o _var/$name/libgpssim_amd.so $HOSTOBJ \
     _var/$name/obj/gss_synth.o _var/$name/obj/gss_run.o _var/$name/obj/gss_producers.o -lm -lpthread

@@ -1,0 +1,84 @@
+#!/bin/bash
+# One GPU-box session (gpurun), built from steps given on the command line, run in order.  Every
+# GPU step has its own time limit; the first step that fails ends the session (no retries), and
+# everything goes under gpurun_out/<tag>/.
+#
+#   bash tools/gpu.sh TAG step [step ...]
+#
+# steps:
+#   tests            pytest -m gpu (whole suite)          quick   the fast-path + parity GPU tests
+#   smoke            __graft_entry__.smoke()              bench   bench.py as the driver runs it
+#   ablate:V1,V2,..  kernel time of the current build and _var/<Vi> (tools/ablate.sh builds),
+#                    interleaved ROUNDS (default 2) times, bench.py --no-* legs off
+#   clock:V1,V2,..   in-kernel clock stamps of _var/<Vi> (LIN_STAMP builds), interleaved ROUNDS
+#   prof             rocprofv3 kernel trace + stats, then one PMC pass per counter group
+#                    (tools/profile.sh: traffic, SQ, LDS), never combined with other domains
+#   e2e:N            tools/e2e_cfg_probe.py N (gss_run over configs[N] end to end, traced)
+#   cmd:'...'        any other command, under a 300 s limit
+# env: BENCH_ARGS (bench step), STEPS/WARMUP (ablate), ROUNDS.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+log=$OUT/session.log
+echo "== $(date) $*" >> $log
+step() {  # name, exit status
+    echo "$1 rc=$2" >> $log
+    [ "$2" -eq 0 ] || { echo "session stopped at $1 (rc=$2)" >> $log; exit "$2"; }
+}
+for s in "$@"; do
+    case "$s" in
+    tests)
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider \
+            --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+        step tests $? ;;
+    quick)
+        timeout -k 10 600 python -u -m pytest tests/test_gpu_lin.py tests/test_gpu_parity.py -x -q \
+            -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_quick.log 2>&1
+        step quick $? ;;
+    smoke)
+        timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+        step smoke $? ;;
+    bench)
+        timeout -k 10 600 python bench.py ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err
+        step bench $? ;;
+    ablate:*)
+        vs=${s#ablate:}
+        for r in $(seq ${ROUNDS:-2}); do
+            for v in cur ${vs//,/ }; do
+                lib=gps-sdr-sim_amd/lib/libgpssim_amd.so
+                [ "$v" != cur ] && lib=_var/$v/libgpssim_amd.so
+                line=$(GSS_ALLOW_LIB_OVERRIDE=1 GSS_LIB_PATH=$lib timeout -k 10 200 python bench.py \
+                    --steps ${STEPS:-20} --warmup ${WARMUP:-5} --no-configs --no-e2e \
+                    --no-cpu-baseline --no-exact --no-pmc --no-sustained 2>>$OUT/ablate.err | tail -1)
+                step "ablate $v" $?
+                echo "$v $(echo "$line" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["stages_ms"]["fast_path"], d["value"])')" >> $OUT/ablate.log
+            done
+        done ;;
+    clock:*)
+        vs=${s#clock:}
+        for r in $(seq ${ROUNDS:-2}); do
+            for v in ${vs//,/ }; do
+                GSS_ALLOW_LIB_OVERRIDE=1 GSS_LIB_PATH=_var/$v/libgpssim_amd.so timeout -k 10 200 \
+                    python tools/clock_stamp.py --label $v >> $OUT/clock.jsonl 2>>$OUT/clock.err
+                step "clock $v" $?
+            done
+        done ;;
+    prof)
+        bash tools/profile.sh $TAG/prof
+        step prof $? ;;
+    e2e:*)
+        n=${s#e2e:}
+        GSS_RUN_TRACE=1 timeout -k 10 200 python tools/e2e_cfg_probe.py $n > $OUT/e2e_cfg$n.out \
+            2> $OUT/e2e_cfg$n.err
+        step "e2e $n" $? ;;
+    cmd:*)
+        timeout -k 10 300 bash -c "${s#cmd:}" >> $OUT/cmd.log 2>&1
+        step "cmd" $? ;;
+    *)
+        step "unknown step $s" 2 ;;
+    esac
+done
+echo done >> $log
