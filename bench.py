@@ -59,6 +59,32 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters
 METRIC = "IQ MSamples/s (and × real-time) at 2.6 MS/s, 12 sats, -b 16; 1/2/4/8 GPU"
 BOX_CORES = 16                 # host threads for the planner/proofs (the box's CPU share per GPU)
 
+# The fast kernel's compute rooflines, in channel-samples/s: every SIMD issuing
+# nothing but the step loop at the top clock.  VALU: per wave channel-step v_lshl_add_u64 4.60 +
+# v_lshrrev_b32_sdwa with an SGPR window 4.38 + v_alignbit_b32 4.37 + v_and_b32 2.75 SIMD cycles
+# at 4 waves per SIMD (profiles/round2/issue_ubench2.log) + a quarter of a
+# v_mfma_f32_16x16x32_f16, 3.5 (profiles/round3/mfma_issue_ubench.log: 57.3 vs 43.4 cycles per
+# body); LDS: one conflict-free ds_read_b32 (2 LDS cycles for 64 channel-samples) per CU-cycle
+# pair (MI355X_MICROARCH.md, LDS).  Same step loop for -b 16, -b 8 and -b 1.
+SIMDS, CUS, CLOCK_MAX_HZ = 1024, 256, 2.4e9
+VALU_CYC_PER_CHSTEP = 4.60 + 4.38 + 4.37 + 2.75 + 3.5
+VALU_PEAK_CHS = SIMDS * 64 * CLOCK_MAX_HZ / VALU_CYC_PER_CHSTEP
+LDS_PEAK_CHS = CUS * CLOCK_MAX_HZ * 64 / 2.0
+
+
+def compute_roofline(ch_samples, kern_ms):
+    """achieved channel-samples/s of one fast-kernel launch against the VALU issue bound (the
+    binding pipe) and the LDS bound"""
+    if kern_ms <= 0:
+        return None
+    a = ch_samples / (kern_ms * 1e-3)
+    return {"bound": "valu", "achieved": round(a / 1e12, 4), "peak": round(VALU_PEAK_CHS / 1e12, 4),
+            "unit": "T channel-samples/s", "frac": round(a / VALU_PEAK_CHS, 4),
+            "lds_peak": round(LDS_PEAK_CHS / 1e12, 4), "lds_frac": round(a / LDS_PEAK_CHS, 4),
+            "channel_samples_per_launch": int(ch_samples),
+            "model": f"{VALU_CYC_PER_CHSTEP:.2f} SIMD cycles per wave channel-step, "
+                     f"{SIMDS} SIMDs at {CLOCK_MAX_HZ / 1e9:.1f} GHz"}
+
 # BASELINE.json configs[2..4] (per_config); configs[1] is the headline, configs[0] the CPU case
 CONFIGS = [
     {"name": "configs[2]", "desc": "dynamic -u circle.csv -s 2600000 -b 8, 300 s",
@@ -80,13 +106,14 @@ def cpu_quota():
         return None
 
 
-def cpu_baseline(seconds=30):
+def cpu_baseline(seconds=30, over_seconds=10):
     """The reference program (compiled from its own sources by oracle/Makefile) on a bounded
     sample of the static scenario to /dev/null: one process on one core, then one process per
-    core the affinity mask offers (it is single-threaded by construction), each pinned to its
-    core.  `cores` is the affinity size; `cpu_quota` the cgroup's CPU limit when one is set (the
-    aggregate can never exceed it).  Falls back to the repo's CPU restatement ("port") when the
-    reference binary is absent."""
+    CPU the box grants (it is single-threaded by construction): min(affinity mask, ceil(cgroup
+    cpu.max quota)) processes, each pinned to its own core -- `cores` is that number, the CPUs
+    the aggregate actually had.  `oversubscribed` is one process per core of the whole affinity
+    mask (a shorter sample), which the quota throttles, kept only for comparison.  Falls back to
+    the repo's CPU restatement ("port") when the reference binary is absent."""
     ref = os.path.join(REPO, "oracle", "_ref", "gps-sdr-sim")
     port = os.path.join(REPO, "oracle", "_ref", "gss_oracle_cli")
     kind, exe = ("reference", ref) if os.path.exists(ref) else ("port", port)
@@ -96,14 +123,13 @@ def cpu_baseline(seconds=30):
         avail = sorted(os.sched_getaffinity(0))
     except AttributeError:
         avail = list(range(os.cpu_count() or 1))
-    cores = len(avail)
-    args = [exe, "-e", NAV, "-l", ",".join(map(str, LOC)), "-d", str(seconds), "-s",
-            str(int(FS)), "-b", "16", "-o", "/dev/null"]
+    quota = cpu_quota()
+    cores = len(avail) if quota is None else max(1, min(len(avail), int(-(-quota // 1))))
     env = dict(os.environ, GSS_THREADS="1")
-    blocks = int(seconds * 10) - 1
-    samples = blocks * FS / 10
 
-    def run(n):
+    def run(n, sec):
+        args = [exe, "-e", NAV, "-l", ",".join(map(str, LOC)), "-d", str(sec), "-s",
+                str(int(FS)), "-b", "16", "-o", "/dev/null"]
         t0 = time.perf_counter()
         # pinned in the child before it runs the program (no launcher such as taskset, whose
         # own exec would be one more hop)
@@ -114,21 +140,35 @@ def cpu_baseline(seconds=30):
         ok = all(p.wait() == 0 for p in ps)
         return (time.perf_counter() - t0) if ok else None
 
-    w1 = run(1)
-    wn = run(cores) if w1 is not None and cores > 1 else w1
+    def rate(n, sec, wall):
+        return n * (int(sec * 10) - 1) * FS / 10 / wall / 1e6
+
+    blocks = int(seconds * 10) - 1
+    w1 = run(1, seconds)
+    wn = run(cores, seconds) if w1 is not None and cores > 1 else w1
     if w1 is None or wn is None:
         return None
-    one = samples / w1 / 1e6
-    agg = cores * samples / wn / 1e6
+    one, agg = rate(1, seconds, w1), rate(cores, seconds, wn)
+    over = None
+    if len(avail) > cores:
+        wo = run(len(avail), over_seconds)
+        if wo is not None:
+            over = {"value": round(rate(len(avail), over_seconds, wo), 2),
+                    "processes": len(avail),
+                    "sample": f"static -d {over_seconds} -b 16 per process, {len(avail)} "
+                              f"processes on the affinity mask under a {quota}-CPU quota: "
+                              f"wall {wo:.2f} s"}
     return {"value": round(agg, 2), "unit": "MS/s", "cores": cores, "kind": kind,
-            "cpu_quota": cpu_quota(),
+            "cpu_quota": quota, "affinity_cores": len(avail),
             "single_core": {"value": round(one, 3), "cores": 1,
                             "x_realtime": round(one / (FS / 1e6), 2)},
             "x_realtime": round(agg / (FS / 1e6), 2),
+            "oversubscribed": over,
             "sample": f"static -d {seconds} -b 16 -o /dev/null ({blocks} blocks x 260000 "
                       f"samples) per process; 1 process: wall {w1:.2f} s; {cores} concurrent "
-                      f"processes, one per core of the affinity mask (cores {avail[0]}.."
-                      f"{avail[-1]}): wall {wn:.2f} s"}
+                      f"processes, one per granted CPU (min(affinity {len(avail)}, quota "
+                      f"{quota})), pinned to cores {avail[0]}..{avail[cores - 1]}: wall "
+                      f"{wn:.2f} s"}
 
 
 def progress(msg):
@@ -285,6 +325,7 @@ def per_config(G, torch, dev, dev_t, stream, steps, warmup, threads, e2e=True):
         msps = samples * steps / el / 1e6
         per_launch = (res.n_fast * res.bb) / len(res.batches)
         achieved = per_launch / (lin_ms * 1e-3) / 1e9 if lin_ms > 0 else 0.0
+        comp = compute_roofline(res.ch_samples_fast / len(res.batches), lin_ms)
         out.append({
             "config": c["name"], "workload": c["desc"], "fmt": c["fmt"],
             "value": round(msps, 2), "unit": "MS/s", "x_realtime": round(msps / (c["fs"] / 1e6), 1),
@@ -292,10 +333,13 @@ def per_config(G, torch, dev, dev_t, stream, steps, warmup, threads, e2e=True):
             "blocks_fast_path": res.n_fast, "blocks_total": res.nblk,
             "launches_per_step": len(res.batches), "channels_max": res.nch_max,
             "bytes_per_step": res.nblk * res.bb,
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "algorithmic_bytes_per_sample": res.bb / res.npb,
-                         "kernel_ms_per_launch": round(lin_ms, 3)},
+            # the binding roofline: the step loop's VALU issue (the -b 8 / -b 1 outputs are 2 and
+            # 0.25 B per sample, far below the HBM write bound); the HBM one beside it
+            "roofline": dict(comp or {}, kernel_ms_per_launch=round(lin_ms, 3)),
+            "roofline_hbm": {"bound": "hbm", "achieved": round(achieved, 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(achieved / HBM_PEAK_GBS, 4),
+                             "algorithmic_bytes_per_sample": res.bb / res.npb},
             "host_plan_s": round(plan_s, 3), "host_linearize_s": round(res.lin_s, 3)})
         res.free()
         del blk, nch, s
@@ -329,29 +373,29 @@ E2E_SLOT_BYTES = 128 * 1040000  # gss_run slot size: 128 blocks at 2.6 MS/s -b 1
 def e2e_run(G, dev, threads, window=1800.0, batch=None, fs=FS, fmt=16, kw=None, slope=True,
             desc=None):
     """gss_run over a whole run into a discarding sink, wall-clocked (planner, proofs, uploads,
-    kernels, D2H into pinned buffers and the sink, overlapped).  With `slope` a second run of a
-    third of the length gives the steady-state rate (the slope; the rest is the fixed start-up).
-    Read against d2h_ceiling_GBps, the measured device -> pinned host copy rate of one slot."""
+    kernels, D2H into pinned buffers and the sink, overlapped).  With `slope` the steady-state
+    rate comes from the same run's sink calls (one per batch, in run order): bytes delivered
+    from the call that completes the first quarter of the run to the last call, over the time
+    between them; `startup_s` is the time to the first call.  Read against d2h_ceiling_GBps, the
+    measured device -> pinned host copy rate of one slot in this process."""
     kw = kw if kw is not None else {"llh": LOC}
     bb = G.block_bytes(int(round(fs / 10)), fmt)
     if batch is None:
         batch = max(1, E2E_SLOT_BYTES // bb)
 
-    def one(w):
-        s = G.Scenario(NAV, duration=w, samp_freq=fs, data_format=fmt, **kw)
-        got = {"bytes": 0, "blocks": 0}
+    s = G.Scenario(NAV, duration=window, samp_freq=fs, data_format=fmt, **kw)
+    got = {"bytes": 0, "blocks": 0}
+    marks = []                                       # (time, bytes so far) after each sink call
 
-        def sink(mv, first, nb):
-            got["bytes"] += len(mv)
-            got["blocks"] += nb
+    def sink(mv, first, nb):
+        got["bytes"] += len(mv)
+        got["blocks"] += nb
+        marks.append((time.perf_counter(), got["bytes"]))
 
-        t0 = time.perf_counter()
-        dev.run(s, sink, batch=batch, threads=threads)
-        return time.perf_counter() - t0, got["blocks"], got["bytes"], s.n_per_blk
-
-    if slope:
-        ws, bs, _, _ = one(window / 3)
-    wall, blocks, nbytes, n_per_blk = one(window)
+    t0 = time.perf_counter()
+    dev.run(s, sink, batch=batch, threads=threads)
+    wall = time.perf_counter() - t0
+    blocks, nbytes, n_per_blk = got["blocks"], got["bytes"], s.n_per_blk
     samples = blocks * n_per_blk
     ceiling = d2h_ceiling(batch * bb)
     out = {"value": round(samples / wall / 1e6, 2), "unit": "MS/s",
@@ -361,12 +405,79 @@ def e2e_run(G, dev, threads, window=1800.0, batch=None, fs=FS, fmt=16, kw=None, 
            "frac_of_d2h_ceiling": round(nbytes / wall / 1e9 / ceiling, 3) if ceiling else None,
            "workload": (desc or f"static -b {fmt}, {window:g} s") +
                        f" through gss_run (batch {batch} blocks), discarding sink"}
-    if slope:
-        sl = (blocks - bs) / (wall - ws)
-        out.update({"steady_MSps": round(sl * n_per_blk / 1e6, 1),
-                    "steady_d2h_GBps": round(sl * nbytes / blocks / 1e9, 2),
-                    "startup_s": round(wall - blocks / sl, 3)})
+    if slope and len(marks) >= 8:
+        q = next(i for i, (_, b) in enumerate(marks) if b >= nbytes / 4)
+        (tq, bq), (tl, bl) = marks[q], marks[-1]
+        if tl > tq and bl > bq:
+            rate = (bl - bq) / (tl - tq)                 # bytes/s in the run's steady part
+            out.update({"steady_MSps": round(rate / bb * n_per_blk / 1e6, 1),
+                        "steady_d2h_GBps": round(rate / 1e9, 2),
+                        "steady_frac_of_d2h_ceiling": round(rate / 1e9 / ceiling, 3)
+                        if ceiling else None,
+                        "startup_s": round(marks[0][0] - t0, 3),
+                        "steady_window": f"sink calls {q + 1}..{len(marks)} of {len(marks)}"})
     return out
+
+GATHER_FS, GATHER_WINDOW_S = 2.0e7, 450.0   # configs[3]: 3600 s at 20 MS/s over 8 GPUs
+
+
+def gather_leg(G, torch, td, dev, dev_t, rank, world, coll_t, walker, threads, window_s,
+               host_wire):
+    """BASELINE configs[3] as a whole-node run (N > 1 only): static -s 20000000 -b 16, each rank
+    owning window_s seconds of one world * window_s run (weak scaling: 450 s per rank is
+    configs[3]'s 3600 s at 8 GPUs), each rank's window planned (baton, chain run ahead) and
+    resident, then rendered chunk by chunk and gathered in run order to rank 0 over RCCL point to
+    point (gpssim_amd.node: render_chunks, chunk_source, ordered_gather) into a discarding sink.
+    Timed from the first render launch to the last byte at rank 0 (max over ranks): the
+    node's data path, xGMI included, file system excluded."""
+    from gpssim_amd.node import chunk_plan, chunk_source, ordered_gather, rank_blocks, \
+        render_chunks
+    from gpssim_amd.render import DeviceWindow
+    from gpssim_amd.shard import Baton, plan_window
+    t0 = time.perf_counter()
+    scn = G.Scenario(NAV, llh=LOC, duration=window_s * world, samp_freq=GATHER_FS,
+                     data_format=16)
+    nb_all, npb = scn.n_blocks, scn.n_per_blk
+    bb = G.block_bytes(npb, 16)
+    chunk = max(1, (256 << 20) // bb)
+    b0, b1 = rank_blocks(nb_all, rank, world)
+    blk, nch, ck, pt = plan_window(scn, b0, b1 - b0, baton=Baton(td, rank, world, device=coll_t),
+                                   threads=threads, walker=walker)
+    win = DeviceWindow(torch, dev, dev_t, blk, nch, scn.nav_table(), npb, 16, ck=ck,
+                       threads=threads, batch=chunk)
+    plan_s = time.perf_counter() - t0
+    got = {"bytes": 0}
+
+    def sink(t):
+        got["bytes"] += t.numel()
+
+    def make_buf(nb):
+        return torch.empty(nb * bb, dtype=torch.uint8, device="cpu" if host_wire else dev_t)
+
+    plan = chunk_plan(nb_all, world, chunk)
+    td.barrier()
+    torch.cuda.synchronize(dev_t)
+    t1 = time.perf_counter()
+    _, evs = render_chunks(torch, win, dev_t)
+    get_chunk = chunk_source(torch, win, b0, chunk, evs, dev_t,
+                             host_wire=host_wire and rank != 0)
+    ordered_gather(plan, rank, td, get_chunk, make_buf, sink if rank == 0 else None)
+    torch.cuda.synchronize(dev_t)
+    el = time.perf_counter() - t1
+    t = torch.tensor([el, plan_s], dtype=torch.float64, device=coll_t)
+    td.all_reduce(t, op=td.ReduceOp.MAX)
+    el, plan_s = t.tolist()
+    total = nb_all * bb
+    win.free()
+    return {"workload": f"static -s 20000000 -b 16, {window_s * world:g} s over {world} ranks "
+                        f"({window_s:g} s = {b1 - b0} blocks per rank), rendered and gathered "
+                        f"in run order to rank 0 (chunks of {chunk} blocks), discarding sink",
+            "wire": "gloo via host memory (rehearsal)" if host_wire else "RCCL point to point",
+            "bytes": total, "bytes_at_rank0": got["bytes"] if rank == 0 else None,
+            "wall_s": round(el, 3), "GBps_at_rank0": round(total / el / 1e9, 2),
+            "MSps": round(nb_all * npb / el / 1e6, 1), "host_plan_s_max": round(plan_s, 3),
+            "spec_rows_translated_rank": pt.get("spec_hits")}
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -386,6 +497,10 @@ def main():
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the live rocprofv3 traffic passes (roofline.traffic)")
     ap.add_argument("--threads", type=int, default=BOX_CORES)
+    ap.add_argument("--no-gather", action="store_true",
+                    help="skip the whole-node gather leg (N > 1: configs[3] to rank 0)")
+    ap.add_argument("--gather-window", type=float, default=GATHER_WINDOW_S,
+                    help="seconds per rank of the gather leg's 20 MS/s run")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -419,20 +534,28 @@ def main():
     # ---- host control plane for this rank's window (untimed setup) ----
     # planned once per node: each rank seeks to its window, produces its rows, and receives the
     # 16 slot carriers at its first block from rank r-1 (gpssim_amd.shard)
-    from gpssim_amd.shard import Baton, plan_rank
+    # the carrier chain run ahead on this GPU (shard.device_walker) unless GSS_BENCH_HOST_CHAIN=1
+    from gpssim_amd.shard import Baton, device_walker, plan_rank
+    dev = G.Device(local)
+    walker = None if os.environ.get("GSS_BENCH_HOST_CHAIN") == "1" else device_walker(dev, torch)
     baton = Baton(td, rank, world, device=coll_t) if dist else None
     t_plan0 = time.perf_counter()
     blk, nch, ck, nav, npb, plan_t = plan_rank(NAV, rank, world, args.window, llh=LOC,
                                                samp_freq=FS, data_format=args.fmt,
-                                               threads=args.threads, baton=baton)
+                                               threads=args.threads, baton=baton, walker=walker)
     host_plan_s = time.perf_counter() - t_plan0
     progress(f"planned {len(nch)} blocks in {host_plan_s:.2f} s")
 
-    dev = G.Device(local)
     stream = torch.cuda.current_stream(dev_t).cuda_stream
     res = DeviceWindow(torch, dev, dev_t, blk, nch, nav, npb, args.fmt, ck=ck,
                        threads=args.threads, batch=len(nch))
     nblk = res.nblk
+
+    if single and not args.no_exact and res.d_ck is None:
+        # the exact path leg walks from the planner's checkpoints as in earlier rounds (rows
+        # planned with the chain run ahead carry none)
+        from gpssim_amd.render import block_checkpoints
+        res.d_ck = torch.from_numpy(block_checkpoints(blk, nch, npb)).to(dev_t)
 
     def step_serial():
         dev.synth_device(res.d_blk.data_ptr(), res.d_nch.data_ptr(), res.nch_max,
@@ -470,7 +593,8 @@ def main():
         torch.cuda.synchronize(dev_t)
         sustained_ms = round(dev.timing_lin()[1], 3)
     mine = [host_plan_s, plan_t["seek_s"], plan_t["rows_s"], plan_t["wait_s"],
-            plan_t["chain_s"], host_lin_s, float(plan_t["rows_out"])]
+            plan_t["chain_s"], host_lin_s, float(plan_t["rows_out"]),
+            float(plan_t.get("spec_hits", -1))]
     per_rank = [mine]
     if dist:
         t = torch.tensor([elapsed, ck_ms, syn_ms, host_plan_s, lin_ms, host_lin_s],
@@ -485,7 +609,10 @@ def main():
         {"rank": r, "host_plan_s": round(v[0], 3), "seek_s": round(v[1], 3),
          "rows_s": round(v[2], 3), "baton_wait_s": round(v[3], 3),
          "carrier_chain_s": round(v[4], 3), "host_linearize_s": round(v[5], 3),
-         "rows_produced": int(v[6])} for r, v in enumerate(per_rank)]
+         "rows_produced": int(v[6]),
+         "carrier_chain": "run ahead on the GPU" if v[7] >= 0 else "host walk",
+         "spec_rows_translated": int(v[7]) if v[7] >= 0 else None}
+        for r, v in enumerate(per_rank)]
 
     samples_rank = nblk * npb
     exact = None
@@ -508,6 +635,7 @@ def main():
     # the dominant kernel is gss_lin_kernel; its algorithmic bytes are the certified blocks'
     bytes_launch = res.n_fast * res.bb
     achieved = bytes_launch / (lin_ms * 1e-3) / 1e9 if lin_ms > 0 else 0.0
+    comp_head = compute_roofline(res.ch_samples_fast, lin_ms)
     workload = (f"static -l {LOC[0]},{LOC[1]},{LOC[2]:g} -s 2600000 -b {args.fmt}, "
                 f"{args.window:g} s per GPU ({nblk} blocks x {npb} samples)")
     version = G.lib().gss_version().decode()
@@ -525,6 +653,11 @@ def main():
             traffic_src = f"{traffic_src}; committed profile: {s2}"
 
     progress(f"traffic: {traffic_src[:120]}")
+    gather = None
+    if dist and not args.no_gather:
+        gather = gather_leg(G, torch, td, dev, dev_t, rank, world, coll_t, walker, args.threads,
+                            args.gather_window, host_wire=rehearse)
+        progress(f"gather: {gather['GBps_at_rank0']} GB/s at rank 0")
     configs = e2e = None
     # the headline's end-to-end leg before the per-config legs: after configs[4]'s -b 1 leg (rows
     # and prover threads) this process's -b 16 downloads ran at ~39 instead of ~56 GB/s, which
@@ -566,8 +699,10 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "profile": prof},
+        "roofline_compute": comp_head,
         "cpu_baseline": cpu,
         "per_config": configs,
+        "gather": gather,
         "e2e": e2e,
         "exact_path": exact,
         "lib": {"path": os.path.relpath(G.LIB_PATH, REPO), "version": version, "sha16": sha},

@@ -149,7 +149,8 @@ GSS_LIN_FN gss_lin_kc gss_lin_kernel_at(uint64_t x0, uint64_t xs, uint64_t z0, u
     const int64_t n0 = p & ~(int64_t)(GSS_LIN_SEG - 1);
     const unsigned __int128 zn = (unsigned __int128)z0 + (unsigned __int128)(uint64_t)n0 * zs;
     const int64_t chips = (int64_t)(zn >> 50), e0 = gss_lin_e0((uint64_t)chips);
-    const __int128 z = (__int128)z0 + (__int128)c * (__int128)zs - ((__int128)(chips - e0) << 50);
+    const __int128 z = (__int128)z0 + (__int128)c * (__int128)zs -
+                      (__int128)(chips - e0) * ((__int128)1 << 50);
     const unsigned __int128 zk = (unsigned __int128)((z + (int64_t)gss_lin_za(zs)) >> GSS_LIN_CSH);
     const uint64_t za = (uint64_t)(uint32_t)zk + (uint32_t)lane;       /* anchor add, carry */
     const uint64_t zw = (uint64_t)(uint32_t)za + (uint64_t)s * gss_lin_dz(zs);   /* low word */

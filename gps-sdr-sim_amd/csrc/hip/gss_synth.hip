@@ -526,7 +526,8 @@ static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole ch
    2 no chip-window loads, 4 no LUT reads, 8 every block stores into one of 8 blocks (L2),
    32 no alignbit (VALU work), 64 no window reads in the render loop (LDS work), 128 the LUT
    address without the chip sign (no bank conflicts between a cell's two signs), 256 windows
-   made by the scalar unit in SGPRs (no window pass, no LDS window reads) */
+   made by the scalar unit in SGPRs (no window pass, no LDS window reads), 512 no window pass
+   (the loop still reads the records' windows from LDS) */
 #ifndef LIN_ABLATE
 #define LIN_ABLATE 0
 #endif
@@ -1271,7 +1272,7 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
         /* the channels with a gain change or patches in this chunk (wave-uniform) */
         const uint64_t fmask = __builtin_amdgcn_ballot_w64(my_flags != 0);
         wave_sync_lds();
-#if !LIN_SWIN && !(LIN_ABLATE & 256)
+#if !LIN_SWIN && !(LIN_ABLATE & (256 | 512))
         /* ---- the chip windows, lane (k, s) ---- */
         for (int i = lane; i < nc * LIN_CH; i += 64) {
             const int k = i / LIN_CH;

@@ -153,7 +153,7 @@ static i128 to_fix(double x, int k, int *inexact)
     if (x == 0.0)
         return 0;
     if (sh >= 0)
-        return (i128)m << sh;
+        return (i128)m * ((i128)1 << sh);            /* no left shift of a negative value */
     if (sh < -62) {
         *inexact = 1;
         return 0;

@@ -4,13 +4,16 @@ options>` under torchrun, one process per GPU.
 Every rank renders its contiguous block range of the run on its own GPU into HBM (the time-window
 shard: [B r/N, B (r+1)/N), the partition the C CLI's pwrite path uses, gps_sdr_sim.c).  Each rank
 plans only its own window (gpssim_amd.shard.plan_window: seek, deferred rows, the slot carriers
-handed on from the rank before).  Rank 0
+handed on from the rank before, the chain run ahead on its GPU).  Rank 0
 then writes the whole run to the reference's sink -- a file, or stdout with `-o -`
 (gpssim.c:2101-2111, 2276-2287) -- in run order: its own chunks straight from HBM, every other
 rank's chunks received point to point over RCCL (xGMI) into two alternating receive buffers, the
 next chunk in flight while the current one is copied to pinned host memory and written.  Chunks
-are `GSS_CHUNK_BLOCKS` blocks (default 256: 266 MB at -b 16, 2.6 MS/s), so rank 0 holds two of
-them beside its own slice.  The gather is the only collective; it moves each byte once.
+are `GSS_CHUNK_BLOCKS` blocks (default: about 256 MB, 256 blocks at -b 16, 2.6 MS/s), so rank 0
+holds two of them beside its own slice.  Rendering and sending overlap: a rank launches all its
+chunks on a render stream of their own, and each chunk is sent (or written) as soon as its own
+render event has passed, while the later chunks still render.  The gather is the only
+collective; it moves each byte once.
 
 With WORLD_SIZE == 1 it is the single-process run (gss_run, overlapped planner/GPU/sink).
 Backend: nccl (RCCL) for GPU tensors; gloo moves the chunks through host memory (tests).
@@ -25,6 +28,39 @@ from . import Device, Scenario, block_bytes
 def rank_blocks(n_blocks, rank, world):
     """[first, last) blocks of `rank` (same partition as the C CLI, gps_sdr_sim.c run_rank)."""
     return n_blocks * rank // world, n_blocks * (rank + 1) // world
+
+
+def default_chunk_blocks(bb):
+    """blocks per gather chunk: GSS_CHUNK_BLOCKS, else about 256 MB of output"""
+    env = os.environ.get("GSS_CHUNK_BLOCKS")
+    return int(env) if env else max(1, (256 << 20) // bb)
+
+
+def render_chunks(torch, win, dev_t):
+    """Launch every batch (= gather chunk) of DeviceWindow win on a render stream of its own, in
+    order; returns (stream, per-batch completion events)."""
+    st = torch.cuda.Stream(dev_t)
+    evs = []
+    for i in range(len(win.batches)):
+        win.step_batch(i, st.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(st)
+        evs.append(ev)
+    return st, evs
+
+
+def chunk_source(torch, win, first_block, chunk_blocks, evs, dev_t, host_wire):
+    """get_chunk(first, nb) for ordered_gather: the chunk's bytes in HBM once its render event
+    has passed (the caller's stream waits for it, so a send or copy queued behind runs after it,
+    while later chunks still render); host_wire: a host copy (gloo)"""
+    bb = win.bb
+
+    def get_chunk(first, nb):
+        i = (first - first_block) // chunk_blocks
+        torch.cuda.current_stream(dev_t).wait_event(evs[i])
+        t = win.out[(first - first_block) * bb:(first - first_block + nb) * bb]
+        return t.cpu() if host_wire else t
+    return get_chunk
 
 
 def chunk_plan(n_blocks, world, chunk_blocks):
@@ -100,28 +136,25 @@ def run_node(argv, rank, world, local, backend="nccl", chunk_blocks=None, thread
     import torch
     import torch.distributed as dist
     from .render import DeviceWindow
-    from .shard import Baton, plan_window
+    from .shard import Baton, device_walker, plan_window
 
-    chunk_blocks = chunk_blocks or int(os.environ.get("GSS_CHUNK_BLOCKS", "256"))
     scn, out_file = Scenario.from_cli(argv)
     n_blocks, npb, fmt = scn.n_blocks, scn.n_per_blk, scn.data_format
     bb = block_bytes(npb, fmt)
+    chunk_blocks = chunk_blocks or default_chunk_blocks(bb)
     torch.cuda.set_device(local)
     dev_t = torch.device("cuda", local)
     dev = Device(local)
     b0, b1 = rank_blocks(n_blocks, rank, world)
     baton = Baton(dist, rank, world, device=dev_t if backend == "nccl" else "cpu")
-    blk, nch, ck, _ = plan_window(scn, b0, b1 - b0, baton=baton, threads=threads)
+    blk, nch, ck, _ = plan_window(scn, b0, b1 - b0, baton=baton, threads=threads,
+                                  walker=device_walker(dev, torch))
     win = DeviceWindow(torch, dev, dev_t, blk, nch, scn.nav_table(), npb, fmt, ck=ck,
-                       threads=threads)
-    win.step(torch.cuda.current_stream(dev_t).cuda_stream)
-    torch.cuda.synchronize(dev_t)
-    win.free_inputs()
+                       threads=threads, batch=chunk_blocks)
     wire_gpu = backend == "nccl"
-
-    def get_chunk(first, nb):
-        t = win.out[(first - b0) * bb:(first - b0 + nb) * bb]
-        return t if (wire_gpu or rank == 0) else t.cpu()
+    _, evs = render_chunks(torch, win, dev_t)
+    get_chunk = chunk_source(torch, win, b0, chunk_blocks, evs, dev_t,
+                             host_wire=not (wire_gpu or rank == 0))
 
     def make_buf(nb):
         return torch.empty(nb * bb, dtype=torch.uint8, device=dev_t if wire_gpu else "cpu")
@@ -138,7 +171,9 @@ def run_node(argv, rank, world, local, backend="nccl", chunk_blocks=None, thread
             os.close(fd)
     else:
         ordered_gather(plan, rank, dist, get_chunk, make_buf, None)
+    torch.cuda.synchronize(dev_t)
     dist.barrier()
+    win.free()
     dev.close()
     return total
 

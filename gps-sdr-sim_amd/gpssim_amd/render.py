@@ -9,7 +9,19 @@ import time
 
 import numpy as np
 
-from . import CHAN_DTYPE, LIN_DTYPE, MAXCH, NCK, block_bytes, ca_table, linearize
+from . import (CHAN_DTYPE, LIN_DTYPE, MAXCH, NCK, block_bytes, ca_table, carr_advance_ck,
+               linearize)
+
+
+def block_checkpoints(blk, nch, n_per_blk, blocks=None):
+    """the carrier checkpoints [nblk, 16, NCK] of the exact path's Stage A (gss_carr_advance_ck
+    from each row's carr0), for `blocks` (default all); zeros elsewhere"""
+    ck = np.zeros((len(nch), MAXCH, NCK), np.float64)
+    for b in (range(len(nch)) if blocks is None else blocks):
+        for k in range(int(nch[b])):
+            ck[b, k] = carr_advance_ck(float(blk[b, k]["carr0"]), float(blk[b, k]["carr_step"]),
+                                       n_per_blk)[1]
+    return ck
 
 
 class DeviceWindow:
@@ -24,6 +36,9 @@ class DeviceWindow:
         self.lin_s = time.perf_counter() - t0
         self.nblk = len(nch)
         self.n_fast = int(fast.sum())
+        # channel-samples the fast kernel renders per pass (its compute roofline's unit)
+        self.ch_samples_fast = int(np.asarray(nch)[fast.astype(bool)].astype(np.int64).sum()) * \
+            int(n_per_blk)
         self.nch_max = int(nch.max()) if len(nch) else 1
         ca = ca_table()
         self.n_ca, self.n_nav = len(ca), len(nav)
@@ -32,6 +47,10 @@ class DeviceWindow:
         def up(a):
             return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev_t)
 
+        if ck is None and self.n_fast < self.nblk:
+            # rows planned without checkpoints (the chain run ahead, shard.plan_window): the
+            # exact path's Stage A starts from them, so give the uncertified blocks theirs
+            ck = block_checkpoints(blk, nch, n_per_blk, np.nonzero(fast == 0)[0])
         self.d_blk, self.d_nch, self.d_lin = up(blk), up(nch), up(lin)
         self.d_ck = up(ck) if ck is not None else None
         self.d_ca, self.d_nav, self.d_fast = up(ca), up(nav), up(fast)
@@ -49,8 +68,13 @@ class DeviceWindow:
 
     def step(self, stream=0):
         """Render every block of the window into self.out (stream-ordered)."""
+        for i in range(len(self.batches)):
+            self.step_batch(i, stream)
+
+    def step_batch(self, i, stream=0):
+        """Render batch i (blocks batches[i][0] .. batches[i][1]) into its part of self.out."""
         cs, ls, ks = CHAN_DTYPE.itemsize * MAXCH, LIN_DTYPE.itemsize * MAXCH, 8 * MAXCH * NCK
-        for b0, b1, d_fb, n_fb in self.batches:
+        for b0, b1, d_fb, n_fb in self.batches[i:i + 1]:
             self.dev.synth_lin_device(
                 self.d_blk.data_ptr() + b0 * cs, self.d_nch.data_ptr() + b0 * 4, self.nch_max,
                 self.d_lin.data_ptr() + b0 * ls, self.d_fast.data_ptr() + b0 * 4,

@@ -250,3 +250,34 @@ def test_worker_pool_after_fork():
             pytest.fail("the child's planning hung (worker pool after fork)")
         time.sleep(0.05)
     assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status
+
+
+@pytest.mark.parametrize("fmt,fs,dur,first,count", [(1, 2.6e6, 1200.0, 4000, 5000),
+                                                    (16, 2.0e7, 60.0, 200, 150)])
+def test_plan_window_chain_run_ahead(fmt, fs, dur, first, count):
+    """shard.plan_window with the chain run ahead (speculative walks, here on the host:
+    gss_spec_host; bench.py and node.py use the GPU's) gives the host chain's rows bit for bit,
+    across 30 s updates and in more than one 4,096-block chunk for the first case."""
+    from gpssim_amd.shard import host_walker, plan_window
+    s1 = G.Scenario(NAV, llh=LOC, duration=dur, samp_freq=fs, data_format=fmt)
+    b1, n1, ck1, _ = plan_window(s1, first, count, threads=8)
+    s2 = G.Scenario(NAV, llh=LOC, duration=dur, samp_freq=fs, data_format=fmt)
+    b2, n2, ck2, t2 = plan_window(s2, first, count, threads=8, walker=host_walker(8))
+    assert np.array_equal(n1, n2)
+    assert np.array_equal(b1.view(np.uint8), b2.view(np.uint8))
+    assert ck2 is None and t2["spec_hits"] > 0.9 * int(n2.sum())
+
+
+def test_host_threads_under_sanitizers(tmp_path):
+    """gss_run's host threads (rows / planner / prover, each on its own worker pool) over the host
+    plane's C sources, built with ThreadSanitizer and with AddressSanitizer + UBSan
+    (tools/sanitize.sh, tests/helpers/run_harness.c): no report, rows equal the serial chain."""
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["bash", os.path.join(repo, "tools", "sanitize.sh")],
+                       env=dict(os.environ, SECS="60", OUT=str(tmp_path)),
+                       capture_output=True, text=True, timeout=900)
+    logs = "".join(open(os.path.join(tmp_path, f)).read() for f in sorted(os.listdir(tmp_path)))
+    assert r.returncode == 0, logs[-3000:]
+    assert "sanitizer reports: 0" in logs and "sanitizer reports: 1" not in logs

@@ -24,19 +24,20 @@ def _paths():
             sys.path.insert(0, p)
 
 
-def _worker(rank, world, port, result_path, window_s=WINDOW_S):
+def _worker(rank, world, port, result_path, window_s=WINDOW_S, run_ahead=False):
     _paths()
     import numpy as np
     import torch
     import torch.distributed as dist
     import gpssim_amd as G
     import oracle
-    from gpssim_amd.shard import Baton, plan_rank, rank_range
+    from gpssim_amd.shard import Baton, host_walker, plan_rank, rank_range
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     blk, nch, ck, nav, npb, t = plan_rank(NAV, rank, world, window_s, llh=LOC, threads=2,
-                                          baton=Baton(dist, rank, world))
+                                          baton=Baton(dist, rank, world),
+                                          walker=host_walker(2) if run_ahead else None)
     # the rank produced rows for its own window only (rank 1 seeked past rank 0's blocks)
     assert t["rows_out"] == len(nch) == rank_range(rank, world, window_s)[1]
     out, rc = oracle.synth(blk, nch, G.ca_table(), nav, npb, 16)
@@ -63,18 +64,21 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,window_s,gold", [
-    (2, WINDOW_S, "static_d30_b16"),
+@pytest.mark.parametrize("world,window_s,gold,run_ahead", [
+    (2, WINDOW_S, "static_d30_b16", False),
     # rank 1 starts at block 309: its seek replays the 30 s nav/allocation update after block
     # 299 (gpssim.c:2294-2345) and its own window crosses the one after block 599
-    (2, 31.0, "static_d300_b16"),
+    (2, 31.0, "static_d300_b16", False),
+    # the same with each rank's chain run ahead (speculative walks, shard.chain_run_ahead)
+    (2, 31.0, "static_d300_b16", True),
     # three ranks: the middle one both receives and hands on the baton
-    (3, WINDOW_S, "static_d30_b16"),
+    (3, WINDOW_S, "static_d30_b16", False),
 ])
-def test_two_rank_time_window_shards(tmp_path, golden, world, window_s, gold):
+def test_two_rank_time_window_shards(tmp_path, golden, world, window_s, gold, run_ahead):
     import torch.multiprocessing as mp
     res = tmp_path / "r.json"
-    mp.spawn(_worker, args=(world, _free_port(), str(res), window_s), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(res), window_s, run_ahead), nprocs=world,
+             join=True)
     r = json.load(open(res))
     n = int(round(window_s * 10)) - 1
     assert r["firsts"] == [k * n for k in range(world)]
