@@ -171,6 +171,39 @@ def cpu_baseline(seconds=30, over_seconds=10):
                       f"{wn:.2f} s"}
 
 
+def host_state():
+    """cgroup CPU accounting (cpu.stat), this process's threads and resident memory: recorded
+    around each end-to-end leg (the bench-process e2e slowdown)"""
+    st = {}
+    try:
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            k, v = line.split()
+            if k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec"):
+                st[k] = int(v)
+    except (OSError, ValueError):
+        pass
+    try:
+        for line in open("/proc/self/status"):
+            if line.startswith(("Threads:", "VmRSS:", "VmHWM:")):
+                k, v = line.split(":", 1)
+                st[k] = int(v.split()[0])
+    except (OSError, ValueError):
+        pass
+    st["t"] = time.perf_counter()
+    return st
+
+
+def host_delta(a, b):
+    d = {k: b[k] - a[k] for k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec")
+         if k in a and k in b}
+    if "t" in a and "usage_usec" in d and b["t"] > a["t"]:
+        d["cpus_used"] = round(d["usage_usec"] / 1e6 / (b["t"] - a["t"]), 2)
+    for k in ("Threads", "VmRSS", "VmHWM"):
+        if k in b:
+            d[k + "_after"] = b[k]
+    return d
+
+
 def progress(msg):
     """a progress line on stderr (the JSON result is the last stdout line)"""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -392,9 +425,11 @@ def e2e_run(G, dev, threads, window=1800.0, batch=None, fs=FS, fmt=16, kw=None, 
         got["blocks"] += nb
         marks.append((time.perf_counter(), got["bytes"]))
 
+    h0 = host_state()
     t0 = time.perf_counter()
     dev.run(s, sink, batch=batch, threads=threads)
     wall = time.perf_counter() - t0
+    h1 = host_state()
     blocks, nbytes, n_per_blk = got["blocks"], got["bytes"], s.n_per_blk
     samples = blocks * n_per_blk
     ceiling = d2h_ceiling(batch * bb)
@@ -404,7 +439,8 @@ def e2e_run(G, dev, threads, window=1800.0, batch=None, fs=FS, fmt=16, kw=None, 
            "d2h_GBps": round(nbytes / wall / 1e9, 2), "d2h_ceiling_GBps": ceiling,
            "frac_of_d2h_ceiling": round(nbytes / wall / 1e9 / ceiling, 3) if ceiling else None,
            "workload": (desc or f"static -b {fmt}, {window:g} s") +
-                       f" through gss_run (batch {batch} blocks), discarding sink"}
+                       f" through gss_run (batch {batch} blocks), discarding sink",
+           "host": host_delta(h0, h1)}
     if slope and len(marks) >= 8:
         q = next(i for i, (_, b) in enumerate(marks) if b >= nbytes / 4)
         (tq, bq), (tl, bl) = marks[q], marks[-1]

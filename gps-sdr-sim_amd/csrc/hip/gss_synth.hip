@@ -544,16 +544,29 @@ static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole ch
 #define LIN_STAMP_WAVES (1 << 20)
 __device__ uint64_t g_lin_stamp[LIN_STAMP_WAVES][4];
 #endif
-/* LIN_SWIN 1 (the default): the steps' chip windows come from the chunk window table (gss_lin.h,
+/* LIN_SWIN 1: the steps' chip windows come from the chunk window table (gss_lin.h,
    gss_tw16_kernel): per channel and chunk one 64-byte row -- the 16 windows of a chunk whose
    code base has chip E, for the channel's C/A row -- at a wave-uniform address, read by one
    s_load_dwordx16 into SGPRs that the chip-sign shift takes directly.  No window pass, no LDS
-   window reads, no per-workgroup copy of the bit-streams.  LIN_SWIN 0 (round 3): the lanes build
-   each chunk's windows from the bit-streams in LDS and the loop reads them back by broadcast LDS
-   reads.  In-kernel clock stamps (tools/clock_stamp.py, profiles/round4/): an ablation with the
-   windows made in SGPRs took the wave 20 % fewer cycles than the LDS windows. */
+   window reads, no per-workgroup copy of the bit-streams.  LIN_SWIN 0 (the default, round 3):
+   the lanes build each chunk's windows from the bit-streams in LDS and the loop reads them back
+   by broadcast LDS reads.  In-kernel clock stamps (tools/clock_stamp.py, profiles/round4/): an
+   ablation with the windows made in SGPRs took the wave 20 % fewer cycles than the LDS
+   windows, but the table's scalar loads wait on the LDS reads' counter: each pair's load is
+   exposed (~1.5k cycles), 102k cycles per wave against 62k (not the default). */
 #ifndef LIN_SWIN
-#define LIN_SWIN 1
+#define LIN_SWIN 0
+#endif
+/* LIN_SWIN 3: each channel's row of the chunk window table is loaded by an s_load_dwordx16 the
+   compiler does not see, into 16 SGPRs it never allocates (the kernel is limited to
+   LIN_SW_SGPRS by amdgpu_num_sgpr; the buffer sits above that), issued one channel ahead (while
+   the channel before renders); at the channel's start an explicit s_waitcnt and 8 s_mov_b64
+   hand the windows to ordinary SGPRs.  Hidden from the compiler, the load leaves its LDS waits
+   counted (a pending load only makes one of them wait for one more LDS read), so the LUT reads
+   stay pipelined.  One channel per 4x4x4 MFMA (LIN_MFMA 1). */
+#if LIN_SWIN == 3
+#define LIN_SW_SGPRS (LIN_MFMA == 2 ? 68 : 84)     /* hidden: s[84:99], pairs also s[68:83] */
+static_assert(LIN_MFMA >= 1, "LIN_SWIN 3 accumulates on the matrix cores");
 #endif
 #if LIN_SWIN || (LIN_ABLATE & 256)
 #define LIN_WCON "s"                       /* the shift takes the window from an SGPR            */
@@ -587,14 +600,25 @@ __device__ uint64_t g_lin_stamp[LIN_STAMP_WAVES][4];
 typedef _Float16 lin_half4 __attribute__((ext_vector_type(4)));
 typedef _Float16 lin_half8 __attribute__((ext_vector_type(8)));
 typedef float lin_f4 __attribute__((ext_vector_type(4)));
-#define LIN_MAGF  12582976.0f                   /* 1.5 2^23 + 64                          */
+/* LIN_PK2 (the default with the MFMA accumulation): the gains enter the matrix cores doubled
+   (2 g, still exact f16 integers: |2 g| <= 2048, their data-bit differences |2 (g1 - g0)| <=
+   4096 and even) and the accumulators start at 1.5 2^23 + 128, so that each sum holds
+   2 (sum + 64), an even integer below 2^23 in magnitude: exact, and its IEEE bits
+   0x4B400000 + 2 (sum + 64) put (sum + 64) >> 7 + 2^14 in bits 8..23.  The -b 16 sample word is
+   then one byte permutation of the I and Q bits and one packed 16-bit add of 0xC000 (2 VALU
+   instead of 3); -b 8 takes bits 12.., -b 1 compares with 0x4B400000 + 256. */
+#ifndef LIN_PK2
+#define LIN_PK2 1
+#endif
+#define LIN_GS    (LIN_PK2 ? 2 : 1)             /* the gain scale on the matrix cores     */
+#define LIN_MAGF  (12582912.0f + 64.0f * LIN_GS)   /* 1.5 2^23 + 64 LIN_GS               */
 #define LIN_MAGB  0x4B400000u                   /* IEEE bits of 1.5 2^23                  */
 
 /* per (block, segment wave, chunk, channel): the chunk's render parameters, built by the wave's
    lanes in parallel (vector loads and VALU) and read back by the render loop with broadcast LDS
    reads, so that the scalar unit (one per CU, shared by its four SIMDs) does no per-channel
    work */
-struct lin_ct {
+struct alignas(16) lin_ct {
     uint64_t B;                  /* the chunk's base (gss_lin.h)                                */
     uint64_t D;                  /* the 64-sample step dC : dX                                  */
     int32_t g;                   /* signed gain at the chunk start                              */
@@ -604,13 +628,23 @@ struct lin_ct {
     uint32_t q0, dq, tab;        /* first window offset (1/16 chip), its step, the row          */
     uint32_t wa;                 /* LIN_SWIN: byte offset of the chunk's window-table row       */
 #if !LIN_SWIN
-    uint32_t W[LIN_CH];          /* the steps' chip windows                                     */
+    uint32_t W[LIN_CH];          /* the steps' chip windows (16-byte aligned: ds_read_b128)     */
 #endif
 #if LIN_MFMA
     uint32_t A[4][2];            /* the MFMA gain operand of lane 4b + i: g (f16) at slot i      */
-    uint32_t g2, pad2[3];        /* g as an f16 pair (both halves), the pair MFMA's gain         */
+    uint32_t g2;                 /* g as an f16 pair (both halves), the pair MFMA's gain         */
 #endif
+    uint32_t wn;                 /* LIN_SWIN 3: ... of the next chunk's (its first pair preloads) */
 };
+/* the broadcast reads of the record assume these alignments (a misaligned ds_read_b128 is split
+   by the hardware and cost the round-4 LDS-window build 3x) */
+#if !LIN_SWIN
+static_assert(offsetof(lin_ct, W) % 16 == 0 && sizeof(lin_ct) % 16 == 0,
+              "lin_ct.W: 16-byte broadcast reads");
+#endif
+#if LIN_MFMA
+static_assert(offsetof(lin_ct, A) % 8 == 0, "lin_ct.A: 8-byte reads");
+#endif
 
 /* per (block, channel): the render constants of gss_lin.h (written by gss_linseg_kernel) */
 struct lin_chan {
@@ -778,6 +812,61 @@ __device__ __forceinline__ lin_wsrc lin_wsrc_of(const lin_ct &t, const uint32_t 
 #endif
 }
 
+#if LIN_SWIN == 3
+#define LIN_SW_CLOBB "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", \
+                     "s95", "s96", "s97", "s98", "s99"
+#define LIN_SW_CLOBA "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", \
+                     "s79", "s80", "s81", "s82", "s83"
+/* channel row off (a byte offset, any lane's copy) into the hidden buffer s[84:99]; with pairs a
+   second row into s[68:83] (the clobbers put them in the kernel's SGPR count; the compiler
+   allocates none of them) */
+__device__ __forceinline__ void lin_sw_load(const uint32_t *__restrict__ tw, uint32_t off)
+{
+    const uint32_t *p = (const uint32_t *)((const char *)tw + __builtin_amdgcn_readfirstlane(off));
+    asm volatile("s_load_dwordx16 s[84:99], %0, 0x0" : : "s"(p) : LIN_SW_CLOBB);
+}
+__device__ __forceinline__ void lin_sw_load2(const uint32_t *__restrict__ tw, uint32_t off_a,
+                                             uint32_t off_b)
+{
+    const uint32_t *pa = (const uint32_t *)((const char *)tw + __builtin_amdgcn_readfirstlane(off_a));
+    const uint32_t *pb = (const uint32_t *)((const char *)tw + __builtin_amdgcn_readfirstlane(off_b));
+    asm volatile("s_load_dwordx16 s[68:83], %0, 0x0\n\ts_load_dwordx16 s[84:99], %1, 0x0"
+                 : : "s"(pa), "s"(pb) : LIN_SW_CLOBA, LIN_SW_CLOBB);
+}
+/* wait for the loads (and every LDS read) and copy a hidden buffer into 16 SGPRs the compiler
+   owns: the steps then schedule like any SGPR operand, and the buffer is free for the next
+   load */
+#define LIN_SW_TAKE(BUF, W)                                                                       \
+    asm volatile("s_waitcnt lgkmcnt(0)\n\t"                                                      \
+                 "s_mov_b64 %0, s[" #BUF "+0:" #BUF "+1]\n\ts_mov_b64 %1, s[" #BUF "+2:" #BUF "+3]\n\t" \
+                 "s_mov_b64 %2, s[" #BUF "+4:" #BUF "+5]\n\ts_mov_b64 %3, s[" #BUF "+6:" #BUF "+7]\n\t" \
+                 "s_mov_b64 %4, s[" #BUF "+8:" #BUF "+9]\n\ts_mov_b64 %5, s[" #BUF "+10:" #BUF "+11]\n\t" \
+                 "s_mov_b64 %6, s[" #BUF "+12:" #BUF "+13]\n\ts_mov_b64 %7, s[" #BUF "+14:" #BUF "+15]" \
+                 : "=s"(W[0]), "=s"(W[1]), "=s"(W[2]), "=s"(W[3]), "=s"(W[4]), "=s"(W[5]),      \
+                   "=s"(W[6]), "=s"(W[7]))
+__device__ __forceinline__ void lin_sw_split(const uint64_t (&w)[8], uint32_t (&ws)[LIN_CH])
+{
+    static_assert(LIN_CH == 16, "16 windows");
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        ws[2 * i] = (uint32_t)w[i];
+        ws[2 * i + 1] = (uint32_t)(w[i] >> 32);
+    }
+}
+__device__ __forceinline__ void lin_sw_take(uint32_t (&ws)[LIN_CH])          /* s[84:99] */
+{
+    uint64_t w[8];
+    LIN_SW_TAKE(84, w);
+    lin_sw_split(w, ws);
+}
+__device__ __forceinline__ void lin_sw_take_a(uint32_t (&ws)[LIN_CH])        /* s[68:83] */
+{
+    uint64_t w[8];
+    LIN_SW_TAKE(68, w);
+    lin_sw_split(w, ws);
+}
+#endif
+
 /* one channel's contribution to the chunk's LIN_CH steps: the lane's anchor P (carrier : code,
    high : low word, gss_lin.h) and its 64-sample step D, the steps' chip windows (LDS, the same for every lane),
    the LUT mask M, the signed gain (with LANE_GAIN: the gain difference, applied from sample
@@ -843,6 +932,52 @@ __device__ __forceinline__ void lin_channel_chunk_m(lin_f4 (&cq)[LIN_CH / 2], li
         P += D;
     }
 }
+
+#if LIN_SWIN == 3
+/* LIN_SWIN 3: channel k's 16 steps from windows ws (SGPRs), one 4x4x4 MFMA per two steps */
+__device__ __forceinline__ void lin_sw_steps(lin_f4 (&cq)[LIN_CH / 2], const lin_ct &t, int k,
+                                             int lane, const uint64_t *s_lane, uint32_t M,
+                                             const int32_t *__restrict__ s_lut,
+                                             const uint32_t (&ws)[LIN_CH])
+{
+    uint64_t P = s_lane[k * 64 + lane] + t.B;
+    const uint64_t D = t.D;
+    const lin_half4 A = __builtin_bit_cast(lin_half4, *(const uint2 *)t.A[lane & 3]);
+    uint32_t e0 = 0;
+#pragma unroll
+    for (int s = 0; s < LIN_CH; s++) {
+        uint32_t tt;
+        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
+            "src1_sel:DWORD" : "=v"(tt) : "v"((uint32_t)P), "s"(ws[s]));      /* bit 0: sign */
+        const uint32_t a = __builtin_amdgcn_alignbit(tt, (uint32_t)(P >> 32), 21) & M;
+        const uint32_t e = *(const uint32_t *)((const char *)s_lut + a);
+        if (s & 1) {
+            const uint2 bb = make_uint2(e0, e);
+            cq[s / 2] = __builtin_amdgcn_mfma_f32_4x4x4f16(A, __builtin_bit_cast(lin_half4, bb),
+                                                          cq[s / 2], 0, 0, 0);
+        } else {
+            e0 = e;
+        }
+        P += D;
+    }
+}
+
+/* channel k, its windows taken from the hidden buffer (loaded while channel k - 1 rendered);
+   the next channel's row goes into the buffer while this one renders (LIN_MFMA 1) */
+__device__ __forceinline__ void lin_sw_channel(lin_f4 (&cq)[LIN_CH / 2], const lin_ct *T, int k,
+                                               int nc, int lane, const uint64_t *s_lane,
+                                               uint32_t M, const int32_t *__restrict__ s_lut,
+                                               const uint32_t *__restrict__ tw)
+{
+    const uint32_t wn = k + 1 < nc ? T[k + 1].wa : 0u;
+    uint32_t ws[LIN_CH];
+    lin_sw_take(ws);                                 /* this channel's windows */
+    if (k + 1 < nc)
+        lin_sw_load(tw, wn);                         /* the next channel's, meanwhile */
+    lin_sw_steps(cq, T[k], k, lane, s_lane, M, s_lut, ws);
+}
+
+#endif
 
 /* LIN_MFMA 2: two channels' steps, one v_mfma_f32_16x16x32_f16 per two steps (B = channel a's
    words of steps s, s+1 and channel b's; A = the pair's gains, lin_pair_gains).  FIRST: the
@@ -911,6 +1046,60 @@ __device__ __forceinline__ void lin_pair_sel(int lane, uint32_t &sel0, uint32_t 
     sel0 = act && r < 2 ? half : 0u;
     sel1 = act && r >= 2 ? half : 0u;
 }
+
+#if LIN_SWIN == 3
+#if LIN_MFMA == 2
+/* channels k0, k0 + 1 from the hidden buffers s[68:83], s[84:99] (loaded while the pair before
+   rendered); the next pair's rows (or the lone last channel's) load meanwhile.  FIRST: the
+   chunk's first pair, whose MFMAs take the bias c0 as C (no initialisation moves) */
+template <bool FIRST>
+__device__ __forceinline__ void lin_sw_pair(lin_f4 (&cq)[LIN_CH / 2], lin_f4 c0, const lin_ct *T, int k0,
+                                            int nc, int lane, const uint64_t *s_lane, uint32_t M,
+                                            const int32_t *__restrict__ s_lut,
+                                            const uint32_t *__restrict__ tw, uint32_t psel0,
+                                            uint32_t psel1, bool more)
+{
+    const lin_ct &ta = T[k0], &tb = T[k0 + 1];
+    uint64_t Pa = s_lane[k0 * 64 + lane] + ta.B, Pb = s_lane[(k0 + 1) * 64 + lane] + tb.B;
+    const uint64_t Da = ta.D, Db = tb.D;
+    const lin_half8 A = lin_pair_gains(ta.g2, tb.g2, psel0, psel1);
+    /* the rows to load while this pair renders: the next pair's (or the lone last channel's), or
+       after the last pair the next chunk's first pair (more: there is a next chunk) */
+    const int kn = k0 + 2;
+    const bool in = kn < nc;
+    const uint32_t wna = in ? T[kn].wa : T[0].wn;
+    const uint32_t wnb = in ? (kn + 1 < nc ? T[kn + 1].wa : wna) : T[nc > 1 ? 1 : 0].wn;
+    uint32_t wsa[LIN_CH], wsb[LIN_CH];
+    lin_sw_take_a(wsa);
+    lin_sw_take(wsb);
+    if (in || more)
+        lin_sw_load2(tw, wna, wnb);
+    uint32_t ea0 = 0, eb0 = 0;
+#pragma unroll
+    for (int s = 0; s < LIN_CH; s++) {
+        uint32_t ta_, tb_;
+        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
+            "src1_sel:DWORD" : "=v"(ta_) : "v"((uint32_t)Pa), "s"(wsa[s]));
+        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
+            "src1_sel:DWORD" : "=v"(tb_) : "v"((uint32_t)Pb), "s"(wsb[s]));
+        const uint32_t aa = __builtin_amdgcn_alignbit(ta_, (uint32_t)(Pa >> 32), 21) & M;
+        const uint32_t ab = __builtin_amdgcn_alignbit(tb_, (uint32_t)(Pb >> 32), 21) & M;
+        const uint32_t ea = *(const uint32_t *)((const char *)s_lut + aa);
+        const uint32_t eb = *(const uint32_t *)((const char *)s_lut + ab);
+        if (s & 1) {
+            const uint4 bb = make_uint4(ea0, ea, eb0, eb);
+            cq[s / 2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, __builtin_bit_cast(lin_half8, bb),
+                                                              FIRST ? c0 : cq[s / 2], 0, 0, 0);
+        } else {
+            ea0 = ea;
+            eb0 = eb;
+        }
+        Pa += Da;
+        Pb += Db;
+    }
+}
+#endif
+#endif
 
 /* the MFMA gain operand of this lane (g at slot lane mod 4, f16 bits gh) */
 __device__ __forceinline__ lin_half4 lin_gain_operand(uint32_t gh, int lane)
@@ -1000,25 +1189,35 @@ __device__ __forceinline__ uint32_t lin_qb(const lin_f4 (&cq)[LIN_CH / 2], int s
    the destination: two shifts, no perm */
 __device__ __forceinline__ uint32_t lin_w16(const lin_f4 (&cq)[LIN_CH / 2], int s)
 {
+#if LIN_PK2
+    /* bytes 1, 2 of the I bits (low half) and of the Q bits (high half): 2^14 + (sum + 64) >> 7
+       each, then + 0xC000 per half = (sum + 64) >> 7 mod 2^16 */
+    const uint32_t pq = __builtin_amdgcn_perm(lin_qb(cq, s), lin_ib(cq, s), 0x06050201u);
+    uint32_t r;
+    asm("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(pq), "s"(0xC000C000u));
+    return r;
+#else
     uint32_t d = lin_ib(cq, s) >> 7;
     asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "
         "src1_sel:DWORD" : "+v"(d) : "v"(7u), "v"(lin_qb(cq, s)));
     return d ^ 0x80008000u;
+#endif
 }
 __device__ __forceinline__ uint32_t lin_w8(const lin_f4 (&cq)[LIN_CH / 2], int s)
 {
-    uint32_t d = lin_ib(cq, s) >> 11;                 /* bytes 2, 3: not stored */
+    constexpr uint32_t sh = LIN_PK2 ? 12u : 11u;
+    uint32_t d = lin_ib(cq, s) >> sh;                 /* bytes 2, 3: not stored */
     asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "
-        "src1_sel:DWORD" : "+v"(d) : "v"(11u), "v"(lin_qb(cq, s)));
+        "src1_sel:DWORD" : "+v"(d) : "v"(sh), "v"(lin_qb(cq, s)));
     return d;
 }
 __device__ __forceinline__ bool lin_ipos(const lin_f4 (&cq)[LIN_CH / 2], int s)
 {
-    return lin_ib(cq, s) >= LIN_MAGB + 128u;
+    return lin_ib(cq, s) >= LIN_MAGB + 128u * LIN_GS;
 }
 __device__ __forceinline__ bool lin_qpos(const lin_f4 (&cq)[LIN_CH / 2], int s)
 {
-    return lin_qb(cq, s) >= LIN_MAGB + 128u;
+    return lin_qb(cq, s) >= LIN_MAGB + 128u * LIN_GS;
 }
 
 template <int FMT, bool TAIL, class ACC>
@@ -1141,7 +1340,7 @@ __device__ __forceinline__ void lin_patch_fix(lin_f4 (&cq)[LIN_CH / 2],
         const int q = pp - nb0;
         const int64_t d = lane == (q & 63) ? Lk->pdelta[j] : 0;
         const int di = (int)((uint32_t)d << 10) >> 10;
-        const float fi = (float)di, fq = (float)(int)((d - di) >> 22);
+        const float fi = (float)(di * LIN_GS), fq = (float)((int)((d - di) >> 22) * LIN_GS);
         /* every accumulator takes fi (fq) times a wave-uniform 0 or 1: in-place multiply-adds
            (exact), no branches and no selects that would keep two copies of the set live */
         const int sq = __builtin_amdgcn_readfirstlane(q >> 6);
@@ -1159,7 +1358,12 @@ template <int FMT>
 #ifndef LIN_MINB
 #define LIN_MINB 8                         /* workgroups per CU the register budget must allow  */
 #endif
-__global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
+#if LIN_SWIN == 3
+#define LIN_KATTR __attribute__((amdgpu_num_sgpr(LIN_SW_SGPRS)))
+#else
+#define LIN_KATTR
+#endif
+__global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kernel(
     const gss_lin_t *__restrict__ lin, const lin_seg *__restrict__ segs,
     const lin_chan *__restrict__ chans, const int32_t *__restrict__ nch,
     const int32_t *__restrict__ fast, const uint32_t *__restrict__ cab,
@@ -1226,6 +1430,9 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
 #if LIN_STAMP
     const uint64_t st_t0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
+#if LIN_SWIN == 3
+    bool sw_ahead = false;                 /* the chunk's first pair is already loading */
+#endif
 
     for (int c = 0; c < LIN_STEPS / LIN_CH; c++) {
         const int nb0 = n0 + c * (64 * LIN_CH);           /* first sample of the chunk */
@@ -1259,9 +1466,12 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
                the table; gss_lin_win16_ok keeps a certified channel inside it) */
             t.wa = (ck.tab * GSS_LIN_TWE + min((uint32_t)(zb >> 50), (uint32_t)(GSS_LIN_TWE - 1))) *
                    (uint32_t)(LIN_CH * sizeof(uint32_t));
+            const uint64_t zn = zb + (uint64_t)(64 * LIN_CH) * ck.zs;   /* the next chunk's base */
+            t.wn = (ck.tab * GSS_LIN_TWE + min((uint32_t)(zn >> 50), (uint32_t)(GSS_LIN_TWE - 1))) *
+                   (uint32_t)(LIN_CH * sizeof(uint32_t));
 #endif
 #if LIN_MFMA
-            const uint32_t gh = lin_f16_bits(t.g);        /* lane 4b + i's gain operand */
+            const uint32_t gh = lin_f16_bits(t.g * LIN_GS);  /* lane 4b + i's gain operand */
             t.A[0][0] = gh;         t.A[0][1] = 0;
             t.A[1][0] = gh << 16;   t.A[1][1] = 0;
             t.A[2][0] = 0;          t.A[2][1] = gh;
@@ -1298,7 +1508,34 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
 #ifndef LIN_C0
 #define LIN_C0 1        /* the first channel (pair)'s MFMAs take the bias as C, no init moves */
 #endif
-#if LIN_MFMA == 2
+#if LIN_MFMA == 2 && LIN_SWIN == 3
+        /* the first pair's rows: loaded during the chunk before, or now */
+        if (nc > 0 && !sw_ahead)
+            lin_sw_load2(tw, T[0].wa, T[nc > 1 ? 1 : 0].wa);
+        const bool more = c + 1 < LIN_STEPS / LIN_CH && nb0 + 64 * LIN_CH < n_per_blk;
+        int k0 = 0;
+        if (nc >= 2) {                                    /* the first pair sets acc = bias + ... */
+            lin_sw_pair<true>(acc, c0, T, 0, nc, lane, s_lane, M, s_lut, tw, psel0, psel1, more);
+            k0 = 2;
+        } else {
+#pragma unroll
+            for (int s = 0; s < LIN_CH / 2; s++)
+                acc[s] = c0;
+        }
+        for (; k0 + 1 < nc; k0 += 2)                      /* uniform loop over channel pairs */
+            lin_sw_pair<false>(acc, c0, T, k0, nc, lane, s_lane, M, s_lut, tw, psel0, psel1, more);
+        if (k0 < nc) {                                    /* the lone last channel: s[68:83] */
+            uint32_t ws[LIN_CH], wb[LIN_CH];
+            lin_sw_take_a(ws);
+            lin_sw_take(wb);                              /* (its duplicate, unused) */
+            (void)wb;
+            if (more)                                     /* the next chunk's first pair */
+                lin_sw_load2(tw, T[0].wn, T[nc > 1 ? 1 : 0].wn);
+            lin_sw_steps(acc, T[k0], k0, lane, s_lane, M, s_lut, ws);
+            k0 = nc;
+        }
+        sw_ahead = nc > 0 && more;
+#elif LIN_MFMA == 2
         int k0 = 0;
         if (LIN_C0 && nc >= 2) {                          /* the first pair sets acc = bias + ... */
             const lin_ct &ta = T[0], &tb = T[1];
@@ -1318,6 +1555,15 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
                                   lin_wsrc_of(tb, tw), M,
                                   lin_pair_gains(ta.g2, tb.g2, psel0, psel1), s_lut);
         }
+#elif LIN_SWIN == 3
+#pragma unroll
+        for (int s = 0; s < LIN_CH / 2; s++)
+            acc[s] = c0;
+        if (nc > 0)
+            lin_sw_load(tw, T[0].wa);
+        for (int k = 0; k < nc; k++)                      /* uniform channel loop */
+            lin_sw_channel(acc, T, k, nc, lane, s_lane, M, s_lut, tw);
+        const int k0 = nc;
 #else
         int k0 = 0;
         if (LIN_C0 && nc >= 1) {                          /* the first channel sets acc = bias + ... */
@@ -1350,7 +1596,7 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) void gss_lin_kernel(
                 uint32_t l2 = (uint32_t)lane;
                 asm volatile("" : "+v"(l2));
                 lin_channel_chunk_m<true>(acc, c0, s_lane[k * 64 + l2] + B, D, lin_wsrc_of(t, tw), M,
-                                          lin_gain_operand(lin_f16_bits(t.gd), (int)l2), t.pos1,
+                                          lin_gain_operand(lin_f16_bits(t.gd * LIN_GS), (int)l2), t.pos1,
                                           nb0 + (int)l2, s_lut);
             }
             if (__builtin_expect(fl & 2u, 0))
@@ -1464,7 +1710,8 @@ extern "C" int gss_dev_ordinal(const gss_dev *d) { return d->ordinal; }
 
 extern "C" const char *gss_build_info(void)
 {
-    return "lin_mfma=" GSS_STR(LIN_MFMA) " lin_ch=" GSS_STR(LIN_CH) " arch=gfx950";
+    return "lin_mfma=" GSS_STR(LIN_MFMA) " lin_ch=" GSS_STR(LIN_CH) " lin_swin=" GSS_STR(LIN_SWIN)
+           " arch=gfx950";
 }
 
 extern "C" size_t gss_block_bytes(int n, int fmt)

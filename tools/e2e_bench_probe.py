@@ -1,0 +1,59 @@
+"""Why the e2e legs run slower inside bench.py than in a fresh process: one
+configuration's gss_run leg first in a fresh process, then after that configuration's kernel leg
+(the DeviceWindow the bench times before it), then once more; each leg with the host's CPU
+accounting and the run's per-batch steady rate (bench.e2e_run).  GPU box only.
+
+usage: python tools/e2e_bench_probe.py <config index 2|3|4> [repeats]"""
+import json
+import os
+import sys
+import time
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path[:0] = [os.path.join(REPO, "gps-sdr-sim_amd"), REPO]
+import torch  # noqa: E402
+import gpssim_amd as G  # noqa: E402
+import bench as B  # noqa: E402
+
+
+def kernel_leg(dev, dev_t, stream, c, threads=16):
+    from gpssim_amd.render import DeviceWindow
+    t0 = time.perf_counter()
+    s = G.Scenario(B.NAV, duration=c["window"], samp_freq=c["fs"], data_format=c["fmt"], **c["kw"])
+    blk, nch = s.all_blocks(batch=2000, threads=threads)
+    res = DeviceWindow(torch, dev, dev_t, blk, nch, s.nav_table(), s.n_per_blk, c["fmt"],
+                       threads=threads, batch=3000)
+    for _ in range(3):
+        res.step(stream)
+    torch.cuda.synchronize(dev_t)
+    res.free()
+    del blk, nch, s
+    return round(time.perf_counter() - t0, 2)
+
+
+def main():
+    idx = int(sys.argv[1])
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    c = B.CONFIGS[idx - 2]
+    dev_t = torch.device("cuda", 0)
+    dev = G.Device(0)
+    stream = torch.cuda.current_stream(dev_t).cuda_stream
+
+    def leg(tag):
+        r = B.e2e_run(G, dev, 16, c["window"], fs=c["fs"], fmt=c["fmt"], kw=c["kw"], slope=True,
+                      desc=c["desc"])
+        out = {"leg": tag, "value": r["value"], "wall_s": r["wall_s"],
+               "frac": r["frac_of_d2h_ceiling"], "steady_frac": r.get("steady_frac_of_d2h_ceiling"),
+               "ceiling": r["d2h_ceiling_GBps"], "startup_s": r.get("startup_s"), "host": r["host"]}
+        print(json.dumps(out), flush=True)
+
+    leg("fresh")
+    for i in range(reps):
+        print(json.dumps({"kernel_leg_s": kernel_leg(dev, dev_t, stream, c)}), flush=True)
+        leg(f"after kernel leg {i + 1}")
+    leg("again")
+    dev.close()
+
+
+if __name__ == "__main__":
+    main()

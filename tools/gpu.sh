@@ -14,6 +14,11 @@
 #   prof             rocprofv3 kernel trace + stats, then one PMC pass per counter group
 #                    (tools/profile.sh: traffic, SQ, LDS), never combined with other domains
 #   e2e:N            tools/e2e_cfg_probe.py N (gss_run over configs[N] end to end, traced)
+#   e2eab:V1,V2,..   bench.py's e2e leg of the current build and _var/<Vi>, interleaved ROUNDS
+#   rehearse:N       the driver's torchrun bench as N ranks on this one GPU (GSS_BENCH_REHEARSE:
+#                    gloo collectives, every rank on GPU 0), args REHEARSE_ARGS
+#   pmcclk:V1,V2,..  per-dispatch clock and cycles from PMC (GRBM_GUI_ACTIVE, SQ busy/wave
+#                    cycles) of the current build and _var/<Vi>, one rocprofv3 pass each
 #   cmd:'...'        any other command, under a 300 s limit
 # env: BENCH_ARGS (bench step), STEPS/WARMUP (ablate), ROUNDS.
 set -o pipefail
@@ -69,6 +74,44 @@ for s in "$@"; do
     prof)
         bash tools/profile.sh $TAG/prof
         step prof $? ;;
+    e2eab:*)
+        vs=${s#e2eab:}
+        for r in $(seq ${ROUNDS:-2}); do
+            for v in cur ${vs//,/ }; do
+                lib=gps-sdr-sim_amd/lib/libgpssim_amd.so
+                [ "$v" != cur ] && lib=_var/$v/libgpssim_amd.so
+                line=$(GSS_ALLOW_LIB_OVERRIDE=1 GSS_LIB_PATH=$lib timeout -k 10 200 python bench.py \
+                    --steps 1 --warmup 0 --no-cpu-baseline --no-exact --no-configs --no-pmc \
+                    --no-sustained 2>>$OUT/e2eab.err | tail -1)
+                step "e2eab $v" $?
+                echo "$v $(echo "$line" | python3 -c 'import json,sys; d=json.load(sys.stdin)["e2e"]; print(d["value"], d["d2h_GBps"], d["frac_of_d2h_ceiling"], d.get("steady_frac_of_d2h_ceiling"))')" >> $OUT/e2eab.log
+            done
+        done ;;
+    rehearse:*)
+        n=${s#rehearse:}
+        GSS_BENCH_REHEARSE=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
+            --nproc-per-node $n --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus $n \
+            ${REHEARSE_ARGS:---steps 3 --warmup 1 --no-pmc} > $OUT/rehearse$n.json \
+            2> $OUT/rehearse$n.err
+        step "rehearse $n" $? ;;
+    pmcclk:*)
+        vs=${s#pmcclk:}
+        BA="--steps 20 --warmup 5 --no-exact --no-configs --no-e2e --no-cpu-baseline --no-pmc"
+        for v in cur ${vs//,/ }; do
+            lib=gps-sdr-sim_amd/lib/libgpssim_amd.so
+            [ "$v" != cur ] && lib=_var/$v/libgpssim_amd.so
+            d=$OUT/pmcclk_$v
+            mkdir -p $d
+            GSS_ALLOW_LIB_OVERRIDE=1 GSS_LIB_PATH=$lib timeout -k 10 300 rocprofv3 --kernel-trace \
+                --stats -d $d/kt -o kt -f csv -- python3 bench.py $BA > $d/kt.log 2>&1
+            step "pmcclk kt $v" $?
+            GSS_ALLOW_LIB_OVERRIDE=1 GSS_LIB_PATH=$lib timeout -k 10 300 rocprofv3 --pmc \
+                GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_WAIT_ANY \
+                SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS --kernel-trace -d $d/pmc -o pmc \
+                -f csv -- python3 bench.py $BA > $d/pmc.log 2>&1
+            step "pmcclk pmc $v" $?
+            python3 tools/prof_summary.py $d 20 5 > $d/summary.json
+        done ;;
     e2e:*)
         n=${s#e2e:}
         GSS_RUN_TRACE=1 timeout -k 10 200 python tools/e2e_cfg_probe.py $n > $OUT/e2e_cfg$n.out \
