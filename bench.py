@@ -374,7 +374,7 @@ def per_config(G, torch, dev, dev_t, stream, steps, warmup, threads, e2e=True):
                              "frac": round(achieved / HBM_PEAK_GBS, 4),
                              "algorithmic_bytes_per_sample": res.bb / res.npb},
             "host_plan_s": round(plan_s, 3), "host_linearize_s": round(res.lin_s, 3)})
-        res.free()
+        res.free(release=False)               # (released memory slows the next leg's downloads)
         del blk, nch, s
         progress(f"{c['name']}: {out[-1]['value']} MS/s")
         if e2e:
@@ -408,8 +408,8 @@ def e2e_run(G, dev, threads, window=1800.0, batch=None, fs=FS, fmt=16, kw=None, 
     """gss_run over a whole run into a discarding sink, wall-clocked (planner, proofs, uploads,
     kernels, D2H into pinned buffers and the sink, overlapped).  With `slope` the steady-state
     rate comes from the same run's sink calls (one per batch, in run order): bytes delivered
-    from the call that completes the first quarter of the run to the last call, over the time
-    between them; `startup_s` is the time to the first call.  Read against d2h_ceiling_GBps, the
+    after the first call up to the last, over the time between them; `startup_s` is the time to
+    the first call.  Read against d2h_ceiling_GBps, the
     measured device -> pinned host copy rate of one slot in this process."""
     kw = kw if kw is not None else {"llh": LOC}
     bb = G.block_bytes(int(round(fs / 10)), fmt)
@@ -442,7 +442,10 @@ def e2e_run(G, dev, threads, window=1800.0, batch=None, fs=FS, fmt=16, kw=None, 
                        f" through gss_run (batch {batch} blocks), discarding sink",
            "host": host_delta(h0, h1)}
     if slope and len(marks) >= 8:
-        q = next(i for i, (_, b) in enumerate(marks) if b >= nbytes / 4)
+        # from the first sink call on: every later call's bytes were copied after the first
+        # copy ended (one copy stream), so the slope cannot exceed the copy rate by more than
+        # one slot; a later anchor can sit behind a backlog of finished slots and overstate it
+        q = 0
         (tq, bq), (tl, bl) = marks[q], marks[-1]
         if tl > tq and bl > bq:
             rate = (bl - bq) / (tl - tq)                 # bytes/s in the run's steady part
@@ -676,7 +679,26 @@ def main():
                 f"{args.window:g} s per GPU ({nblk} blocks x {npb} samples)")
     version = G.lib().gss_version().decode()
     sha = lib_sha16(G.LIB_PATH)
-    res.free()
+    # the buffers stay in torch's cache: memory returned to the driver is wiped by the copy
+    # engines in the background, which slowed the e2e legs' downloads by up to 1/3 for seconds
+    # (tools/e2e_bench_probe.py: 0.65 of the D2H ceiling after a release, 0.93 with the memory
+    # kept)
+    res.free(release=False)
+    gather = None
+    if dist and not args.no_gather:
+        gather = gather_leg(G, torch, td, dev, dev_t, rank, world, coll_t, walker, args.threads,
+                            args.gather_window, host_wire=rehearse)
+        progress(f"gather: {gather['GBps_at_rank0']} GB/s at rank 0")
+    configs = e2e = None
+    # the headline's end-to-end leg first, then the per-config legs (each after its own kernel
+    # leg, whose memory stays cached)
+    if single and not args.no_e2e:
+        e2e = e2e_run(G, dev, args.threads, args.e2e_window, batch=128)
+        progress(f"e2e: {e2e['value']} MS/s")
+    if single and not args.no_configs:
+        configs = per_config(G, torch, dev, dev_t, stream, min(args.steps, 3), 1, args.threads,
+                             e2e=not args.no_e2e)
+    # the live PMC passes last: their processes' device memory is wiped when they exit (above)
     traffic, traffic_src, prof = None, "not measured (--no-pmc)", None
     if single and not args.no_pmc:
         traffic, traffic_src, prof = live_traffic(args.fmt, args.window, args.threads, lin_ms,
@@ -687,23 +709,7 @@ def main():
             traffic, traffic_src = t2, s2
         else:
             traffic_src = f"{traffic_src}; committed profile: {s2}"
-
     progress(f"traffic: {traffic_src[:120]}")
-    gather = None
-    if dist and not args.no_gather:
-        gather = gather_leg(G, torch, td, dev, dev_t, rank, world, coll_t, walker, args.threads,
-                            args.gather_window, host_wire=rehearse)
-        progress(f"gather: {gather['GBps_at_rank0']} GB/s at rank 0")
-    configs = e2e = None
-    # the headline's end-to-end leg before the per-config legs: after configs[4]'s -b 1 leg (rows
-    # and prover threads) this process's -b 16 downloads ran at ~39 instead of ~56 GB/s, which
-    # a fresh process does not show (cause not found)
-    if single and not args.no_e2e:
-        e2e = e2e_run(G, dev, args.threads, args.e2e_window, batch=128)
-        progress(f"e2e: {e2e['value']} MS/s")
-    if single and not args.no_configs:
-        configs = per_config(G, torch, dev, dev_t, stream, min(args.steps, 3), 1, args.threads,
-                             e2e=not args.no_e2e)
 
     out = {
         "metric": METRIC,

@@ -544,26 +544,29 @@ static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole ch
 #define LIN_STAMP_WAVES (1 << 20)
 __device__ uint64_t g_lin_stamp[LIN_STAMP_WAVES][4];
 #endif
-/* LIN_SWIN 1: the steps' chip windows come from the chunk window table (gss_lin.h,
-   gss_tw16_kernel): per channel and chunk one 64-byte row -- the 16 windows of a chunk whose
-   code base has chip E, for the channel's C/A row -- at a wave-uniform address, read by one
-   s_load_dwordx16 into SGPRs that the chip-sign shift takes directly.  No window pass, no LDS
-   window reads, no per-workgroup copy of the bit-streams.  LIN_SWIN 0 (the default, round 3):
-   the lanes build each chunk's windows from the bit-streams in LDS and the loop reads them back
-   by broadcast LDS reads.  In-kernel clock stamps (tools/clock_stamp.py, profiles/round4/): an
-   ablation with the windows made in SGPRs took the wave 20 % fewer cycles than the LDS
-   windows, but the table's scalar loads wait on the LDS reads' counter: each pair's load is
-   exposed (~1.5k cycles), 102k cycles per wave against 62k (not the default). */
+/* Where a step's 32-chip window comes from.
+   LIN_SWIN 3 (the default, round 4): from the chunk window table (gss_lin.h, gss_tw16_kernel,
+   per C/A row and chunk start chip E one 64-byte row of the 16 steps' windows, 5.2 MB, rebuilt
+   per call).  Each channel's row is loaded by an s_load_dwordx16 the compiler does not see, into
+   16 SGPRs it never allocates (the kernel is limited to LIN_SW_SGPRS by amdgpu_num_sgpr; the
+   buffers s[68:83] and s[84:99] sit above that), issued one pair ahead (while the pair before
+   renders; the last pair of a chunk loads the next chunk's first); at the pair's start an
+   explicit s_waitcnt and s_mov_b64s hand the windows to ordinary SGPRs, which the chip-sign
+   shift takes directly.  Hidden from the compiler, a load in flight leaves the LDS waits counted
+   (a pending load only makes one of them wait for one more LDS read), so the LUT reads stay
+   pipelined.  No window pass, no broadcast window reads, no bit-streams in LDS.  Interleaved on
+   one box: 1.62-1.64 ms per 300 s launch against 1.76 for LIN_SWIN 0 (profiles/round4/).
+   LIN_SWIN 0 (rounds 2-3): the lanes build each chunk's windows from the bit-streams in LDS and
+   the loop reads them back by broadcast LDS reads.
+   LIN_SWIN 1 (measurement): the same table by compiler-visible s_loads: they share lgkmcnt with
+   the LUT reads, so each pair's load is waited for with every LDS read drained (+16 %). */
 #ifndef LIN_SWIN
+#if LIN_MFMA
+#define LIN_SWIN 3
+#else
 #define LIN_SWIN 0
 #endif
-/* LIN_SWIN 3: each channel's row of the chunk window table is loaded by an s_load_dwordx16 the
-   compiler does not see, into 16 SGPRs it never allocates (the kernel is limited to
-   LIN_SW_SGPRS by amdgpu_num_sgpr; the buffer sits above that), issued one channel ahead (while
-   the channel before renders); at the channel's start an explicit s_waitcnt and 8 s_mov_b64
-   hand the windows to ordinary SGPRs.  Hidden from the compiler, the load leaves its LDS waits
-   counted (a pending load only makes one of them wait for one more LDS read), so the LUT reads
-   stay pipelined.  One channel per 4x4x4 MFMA (LIN_MFMA 1). */
+#endif
 #if LIN_SWIN == 3
 #define LIN_SW_SGPRS (LIN_MFMA == 2 ? 68 : 84)     /* hidden: s[84:99], pairs also s[68:83] */
 static_assert(LIN_MFMA >= 1, "LIN_SWIN 3 accumulates on the matrix cores");
@@ -634,6 +637,9 @@ struct alignas(16) lin_ct {
     uint32_t A[4][2];            /* the MFMA gain operand of lane 4b + i: g (f16) at slot i      */
     uint32_t g2;                 /* g as an f16 pair (both halves), the pair MFMA's gain         */
 #endif
+    uint32_t na, nb;             /* LIN_SWIN 3, pairs: the rows to load while the pair (k, k + 1)
+                                    renders -- the next pair's, the lone last channel's (twice)
+                                    or the next chunk's first pair's (lin_sw_pair)              */
     uint32_t wn;                 /* LIN_SWIN 3: ... of the next chunk's (its first pair preloads) */
 };
 /* the broadcast reads of the record assume these alignments (a misaligned ds_read_b128 is split
@@ -819,20 +825,29 @@ __device__ __forceinline__ lin_wsrc lin_wsrc_of(const lin_ct &t, const uint32_t 
                      "s79", "s80", "s81", "s82", "s83"
 /* channel row off (a byte offset, any lane's copy) into the hidden buffer s[84:99]; with pairs a
    second row into s[68:83] (the clobbers put them in the kernel's SGPR count; the compiler
-   allocates none of them) */
+   allocates none of them).  clang warns that registers above the amdgpu_num_sgpr limit "may not
+   be preserved across the asm statement": nothing but these statements names them (the limit
+   keeps the allocator, spills and the ABI below s68), which the GPU tests of this build check
+   byte for byte, so the warning is silenced here only. */
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void lin_sw_load(const uint32_t *__restrict__ tw, uint32_t off)
 {
-    const uint32_t *p = (const uint32_t *)((const char *)tw + __builtin_amdgcn_readfirstlane(off));
+    const uint32_t *p = (const uint32_t *)((const char *)tw +
+                                           (uint32_t)__builtin_amdgcn_readfirstlane(off));
     asm volatile("s_load_dwordx16 s[84:99], %0, 0x0" : : "s"(p) : LIN_SW_CLOBB);
 }
 __device__ __forceinline__ void lin_sw_load2(const uint32_t *__restrict__ tw, uint32_t off_a,
                                              uint32_t off_b)
 {
-    const uint32_t *pa = (const uint32_t *)((const char *)tw + __builtin_amdgcn_readfirstlane(off_a));
-    const uint32_t *pb = (const uint32_t *)((const char *)tw + __builtin_amdgcn_readfirstlane(off_b));
+    const uint32_t *pa = (const uint32_t *)((const char *)tw +
+                                            (uint32_t)__builtin_amdgcn_readfirstlane(off_a));
+    const uint32_t *pb = (const uint32_t *)((const char *)tw +
+                                            (uint32_t)__builtin_amdgcn_readfirstlane(off_b));
     asm volatile("s_load_dwordx16 s[68:83], %0, 0x0\n\ts_load_dwordx16 s[84:99], %1, 0x0"
                  : : "s"(pa), "s"(pb) : LIN_SW_CLOBA, LIN_SW_CLOBB);
 }
+#pragma clang diagnostic pop
 /* wait for the loads (and every LDS read) and copy a hidden buffer into 16 SGPRs the compiler
    owns: the steps then schedule like any SGPR operand, and the buffer is free for the next
    load */
@@ -1063,17 +1078,16 @@ __device__ __forceinline__ void lin_sw_pair(lin_f4 (&cq)[LIN_CH / 2], lin_f4 c0,
     uint64_t Pa = s_lane[k0 * 64 + lane] + ta.B, Pb = s_lane[(k0 + 1) * 64 + lane] + tb.B;
     const uint64_t Da = ta.D, Db = tb.D;
     const lin_half8 A = lin_pair_gains(ta.g2, tb.g2, psel0, psel1);
-    /* the rows to load while this pair renders: the next pair's (or the lone last channel's), or
-       after the last pair the next chunk's first pair (more: there is a next chunk) */
-    const int kn = k0 + 2;
-    const bool in = kn < nc;
-    const uint32_t wna = in ? T[kn].wa : T[0].wn;
-    const uint32_t wnb = in ? (kn + 1 < nc ? T[kn + 1].wa : wna) : T[nc > 1 ? 1 : 0].wn;
+    /* the rows to load while this pair renders (the record's na, nb): the next pair's (or the
+       lone last channel's), or after the last pair the next chunk's first pair (more: there is a
+       next chunk) */
+    uint32_t na = ta.na, nb = ta.nb;
+    asm volatile("" : "+v"(na), "+v"(nb));       /* read with the record, before the wait below */
     uint32_t wsa[LIN_CH], wsb[LIN_CH];
     lin_sw_take_a(wsa);
     lin_sw_take(wsb);
-    if (in || more)
-        lin_sw_load2(tw, wna, wnb);
+    if (k0 + 2 < nc || more)
+        lin_sw_load2(tw, na, nb);
     uint32_t ea0 = 0, eb0 = 0;
 #pragma unroll
     for (int s = 0; s < LIN_CH; s++) {
@@ -1355,8 +1369,9 @@ __device__ __forceinline__ void lin_patch_fix(lin_f4 (&cq)[LIN_CH / 2],
 
 
 template <int FMT>
-#ifndef LIN_MINB
-#define LIN_MINB 8                         /* workgroups per CU the register budget must allow  */
+#ifndef LIN_MINB                           /* workgroups per CU the register budget aims at:   */
+#define LIN_MINB (LIN_SWIN == 3 ? 4 : 8)   /* with SGPR windows the loads pipeline deeper at 5-6
+                                              waves per SIMD (8 would spill)                   */
 #endif
 #if LIN_SWIN == 3
 #define LIN_KATTR __attribute__((amdgpu_num_sgpr(LIN_SW_SGPRS)))
@@ -1440,6 +1455,9 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
             break;
         /* ---- the chunk's parameters, lane k for channel k ---- */
         uint32_t my_flags = 0;
+#if LIN_SWIN == 3
+        uint32_t my_wa = 0, my_wn = 0;
+#endif
         if (lane < nc) {
             const lin_chan ck = CH[lane];
             const lin_seg sk = S[(size_t)lane * nseg];
@@ -1469,6 +1487,10 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
             const uint64_t zn = zb + (uint64_t)(64 * LIN_CH) * ck.zs;   /* the next chunk's base */
             t.wn = (ck.tab * GSS_LIN_TWE + min((uint32_t)(zn >> 50), (uint32_t)(GSS_LIN_TWE - 1))) *
                    (uint32_t)(LIN_CH * sizeof(uint32_t));
+#if LIN_SWIN == 3
+            my_wa = t.wa;
+            my_wn = t.wn;
+#endif
 #endif
 #if LIN_MFMA
             const uint32_t gh = lin_f16_bits(t.g * LIN_GS);  /* lane 4b + i's gain operand */
@@ -1480,6 +1502,19 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
 #endif
         }
         /* the channels with a gain change or patches in this chunk (wave-uniform) */
+#if LIN_SWIN == 3 && LIN_MFMA == 2
+        {
+            /* the rows each pair (k, k + 1) loads ahead (gather from lanes k + 2, k + 3, 0, 1:
+               once per chunk in parallel, instead of selects per pair) */
+            const uint32_t wa2 = __shfl_down(my_wa, 2), wa3 = __shfl_down(my_wa, 3);
+            const uint32_t wn0 = __shfl(my_wn, 0), wn1 = __shfl(my_wn, nc > 1 ? 1 : 0);
+            if (lane < nc) {
+                const bool in2 = lane + 2 < nc, in3 = lane + 3 < nc;
+                T[lane].na = in2 ? wa2 : wn0;
+                T[lane].nb = in3 ? wa3 : in2 ? wa2 : wn1;
+            }
+        }
+#endif
         const uint64_t fmask = __builtin_amdgcn_ballot_w64(my_flags != 0);
         wave_sync_lds();
 #if !LIN_SWIN && !(LIN_ABLATE & (256 | 512))
@@ -1518,9 +1553,13 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
             lin_sw_pair<true>(acc, c0, T, 0, nc, lane, s_lane, M, s_lut, tw, psel0, psel1, more);
             k0 = 2;
         } else {
+            /* (the copies pinned inside this branch: hoisted, they cost 32 moves every chunk) */
 #pragma unroll
-            for (int s = 0; s < LIN_CH / 2; s++)
-                acc[s] = c0;
+            for (int s = 0; s < LIN_CH / 2; s++) {
+                lin_f4 v = c0;
+                asm volatile("" : "+v"(v));
+                acc[s] = v;
+            }
         }
         for (; k0 + 1 < nc; k0 += 2)                      /* uniform loop over channel pairs */
             lin_sw_pair<false>(acc, c0, T, k0, nc, lane, s_lane, M, s_lut, tw, psel0, psel1, more);

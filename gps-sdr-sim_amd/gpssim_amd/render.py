@@ -88,7 +88,12 @@ class DeviceWindow:
             setattr(self, a, None)
         self.batches = []
 
-    def free(self):
+    def free(self, release=True):
+        """Drop the window's buffers; release=False keeps them in torch's cache instead of
+        returning them to the driver, which wipes released device memory with the copy engines
+        in the background and so slows this process's device -> host copies for a while
+        (tools/e2e_bench_probe.py)."""
         self.free_inputs()
         self.out = None
-        self.torch.cuda.empty_cache()
+        if release:
+            self.torch.cuda.empty_cache()

@@ -15,10 +15,11 @@
 #                    (tools/profile.sh: traffic, SQ, LDS), never combined with other domains
 #   e2e:N            tools/e2e_cfg_probe.py N (gss_run over configs[N] end to end, traced)
 #   e2eab:V1,V2,..   bench.py's e2e leg of the current build and _var/<Vi>, interleaved ROUNDS
-#   rehearse:N       the driver's torchrun bench as N ranks on this one GPU (GSS_BENCH_REHEARSE:
-#                    gloo collectives, every rank on GPU 0), args REHEARSE_ARGS
+#   rehearse:N[:T]   the driver's torchrun bench as N ranks on this one GPU (GSS_BENCH_REHEARSE:
+#                    gloo collectives, every rank on GPU 0), args REHEARSE_ARGS, output tag T
 #   pmcclk:V1,V2,..  per-dispatch clock and cycles from PMC (GRBM_GUI_ACTIVE, SQ busy/wave
 #                    cycles) of the current build and _var/<Vi>, one rocprofv3 pass each
+#   env:K=V          export K=V for the steps after it (e.g. env:BENCH_ARGS='--steps 20')
 #   cmd:'...'        any other command, under a 300 s limit
 # env: BENCH_ARGS (bench step), STEPS/WARMUP (ablate), ROUNDS.
 set -o pipefail
@@ -88,12 +89,12 @@ for s in "$@"; do
             done
         done ;;
     rehearse:*)
-        n=${s#rehearse:}
+        a=${s#rehearse:}; n=${a%%:*}; t=""; [ "$a" != "$n" ] && t=_${a#*:}
         GSS_BENCH_REHEARSE=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
             --nproc-per-node $n --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus $n \
-            ${REHEARSE_ARGS:---steps 3 --warmup 1 --no-pmc} > $OUT/rehearse$n.json \
-            2> $OUT/rehearse$n.err
-        step "rehearse $n" $? ;;
+            ${REHEARSE_ARGS:---steps 3 --warmup 1 --no-pmc} > $OUT/rehearse$n$t.json \
+            2> $OUT/rehearse$n$t.err
+        step "rehearse $n$t" $? ;;
     pmcclk:*)
         vs=${s#pmcclk:}
         BA="--steps 20 --warmup 5 --no-exact --no-configs --no-e2e --no-cpu-baseline --no-pmc"
@@ -117,6 +118,9 @@ for s in "$@"; do
         GSS_RUN_TRACE=1 timeout -k 10 200 python tools/e2e_cfg_probe.py $n > $OUT/e2e_cfg$n.out \
             2> $OUT/e2e_cfg$n.err
         step "e2e $n" $? ;;
+    env:*)
+        export "${s#env:}"
+        step "env ${s#env:}" 0 ;;
     cmd:*)
         timeout -k 10 300 bash -c "${s#cmd:}" >> $OUT/cmd.log 2>&1
         step "cmd" $? ;;
