@@ -998,6 +998,7 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
 {
     if (!d || !s || !sink || first_block < 0)
         return gss_fail(GSS_E_ARG, "invalid run arguments");
+    const double t_enter = trace_on() ? tnow() : 0.0;
     gss_scn_info_t info;
     int rc = gss_scn_info(s, &info);
     if (rc) return rc;
@@ -1157,6 +1158,8 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         cleanup();
         return err;
     }
+    if (trace_on())
+        fprintf(stderr, "trace setup enter %.6f ready %.6f\n", t_enter, tnow());
     std::thread th([&r, ordinal] {
         (void)hipSetDevice(ordinal);                   /* pinned reallocations */
         planner(&r);

@@ -1448,6 +1448,46 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
 #if LIN_SWIN == 3
     bool sw_ahead = false;                 /* the chunk's first pair is already loading */
 #endif
+    /* ---- lane k: channel k's rows, the same for every chunk of the wave: loaded once, the
+       record's constant fields written once, the lines advanced by one chunk per chunk ---- */
+    uint64_t xb = 0, zb = 0, xs10 = 0, zs10 = 0;       /* chunk bases, per-chunk advances     */
+    int32_t pos1 = INT32_MAX;
+    uint32_t pflag = 0, gh0 = 0, gh1 = 0;
+#if LIN_SWIN
+    uint32_t trow = 0, wa_next = 0;                    /* table row base, this chunk's row     */
+#endif
+    int g_after = -1;                                  /* the gain the record holds (none yet) */
+    if (lane < nc) {
+        const lin_chan ck = CH[lane];
+        const lin_seg sk = S[(size_t)lane * nseg];
+        xb = sk.x;
+        zb = sk.z;
+        xs10 = ck.xs << 10;
+        zs10 = ck.zs << 10;
+        static_assert(64 * LIN_CH == 1024, "one chunk = 2^10 samples");
+        pos1 = sk.pos1;
+        pflag = sk.npatch != 0 ? 2u : 0u;
+        const int g0 = (int)(int16_t)(sk.g01 & 0xFFFF), g1 = sk.g01 >> 16;
+        gh0 = (uint32_t)g0;
+        gh1 = (uint32_t)g1;
+#if LIN_MFMA
+        gh0 = lin_f16_bits(g0 * LIN_GS);
+        gh1 = lin_f16_bits(g1 * LIN_GS);
+#endif
+        lin_ct &t = T[lane];
+        t.D = ck.d;
+        t.gd = g1 - g0;
+        t.pos1 = sk.pos1;
+        t.dq = ck.dq;
+        t.tab = ck.tab;
+#if LIN_SWIN
+        /* a chunk's row of the window table: its C/A row and code base chip E (clamped to the
+           table; gss_lin_win16_ok keeps a certified channel inside it) */
+        trow = ck.tab * GSS_LIN_TWE;
+        wa_next = (trow + min((uint32_t)(zb >> 50), (uint32_t)(GSS_LIN_TWE - 1))) *
+                  (uint32_t)(LIN_CH * sizeof(uint32_t));
+#endif
+    }
 
     for (int c = 0; c < LIN_STEPS / LIN_CH; c++) {
         const int nb0 = n0 + c * (64 * LIN_CH);           /* first sample of the chunk */
@@ -1459,47 +1499,44 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
         uint32_t my_wa = 0, my_wn = 0;
 #endif
         if (lane < nc) {
-            const lin_chan ck = CH[lane];
-            const lin_seg sk = S[(size_t)lane * nseg];
-            /* the chunk's base B (gss_lin.h): the segment's lines plus c chunks */
-            const uint64_t off = (uint64_t)c * (64 * LIN_CH);
-            const uint64_t xb = sk.x + off * ck.xs;
-            const uint64_t zb = sk.z + off * ck.zs;
-            const int g0 = (int)(int16_t)(sk.g01 & 0xFFFF), g1 = sk.g01 >> 16;
-            const bool chg = sk.pos1 < nb0 + 64 * LIN_CH;    /* a data bit by the chunk's end */
             lin_ct &t = T[lane];
+            /* the chunk's base B (gss_lin.h): the segment's lines plus c chunks */
             t.B = (xb & ~0xFFFFFFFFull) | (uint32_t)(zb >> GSS_LIN_CSH);
-            t.D = ck.d;
-            t.g = chg && sk.pos1 <= nb0 ? g1 : g0;
-            t.gd = g1 - g0;
-            t.pos1 = sk.pos1;
-            t.flags = (chg && sk.pos1 > nb0 ? 1u : 0u) | (sk.npatch != 0 ? 2u : 0u);
+            const bool after = pos1 <= nb0;                /* the data bit changed before it */
+            const bool chg = pos1 < nb0 + 64 * LIN_CH;     /* ... or changes inside it      */
+            t.flags = (chg && !after ? 1u : 0u) | pflag;
             my_flags = t.flags;
+#if !LIN_SWIN
             /* 1/16 chip below lane 0's first chip, plus CBW_PRE chips */
             t.q0 = (uint32_t)(zb >> 46) + (16 * CBW_PRE - 1);
-            t.dq = ck.dq;
-            t.tab = ck.tab;
+#endif
+            const uint64_t zn = zb + zs10;                 /* the next chunk's code base */
 #if LIN_SWIN
-            /* the chunk's row of the window table: its C/A row and code base chip E (clamped to
-               the table; gss_lin_win16_ok keeps a certified channel inside it) */
-            t.wa = (ck.tab * GSS_LIN_TWE + min((uint32_t)(zb >> 50), (uint32_t)(GSS_LIN_TWE - 1))) *
-                   (uint32_t)(LIN_CH * sizeof(uint32_t));
-            const uint64_t zn = zb + (uint64_t)(64 * LIN_CH) * ck.zs;   /* the next chunk's base */
-            t.wn = (ck.tab * GSS_LIN_TWE + min((uint32_t)(zn >> 50), (uint32_t)(GSS_LIN_TWE - 1))) *
-                   (uint32_t)(LIN_CH * sizeof(uint32_t));
+            const uint32_t wn = (trow + min((uint32_t)(zn >> 50), (uint32_t)(GSS_LIN_TWE - 1))) *
+                                (uint32_t)(LIN_CH * sizeof(uint32_t));
+            t.wa = wa_next;
+            t.wn = wn;
 #if LIN_SWIN == 3
-            my_wa = t.wa;
-            my_wn = t.wn;
+            my_wa = wa_next;
+            my_wn = wn;
 #endif
+            wa_next = wn;
 #endif
+            if ((int)after != g_after) {                   /* the gain the chunk starts with */
+                g_after = (int)after;
+                const uint32_t gh = after ? gh1 : gh0;
 #if LIN_MFMA
-            const uint32_t gh = lin_f16_bits(t.g * LIN_GS);  /* lane 4b + i's gain operand */
-            t.A[0][0] = gh;         t.A[0][1] = 0;
-            t.A[1][0] = gh << 16;   t.A[1][1] = 0;
-            t.A[2][0] = 0;          t.A[2][1] = gh;
-            t.A[3][0] = 0;          t.A[3][1] = gh << 16;
-            t.g2 = gh | (gh << 16);
+                t.A[0][0] = gh;         t.A[0][1] = 0;     /* lane 4b + i's gain operand */
+                t.A[1][0] = gh << 16;   t.A[1][1] = 0;
+                t.A[2][0] = 0;          t.A[2][1] = gh;
+                t.A[3][0] = 0;          t.A[3][1] = gh << 16;
+                t.g2 = gh | (gh << 16);
+#else
+                t.g = (int32_t)gh;
 #endif
+            }
+            xb += xs10;
+            zb = zn;
         }
         /* the channels with a gain change or patches in this chunk (wave-uniform) */
 #if LIN_SWIN == 3 && LIN_MFMA == 2
