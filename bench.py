@@ -12,8 +12,9 @@ byte stream (3.12 GB) to HBM.  Multi-GPU (torchrun, one process per GPU): rank r
 window [300 r, 300 (r+1)) s of one longer static run -- a weak-scaling time-window shard with no
 data-path collective; RCCL carries only the planner's 128-byte carrier hand-off,
 the barrier and the max-over-ranks timing.  The host control plane (ephemeris, ranges, nav
-words, exact carrier planner) and the host proof run before the timed region (host_plan_s,
-host_linearize_s), each rank planning only its own window (gpssim_amd/shard.py).
+words, exact carrier planner) and the proofs (on the GPU: gss_linearize_device) run before the
+timed region (host_plan_s, host_linearize_s), each rank planning only its own window
+(gpssim_amd/shard.py).
 
 Extra JSON fields besides the driver contract:
   x_realtime, stages_ms, host_plan_s, host_linearize_s (max over ranks), lib (the library that
@@ -373,7 +374,8 @@ def per_config(G, torch, dev, dev_t, stream, steps, warmup, threads, e2e=True):
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(achieved / HBM_PEAK_GBS, 4),
                              "algorithmic_bytes_per_sample": res.bb / res.npb},
-            "host_plan_s": round(plan_s, 3), "host_linearize_s": round(res.lin_s, 3)})
+            "host_plan_s": round(plan_s, 3), "host_linearize_s": round(res.lin_s, 3),
+            "proofs_on": res.proof})
         res.free(release=False)               # (released memory slows the next leg's downloads)
         del blk, nch, s
         progress(f"{c['name']}: {out[-1]['value']} MS/s")
@@ -735,7 +737,8 @@ def main():
                       "fast_path_sustained": sustained_ms},
         "blocks_fast_path": res.n_fast, "blocks_total": nblk,
         "host_plan_s": round(host_plan_s, 3),
-        "host_linearize_s": round(host_lin_s, 3),
+        "host_linearize_s": round(host_lin_s, 3),   # the proofs' time (on proofs_on)
+        "proofs_on": "gpu (gss_linearize_device)",
         "host_plan_per_rank": host_plan_per_rank,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -133,8 +133,8 @@ GSS_LIN_FN uint64_t gss_lin_lane(uint64_t xs, uint64_t zs, uint32_t l)
     return ((uint64_t)lx << 32) | lz;
 }
 
-#if !defined(__HIP_DEVICE_COMPILE__)
-/* the kernel's LUT cell and chip at block sample p (host side: 128-bit code line) */
+/* the kernel's LUT cell and chip at block sample p (128-bit code line; the proof's, on the host
+   and in gss_linearize_device) */
 typedef struct {
     int cell, chip;
 } gss_lin_kc;
@@ -165,6 +165,5 @@ GSS_LIN_FN gss_lin_kc gss_lin_kernel_at(uint64_t x0, uint64_t xs, uint64_t z0, u
     r.chip = (int)((uint64_t)(kz >> 24) % 1023u);
     return r;
 }
-#endif
 
 #endif /* GSS_LIN_H */

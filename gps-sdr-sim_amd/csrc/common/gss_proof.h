@@ -1,0 +1,392 @@
+/*
+ * gss_proof.h — the fast path's proof for one channel of one block (lin_channel), shared bit for
+ * bit by the host (csrc/host/linearize.c: gss_linearize) and the GPU (csrc/hip/gss_proof.hip:
+ * gss_linearize_device).  The method is linearize.c's header comment; this file holds its
+ * arithmetic: the exact first-hit descent (first_in, first_below), the ambiguous-sample
+ * enumeration, the code-wrap and signed-gain schedule and the patches.  Everything here is exact
+ * integer arithmetic plus the IEEE walks of gss_phase.h (no contraction: -ffp-contract=off on
+ * both sides), so both builds produce the same gss_lin_t rows.
+ * Device constraints kept for the host too: no recursion (first_in descends iteratively, at most
+ * GSS_PF_EUCLID_MAX levels; deeper gives the channel up) and no 128-bit division (gss_pf_udiv).
+ */
+#ifndef GSS_PROOF_H
+#define GSS_PROOF_H
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+#include "gpssim_amd.h"
+#include "gss_phase.h"
+#include "gss_lin.h"
+
+#if defined(__HIPCC__)
+#define GSS_PF static __host__ __device__ inline
+#else
+#define GSS_PF static inline
+#endif
+
+typedef unsigned __int128 u128;
+typedef __int128 i128;
+
+/* floor(a / b) for a quotient below 2^64 (b > 0): native on the host, shift-subtract on the GPU
+   (no 128-bit division there); the two agree whenever the quotient fits */
+GSS_PF uint64_t gss_pf_udiv(u128 a, uint64_t b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    if ((uint64_t)(a >> 64) == 0)
+        return (uint64_t)a / b;
+    uint64_t q = 0;
+    u128 r = a >> 64;                                    /* < b: the quotient fits 64 bits */
+    uint64_t lo = (uint64_t)a;
+    for (int i = 63; i >= 0; i--) {
+        r = (r << 1) | ((lo >> i) & 1u);
+        if (r >= b) {
+            r -= b;
+            q |= (uint64_t)1 << i;
+        }
+    }
+    return q;
+#else
+    return (uint64_t)(a / b);
+#endif
+}
+
+/* ---- exact first hit ------------------------------------------------------------------------- */
+/* Smallest x in [0, lim] with lo <= (s x) mod m <= hi, for 1 <= lo <= hi < m < 2^62 and s < m;
+ * UINT64_MAX if there is none.  Every candidate is >= ceil(lo/s); if s x reaches [lo, hi] before
+ * its first wrap, that is x.  Otherwise [lo, hi] holds no multiple of s (so hi - lo < s), and x
+ * exists for wrap count y iff some multiple of s lies in [lo + m y, hi + m y], i.e. (m y) mod s
+ * lies in [s - hi mod s, s - lo mod s]: the same question for (m mod s, s), Euclid's descent, with
+ * x = ceil((lo + m y) / s) of the least y.  x <= lim needs y <= lim s / m: the descent stops as
+ * soon as that bound (an overestimate in double, so nothing is cut wrongly) is out of reach. */
+#define GSS_PF_EUCLID_MAX 64       /* descent levels kept (a deeper one gives up: uncertified) */
+#define GSS_PF_GIVE_UP (UINT64_MAX - 1)
+GSS_PF uint64_t first_in(uint64_t s, uint64_t m, uint64_t lo, uint64_t hi, uint64_t lim)
+{
+    /* the descent, level by level (iterative: the GPU proof has no call stack to spare); each
+       level that needs the next one's answer keeps (s, m, lo, lim) for the way back up */
+    uint64_t fs[GSS_PF_EUCLID_MAX], fm[GSS_PF_EUCLID_MAX], flo[GSS_PF_EUCLID_MAX],
+        flim[GSS_PF_EUCLID_MAX];
+    int d = 0;
+    uint64_t r;
+    for (;;) {
+        if (s == 0) {
+            r = UINT64_MAX;
+            break;
+        }
+        const uint64_t x = (lo + s - 1) / s;
+        if (x > lim) {
+            r = UINT64_MAX;
+            break;
+        }
+        if (s * x <= hi) {                               /* s x <= lo + s - 1 < 2^63 */
+            r = x;
+            break;
+        }
+        if (d == GSS_PF_EUCLID_MAX)
+            return GSS_PF_GIVE_UP;
+        const uint64_t lr = lo % s, hr = hi % s;         /* 1 <= lr <= hr < s (no multiple inside) */
+        const double yd = (double)lim * (double)s / (double)m + 2.0;
+        const uint64_t ylim = yd < 0x1p52 ? (uint64_t)yd : UINT64_MAX;
+        fs[d] = s; fm[d] = m; flo[d] = lo; flim[d] = lim;
+        d++;
+        const uint64_t ns = m % s;
+        m = s;
+        lo = s - hr;
+        hi = s - lr;
+        s = ns;
+        lim = ylim;
+    }
+    while (d > 0) {                                      /* y = r: x = ceil((lo + m y) / s) */
+        d--;
+        if (r == UINT64_MAX)
+            return UINT64_MAX;
+        const uint64_t v = gss_pf_udiv((u128)flo[d] + (u128)fm[d] * r + fs[d] - 1, fs[d]);
+        r = v <= flim[d] ? v : UINT64_MAX;
+    }
+    return r;
+}
+
+/* Smallest p in [0, n) with (a + p s) mod m < w (0 <= a, s < m < 2^62, 0 < w <= m), or n. */
+GSS_PF uint64_t first_below(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint64_t w)
+{
+    if (n == 0)
+        return 0;
+    if (a < w)
+        return 0;
+    /* (a + p s) mod m < w  <=>  (s p) mod m in [m - a, m - a + w - 1], a range below m as a >= w */
+    const uint64_t p = first_in(s, m, m - a, m - a + w - 1, n - 1);
+    if (p == GSS_PF_GIVE_UP)
+        return GSS_PF_GIVE_UP;
+    return p < n ? p : n;
+}
+
+/* ---- fixed point ----------------------------------------------------------------------------- */
+/* x * 2^k rounded to nearest (ties away); *inexact set if rounding happened.  |x| < 2^60. */
+GSS_PF i128 to_fix(double x, int k, int *inexact)
+{
+    int e;
+    double fr = frexp(x, &e);                        /* x = fr * 2^e, 0.5 <= |fr| < 1 */
+    int64_t m = (int64_t)ldexp(fr, 53);              /* exact: x = m * 2^(e-53) */
+    int sh = e - 53 + k;
+    if (x == 0.0)
+        return 0;
+    if (sh >= 0)
+        return (i128)m * ((i128)1 << sh);            /* no left shift of a negative value */
+    if (sh < -62) {
+        *inexact = 1;
+        return 0;
+    }
+    int64_t am = m < 0 ? -m : m;
+    int64_t q = am >> -sh, r = am - (q << -sh);
+    if (r != 0) {
+        *inexact = 1;
+        if (r >= ((int64_t)1 << (-sh - 1)))
+            q++;
+    }
+    return m < 0 ? -(i128)q : (i128)q;
+}
+
+/* Step 2: the samples p in [1, n) where the line L0 + p S comes within delta of a cell boundary
+   (a multiple of 2^lgB).  Writes up to cap of them in ascending order to hit[]; returns their
+   number, or -1 if there are more (or delta is not small against B).  Each hit is the next
+   sample whose residue falls below 2 delta (first_below: O(log B) per hit). */
+GSS_PF int ambiguous(i128 L0, i128 S, i128 delta, int lgB, int64_t n, int64_t *hit, int cap)
+{
+    const uint64_t B = (uint64_t)1 << lgB;           /* lgB <= 55 */
+    if (delta >= (i128)(B / 4))
+        return -1;
+    if (delta <= 0)
+        return 0;                                    /* nothing within a zero distance */
+    /* residues mod the power of two B: the low lgB bits of the two's complement value */
+    const uint64_t st = (uint64_t)S & (B - 1);
+    /* r(p) in [0, delta) or [B - delta, B)  <=>  (r(p) + delta) mod B < 2 delta */
+    const uint64_t a0 = ((uint64_t)L0 + (uint64_t)delta) & (B - 1);
+    const uint64_t w = 2 * (uint64_t)delta;
+    int nh = 0;
+    int64_t p0 = 1;
+    while (p0 < n) {
+        const uint64_t a = (a0 + (uint64_t)p0 * st) & (B - 1);    /* mod 2^64, then mod B */
+        const uint64_t m = (uint64_t)(n - p0);
+        const uint64_t i = first_below(m, B, a, st, w);
+        if (i == GSS_PF_GIVE_UP)
+            return -1;
+        if (i >= m)
+            break;
+        if (nh == cap)
+            return -1;
+        hit[nh++] = p0 + (int64_t)i;
+        p0 += (int64_t)i + 1;
+    }
+    return nh;
+}
+
+/* ---- one block ------------------------------------------------------------------------------ */
+#define LIN_CARR_LGB 55          /* 2^55 units of 2^-64 cycle = one of the 512 LUT cells */
+#define LIN_CODE_LGB 50          /* 2^50 units of 2^-50 chip = one chip */
+#define LIN_CARR_ERR ((i128)1 << 12)    /* one step's rounding (bound), units of 2^-64 cycle */
+#define LIN_CODE_ERR ((i128)1 << 7)     /* one step's rounding (bound), units of 2^-50 chip  */
+#define LIN_MAXHIT 64            /* ambiguous samples examined per chain */
+
+GSS_PF int signed_gain(int gain, const uint32_t *nav, int iword, int ibit)
+{
+    return ((nav[iword] >> (29 - ibit)) & 1u) ? gain : -gain;
+}
+
+GSS_PF int find_hit(const int64_t *hit, int nh, int64_t q)
+{
+    for (int i = 0; i < nh; i++)
+        if (hit[i] == q)
+            return i;
+    return -1;
+}
+
+/* code wraps between the block start and state c, from the counters */
+GSS_PF int64_t wraps_of(const gss_code_state *c, const gss_chan_blk_t *p)
+{
+    return ((int64_t)(c->iword - p->iword) * 30 + (c->ibit - p->ibit)) * 20 +
+           (c->icode - p->icode);
+}
+
+/* cos + 2^22 sin of LUT cell c (the kernel's packed I/Q term, gpssim.c:15-83), from the tables of
+   gss_lut */
+GSS_PF int64_t lut_packed(const int32_t *lcos, const int32_t *lsin, int c)
+{
+    return (int64_t)lcos[c] + (int64_t)lsin[c] * ((int64_t)1 << 22);
+}
+
+GSS_PF int ca_sign(const uint32_t *ca, int chip)          /* codeCA (gpssim.c:2220) */
+{
+    return ((ca[chip >> 5] >> (chip & 31)) & 1u) ? 1 : -1;
+}
+
+/* 1 if the line value v lies within d of a multiple of 2^lgB */
+GSS_PF int near_boundary(i128 v, i128 d, int lgB)
+{
+    const uint64_t B = (uint64_t)1 << lgB;           /* (v + d) mod B: the low lgB bits */
+    return (i128)(((uint64_t)v + (uint64_t)d) & (B - 1)) < 2 * d;
+}
+
+/* merge two ascending sample lists and {0}: ascending, no duplicates */
+GSS_PF int merge_hits(const int64_t *a, int na, const int64_t *b, int nb, int64_t *out)
+{
+    int i = 0, j = 0, n = 0;
+    out[n++] = 0;
+    while (i < na || j < nb) {
+        int64_t v = (j >= nb || (i < na && a[i] <= b[j])) ? a[i++] : b[j++];
+        if (v != out[n - 1])
+            out[n++] = v;
+    }
+    return n;
+}
+
+/* 1 if certified (lin filled), 0 if this channel needs the exact path */
+GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, const uint32_t *ca,
+                       const int32_t *lcos, const int32_t *lsin, gss_lin_t *lin)
+{
+    int inexact = 0;
+    int64_t hx[LIN_MAXHIT], hz[LIN_MAXHIT], hq[2 * LIN_MAXHIT + 1];
+    gss_code_state at_hz[LIN_MAXHIT];
+
+    /* ---- the two lines and the samples where they decide nothing (gpssim.c:2212-2250) ---- */
+    const double x0 = p->carr0, s = p->carr_step;
+    if (!(x0 >= 0.0 && x0 < 1.0) || !(s > -0.5 && s < 0.5))
+        return 0;
+    const i128 X0 = to_fix(x0, 64, &inexact), XS = to_fix(s, 64, &inexact);
+    const i128 DX1 = 2 + (i128)n * (LIN_CARR_ERR + 1);           /* line vs reference */
+    const double c0 = p->code0, cs = p->code_step;
+    if (!(c0 >= 0.0 && c0 < GSS_CA_SEQ_LEN_D) || !(cs > 0.0 && cs < 1.0))
+        return 0;
+    const int64_t ZS = (int64_t)to_fix(cs, 50, &inexact);
+    /* An exact chain: the integer-carrier variant's rows (--carrier=int, gpssim.c:2252) are
+       multiples of 2^-25 cycle, so every IEEE step and wrap of the reference is exact and the
+       line IS the reference.  The kernel then rounds nothing either (xs is a multiple of 2^39,
+       gss_lin.h): its carrier word is the line's, a multiple of 2^7, plus the code word's
+       carries, fewer than 2^7 (KDEV below 2^39 units of 2^-64): no sample can change cell. */
+    int ix = 0;
+    (void)to_fix(x0, 25, &ix);
+    (void)to_fix(s, 25, &ix);
+    const int exact_carr = !ix && GSS_LIN_KDEV_CARR((uint64_t)ZS) < ((uint64_t)1 << 39);
+    const int nhx = exact_carr ? 0 : ambiguous(X0, XS, DX1 + GSS_LIN_KDEV_CARR((uint64_t)ZS),
+                                               LIN_CARR_LGB, n, hx, LIN_MAXHIT);
+    if (nhx < 0)
+        return 0;
+    if (p->iword < 0 || p->iword >= GSS_NAV_WORDS || p->ibit < 0 || p->ibit >= 30 ||
+        p->icode < 0 || p->icode >= 20)
+        return 0;
+    const int64_t Z0 = (int64_t)to_fix(c0, 50, &inexact);
+    const int64_t per = (int64_t)GSS_CA_LEN << LIN_CODE_LGB;
+    /* the kernel reads one 32-chip window per 64-sample step, starting up to 2 chips below
+       lane 0's chip: from the LDS window pass (GSS_LIN_WIN_OK) or the chunk window table
+       (gss_lin_win16_ok); both hold, so that either build of the kernel may render the block */
+    if (ZS <= 0 || Z0 >= per || !GSS_LIN_WIN_OK((uint64_t)ZS) ||
+        !gss_lin_win16_ok((uint64_t)ZS, n))
+        return 0;
+    const int nhz = ambiguous(Z0, ZS, 2 + (i128)n * (LIN_CODE_ERR + 1) + GSS_LIN_KDEV_CODE,
+                              LIN_CODE_LGB, n, hz, LIN_MAXHIT);
+    if (nhz < 0)
+        return 0;
+    lin->x0 = (uint64_t)X0;
+    lin->xs = (uint64_t)XS;
+    lin->z0 = (uint64_t)Z0;
+    lin->zs = (uint64_t)ZS;
+
+    /* exact code state at the code's ambiguous samples */
+    gss_code_state st = {c0, p->icode, p->ibit, p->iword};
+    int64_t at = 0;
+    for (int i = 0; i < nhz; i++) {
+        gss_code_walk_cc(&st, cs, hz[i] - at);
+        at = hz[i];
+        at_hz[i] = st;
+    }
+
+    /* ---- code wraps, data bits and the signed-gain schedule ---- */
+    int ng = 0;
+    int g = signed_gain(p->gain, nav, p->iword, p->ibit);
+    lin->gpos[ng] = 0;
+    lin->gval[ng++] = g;
+    gss_code_state cnt = {0.0, p->icode, p->ibit, p->iword};
+    /* the line's k-th wrap is the first q with Z0 + q ZS >= k per: q = ceil((k per - Z0) / ZS). */
+    /* Only the wraps that start a data bit matter: wrap 20 - icode, then every 20th (icode counts
+       0..19, gss_code_count_wrap).  The ones between decide nothing, and a later wrap lies >= 1023
+       samples further on (code_step < 1), so the loop ends where the per-wrap loop would. */
+    for (int64_t k = 20 - p->icode;; k += 20) {
+        const i128 num = (i128)k * per - Z0;             /* > 0: k >= 1, Z0 < per */
+        const uint64_t qd = gss_pf_udiv((u128)num, (uint64_t)ZS);
+        int64_t q = (int64_t)qd + ((u128)qd * (uint64_t)ZS < (u128)num);
+        if (q - 1 >= n)
+            break;
+        int j = find_hit(hz, nhz, q - 1);
+        if (j >= 0 && wraps_of(&at_hz[j], p) >= k)
+            q--;                                 /* the exact value wrapped one sample earlier */
+        else if ((j = find_hit(hz, nhz, q)) >= 0 && wraps_of(&at_hz[j], p) < k)
+            q++;                                 /* ... or one sample later */
+        if (q >= n)
+            break;
+        cnt.icode = 19;                          /* the 19 wraps since the last data bit */
+        gss_code_count_wrap(&cnt);               /* a new data bit */
+        if (cnt.iword >= GSS_NAV_WORDS)
+            return 0;                            /* dwrd[60]: the exact path reports it */
+        const int g2 = signed_gain(p->gain, nav, cnt.iword, cnt.ibit);
+        if (g2 != g) {
+            /* the kernel takes at most one change per 4096-sample wave segment (they are
+               >= 20 code periods = 20 ms apart in any real run) */
+            if (ng == GSS_NGC || (ng > 1 && q - lin->gpos[ng - 1] < 4096))
+                return 0;
+            lin->gpos[ng] = (int32_t)q;
+            lin->gval[ng++] = g2;
+            g = g2;
+        }
+    }
+    for (int i = ng; i < GSS_NGC; i++) {
+        lin->gpos[i] = INT32_MAX;
+        lin->gval[i] = g;
+    }
+
+    /* ---- patches: the exact term where the kernel's differs ---- */
+    const int nq = merge_hits(hx, nhx, hz, nhz, hq);
+    double x = x0;
+    int64_t xat = 0;
+    int np = 0, gi = 0;
+    for (int i = 0; i < nq; i++) {
+        const int64_t q = hq[i];
+        int cell, chip;
+        if (q == 0) {
+            cell = (int)floor(x0 * 512.0);
+        } else if (near_boundary(X0 + (i128)q * XS, DX1, LIN_CARR_LGB)) {
+            x = gss_carr_walk_cc(x, s, q - xat);     /* the reference may differ from the line */
+            xat = q;
+            cell = (int)floor(x * 512.0);
+            if (cell > 511)      /* carr += 1.0 rounded to 1.0: the reference reads cosTable512[512]
+                                    (SURVEY A.7); the exact path renders it */
+                return 0;
+        } else {                                 /* proven: exact = line */
+            cell = (int)((uint64_t)(X0 + (i128)q * XS) >> LIN_CARR_LGB);
+        }
+        int j;
+        if (q == 0)
+            chip = (int)floor(c0);
+        else if ((j = find_hit(hz, nhz, q)) >= 0)
+            chip = (int)floor(at_hz[j].ph);
+        else
+            chip = (int)((uint64_t)((Z0 + (i128)q * ZS) >> LIN_CODE_LGB) % GSS_CA_LEN);
+        const gss_lin_kc kk = gss_lin_kernel_at((uint64_t)X0, (uint64_t)XS, (uint64_t)Z0,
+                                                 (uint64_t)ZS, q);
+        const int kcell = kk.cell, kchip = kk.chip;
+        const int64_t te = ca_sign(ca, chip) * lut_packed(lcos, lsin, cell);
+        const int64_t tk = ca_sign(ca, kchip) * lut_packed(lcos, lsin, kcell);
+        if (te == tk)
+            continue;
+        while (gi + 1 < GSS_NGC && lin->gpos[gi + 1] <= q)
+            gi++;
+        if (np == GSS_NPATCH)
+            return 0;
+        lin->ppos[np] = (int32_t)q;
+        lin->pdelta[np++] = (int64_t)lin->gval[gi] * (te - tk);
+    }
+    (void)inexact;
+    return 1;
+}
+
+
+#endif /* GSS_PROOF_H */

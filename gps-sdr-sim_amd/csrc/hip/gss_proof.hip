@@ -1,0 +1,145 @@
+/*
+ * gss_proof.hip — the fast path's proofs on the GPU (gss_linearize_device): the same per-channel
+ * proof as the host's gss_linearize (csrc/common/gss_proof.h, compiled for both), one lane per
+ * (block, channel), sixteen blocks per workgroup.  gss_run uses it so that the 24 h -b 1 run's
+ * proofs (60 % of its host CPU time: 15-17 µs per block on one core) leave the host; the rows it
+ * writes are byte for byte the host's (tests/test_gpu_proof.py).
+ *
+ * Per block the host proves channels in order and stops at the first that fails; here all
+ * channels run at once, so the rows after a block's first failing channel are reset to the
+ * host's initial state afterwards (they are never rendered: the block goes to the exact path).
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <mutex>
+#include "gpssim_amd.h"
+#include "../common/gss_proof.h"
+
+extern "C" int gss_fail(int code, const char *fmt, ...);
+extern "C" int gss_dev_ordinal(const gss_dev *d);
+
+namespace {
+
+struct proof_lut {                     /* gss_lut's tables as a kernel argument (|v| <= 250) */
+    int16_t c[512], s[512];
+};
+
+const proof_lut &host_lut()
+{
+    static proof_lut L;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        int32_t s[512], c[512];
+        gss_lut(s, c);
+        for (int i = 0; i < 512; i++) {
+            L.s[i] = (int16_t)s[i];
+            L.c[i] = (int16_t)c[i];
+        }
+    });
+    return L;
+}
+
+__device__ void lin_row_init(gss_lin_t *l)
+{
+    memset(l, 0, sizeof *l);
+    for (int i = 0; i < GSS_NGC; i++)
+        l->gpos[i] = INT32_MAX;
+    for (int i = 0; i < GSS_NPATCH; i++)
+        l->ppos[i] = INT32_MAX;
+}
+
+constexpr int PF_BLOCKS = 16;          /* blocks per workgroup, one lane per channel slot */
+
+/* force_exact > 0 (gss_run's test hook GSS_RUN_FORCE_EXACT): blocks first + b with
+   (first + b) % force_exact == 0 are sent to the exact path as well */
+__global__ __launch_bounds__(PF_BLOCKS * GSS_MAXCH) void gss_proof_kernel(
+    const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch, int nblk,
+    int n_per_blk, const uint32_t *__restrict__ ca, int n_ca, const uint32_t *__restrict__ nav,
+    int n_nav, proof_lut lut, gss_lin_t *__restrict__ lin, int32_t *__restrict__ fast,
+    int64_t first, int force_exact)
+{
+    __shared__ int32_t lcos[512], lsin[512];
+    __shared__ int fail_k[PF_BLOCKS * GSS_MAXCH];
+    __shared__ int gabs[PF_BLOCKS * GSS_MAXCH];
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) {
+        lcos[i] = lut.c[i];
+        lsin[i] = lut.s[i];
+    }
+    __syncthreads();
+    const int t = threadIdx.x, bl = t / GSS_MAXCH, k = t % GSS_MAXCH;
+    const int b = blockIdx.x * PF_BLOCKS + bl;
+    int failed = 0, g = 0;
+    gss_lin_t *l = lin + (size_t)b * GSS_MAXCH + k;
+    int nc = 0;
+    if (b < nblk) {
+        lin_row_init(l);
+        nc = nch[b];
+        if (nc < 0 || nc > GSS_MAXCH) {
+            failed = k == 0;                            /* the block fails before any channel */
+        } else if (k < nc) {
+            const gss_chan_blk_t *p = blk + (size_t)b * GSS_MAXCH + k;
+            g = p->gain < 0 ? -p->gain : p->gain;
+            if (p->nav_tbl < 0 || p->nav_tbl >= n_nav || p->ca_tbl < 0 || p->ca_tbl >= n_ca) {
+                failed = 1;
+            } else {
+                int ok = lin_channel(p, n_per_blk, nav + (size_t)p->nav_tbl * GSS_NAV_WORDS,
+                                     ca + (size_t)p->ca_tbl * GSS_CA_WORDS, lcos, lsin, l);
+                if (p->gain > 1024 || p->gain < -1024)
+                    ok = 0;
+                failed = !ok;
+            }
+        }
+    }
+    fail_k[t] = failed ? k : GSS_MAXCH;
+    gabs[t] = g;
+    __syncthreads();
+    /* the block's first failing channel and its gain sum (the host's loop order) */
+    int kf = GSS_MAXCH, gsum = 0;
+    for (int j = 0; j < GSS_MAXCH; j++) {
+        const int f = fail_k[bl * GSS_MAXCH + j];
+        kf = f < kf ? f : kf;
+    }
+    for (int j = 0; j < GSS_MAXCH && j <= kf; j++)
+        gsum += gabs[bl * GSS_MAXCH + j];
+    if (b < nblk) {
+        if (k > kf)
+            lin_row_init(l);                            /* the host never reached this channel */
+        if (k == 0) {
+            int ok = kf == GSS_MAXCH && gsum <= 8000;
+            if (force_exact > 0 && (first + b) % force_exact == 0)
+                ok = 0;
+            fast[b] = ok;
+        }
+    }
+}
+
+}  // namespace
+
+/* gss_run's launch (force_exact: its test hook); not exported (exports.map) */
+int run_proof_launch(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
+                     const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
+                     gss_lin_t *lin, int32_t *fast, int64_t first, int force_exact,
+                     hipStream_t st)
+{
+    if (nblk <= 0)
+        return 0;
+    hipLaunchKernelGGL(gss_proof_kernel, dim3((unsigned)((nblk + PF_BLOCKS - 1) / PF_BLOCKS)),
+                       dim3(PF_BLOCKS * GSS_MAXCH), 0, st, blk, nch, nblk, n_per_blk, ca_bits,
+                       n_ca, nav, n_nav, host_lut(), lin, fast, first, force_exact);
+    return hipGetLastError() == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "proof kernel launch");
+}
+
+extern "C" int gss_linearize_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
+                                    int nblk, int n_per_blk, const uint32_t *ca_bits, int n_ca,
+                                    const uint32_t *nav, int n_nav, gss_lin_t *lin, int32_t *fast,
+                                    void *stream)
+{
+    if (!d || !blk || !nch || !lin || !fast || nblk < 0 || n_per_blk <= 0 ||
+        (n_nav > 0 && !nav) || (n_ca > 0 && !ca_bits) || n_ca < 0)
+        return gss_fail(GSS_E_ARG, "invalid linearize_device arguments");
+    if (hipSetDevice(gss_dev_ordinal(d)) != hipSuccess)
+        return gss_fail(GSS_E_HIP, "hipSetDevice");
+    return run_proof_launch(blk, nch, nblk, n_per_blk, ca_bits, n_ca, nav, n_nav, lin, fast, 0, 0,
+                            (hipStream_t)stream);
+}

@@ -179,11 +179,19 @@ struct Slot {
     int32_t *d_status = nullptr, *h_status = nullptr;
     hipEvent_t rendered = nullptr;   /* compute stream: the slot's kernels are done      */
     hipEvent_t done = nullptr;       /* copy stream: the slot's bytes are in h_out        */
+    /* GPU proofs, launched by the planner (proof_ahead) */
+    hipStream_t pst = nullptr;       /* the slot's proof stream                          */
+    hipEvent_t navd = nullptr;       /* its nav rows are built (the planner's nav stream) */
+    hipEvent_t proved = nullptr;     /* its rows are on the device and proven            */
 };
 
 struct Run {
     gss_scn *scn;
     int batch, threads, n_per_blk, use_lin, carrier_int;
+    int gpu_proof = 0;               /* the proofs on the GPU (gss_proof.hip), run ahead by the
+                                        planner on each slot's own stream (proof_ahead)        */
+    hipStream_t nav_st = nullptr;    /* ... the planner's stream for the slots' nav rows      */
+    const uint32_t *d_ca = nullptr;  /* the run's device C/A table                            */
     int force_exact;                 /* GSS_RUN_FORCE_EXACT=k: every k-th block to the exact
                                         path (tests of the mixed batch), 0 = off */
     int64_t first, last;             /* [first, last) block range of the run */
@@ -254,6 +262,13 @@ static_assert(sizeof(gss_spec_in_t) <= 256 && 256 + sizeof(gss_spec_t) <= 1024,
    and they are computed afterwards for the uncertified blocks only, from each row's carr0 by
    the same exact walk.  The integer-carrier chain records them for free and keeps doing so. */
 static bool lazy_ck(const Run &r) { return r.use_lin && !r.carrier_int; }
+
+}  // namespace
+int run_proof_launch(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
+                     const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
+                     gss_lin_t *lin, int32_t *fast, int64_t first, int force_exact,
+                     hipStream_t st);                  /* gss_proof.hip */
+namespace {
 
 static void fill_fb_ck(const Run &r, Slot &sl)
 {
@@ -654,7 +669,8 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
         for (int i = 0; i < nb; i++)
             m = sl.nch[i] > m ? sl.nch[i] : m;
         sl.nch_max = m;
-        if (r.use_lin) {
+        sl.n_fb = 0;
+        if (r.use_lin && !r.gpu_proof) {
             const uint32_t *rows = nullptr;
             int n_rows = 0;
             gss_scn_nav_table(r.scn, &rows, &n_rows);
@@ -746,7 +762,8 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
             sl.lin_n_nav = n_rows;
             return 0;
         }
-        if (r.use_lin) {                               /* the proofs, on the planner thread */
+        sl.n_fb = 0;
+        if (r.use_lin && !r.gpu_proof) {               /* the proofs, on the planner thread */
             if (trace_on())
                 fprintf(stderr, "trace scn_done %.6f\n", tnow());
             rc = gss_linearize(sl.blk, sl.nch, nb, r.n_per_blk, r.ca, 32, rows, n_rows, sl.lin,
@@ -764,6 +781,8 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
     }
 }
 
+int proof_ahead(Run &r, Slot &sl);
+
 void planner(Run *r)
 {
     int64_t cursor = 0;
@@ -778,6 +797,8 @@ void planner(Run *r)
         }
         const double t0 = trace_on() ? tnow() : 0.0;
         int rc = up_rc ? up_rc : plan_into(*r, sl, &cursor);
+        if (!rc && !sl.end && r->gpu_proof)
+            rc = proof_ahead(*r, sl);
         if (trace_on())
             fprintf(stderr, "trace plan slot %d nb %d %.6f %.6f\n", i % NSLOT, sl.nb, t0, tnow());
         {
@@ -857,19 +878,116 @@ int nav_reserve(Run &r, size_t rows, hipStream_t st)
     return 0;
 }
 
-int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, int fmt,
-           size_t bb, hipStream_t st, hipStream_t cp)
+/* a slot's inputs on the device, one allocation (sl.d_in) */
+struct SlotDev {
+    gss_chan_blk_t *blk;
+    int32_t *nch;
+    double *ck;
+    gss_nav_src_t *src;
+    gss_lin_t *lin;
+    int32_t *fast;                   /* fast[nb], then the exact-path block list */
+    size_t need;
+};
+
+SlotDev slot_dev(const Slot &sl)
 {
-    /* the slot's previous D2H must have read d_out before the kernels rewrite it */
-    RUN_TRY(hipStreamWaitEvent(st, sl.done, 0));
     const size_t s_blk = sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)sl.nb;
     const size_t s_nch = sizeof(int32_t) * (size_t)sl.nb;
     const size_t s_ck = sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb;
     const size_t s_nav = sizeof(gss_nav_src_t) * (size_t)(sl.n_nav > 0 ? sl.n_nav : 1);
     const size_t s_lin = sl.lin ? sizeof(gss_lin_t) * GSS_MAXCH * (size_t)sl.nb : 0;
     const size_t s_fast = sl.lin ? sizeof(int32_t) * 2 * (size_t)sl.nb : 0;
-    const size_t need = al256(s_blk) + al256(s_nch) + al256(s_ck) + al256(s_nav) + al256(s_lin) +
-                        al256(s_fast);
+    SlotDev v;
+    v.need = al256(s_blk) + al256(s_nch) + al256(s_ck) + al256(s_nav) + al256(s_lin) +
+             al256(s_fast);
+    uint8_t *p = sl.d_in;
+    v.blk = (gss_chan_blk_t *)p;
+    v.nch = (int32_t *)(p + al256(s_blk));
+    v.ck = (double *)(p + al256(s_blk) + al256(s_nch));
+    v.src = (gss_nav_src_t *)(p + al256(s_blk) + al256(s_nch) + al256(s_ck));
+    v.lin = (gss_lin_t *)((uint8_t *)v.src + al256(s_nav));
+    v.fast = (int32_t *)((uint8_t *)v.lin + al256(s_lin));
+    return v;
+}
+
+/* GPU proofs, run ahead (planner thread, right after the slot is planned): the slot's rows go
+   to its device buffer on its own stream, its new nav rows are built on the planner's nav
+   stream (in slot order: a row may continue the one before it), and the proof kernel runs as
+   soon as both are there, so that several slots' proofs overlap the downloads of the slots
+   before them instead of waiting on the render stream.  The device nav table was reserved for
+   the whole run at set-up, so it never moves under the renders. */
+int proof_ahead(Run &r, Slot &sl)
+{
+    const size_t need = slot_dev(sl).need;
+    if (need > sl.d_in_cap) {                          /* the slot is FREE: nothing reads it */
+        (void)hipFree(sl.d_in);
+        sl.d_in = nullptr;
+        sl.d_in_cap = 0;
+        RUN_TRY(hipMalloc((void **)&sl.d_in, need));
+        sl.d_in_cap = need;
+    }
+    const SlotDev v = slot_dev(sl);
+    const int n_rows = sl.nav_first + sl.n_nav;
+    if ((size_t)n_rows > r.d_nav_cap)
+        return gss_fail(GSS_E_RANGE, "nav rows %d past the run's reservation %zu", n_rows,
+                        r.d_nav_cap);
+    if (sl.n_nav > 0) {
+        RUN_TRY(hipMemcpyAsync(v.src, sl.nav, sizeof(gss_nav_src_t) * (size_t)sl.n_nav,
+                               hipMemcpyHostToDevice, r.nav_st));
+        int rc = gss_nav_rows_device(r.dev, v.src, sl.nav_first, sl.n_nav, r.d_nav, r.nav_st);
+        if (rc)
+            return rc;
+    }
+    RUN_TRY(hipEventRecord(sl.navd, r.nav_st));
+    RUN_TRY(hipMemcpyAsync(v.blk, sl.blk, sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)sl.nb,
+                           hipMemcpyHostToDevice, sl.pst));
+    RUN_TRY(hipMemcpyAsync(v.nch, sl.nch, sizeof(int32_t) * (size_t)sl.nb, hipMemcpyHostToDevice,
+                           sl.pst));
+    if (!lazy_ck(r))               /* (with lazy checkpoints only a rejected block needs them) */
+        RUN_TRY(hipMemcpyAsync(v.ck, sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb,
+                               hipMemcpyHostToDevice, sl.pst));
+    RUN_TRY(hipStreamWaitEvent(sl.pst, sl.navd, 0));
+    int rc = run_proof_launch(v.blk, v.nch, sl.nb, r.n_per_blk, r.d_ca, 32, r.d_nav,
+                              n_rows > 0 ? n_rows : 1, v.lin, v.fast, sl.first, r.force_exact,
+                              sl.pst);
+    if (rc)
+        return rc;
+    RUN_TRY(hipEventRecord(sl.proved, sl.pst));
+    return 0;
+}
+
+/* submit for a slot proven by proof_ahead: render (every block as certified; the rejected ones
+   are redone in drain), then the bytes, the status and the proofs' verdicts to the host */
+int submit_proven(gss_dev *d, Run &r, Slot &sl, int n_per_blk, int fmt, size_t bb,
+                  hipStream_t st, hipStream_t cp)
+{
+    const SlotDev v = slot_dev(sl);
+    const int n_rows = sl.nav_first + sl.n_nav;
+    RUN_TRY(hipStreamWaitEvent(st, sl.proved, 0));
+    RUN_TRY(hipMemsetAsync(sl.d_status, 0, sizeof(int32_t), st));
+    int rc = gss_synth_lin_device(d, v.blk, v.nch, sl.nch_max, v.lin, v.fast, v.fast + sl.nb, 0,
+                                  v.ck, r.d_ca, 32, r.d_nav, n_rows > 0 ? n_rows : 1, sl.nb,
+                                  n_per_blk, fmt, sl.d_out, sl.d_status, st);
+    if (rc)
+        return rc;
+    RUN_TRY(hipEventRecord(sl.rendered, st));
+    RUN_TRY(hipStreamWaitEvent(cp, sl.rendered, 0));
+    RUN_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, bb * (size_t)sl.nb, hipMemcpyDeviceToHost, cp));
+    RUN_TRY(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int32_t), hipMemcpyDeviceToHost, cp));
+    RUN_TRY(hipMemcpyAsync(sl.fast, v.fast, sizeof(int32_t) * (size_t)sl.nb,
+                           hipMemcpyDeviceToHost, cp));
+    RUN_TRY(hipEventRecord(sl.done, cp));
+    return 0;
+}
+
+int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, int fmt,
+           size_t bb, hipStream_t st, hipStream_t cp)
+{
+    /* the slot's previous D2H must have read d_out before the kernels rewrite it */
+    RUN_TRY(hipStreamWaitEvent(st, sl.done, 0));
+    if (sl.lin && r.gpu_proof)
+        return submit_proven(d, r, sl, n_per_blk, fmt, bb, st, cp);
+    const size_t need = slot_dev(sl).need;
     if (need > sl.d_in_cap) {
         RUN_TRY(hipStreamSynchronize(st));
         (void)hipFree(sl.d_in);
@@ -878,23 +996,28 @@ int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, in
         RUN_TRY(hipMalloc((void **)&sl.d_in, need));
         sl.d_in_cap = need;
     }
-    uint8_t *p = sl.d_in;
-    gss_chan_blk_t *d_blk = (gss_chan_blk_t *)p;
-    int32_t *d_nch = (int32_t *)(p + al256(s_blk));
-    double *d_ck = (double *)(p + al256(s_blk) + al256(s_nch));
-    gss_nav_src_t *d_src = (gss_nav_src_t *)(p + al256(s_blk) + al256(s_nch) + al256(s_ck));
-    gss_lin_t *d_lin = (gss_lin_t *)((uint8_t *)d_src + al256(s_nav));
-    int32_t *d_fast = (int32_t *)((uint8_t *)d_lin + al256(s_lin));
+    const SlotDev v = slot_dev(sl);
+    gss_chan_blk_t *d_blk = v.blk;
+    int32_t *d_nch = v.nch;
+    double *d_ck = v.ck;
+    gss_nav_src_t *d_src = v.src;
+    gss_lin_t *d_lin = v.lin;
+    int32_t *d_fast = v.fast;
+    const size_t s_blk = sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)sl.nb;
+    const size_t s_lin = sizeof(gss_lin_t) * GSS_MAXCH * (size_t)sl.nb;
     RUN_TRY(hipMemcpyAsync(d_blk, sl.blk, s_blk, hipMemcpyHostToDevice, st));
-    RUN_TRY(hipMemcpyAsync(d_nch, sl.nch, s_nch, hipMemcpyHostToDevice, st));
-    RUN_TRY(hipMemcpyAsync(d_ck, sl.ck, s_ck, hipMemcpyHostToDevice, st));
+    RUN_TRY(hipMemcpyAsync(d_nch, sl.nch, sizeof(int32_t) * (size_t)sl.nb, hipMemcpyHostToDevice,
+                           st));
+    RUN_TRY(hipMemcpyAsync(d_ck, sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb,
+                           hipMemcpyHostToDevice, st));
     /* the 30 s producer: this slot's new nav rows built on the device (gss_producers.hip) */
     const int n_rows = sl.nav_first + sl.n_nav;
     int rc = nav_reserve(r, (size_t)(n_rows > 0 ? n_rows : 1), st);
     if (rc)
         return rc;
     if (sl.n_nav > 0) {
-        RUN_TRY(hipMemcpyAsync(d_src, sl.nav, s_nav, hipMemcpyHostToDevice, st));
+        RUN_TRY(hipMemcpyAsync(d_src, sl.nav, sizeof(gss_nav_src_t) * (size_t)sl.n_nav,
+                               hipMemcpyHostToDevice, st));
         rc = gss_nav_rows_device(d, d_src, sl.nav_first, sl.n_nav, r.d_nav, st);
         if (rc)
             return rc;
@@ -922,11 +1045,58 @@ int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, in
     return 0;
 }
 
-int drain(Run &r, Slot &sl, size_t bb, gss_sink_fn sink, void *user)
+/* GPU proofs: the blocks they rejected (fast[b] == 0, rare: none in the bench runs) rendered
+   again, this time with the exact path for them (their checkpoints from the rows' exact
+   carriers), and the slot's bytes copied once more; synchronous */
+int redo_rejected(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_rows, int n_per_blk,
+                  int fmt, size_t bb, hipStream_t st)
+{
+    int nf = 0;
+    for (int b = 0; b < sl.nb; b++)
+        if (!sl.fast[b])
+            sl.fast[sl.nb + nf++] = b;
+    if (nf == 0)
+        return 0;
+    sl.n_fb = nf;
+    if (lazy_ck(r))
+        for (int i = 0; i < nf; i++) {
+            const int b = sl.fast[sl.nb + i];
+            for (int k = 0; k < sl.nch[b]; k++) {
+                const size_t e = (size_t)b * GSS_MAXCH + k;
+                (void)gss_carr_advance_ck(sl.blk[e].carr0, sl.blk[e].carr_step, r.n_per_blk,
+                                          sl.ck + e * GSS_NCK);
+            }
+        }
+    const SlotDev v = slot_dev(sl);
+    RUN_TRY(hipMemcpyAsync(v.ck, sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb,
+                           hipMemcpyHostToDevice, st));
+    RUN_TRY(hipMemcpyAsync(v.fast + sl.nb, sl.fast + sl.nb, sizeof(int32_t) * (size_t)nf,
+                           hipMemcpyHostToDevice, st));
+    RUN_TRY(hipMemsetAsync(sl.d_status, 0, sizeof(int32_t), st));
+    int rc = gss_synth_lin_device(d, v.blk, v.nch, sl.nch_max, v.lin, v.fast, v.fast + sl.nb, nf,
+                                  v.ck, d_ca, 32, r.d_nav, n_rows, sl.nb, n_per_blk, fmt,
+                                  sl.d_out, sl.d_status, st);
+    if (rc)
+        return rc;
+    RUN_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, bb * (size_t)sl.nb, hipMemcpyDeviceToHost, st));
+    RUN_TRY(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    RUN_TRY(hipStreamSynchronize(st));
+    if (trace_on())
+        fprintf(stderr, "trace redo first %lld blocks %d\n", (long long)sl.first, nf);
+    return 0;
+}
+
+int drain(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, int fmt,
+          size_t bb, hipStream_t st, gss_sink_fn sink, void *user)
 {
     const double t0 = trace_on() ? tnow() : 0.0;
     RUN_TRY(hipEventSynchronize(sl.done));
     const double t1 = trace_on() ? tnow() : 0.0;
+    if (sl.lin && r.gpu_proof && !*sl.h_status) {
+        int rc = redo_rejected(d, r, sl, d_ca, sl.nav_first + sl.n_nav, n_per_blk, fmt, bb, st);
+        if (rc)
+            return rc;
+    }
     if (*sl.h_status)
         return gss_fail(GSS_E_RANGE, "nav word index ran past dwrd[59]");
     if (sink(user, sl.h_out, bb * (size_t)sl.nb, sl.first, sl.nb))
@@ -963,11 +1133,11 @@ int run_main(gss_dev *d, Run &r, int n_per_blk, int fmt, size_t bb, gss_sink_fn 
         if (sl.end) {
             int rc = 0;
             for (; np > 0 && rc == 0; np--, head = (head + 1) % DEPTH)
-                rc = drain(r, r.slot[pending[head]], bb, sink, user);
+                rc = drain(d, r, r.slot[pending[head]], d_ca, n_per_blk, fmt, bb, st, sink, user);
             return sl.err ? sl.err : rc;
         }
         if (np == DEPTH) {                             /* oldest slot out to the sink */
-            int rc = drain(r, r.slot[pending[head]], bb, sink, user);
+            int rc = drain(d, r, r.slot[pending[head]], d_ca, n_per_blk, fmt, bb, st, sink, user);
             if (rc)
                 return rc;
             head = (head + 1) % DEPTH;
@@ -1033,6 +1203,9 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         if (st) (void)hipStreamSynchronize(st);
         for (hipStream_t c : cp)
             if (c) (void)hipStreamSynchronize(c);
+        if (r.nav_st) (void)hipStreamSynchronize(r.nav_st);
+        for (Slot &sl : r.slot)                        /* proofs run ahead, not yet rendered */
+            if (sl.pst) (void)hipStreamSynchronize(sl.pst);
         for (Slot &sl : r.slot) {
             (void)hipHostFree(sl.blk); (void)hipHostFree(sl.nch); (void)hipHostFree(sl.ck);
             (void)hipHostFree(sl.nav); (void)hipHostFree(sl.h_status);
@@ -1043,6 +1216,12 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             if (sl.done) (void)hipEventDestroy(sl.done);
             if (sl.rendered) (void)hipEventDestroy(sl.rendered);
         }
+        for (Slot &sl : r.slot) {
+            if (sl.pst) (void)hipStreamDestroy(sl.pst);
+            if (sl.navd) (void)hipEventDestroy(sl.navd);
+            if (sl.proved) (void)hipEventDestroy(sl.proved);
+        }
+        if (r.nav_st) (void)hipStreamDestroy(r.nav_st);
         (void)hipFree(d_ca);
         (void)hipFree(r.d_nav);
         if (r.spec_st) (void)hipStreamSynchronize(r.spec_st);
@@ -1134,7 +1313,13 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             const bool want = e && *e ? e[0] != '0' : r.batch >= 1024;
             r.rows_ahead = r.spec && !(opts && opts->carr_in) && want;
         }
-        r.prover = r.rows_ahead && r.use_lin;
+        {
+            /* the proofs on the GPU (default with the fast path); GSS_RUN_PROOF=host: on the
+               host's threads (the planner's, or the prover thread's) */
+            const char *e = getenv("GSS_RUN_PROOF");
+            r.gpu_proof = r.use_lin && !(e && strcmp(e, "host") == 0);
+        }
+        r.prover = r.rows_ahead && r.use_lin && !r.gpu_proof;
         {
             const char *e = getenv("GSS_RUN_PROVER");
             if (e && e[0] == '0')
@@ -1153,6 +1338,26 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         }
         if (!err)
             err = gss_dev_reserve(d, r.batch, info.n_per_blk);
+        if (!err && r.gpu_proof) {
+            /* proofs run ahead on the slots' own streams (proof_ahead); the device nav table
+               reserved for the whole run (at most GSS_MAXCH new rows per 30 s update) */
+            r.dev = d;
+            r.d_ca = d_ca;
+            int lo_pri = 0, hi_pri = 0;
+            (void)hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri);
+            if (hipStreamCreateWithFlags(&r.nav_st, hipStreamNonBlocking) != hipSuccess)
+                err = gss_fail(GSS_E_HIP, "run nav stream");
+            for (Slot &sl : r.slot) {
+                if (err) break;
+                if (hipStreamCreateWithPriority(&sl.pst, hipStreamNonBlocking, hi_pri) !=
+                        hipSuccess ||
+                    hipEventCreateWithFlags(&sl.navd, hipEventDisableTiming) != hipSuccess ||
+                    hipEventCreateWithFlags(&sl.proved, hipEventDisableTiming) != hipSuccess)
+                    err = gss_fail(GSS_E_HIP, "run proof streams");
+            }
+            if (!err)
+                err = nav_reserve(r, ((size_t)info.n_blocks / 300 + 4) * GSS_MAXCH, st);
+        }
     }
     if (err) {
         cleanup();

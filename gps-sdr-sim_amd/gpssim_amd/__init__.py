@@ -119,6 +119,8 @@ _SIGS = {
                                  C.c_int, _P, _P]),
     "gss_linearize": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_int, _P, C.c_int, _P, _P,
                                 C.c_int]),
+    "gss_linearize_device": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, _P, C.c_int, _P, C.c_int, _P,
+                                       _P, _P]),
     "gss_synth_lin_device": (C.c_int, [_P, _P, _P, C.c_int, _P, _P, _P, C.c_int, _P, _P,
                                        C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P,
                                        _P]),
@@ -610,6 +612,15 @@ class Device:
         n, a, b = C.c_int(), C.c_float(), C.c_float()
         _check(lib().gss_dev_timing(self._h, 0, C.byref(n), C.byref(a), C.byref(b)))
         return n.value, a.value, b.value
+
+    def linearize_device(self, blk_ptr, nch_ptr, nblk, n_per_blk, ca_ptr, n_ca, nav_ptr, n_nav,
+                         lin_ptr, fast_ptr, stream=0):
+        """gss_linearize_device: the fast path's proofs on the GPU (device pointers, rows as
+        gss_linearize's, async on stream)."""
+        _check(lib().gss_linearize_device(self._h, C.c_void_p(blk_ptr), C.c_void_p(nch_ptr), nblk,
+                                          n_per_blk, C.c_void_p(ca_ptr), n_ca,
+                                          C.c_void_p(nav_ptr), n_nav, C.c_void_p(lin_ptr),
+                                          C.c_void_p(fast_ptr), C.c_void_p(stream)))
 
     def spec_device(self, in_ptr, nrow, n_per_blk, spec_ptr, stream=0):
         """gss_spec_device on raw device pointers (nrow SPEC_IN_DTYPE rows in, SPEC_DTYPE rows

@@ -1,5 +1,6 @@
-"""Device-resident rendering of a block range: the host plane (Scenario), the host proof
-(gss_linearize) and gss_synth_lin_device in batches, output left in HBM (a torch uint8 tensor).
+"""Device-resident rendering of a block range: the host plane (Scenario), the proofs
+(gss_linearize_device on the GPU, or gss_linearize on the host) and gss_synth_lin_device in
+batches, output left in HBM (a torch uint8 tensor).
 
 Used by bench.py (timed steps over a resident window) and gpssim_amd.node (each rank renders its
 time-window shard before the ordered gather to rank 0); the rows come from gpssim_amd.shard.  torch is only the allocator and stream
@@ -29,11 +30,32 @@ class DeviceWindow:
     blocks (each call's fast-path scratch rows scale with its block count)."""
 
     def __init__(self, torch, dev, dev_t, blk, nch, nav, n_per_blk, fmt, ck=None, threads=8,
-                 batch=3000, out=None):
+                 batch=3000, out=None, proof="gpu"):
         self.torch, self.dev, self.fmt, self.npb = torch, dev, fmt, n_per_blk
+
+        def up(a):
+            return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev_t)
+
         t0 = time.perf_counter()
-        lin, fast = linearize(blk, nch, nav, n_per_blk, threads=threads)
+        if proof == "gpu":                 # the proofs on the GPU: only the fast flags come back
+            self.d_blk, self.d_nch = up(blk), up(np.asarray(nch, np.int32))
+            ca = ca_table()
+            self.d_ca, self.d_nav = up(ca), up(nav)
+            nb = len(nch)
+            self.d_lin = torch.empty(max(1, nb * MAXCH * LIN_DTYPE.itemsize), dtype=torch.uint8,
+                                     device=dev_t)
+            d_fast = torch.empty(max(1, nb), dtype=torch.int32, device=dev_t)
+            stream = torch.cuda.current_stream(dev_t).cuda_stream
+            if nb:
+                dev.linearize_device(self.d_blk.data_ptr(), self.d_nch.data_ptr(), nb, n_per_blk,
+                                     self.d_ca.data_ptr(), len(ca), self.d_nav.data_ptr(),
+                                     len(nav), self.d_lin.data_ptr(), d_fast.data_ptr(), stream)
+            fast = d_fast[:nb].cpu().numpy()           # (synchronises the stream)
+            lin = None
+        else:
+            lin, fast = linearize(blk, nch, nav, n_per_blk, threads=threads)
         self.lin_s = time.perf_counter() - t0
+        self.proof = proof
         self.nblk = len(nch)
         self.n_fast = int(fast.sum())
         # channel-samples the fast kernel renders per pass (its compute roofline's unit)
@@ -44,16 +66,15 @@ class DeviceWindow:
         self.n_ca, self.n_nav = len(ca), len(nav)
         self.bb = block_bytes(n_per_blk, fmt)
 
-        def up(a):
-            return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev_t)
-
         if ck is None and self.n_fast < self.nblk:
             # rows planned without checkpoints (the chain run ahead, shard.plan_window): the
             # exact path's Stage A starts from them, so give the uncertified blocks theirs
             ck = block_checkpoints(blk, nch, n_per_blk, np.nonzero(fast == 0)[0])
-        self.d_blk, self.d_nch, self.d_lin = up(blk), up(nch), up(lin)
+        if lin is not None:
+            self.d_blk, self.d_nch, self.d_lin = up(blk), up(nch), up(lin)
+            self.d_ca, self.d_nav = up(ca), up(nav)
         self.d_ck = up(ck) if ck is not None else None
-        self.d_ca, self.d_nav, self.d_fast = up(ca), up(nav), up(fast)
+        self.d_fast = up(np.asarray(fast, np.int32))
         self.out = out if out is not None else torch.empty(self.nblk * self.bb, dtype=torch.uint8,
                                                            device=dev_t)
         assert self.out.numel() >= self.nblk * self.bb

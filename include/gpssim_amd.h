@@ -152,6 +152,13 @@ int gss_linearize(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n
                   const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
                   gss_lin_t *lin, int32_t *fast, int threads);
 
+/* gss_linearize on the GPU: the same proofs and the same rows, byte for byte (the per-channel
+   proof is csrc/common/gss_proof.h on both sides).  Device pointers; asynchronous on `stream`.
+   gss_run proves its slots with it (GSS_RUN_PROOF=host: on the host threads instead).          */
+int gss_linearize_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch, int nblk,
+                         int n_per_blk, const uint32_t *ca_bits, int n_ca, const uint32_t *nav,
+                         int n_nav, gss_lin_t *lin, int32_t *fast, void *stream);
+
 /* gss_synth_device over the certified fast path.  Device pointers as gss_synth_device, plus
    lin [nblk][GSS_MAXCH] and fast [nblk] from gss_linearize, and the exact path's block list
    fb_list [n_fb] (device; the indices b with fast[b] == 0, n_fb known on the host).  carr_ck

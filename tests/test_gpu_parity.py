@@ -278,12 +278,15 @@ def test_streaming_run_bit_exact(dev, golden):
     assert [x for _, x in blocks] == g["block_sha16"][123:184]
 
 
+@pytest.mark.parametrize("proof", ["gpu", "host"])
 @pytest.mark.parametrize("fmt,every", [(16, 5), (8, 7)])
-def test_streaming_run_mixed_exact(dev, golden, monkeypatch, fmt, every):
+def test_streaming_run_mixed_exact(dev, golden, monkeypatch, fmt, every, proof):
     """gss_run with every k-th block sent to the exact path (GSS_RUN_FORCE_EXACT, a test hook):
     the planner walks the chain without checkpoints and computes them afterwards for those
-    blocks only (fill_fb_ck); whole run and a mid-run range against the golden hashes."""
+    blocks only (fill_fb_ck; with the proofs on the GPU, drain renders the slot again with
+    them: redo_rejected); whole run and a mid-run range against the golden hashes."""
     monkeypatch.setenv("GSS_RUN_FORCE_EXACT", str(every))
+    monkeypatch.setenv("GSS_RUN_PROOF", proof)
     g = golden[f"static_d30_b{fmt}"]
     s = G.Scenario(NAV, llh=LOC, duration=30.0, data_format=fmt)
     bb = G.block_bytes(s.n_per_blk, fmt)
@@ -500,16 +503,20 @@ def test_streaming_run_sink_error_stops_cleanly(dev, golden):
     assert blocks == g["block_sha16"]
 
 
-@pytest.mark.parametrize("spec,ahead,prover,batch", [("0", "1", "1", 57), ("1", "0", "1", 57),
-                                                      ("1", "1", "0", 57), ("1", "1", "1", 57),
-                                                      ("1", "1", "1", 1)])
-def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec, ahead, prover, batch):
+@pytest.mark.parametrize("spec,ahead,prover,proof,batch", [
+    ("0", "1", "1", "host", 57), ("1", "0", "1", "host", 57), ("1", "1", "0", "host", 57),
+    ("1", "1", "1", "host", 57), ("1", "1", "1", "host", 1),
+    ("0", "1", "1", "gpu", 57), ("1", "0", "1", "gpu", 57), ("1", "1", "1", "gpu", 57),
+    ("1", "1", "1", "gpu", 1)])
+def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec, ahead, prover, proof, batch):
     """gss_run with the carrier chain walked on the host (GSS_RUN_SPEC=0) and run ahead on the
     GPU (the default), with the rows produced on the planner thread (GSS_RUN_ROWS_AHEAD=0) or
     ahead on their own (the default; one-block batches too), and the proofs on the planner thread
-    (GSS_RUN_PROVER=0) or their own (the default): a 65 s run across two 30 s updates, whole and
-    from a mid-run block, against the reference's golden hashes."""
+    (GSS_RUN_PROVER=0) or their own, or on the GPU (GSS_RUN_PROOF=gpu, the default): a 65 s run
+    across two 30 s updates, whole and from a mid-run block, against the reference's golden
+    hashes."""
     monkeypatch.setenv("GSS_RUN_SPEC", spec)
+    monkeypatch.setenv("GSS_RUN_PROOF", proof)
     monkeypatch.setenv("GSS_RUN_ROWS_AHEAD", ahead)
     monkeypatch.setenv("GSS_RUN_PROVER", prover)
     g = golden["static_d65_b8_noiono"]

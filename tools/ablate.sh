@@ -13,6 +13,7 @@ F="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -
 $HIPCC $F -c ${SYNTH_SRC:-gps-sdr-sim_amd/csrc/hip/gss_synth.hip} -o _var/$name/obj/gss_synth.o
 $HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_run.hip -o _var/$name/obj/gss_run.o
 $HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_producers.hip -o _var/$name/obj/gss_producers.o
+$HIPCC $F -c gps-sdr-sim_amd/csrc/hip/gss_proof.hip -o _var/$name/obj/gss_proof.o
 HOSTOBJ=gps-sdr-sim_amd/obj/host/*.o
 if [ -n "$HOSTFLAGS" ]; then          # the host proof must agree with the kernel (e.g. GSS_LIN_CH)
     mkdir -p _var/$name/obj/host
@@ -24,4 +25,5 @@ if [ -n "$HOSTFLAGS" ]; then          # the host proof must agree with the kerne
 fi
 $HIPCC -shared -fPIC --offload-arch=gfx950 -Wl,--version-script=gps-sdr-sim_amd/exports.map \
     -o _var/$name/libgpssim_amd.so $HOSTOBJ \
-    _var/$name/obj/gss_synth.o _var/$name/obj/gss_run.o _var/$name/obj/gss_producers.o -lm -lpthread
+    _var/$name/obj/gss_synth.o _var/$name/obj/gss_run.o _var/$name/obj/gss_producers.o \
+    _var/$name/obj/gss_proof.o -lm -lpthread
