@@ -410,6 +410,16 @@ int take_nav_sources(Run &r, Slot &sl, int upto)
     }
     if (n > 0)
         memcpy(sl.nav, src + r.nav_planned, sizeof(gss_nav_src_t) * (size_t)n);
+    /* the chains' next links within the slot's rows, from their prev links: the rows thread's
+       copies (nav_src_h) were taken when each row was new, before its successor existed, and
+       gss_nav_kernel reaches every row but a chain's head through them */
+    for (int i = 0; i < n; i++)
+        sl.nav[i].next = -1;
+    for (int i = 0; i < n; i++) {
+        const int pv = sl.nav[i].prev;
+        if (pv >= r.nav_planned && pv < r.nav_planned + i)
+            sl.nav[pv - r.nav_planned].next = r.nav_planned + i;
+    }
     sl.nav_first = r.nav_planned;
     sl.n_nav = n;
     r.nav_planned += n;
@@ -1314,10 +1324,12 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             r.rows_ahead = r.spec && !(opts && opts->carr_in) && want;
         }
         {
-            /* the proofs on the GPU (default with the fast path); GSS_RUN_PROOF=host: on the
-               host's threads (the planner's, or the prover thread's) */
+            /* GSS_RUN_PROOF=gpu: the proofs on the GPU, run ahead by the planner (proof_ahead).
+               Not the default: one lane per channel-block leaves the proof kernel latency-bound
+               (2.3 ms per slot at 2.6 MS/s, 6.8 ms at 20 MS/s), more than a slot's download
+               takes, and the planner is not far enough ahead to hide it */
             const char *e = getenv("GSS_RUN_PROOF");
-            r.gpu_proof = r.use_lin && !(e && strcmp(e, "host") == 0);
+            r.gpu_proof = r.use_lin && e && strcmp(e, "gpu") == 0;
         }
         r.prover = r.rows_ahead && r.use_lin && !r.gpu_proof;
         {
@@ -1357,6 +1369,9 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             }
             if (!err)
                 err = nav_reserve(r, ((size_t)info.n_blocks / 300 + 4) * GSS_MAXCH, st);
+            /* the C/A table (built on st above) before any proof stream reads it */
+            if (!err && hipStreamSynchronize(st) != hipSuccess)
+                err = gss_fail(GSS_E_HIP, "run set-up");
         }
     }
     if (err) {

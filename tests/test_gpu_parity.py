@@ -305,6 +305,31 @@ def test_streaming_run_mixed_exact(dev, golden, monkeypatch, fmt, every, proof):
     assert [x for _, x in blocks] == g["block_sha16"][101:178]
 
 
+@pytest.mark.parametrize("proof", ["host", "gpu"])
+def test_streaming_run_rows_ahead_midrun_exact_path(dev, golden, monkeypatch, proof):
+    """The rows thread's nav sources are copied when each row is new, before the next frame of
+    its channel exists, so a slot that takes many rows at once (a range starting past a 30 s
+    update) must rebuild their chains' next links (take_nav_sources) or the device nav table
+    misses rows.  The fast path never reads that table; every block on the exact path does."""
+    monkeypatch.setenv("GSS_RUN_SPEC", "1")
+    monkeypatch.setenv("GSS_RUN_ROWS_AHEAD", "1")
+    monkeypatch.setenv("GSS_RUN_FORCE_EXACT", "1")
+    monkeypatch.setenv("GSS_RUN_PROOF", proof)
+    g = golden["static_d65_b8_noiono"]
+    blocks = []
+    s, _ = G.Scenario.from_cli(["-e", NAV, "-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8",
+                                "-i"])
+    bb = G.block_bytes(s.n_per_blk, 8)
+
+    def sink(buf, first, nb):
+        for i in range(nb):
+            blocks.append((first + i, hashlib.sha256(buf[i * bb:(i + 1) * bb]).hexdigest()[:16]))
+
+    dev.run(s, sink, first_block=333, n_blocks=150, batch=64)
+    assert [b for b, _ in blocks] == list(range(333, 483))
+    assert [x for _, x in blocks] == g["block_sha16"][333:483]
+
+
 @pytest.mark.parametrize("world,handoff,gold,args", [
     # every rank plans the blocks before its range itself (no run id)
     (2, False, "static_d30_b16", ["-l", ",".join(map(str, LOC)), "-d", "30", "-b", "16"]),
