@@ -28,37 +28,21 @@
 typedef unsigned __int128 u128;
 typedef __int128 i128;
 
-/* floor(a / b) for a quotient below 2^64 (b > 0): native on the host, shift-subtract on the GPU
-   (no 128-bit division there); the two agree whenever the quotient fits */
+/* floor(a / b) for a quotient below 2^53 (b > 0): a 64-bit division when a fits 64 bits, else
+   a double estimate (relative error 2^-52: off by at most one here) corrected by exact products;
+   no 128-bit division (none on the GPU, a slow library call on the host) */
 GSS_PF uint64_t gss_pf_udiv(u128 a, uint64_t b)
 {
-#if defined(__HIP_DEVICE_COMPILE__)
     if ((uint64_t)(a >> 64) == 0)
         return (uint64_t)a / b;
-    uint64_t q = 0;
-    u128 r = a >> 64;                                    /* < b: the quotient fits 64 bits */
-    uint64_t lo = (uint64_t)a;
-    for (int i = 63; i >= 0; i--) {
-        r = (r << 1) | ((lo >> i) & 1u);
-        if (r >= b) {
-            r -= b;
-            q |= (uint64_t)1 << i;
-        }
-    }
+    uint64_t q = (uint64_t)((double)a / (double)b);
+    while ((u128)q * b > a)
+        q--;
+    while ((u128)(q + 1) * b <= a)
+        q++;
     return q;
-#else
-    return (uint64_t)(a / b);
-#endif
 }
 
-/* ---- exact first hit ------------------------------------------------------------------------- */
-/* Smallest x in [0, lim] with lo <= (s x) mod m <= hi, for 1 <= lo <= hi < m < 2^62 and s < m;
- * UINT64_MAX if there is none.  Every candidate is >= ceil(lo/s); if s x reaches [lo, hi] before
- * its first wrap, that is x.  Otherwise [lo, hi] holds no multiple of s (so hi - lo < s), and x
- * exists for wrap count y iff some multiple of s lies in [lo + m y, hi + m y], i.e. (m y) mod s
- * lies in [s - hi mod s, s - lo mod s]: the same question for (m mod s, s), Euclid's descent, with
- * x = ceil((lo + m y) / s) of the least y.  x <= lim needs y <= lim s / m: the descent stops as
- * soon as that bound (an overestimate in double, so nothing is cut wrongly) is out of reach. */
 #define GSS_PF_EUCLID_MAX 64       /* descent levels kept (a deeper one gives up: uncertified) */
 #define GSS_PF_GIVE_UP (UINT64_MAX - 1)
 GSS_PF uint64_t first_in(uint64_t s, uint64_t m, uint64_t lo, uint64_t hi, uint64_t lim)
@@ -101,8 +85,9 @@ GSS_PF uint64_t first_in(uint64_t s, uint64_t m, uint64_t lo, uint64_t hi, uint6
         d--;
         if (r == UINT64_MAX)
             return UINT64_MAX;
-        const uint64_t v = gss_pf_udiv((u128)flo[d] + (u128)fm[d] * r + fs[d] - 1, fs[d]);
-        r = v <= flim[d] ? v : UINT64_MAX;
+        const u128 num = (u128)flo[d] + (u128)fm[d] * r + fs[d] - 1;
+        /* v <= lim  <=>  num < (lim + 1) s; only then divide (the quotient fits) */
+        r = num < ((u128)flim[d] + 1) * fs[d] ? gss_pf_udiv(num, fs[d]) : UINT64_MAX;
     }
     return r;
 }
@@ -126,8 +111,18 @@ GSS_PF uint64_t first_below(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint
 GSS_PF i128 to_fix(double x, int k, int *inexact)
 {
     int e;
-    double fr = frexp(x, &e);                        /* x = fr * 2^e, 0.5 <= |fr| < 1 */
-    int64_t m = (int64_t)ldexp(fr, 53);              /* exact: x = m * 2^(e-53) */
+    int64_t m;                                       /* exact: x = m * 2^(e-53) */
+    uint64_t bits;
+    memcpy(&bits, &x, sizeof bits);
+    const int E = (int)((bits >> 52) & 0x7FF);
+    if (E != 0 && E != 0x7FF) {                      /* normal: the fields directly */
+        const int64_t M = (int64_t)((bits & (((uint64_t)1 << 52) - 1)) | ((uint64_t)1 << 52));
+        m = (bits >> 63) ? -M : M;
+        e = E - 1022;                                /* frexp's: x = (M / 2^53) * 2^e */
+    } else {
+        const double fr = frexp(x, &e);              /* x = fr * 2^e, 0.5 <= |fr| < 1 */
+        m = (int64_t)ldexp(fr, 53);
+    }
     int sh = e - 53 + k;
     if (x == 0.0)
         return 0;
@@ -295,7 +290,9 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
     gss_code_state st = {c0, p->icode, p->ibit, p->iword};
     int64_t at = 0;
     for (int i = 0; i < nhz; i++) {
+#ifndef GSS_PF_ABLATE_CODE_WALK          /* (measurement builds only: wrong rows) */
         gss_code_walk_cc(&st, cs, hz[i] - at);
+#endif
         at = hz[i];
         at_hz[i] = st;
     }
@@ -354,7 +351,9 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
         if (q == 0) {
             cell = (int)floor(x0 * 512.0);
         } else if (near_boundary(X0 + (i128)q * XS, DX1, LIN_CARR_LGB)) {
+#ifndef GSS_PF_ABLATE_CARR_WALK
             x = gss_carr_walk_cc(x, s, q - xat);     /* the reference may differ from the line */
+#endif
             xat = q;
             cell = (int)floor(x * 512.0);
             if (cell > 511)      /* carr += 1.0 rounded to 1.0: the reference reads cosTable512[512]

@@ -183,12 +183,14 @@ struct Slot {
     hipStream_t pst = nullptr;       /* the slot's proof stream                          */
     hipEvent_t navd = nullptr;       /* its nav rows are built (the planner's nav stream) */
     hipEvent_t proved = nullptr;     /* its rows are on the device and proven            */
+    int gpu_proven = 0;              /* this use of the slot is proven on the GPU         */
 };
 
 struct Run {
     gss_scn *scn;
     int batch, threads, n_per_blk, use_lin, carrier_int;
-    int gpu_proof = 0;               /* the proofs on the GPU (gss_proof.hip), run ahead by the
+    int proof_mode = 0;              /* 0: host proofs, 1: all on the GPU, 2: every other slot */
+    int gpu_proof = 0;               /* any proofs on the GPU (gss_proof.hip), run ahead by the
                                         planner on each slot's own stream (proof_ahead)        */
     hipStream_t nav_st = nullptr;    /* ... the planner's stream for the slots' nav rows      */
     const uint32_t *d_ca = nullptr;  /* the run's device C/A table                            */
@@ -680,7 +682,7 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
             m = sl.nch[i] > m ? sl.nch[i] : m;
         sl.nch_max = m;
         sl.n_fb = 0;
-        if (r.use_lin && !r.gpu_proof) {
+        if (r.use_lin && !sl.gpu_proven) {
             const uint32_t *rows = nullptr;
             int n_rows = 0;
             gss_scn_nav_table(r.scn, &rows, &n_rows);
@@ -773,7 +775,7 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
             return 0;
         }
         sl.n_fb = 0;
-        if (r.use_lin && !r.gpu_proof) {               /* the proofs, on the planner thread */
+        if (r.use_lin && !sl.gpu_proven) {             /* the proofs, on the planner thread */
             if (trace_on())
                 fprintf(stderr, "trace scn_done %.6f\n", tnow());
             rc = gss_linearize(sl.blk, sl.nch, nb, r.n_per_blk, r.ca, 32, rows, n_rows, sl.lin,
@@ -806,8 +808,9 @@ void planner(Run *r)
                 return;
         }
         const double t0 = trace_on() ? tnow() : 0.0;
+        sl.gpu_proven = r->use_lin && (r->proof_mode == 1 || (r->proof_mode == 2 && (i & 1)));
         int rc = up_rc ? up_rc : plan_into(*r, sl, &cursor);
-        if (!rc && !sl.end && r->gpu_proof)
+        if (!rc && !sl.end && sl.gpu_proven)
             rc = proof_ahead(*r, sl);
         if (trace_on())
             fprintf(stderr, "trace plan slot %d nb %d %.6f %.6f\n", i % NSLOT, sl.nb, t0, tnow());
@@ -839,7 +842,7 @@ void prover(Run *r)
                 return;
         }
         const double t0 = trace_on() ? tnow() : 0.0;
-        if (!sl.end && !sl.err) {
+        if (!sl.end && !sl.err && !sl.gpu_proven) {
             int rc = gss_linearize(sl.blk, sl.nch, sl.nb, r->n_per_blk, r->ca, 32, sl.lin_nav,
                                    sl.lin_n_nav, sl.lin, sl.fast, r->threads);
             if (rc) {
@@ -995,7 +998,7 @@ int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, in
 {
     /* the slot's previous D2H must have read d_out before the kernels rewrite it */
     RUN_TRY(hipStreamWaitEvent(st, sl.done, 0));
-    if (sl.lin && r.gpu_proof)
+    if (sl.lin && sl.gpu_proven)
         return submit_proven(d, r, sl, n_per_blk, fmt, bb, st, cp);
     const size_t need = slot_dev(sl).need;
     if (need > sl.d_in_cap) {
@@ -1102,7 +1105,7 @@ int drain(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, int
     const double t0 = trace_on() ? tnow() : 0.0;
     RUN_TRY(hipEventSynchronize(sl.done));
     const double t1 = trace_on() ? tnow() : 0.0;
-    if (sl.lin && r.gpu_proof && !*sl.h_status) {
+    if (sl.lin && sl.gpu_proven && !*sl.h_status) {
         int rc = redo_rejected(d, r, sl, d_ca, sl.nav_first + sl.n_nav, n_per_blk, fmt, bb, st);
         if (rc)
             return rc;
@@ -1329,9 +1332,11 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                (2.3 ms per slot at 2.6 MS/s, 6.8 ms at 20 MS/s), more than a slot's download
                takes, and the planner is not far enough ahead to hide it */
             const char *e = getenv("GSS_RUN_PROOF");
-            r.gpu_proof = r.use_lin && e && strcmp(e, "gpu") == 0;
+            r.proof_mode = !r.use_lin || !e ? 0 : strcmp(e, "gpu") == 0 ? 1 :
+                           strcmp(e, "split") == 0 ? 2 : 0;
+            r.gpu_proof = r.proof_mode != 0;
         }
-        r.prover = r.rows_ahead && r.use_lin && !r.gpu_proof;
+        r.prover = r.rows_ahead && r.use_lin && r.proof_mode != 1;
         {
             const char *e = getenv("GSS_RUN_PROVER");
             if (e && e[0] == '0')

@@ -278,7 +278,7 @@ def test_streaming_run_bit_exact(dev, golden):
     assert [x for _, x in blocks] == g["block_sha16"][123:184]
 
 
-@pytest.mark.parametrize("proof", ["gpu", "host"])
+@pytest.mark.parametrize("proof", ["gpu", "host", "split"])
 @pytest.mark.parametrize("fmt,every", [(16, 5), (8, 7)])
 def test_streaming_run_mixed_exact(dev, golden, monkeypatch, fmt, every, proof):
     """gss_run with every k-th block sent to the exact path (GSS_RUN_FORCE_EXACT, a test hook):
@@ -305,7 +305,7 @@ def test_streaming_run_mixed_exact(dev, golden, monkeypatch, fmt, every, proof):
     assert [x for _, x in blocks] == g["block_sha16"][101:178]
 
 
-@pytest.mark.parametrize("proof", ["host", "gpu"])
+@pytest.mark.parametrize("proof", ["host", "gpu", "split"])
 def test_streaming_run_rows_ahead_midrun_exact_path(dev, golden, monkeypatch, proof):
     """The rows thread's nav sources are copied when each row is new, before the next frame of
     its channel exists, so a slot that takes many rows at once (a range starting past a 30 s
@@ -532,12 +532,12 @@ def test_streaming_run_sink_error_stops_cleanly(dev, golden):
     ("0", "1", "1", "host", 57), ("1", "0", "1", "host", 57), ("1", "1", "0", "host", 57),
     ("1", "1", "1", "host", 57), ("1", "1", "1", "host", 1),
     ("0", "1", "1", "gpu", 57), ("1", "0", "1", "gpu", 57), ("1", "1", "1", "gpu", 57),
-    ("1", "1", "1", "gpu", 1)])
+    ("1", "1", "1", "gpu", 1), ("1", "1", "1", "split", 57), ("1", "0", "1", "split", 1)])
 def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec, ahead, prover, proof, batch):
     """gss_run with the carrier chain walked on the host (GSS_RUN_SPEC=0) and run ahead on the
     GPU (the default), with the rows produced on the planner thread (GSS_RUN_ROWS_AHEAD=0) or
     ahead on their own (the default; one-block batches too), and the proofs on the planner thread
-    (GSS_RUN_PROVER=0) or their own, or on the GPU (GSS_RUN_PROOF=gpu, the default): a 65 s run
+    (GSS_RUN_PROVER=0) or their own, or on the GPU (GSS_RUN_PROOF=gpu; split: every other slot): a 65 s run
     across two 30 s updates, whole and from a mid-run block, against the reference's golden
     hashes."""
     monkeypatch.setenv("GSS_RUN_SPEC", spec)

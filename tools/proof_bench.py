@@ -1,6 +1,6 @@
 """Time gss_linearize_device against gss_linearize on one slot's rows (GPU box only).
 
-usage: python tools/proof_bench.py [fmt] [blocks] [repeats]
+usage: python tools/proof_bench.py [fmt] [blocks] [repeats] [sample rate]
 Prints one JSON line: device ms per call (HIP events), host ms (1 and 16 threads), rows equal."""
 import json
 import os
@@ -19,7 +19,8 @@ def main():
     fmt = int(sys.argv[1]) if len(sys.argv) > 1 else 1
     nb = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-    s = G.Scenario(B.NAV, llh=B.LOC, duration=nb / 10 + 1, samp_freq=2.6e6, data_format=fmt)
+    fs = float(sys.argv[4]) if len(sys.argv) > 4 else 2.6e6
+    s = G.Scenario(B.NAV, llh=B.LOC, duration=nb / 10 + 1, samp_freq=fs, data_format=fmt)
     blk, nch = s.next(nb, 16)[:2]
     nav = s.nav_table()
     n = s.n_per_blk
@@ -51,7 +52,7 @@ def main():
         host[th] = (time.perf_counter() - t0) * 1e3
     same = bool(np.array_equal(d_lin.cpu().numpy(), lin.view(np.uint8).reshape(-1)) and
                 np.array_equal(d_fast.cpu().numpy(), fast))
-    print(json.dumps({"fmt": fmt, "blocks": nb, "channels": int(np.sum(nch)),
+    print(json.dumps({"lib": os.path.relpath(G.LIB_PATH, REPO), "fs": fs, "fmt": fmt, "blocks": nb, "channels": int(np.sum(nch)),
                       "device_ms": [round(x, 3) for x in times],
                       "host_ms_1": round(host[1], 2), "host_ms_16": round(host[16], 2),
                       "same": same, "build": G.build_info()}), flush=True)
