@@ -810,7 +810,7 @@ void planner(Run *r)
         const double t0 = trace_on() ? tnow() : 0.0;
         sl.gpu_proven = r->use_lin && (r->proof_mode == 1 || (r->proof_mode == 2 && (i & 1)));
         int rc = up_rc ? up_rc : plan_into(*r, sl, &cursor);
-        if (!rc && !sl.end && sl.gpu_proven)
+        if (!rc && !sl.end && r->gpu_proof)
             rc = proof_ahead(*r, sl);
         if (trace_on())
             fprintf(stderr, "trace plan slot %d nb %d %.6f %.6f\n", i % NSLOT, sl.nb, t0, tnow());
@@ -931,6 +931,8 @@ SlotDev slot_dev(const Slot &sl)
    the whole run at set-up, so it never moves under the renders. */
 int proof_ahead(Run &r, Slot &sl)
 {
+    /* the nav rows of every slot come from here when any slot is proven on the GPU (a row may
+       continue one that an earlier slot brought); the proof only for the slots that take it */
     const size_t need = slot_dev(sl).need;
     if (need > sl.d_in_cap) {                          /* the slot is FREE: nothing reads it */
         (void)hipFree(sl.d_in);
@@ -952,6 +954,8 @@ int proof_ahead(Run &r, Slot &sl)
             return rc;
     }
     RUN_TRY(hipEventRecord(sl.navd, r.nav_st));
+    if (!sl.gpu_proven)
+        return 0;
     RUN_TRY(hipMemcpyAsync(v.blk, sl.blk, sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)sl.nb,
                            hipMemcpyHostToDevice, sl.pst));
     RUN_TRY(hipMemcpyAsync(v.nch, sl.nch, sizeof(int32_t) * (size_t)sl.nb, hipMemcpyHostToDevice,
@@ -1023,12 +1027,15 @@ int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, in
                            st));
     RUN_TRY(hipMemcpyAsync(d_ck, sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb,
                            hipMemcpyHostToDevice, st));
-    /* the 30 s producer: this slot's new nav rows built on the device (gss_producers.hip) */
+    /* the 30 s producer: this slot's new nav rows built on the device (gss_producers.hip); with
+       GPU proofs in the run the planner has built them already (proof_ahead) */
     const int n_rows = sl.nav_first + sl.n_nav;
-    int rc = nav_reserve(r, (size_t)(n_rows > 0 ? n_rows : 1), st);
+    int rc = r.gpu_proof ? 0 : nav_reserve(r, (size_t)(n_rows > 0 ? n_rows : 1), st);
     if (rc)
         return rc;
-    if (sl.n_nav > 0) {
+    if (r.gpu_proof) {
+        RUN_TRY(hipStreamWaitEvent(st, sl.navd, 0));
+    } else if (sl.n_nav > 0) {
         RUN_TRY(hipMemcpyAsync(d_src, sl.nav, sizeof(gss_nav_src_t) * (size_t)sl.n_nav,
                                hipMemcpyHostToDevice, st));
         rc = gss_nav_rows_device(d, d_src, sl.nav_first, sl.n_nav, r.d_nav, st);

@@ -660,7 +660,7 @@ int gss_carr_chain_spec(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
  * every block, and block b only uses its own range and block b-1's.  Between two 30 s updates the
  * channel set, the ephemeris set and the receiver positions are fixed, so the ranges of a run of
  * blocks up to the next update are independent: threads compute them (range_pass), then the
- * refresh walks the run in order with the same arithmetic as before. */
+ * blocks' refreshes, again in parallel (next_rows). */
 typedef struct {
     const gss_scn *s;
     const gtime_t *g;                       /* [j] receiver time of block j of the run */
@@ -760,97 +760,164 @@ static int update_30s(gss_scn *s, const double *xyz, int push_nav)
     return 0;
 }
 
+/* The per-block refresh of one channel (gpssim.c:2156-2188) from its range at the block (rho)
+   and at the block before (rho_prev): the row, and in *c the channel state the serial loop of
+   the reference leaves behind (azel, Doppler, code state, rho0). */
+typedef struct {
+    double azel[2], f_carr, f_code, code_phase;
+    int iword, ibit, icode;
+} refresh_state;
+
+static void refresh_row(const gss_scn *s, const chan_t *ch, const rng_t *rho_prev,
+                        const rng_t *rho_p, gss_chan_blk_t *p, refresh_state *st)
+{
+    const rng_t rho = *rho_p;                  /* sv_range at the block's time (range_pass) */
+    st->azel[0] = rho.azel[0];
+    st->azel[1] = rho.azel[1];
+
+    /* computeCodePhase(chan, rho, 0.1), gpssim.c:1317-1351 */
+    double rhorate = (rho.range - rho_prev->range) / 0.1;
+    st->f_carr = -rhorate / K_LAMBDA_L1;
+    st->f_code = K_CODE_FREQ + st->f_carr * K_CARR_TO_CODE;
+    double ms = ((gt_diff(rho_prev->g, ch->g0) + 6.0) - rho_prev->range / K_C) * 1000.0;
+    int ims = (int)ms;
+    st->code_phase = (ms - (double)ims) * K_CA_LEN;
+    st->iword = ims / 600;
+    ims -= st->iword * 600;
+    st->ibit = ims / 20;
+    ims -= st->ibit * 20;
+    st->icode = ims;
+
+    /* gain: path loss × antenna pattern, scaled 2^7 (gpssim.c:2179-2186) */
+    double path_loss = 20200000.0 / rho.d;
+    int ibs = (int)((90.0 - rho.azel[1] * K_R2D) / 5.0);
+    double ant_gain = s->ant_pat[ibs];
+    int gain = (int)(path_loss * ant_gain * 128.0);
+
+    p->carr0 = 0.0;                            /* filled by the carrier chain */
+    p->carr_step = st->f_carr * s->delt;
+    if (s->opt.carrier_int)                    /* carr_phasestep (gpssim.c:2175-2177) */
+        p->carr_step = (double)(int)round(512.0 * 65536.0 * st->f_carr * s->delt) /
+                       K_CARR_INT_ONE;
+    p->code0 = st->code_phase;
+    p->code_step = st->f_code * s->delt;
+    p->icode = st->icode;
+    p->ibit = st->ibit;
+    p->iword = st->iword;
+    p->gain = gain;
+    p->ca_tbl = ch->prn - 1;
+    p->nav_tbl = ch->nav_row;
+}
+
+/* the rows of a range pass's blocks in parallel: block j's refresh needs only its range and
+   block j - 1's (the pass's first block: the channel's rho0 before the pass), and the channel set
+   is fixed between two 30 s updates, which end a pass */
+typedef struct {
+    const gss_scn *s;
+    gss_chan_blk_t *blk;
+    int32_t *nch;
+    gss_chain_t *chain;
+    double *carr_ck;
+    const rng_t *rho_start;                    /* [K_MAX_CHAN] rho0 before the pass */
+    const int *fresh;                          /* [K_MAX_CHAN] carr_fresh before the pass */
+} refresh_job;
+
+static void refresh_part(void *arg, int j)
+{
+    const refresh_job *r = (const refresh_job *)arg;
+    const gss_scn *s = r->s;
+    gss_chan_blk_t *row = r->blk + (size_t)j * GSS_MAXCH;
+    gss_chain_t *cr = r->chain + (size_t)j * GSS_MAXCH;
+    const rng_t *rg = s->rg + (size_t)j * K_MAX_CHAN;
+    int k = 0;
+    for (int i = 0; i < K_MAX_CHAN; i++) {
+        const chan_t *ch = &s->chan[i];
+        if (ch->prn <= 0)
+            continue;
+        refresh_state st;
+        refresh_row(s, ch, j ? &rg[i - K_MAX_CHAN] : &r->rho_start[i], &rg[i], &row[k], &st);
+        gss_chain_t *c = &cr[k];
+        memset(c, 0, sizeof *c);
+        c->slot = (int8_t)i;
+        c->reset = (uint8_t)(j == 0 ? r->fresh[i] : 0);
+        c->init = ch->carr_phase;
+        k++;
+    }
+    for (int q = k; q < GSS_MAXCH; q++) {
+        memset(&row[q], 0, sizeof row[q]);
+        memset(&cr[q], 0, sizeof cr[q]);
+        cr[q].slot = -1;
+    }
+    if (r->carr_ck)                            /* padding rows: defined (zero) checkpoints */
+        memset(r->carr_ck + ((size_t)j * GSS_MAXCH + k) * GSS_NCK, 0,
+               sizeof(double) * GSS_NCK * (GSS_MAXCH - k));
+    r->nch[j] = k;
+}
+
 /* Rows of the next blocks without their carrier phase (carr0 = 0): the per-block refresh and the
-   30 s updates of gpssim.c:2154-2352; chain[] records which slot chain each row continues. */
+   30 s updates of gpssim.c:2154-2352; chain[] records which slot chain each row continues.
+   Per range pass (the blocks up to the next 30 s update): the ranges, then the rows, each in
+   parallel over the pass's blocks; the channel state is then left as the reference's serial
+   loop leaves it (its last block's refresh), and the 30 s update runs after the pass. */
 static int next_rows(gss_scn *s, int max_blocks, gss_chan_blk_t *blk, int32_t *nch,
                      gss_chain_t *chain, double *carr_ck, int *n_out, int threads)
 {
-    int nb = 0, jr = 0, nr = 0;                /* block jr of a range pass of nr blocks */
+    int nb = 0;
     while (nb < max_blocks && s->iumd < s->numd) {
-        const double *xyz = s->static_mode ? s->xyz[0] : s->xyz[s->iumd];
-        gss_chan_blk_t *row = blk + (size_t)nb * GSS_MAXCH;
-        int k = 0;
-        if (jr == nr) {
-            nr = range_pass(s, max_blocks - nb, threads);
-            if (nr < 0)
-                return nr;
-            jr = 0;
+        const int nr = range_pass(s, max_blocks - nb, threads);
+        if (nr < 0)
+            return nr;
+        if (nr == 0)
+            break;
+        rng_t rho_start[K_MAX_CHAN];
+        int fresh[K_MAX_CHAN];
+        for (int i = 0; i < K_MAX_CHAN; i++) {
+            rho_start[i] = s->chan[i].rho0;
+            fresh[i] = s->chan[i].carr_fresh;
         }
-        const rng_t *rg = s->rg + (size_t)jr++ * K_MAX_CHAN;
-
-        /* ---- per-block refresh (gpssim.c:2156-2188) ---- */
+        const refresh_job rj = {s, blk + (size_t)nb * GSS_MAXCH, nch + nb,
+                                chain + (size_t)nb * GSS_MAXCH,
+                                carr_ck ? carr_ck + (size_t)nb * GSS_MAXCH * GSS_NCK : NULL,
+                                rho_start, fresh};
+        gss_pool_run(threads, nr, refresh_part, (void *)&rj);
+        /* the channel state after the pass's last block, as the serial loop leaves it */
+        const rng_t *last = s->rg + (size_t)(nr - 1) * K_MAX_CHAN;
         for (int i = 0; i < K_MAX_CHAN; i++) {
             chan_t *ch = &s->chan[i];
             if (ch->prn <= 0)
                 continue;
-            const rng_t rho = rg[i];           /* sv_range at s->grx, xyz (range_pass) */
-            ch->azel[0] = rho.azel[0];
-            ch->azel[1] = rho.azel[1];
-
-            /* computeCodePhase(chan, rho, 0.1), gpssim.c:1317-1351 */
-            double rhorate = (rho.range - ch->rho0.range) / 0.1;
-            ch->f_carr = -rhorate / K_LAMBDA_L1;
-            ch->f_code = K_CODE_FREQ + ch->f_carr * K_CARR_TO_CODE;
-            double ms = ((gt_diff(ch->rho0.g, ch->g0) + 6.0) - ch->rho0.range / K_C) * 1000.0;
-            int ims = (int)ms;
-            ch->code_phase = (ms - (double)ims) * K_CA_LEN;
-            ch->iword = ims / 600;
-            ims -= ch->iword * 600;
-            ch->ibit = ims / 20;
-            ims -= ch->ibit * 20;
-            ch->icode = ims;
-            ch->rho0 = rho;
-
-            /* gain: path loss × antenna pattern, scaled 2^7 (gpssim.c:2179-2186) */
-            double path_loss = 20200000.0 / rho.d;
-            int ibs = (int)((90.0 - rho.azel[1] * K_R2D) / 5.0);
-            double ant_gain = s->ant_pat[ibs];
-            int gain = (int)(path_loss * ant_gain * 128.0);
-
-            gss_chan_blk_t *p = &row[k];
-            p->carr0 = 0.0;                        /* filled by the carrier chain */
-            p->carr_step = ch->f_carr * s->delt;
-            if (s->opt.carrier_int)       /* carr_phasestep (gpssim.c:2175-2177) */
-                p->carr_step = (double)(int)round(512.0 * 65536.0 * ch->f_carr * s->delt) /
-                               K_CARR_INT_ONE;
-            p->code0 = ch->code_phase;
-            p->code_step = ch->f_code * s->delt;
-            p->icode = ch->icode;
-            p->ibit = ch->ibit;
-            p->iword = ch->iword;
-            p->gain = gain;
-            p->ca_tbl = ch->prn - 1;
-            p->nav_tbl = ch->nav_row;
-            gss_chain_t *c = &chain[(size_t)nb * GSS_MAXCH + k];
-            memset(c, 0, sizeof *c);
-            c->slot = (int8_t)i;
-            c->reset = (uint8_t)ch->carr_fresh;
-            c->init = ch->carr_phase;
+            gss_chan_blk_t scratch;
+            refresh_state st;
+            refresh_row(s, ch, nr > 1 ? &last[i - K_MAX_CHAN] : &rho_start[i], &last[i], &scratch,
+                        &st);
+            ch->azel[0] = st.azel[0];
+            ch->azel[1] = st.azel[1];
+            ch->f_carr = st.f_carr;
+            ch->f_code = st.f_code;
+            ch->code_phase = st.code_phase;
+            ch->iword = st.iword;
+            ch->ibit = st.ibit;
+            ch->icode = st.icode;
+            ch->rho0 = last[i];
             ch->carr_fresh = 0;
-            k++;
         }
-        for (int r = k; r < GSS_MAXCH; r++) {
-            memset(&row[r], 0, sizeof row[r]);
-            memset(&chain[(size_t)nb * GSS_MAXCH + r], 0, sizeof chain[0]);
-            chain[(size_t)nb * GSS_MAXCH + r].slot = -1;
+        for (int j = 0; j < nr; j++) {
+            const double *xyz = s->static_mode ? s->xyz[0] : s->xyz[s->iumd];
+            /* ---- 30 s update: nav message, ephemeris set, allocation (gpssim.c:2294-2345);
+               range_pass ends a pass at it, so only its last block can reach one ---- */
+            int igrx = (int)(s->grx.sec * 10.0 + 0.5);
+            if (igrx % 300 == 0) {
+                if (j != nr - 1)
+                    return gss_fail(GSS_E_STATE, "30 s update inside a range pass");
+                int rc = update_30s(s, xyz, 1);
+                if (rc)
+                    return rc;
+            }
+            s->grx = gt_add(s->grx, 0.1);
+            msg(s, "\rTime into run = %4.1f", gt_diff(s->grx, s->g0));
+            s->iumd++;
         }
-        if (carr_ck)             /* padding rows: defined (zero) checkpoints */
-            memset(carr_ck + ((size_t)nb * GSS_MAXCH + k) * GSS_NCK, 0,
-                   sizeof(double) * GSS_NCK * (GSS_MAXCH - k));
-        nch[nb] = k;
-        nb++;
-
-        /* ---- 30 s update: nav message, ephemeris set, allocation (gpssim.c:2294-2345) ---- */
-        int igrx = (int)(s->grx.sec * 10.0 + 0.5);
-        if (igrx % 300 == 0) {
-            int rc = update_30s(s, xyz, 1);
-            if (rc)
-                return rc;
-        }
-
-        s->grx = gt_add(s->grx, 0.1);
-        msg(s, "\rTime into run = %4.1f", gt_diff(s->grx, s->g0));
-        s->iumd++;
+        nb += nr;
     }
     s->rows_out += nb;
     *n_out = nb;
