@@ -81,7 +81,10 @@ static int trace_on()
 #endif
 constexpr int NCOPY = GSS_RUN_NCOPY;                   /* copy streams (DMA engines) */
 constexpr int DEPTH = GSS_RUN_DEPTH;                   /* slots submitted, not yet drained */
-constexpr int NSLOT = DEPTH + 2;
+#ifndef GSS_RUN_AHEAD
+#define GSS_RUN_AHEAD 2
+#endif
+constexpr int NSLOT = DEPTH + GSS_RUN_AHEAD;           /* + slots planned / proven ahead */
 constexpr size_t SLOT_OUT_MAX = (size_t)256 << 20;     /* pinned output bytes per slot */
 
 enum { FREE, PROVING, PLANNED };                  /* PROVING: rows planned, proofs pending */
@@ -179,6 +182,9 @@ struct Slot {
     int32_t *d_status = nullptr, *h_status = nullptr;
     hipEvent_t rendered = nullptr;   /* compute stream: the slot's kernels are done      */
     hipEvent_t done = nullptr;       /* copy stream: the slot's bytes are in h_out        */
+    hipEvent_t tq = nullptr;         /* GSS_RUN_TRACE: the compute stream reached the slot */
+    hipEvent_t tk = nullptr;         /* ... its inputs are uploaded (kernels next)        */
+    hipEvent_t tc = nullptr;         /* ... the copy stream reached its download          */
     /* GPU proofs, launched by the planner (proof_ahead) */
     hipStream_t pst = nullptr;       /* the slot's proof stream                          */
     hipEvent_t navd = nullptr;       /* its nav rows are built (the planner's nav stream) */
@@ -193,6 +199,8 @@ struct Run {
     int gpu_proof = 0;               /* any proofs on the GPU (gss_proof.hip), run ahead by the
                                         planner on each slot's own stream (proof_ahead)        */
     hipStream_t nav_st = nullptr;    /* ... the planner's stream for the slots' nav rows      */
+    hipEvent_t t_base = nullptr;     /* GSS_RUN_TRACE: the GPU clock's origin (compute stream) */
+    int upload_dev = 1;              /* uploads by kernel (h2d); GSS_RUN_UPLOAD=dma: copy engine */
     const uint32_t *d_ca = nullptr;  /* the run's device C/A table                            */
     int force_exact;                 /* GSS_RUN_FORCE_EXACT=k: every k-th block to the exact
                                         path (tests of the mixed batch), 0 = off */
@@ -264,6 +272,75 @@ static_assert(sizeof(gss_spec_in_t) <= 256 && 256 + sizeof(gss_spec_t) <= 1024,
    and they are computed afterwards for the uncertified blocks only, from each row's carr0 by
    the same exact walk.  The integer-carrier chain records them for free and keeps doing so. */
 static bool lazy_ck(const Run &r) { return r.use_lin && !r.carrier_int; }
+
+/* Uploads of the slots' inputs (rows, lines, checkpoints, nav sources: ~10 MB per 2048-block
+   slot) by a kernel reading the pinned host buffers directly, not by the copy engine: an
+   engine copy queues behind the download of the slot before (the same engine, FIFO), so each
+   slot's render started only once the previous slot's bytes were out, and the downloads ran
+   at 0.78 of the link (tools/d2h_overlap.py: a 10 MB upload issued during a 133 MB download
+   finishes with it, 2.09 ms instead of 0.20).  The kernel's reads go host-to-device, the
+   downloads device-to-host: the two directions of the link overlap.  16-byte vector loads,
+   four in flight per lane; the tail bytes (and unaligned buffers) byte by byte. */
+__global__ __launch_bounds__(256) void upload_kernel(const uint4 *__restrict__ src,
+                                                     uint4 *__restrict__ dst, size_t n16,
+                                                     int tail)
+{
+    const size_t stride = (size_t)gridDim.x * 256;
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride],
+                    d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n16; i += stride)
+        dst[i] = src[i];
+    if (blockIdx.x == 0 && (int)threadIdx.x < tail)
+        ((uint8_t *)(dst + n16))[threadIdx.x] = ((const uint8_t *)(src + n16))[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void upload_bytes_kernel(const uint8_t *__restrict__ src,
+                                                           uint8_t *__restrict__ dst, size_t n)
+{
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        dst[i] = src[i];
+}
+
+/* n bytes from src to dst by a kernel on st: pinned host (hipHostMalloc) or device memory on
+   either side */
+static int dev_copy(void *dst, const void *src, size_t n, hipStream_t st)
+{
+    if (n == 0)
+        return 0;
+    if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
+        const size_t n16 = n >> 4;
+        const size_t g = (n16 + 1023) / 1024;
+        hipLaunchKernelGGL(upload_kernel, dim3((unsigned)(g < 1 ? 1 : g > 2048 ? 2048 : g)),
+                           dim3(256), 0, st, (const uint4 *)src, (uint4 *)dst, n16,
+                           (int)(n & 15));
+    } else {
+        const size_t g = (n + 255) / 256;
+        hipLaunchKernelGGL(upload_bytes_kernel, dim3((unsigned)(g > 2048 ? 2048 : g)), dim3(256),
+                           0, st, (const uint8_t *)src, (uint8_t *)dst, n);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "copy kernel launch");
+}
+
+/* host buffer (pinned) to device, stream-ordered on st */
+static int h2d(const Run &r, void *dst, const void *src, size_t n, hipStream_t st)
+{
+    if (n == 0 || r.upload_dev)
+        return dev_copy(dst, src, n, st);
+    return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st) == hipSuccess
+               ? 0 : gss_fail(GSS_E_HIP, "upload of %zu B", n);
+}
+#define RUN_H2D(dst, src, n, st)                                                          \
+    do {                                                                                  \
+        int rc_ = h2d(r, (dst), (src), (n), (st));                                        \
+        if (rc_) return rc_;                                                              \
+    } while (0)
 
 }  // namespace
 int run_proof_launch(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
@@ -602,8 +679,11 @@ int spec_launch(Run &r, Run::SpecBatch &b, int ask)
     if (rc)
         return rc;
     /* the lanes read their rows from, and write their walks to, the pinned host buffers
-       directly (a few hundred bytes each): no copy engine in the loop (the first copy on this
-       stream cost ~8 ms) */
+       directly (a few hundred bytes each): no copy engine in the loop (it queues behind the
+       slots' downloads).  Staging them through device memory by copy kernels (one pass of
+       16-byte copies each way) measured the same: the downloads beside them run at ~0.8 of the
+       link either way, the walks' own traffic (~14 MB per 2048-block slot back to the host,
+       with the 10 MB of uploads) sharing its device-to-host direction */
     rc = gss_spec_device(r.dev, b.h_in, nrow, r.n_per_blk, b.h_spec, r.spec_st);
     if (rc)
         return rc;
@@ -947,8 +1027,7 @@ int proof_ahead(Run &r, Slot &sl)
         return gss_fail(GSS_E_RANGE, "nav rows %d past the run's reservation %zu", n_rows,
                         r.d_nav_cap);
     if (sl.n_nav > 0) {
-        RUN_TRY(hipMemcpyAsync(v.src, sl.nav, sizeof(gss_nav_src_t) * (size_t)sl.n_nav,
-                               hipMemcpyHostToDevice, r.nav_st));
+        RUN_H2D(v.src, sl.nav, sizeof(gss_nav_src_t) * (size_t)sl.n_nav, r.nav_st);
         int rc = gss_nav_rows_device(r.dev, v.src, sl.nav_first, sl.n_nav, r.d_nav, r.nav_st);
         if (rc)
             return rc;
@@ -956,13 +1035,10 @@ int proof_ahead(Run &r, Slot &sl)
     RUN_TRY(hipEventRecord(sl.navd, r.nav_st));
     if (!sl.gpu_proven)
         return 0;
-    RUN_TRY(hipMemcpyAsync(v.blk, sl.blk, sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)sl.nb,
-                           hipMemcpyHostToDevice, sl.pst));
-    RUN_TRY(hipMemcpyAsync(v.nch, sl.nch, sizeof(int32_t) * (size_t)sl.nb, hipMemcpyHostToDevice,
-                           sl.pst));
+    RUN_H2D(v.blk, sl.blk, sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)sl.nb, sl.pst);
+    RUN_H2D(v.nch, sl.nch, sizeof(int32_t) * (size_t)sl.nb, sl.pst);
     if (!lazy_ck(r))               /* (with lazy checkpoints only a rejected block needs them) */
-        RUN_TRY(hipMemcpyAsync(v.ck, sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb,
-                               hipMemcpyHostToDevice, sl.pst));
+        RUN_H2D(v.ck, sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb, sl.pst);
     RUN_TRY(hipStreamWaitEvent(sl.pst, sl.navd, 0));
     int rc = run_proof_launch(v.blk, v.nch, sl.nb, r.n_per_blk, r.d_ca, 32, r.d_nav,
                               n_rows > 0 ? n_rows : 1, v.lin, v.fast, sl.first, r.force_exact,
@@ -989,6 +1065,8 @@ int submit_proven(gss_dev *d, Run &r, Slot &sl, int n_per_blk, int fmt, size_t b
         return rc;
     RUN_TRY(hipEventRecord(sl.rendered, st));
     RUN_TRY(hipStreamWaitEvent(cp, sl.rendered, 0));
+    if (sl.tc)
+        RUN_TRY(hipEventRecord(sl.tc, cp));
     RUN_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, bb * (size_t)sl.nb, hipMemcpyDeviceToHost, cp));
     RUN_TRY(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int32_t), hipMemcpyDeviceToHost, cp));
     RUN_TRY(hipMemcpyAsync(sl.fast, v.fast, sizeof(int32_t) * (size_t)sl.nb,
@@ -1002,6 +1080,8 @@ int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, in
 {
     /* the slot's previous D2H must have read d_out before the kernels rewrite it */
     RUN_TRY(hipStreamWaitEvent(st, sl.done, 0));
+    if (sl.tq)
+        RUN_TRY(hipEventRecord(sl.tq, st));
     if (sl.lin && sl.gpu_proven)
         return submit_proven(d, r, sl, n_per_blk, fmt, bb, st, cp);
     const size_t need = slot_dev(sl).need;
@@ -1013,6 +1093,7 @@ int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, in
         RUN_TRY(hipMalloc((void **)&sl.d_in, need));
         sl.d_in_cap = need;
     }
+    const double tq0 = trace_on() ? tnow() : 0.0;
     const SlotDev v = slot_dev(sl);
     gss_chan_blk_t *d_blk = v.blk;
     int32_t *d_nch = v.nch;
@@ -1022,11 +1103,9 @@ int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, in
     int32_t *d_fast = v.fast;
     const size_t s_blk = sizeof(gss_chan_blk_t) * GSS_MAXCH * (size_t)sl.nb;
     const size_t s_lin = sizeof(gss_lin_t) * GSS_MAXCH * (size_t)sl.nb;
-    RUN_TRY(hipMemcpyAsync(d_blk, sl.blk, s_blk, hipMemcpyHostToDevice, st));
-    RUN_TRY(hipMemcpyAsync(d_nch, sl.nch, sizeof(int32_t) * (size_t)sl.nb, hipMemcpyHostToDevice,
-                           st));
-    RUN_TRY(hipMemcpyAsync(d_ck, sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb,
-                           hipMemcpyHostToDevice, st));
+    RUN_H2D(d_blk, sl.blk, s_blk, st);
+    RUN_H2D(d_nch, sl.nch, sizeof(int32_t) * (size_t)sl.nb, st);
+    RUN_H2D(d_ck, sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb, st);
     /* the 30 s producer: this slot's new nav rows built on the device (gss_producers.hip); with
        GPU proofs in the run the planner has built them already (proof_ahead) */
     const int n_rows = sl.nav_first + sl.n_nav;
@@ -1036,18 +1115,19 @@ int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, in
     if (r.gpu_proof) {
         RUN_TRY(hipStreamWaitEvent(st, sl.navd, 0));
     } else if (sl.n_nav > 0) {
-        RUN_TRY(hipMemcpyAsync(d_src, sl.nav, sizeof(gss_nav_src_t) * (size_t)sl.n_nav,
-                               hipMemcpyHostToDevice, st));
+        RUN_H2D(d_src, sl.nav, sizeof(gss_nav_src_t) * (size_t)sl.n_nav, st);
         rc = gss_nav_rows_device(d, d_src, sl.nav_first, sl.n_nav, r.d_nav, st);
         if (rc)
             return rc;
     }
     const uint32_t *d_nav = r.d_nav;
+    const double tq1 = trace_on() ? tnow() : 0.0;
     RUN_TRY(hipMemsetAsync(sl.d_status, 0, sizeof(int32_t), st));
     if (sl.lin) {
-        RUN_TRY(hipMemcpyAsync(d_lin, sl.lin, s_lin, hipMemcpyHostToDevice, st));
-        RUN_TRY(hipMemcpyAsync(d_fast, sl.fast, sizeof(int32_t) * (size_t)(sl.nb + sl.n_fb),
-                               hipMemcpyHostToDevice, st));
+        RUN_H2D(d_lin, sl.lin, s_lin, st);
+        RUN_H2D(d_fast, sl.fast, sizeof(int32_t) * (size_t)(sl.nb + sl.n_fb), st);
+        if (sl.tk)
+            RUN_TRY(hipEventRecord(sl.tk, st));
         rc = gss_synth_lin_device(d, d_blk, d_nch, sl.nch_max, d_lin, d_fast, d_fast + sl.nb,
                                   sl.n_fb, d_ck, d_ca, 32, d_nav, n_rows, sl.nb, n_per_blk,
                                   fmt, sl.d_out, sl.d_status, st);
@@ -1057,11 +1137,17 @@ int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, in
     }
     if (rc)
         return rc;
+    const double tq2 = trace_on() ? tnow() : 0.0;
     RUN_TRY(hipEventRecord(sl.rendered, st));
     RUN_TRY(hipStreamWaitEvent(cp, sl.rendered, 0));
+    if (sl.tc)
+        RUN_TRY(hipEventRecord(sl.tc, cp));
     RUN_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, bb * (size_t)sl.nb, hipMemcpyDeviceToHost, cp));
     RUN_TRY(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int32_t), hipMemcpyDeviceToHost, cp));
     RUN_TRY(hipEventRecord(sl.done, cp));
+    if (trace_on())
+        fprintf(stderr, "trace submit_parts start %.6f h2d %.6f render %.6f out %.6f\n", tq0, tq1, tq2,
+                tnow());
     return 0;
 }
 
@@ -1088,10 +1174,8 @@ int redo_rejected(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_rows
             }
         }
     const SlotDev v = slot_dev(sl);
-    RUN_TRY(hipMemcpyAsync(v.ck, sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb,
-                           hipMemcpyHostToDevice, st));
-    RUN_TRY(hipMemcpyAsync(v.fast + sl.nb, sl.fast + sl.nb, sizeof(int32_t) * (size_t)nf,
-                           hipMemcpyHostToDevice, st));
+    RUN_H2D(v.ck, sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb, st);
+    RUN_H2D(v.fast + sl.nb, sl.fast + sl.nb, sizeof(int32_t) * (size_t)nf, st);
     RUN_TRY(hipMemsetAsync(sl.d_status, 0, sizeof(int32_t), st));
     int rc = gss_synth_lin_device(d, v.blk, v.nch, sl.nch_max, v.lin, v.fast, v.fast + sl.nb, nf,
                                   v.ck, d_ca, 32, r.d_nav, n_rows, sl.nb, n_per_blk, fmt,
@@ -1121,9 +1205,21 @@ int drain(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, int
         return gss_fail(GSS_E_RANGE, "nav word index ran past dwrd[59]");
     if (sink(user, sl.h_out, bb * (size_t)sl.nb, sl.first, sl.nb))
         return gss_fail(GSS_E_IO, "sink failed at block %lld", (long long)sl.first);
-    if (trace_on())
+    if (trace_on()) {
         fprintf(stderr, "trace drain first %lld wait %.6f %.6f sink_end %.6f\n",
                 (long long)sl.first, t0, t1, tnow());
+        float a = 0, k = 0, b = 0, c = 0, q = 0;       /* GPU clock: ms since the run's base */
+        if (sl.tq && r.t_base && hipEventElapsedTime(&a, r.t_base, sl.tq) == hipSuccess &&
+            hipEventElapsedTime(&b, r.t_base, sl.rendered) == hipSuccess &&
+            hipEventElapsedTime(&c, r.t_base, sl.done) == hipSuccess) {
+            if (!sl.lin || sl.gpu_proven || hipEventElapsedTime(&k, r.t_base, sl.tk) != hipSuccess)
+                k = a;
+            if (hipEventElapsedTime(&q, r.t_base, sl.tc) != hipSuccess)
+                q = b;
+            fprintf(stderr, "trace gpu first %lld start %.3f kernels %.3f rendered %.3f done %.3f "
+                    "copy %.3f\n", (long long)sl.first, a, k, b, c, q);
+        }
+    }
     {
         std::lock_guard<std::mutex> lk(r.mu);
         sl.state = FREE;
@@ -1207,6 +1303,8 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         r.use_lin = !(path && strcmp(path, "walk") == 0);
         const char *fe = getenv("GSS_RUN_FORCE_EXACT");
         r.force_exact = fe && *fe ? atoi(fe) : 0;
+        const char *up = getenv("GSS_RUN_UPLOAD");
+        r.upload_dev = !(up && strcmp(up, "dma") == 0);
     }
     r.batch = batch > 0 ? batch : 100;
     if ((size_t)r.batch * bb > SLOT_OUT_MAX)
@@ -1235,6 +1333,9 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             (void)hipFree(sl.d_in); (void)hipFree(sl.d_status);
             if (sl.done) (void)hipEventDestroy(sl.done);
             if (sl.rendered) (void)hipEventDestroy(sl.rendered);
+            if (sl.tq) (void)hipEventDestroy(sl.tq);
+            if (sl.tk) (void)hipEventDestroy(sl.tk);
+            if (sl.tc) (void)hipEventDestroy(sl.tc);
         }
         for (Slot &sl : r.slot) {
             if (sl.pst) (void)hipStreamDestroy(sl.pst);
@@ -1257,13 +1358,16 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         if (st) (void)hipStreamDestroy(st);
         for (hipStream_t c : cp)
             if (c) (void)hipStreamDestroy(c);
+        if (r.t_base) (void)hipEventDestroy(r.t_base);
     };
     /* buffers */
     {
         gss_ca_table(r.ca);                            /* the proofs' copy, on the host */
         if (hipMalloc((void **)&d_ca, sizeof r.ca) != hipSuccess ||
             hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
-            !make_streams(cp))
+            !make_streams(cp) ||
+            (trace_on() && (hipEventCreate(&r.t_base) != hipSuccess ||
+                            hipEventRecord(r.t_base, st) != hipSuccess)))
             err = gss_fail(GSS_E_HIP, "run setup failed");
         /* the kernels' copy built on the device by the 30 s producer (gss_producers.hip) */
         if (!err)
@@ -1284,8 +1388,14 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                 pool_get((void **)&sl.d_out, bb * nb, false, ordinal, &sl.d_out_bytes) !=
                     hipSuccess ||
                 hipMalloc((void **)&sl.d_status, sizeof(int32_t)) != hipSuccess ||
-                hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&sl.rendered, hipEventDisableTiming) != hipSuccess)
+                hipEventCreateWithFlags(&sl.done, trace_on() ? hipEventDefault
+                                                             : hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&sl.rendered, trace_on() ? hipEventDefault
+                                                                 : hipEventDisableTiming) !=
+                    hipSuccess ||
+                (trace_on() && (hipEventCreate(&sl.tq) != hipSuccess ||
+                                hipEventCreate(&sl.tk) != hipSuccess ||
+                                hipEventCreate(&sl.tc) != hipSuccess)))
                 err = gss_fail(GSS_E_NOMEM, "run buffers (%zu B per slot)", bb * nb);
             if (!err && r.use_lin &&
                 (hipHostMalloc((void **)&sl.lin, sizeof(gss_lin_t) * GSS_MAXCH * nb,
