@@ -1,3 +1,9 @@
+"""Per-slot GPU-clock stages of a GSS_RUN_TRACE=1 gss_run log ("trace gpu" lines, HIP events
+on the run's streams): upload (start -> kernels), render kernels (-> rendered), the download
+(copy start -> done), how long a rendered slot waited for the copy engine, and the interval
+between downloads finished, medians over the last run in the log.
+
+usage: python tools/gpu_clock_summary.py <stderr log>"""
 import sys, statistics as S
 L=[l for l in open(sys.argv[1]) if l.startswith('trace gpu')]
 runs=[];cur=[]
