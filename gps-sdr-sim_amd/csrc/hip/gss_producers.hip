@@ -83,45 +83,80 @@ extern "C" int gss_nav_rows_device(gss_dev *d, const gss_nav_src_t *src, int fir
 /* one lane per segment of a row (gss_spec_seg_walk).  Rows laid out [nblk][GSS_MAXCH] are taken
    channel-major, so that a wave's lanes walk the segments of consecutive blocks of one channel:
    close steps, nearly the same cycles and binades (uniform control flow) instead of 16 different
-   Dopplers per wave. */
-__global__ void gss_spec_kernel(gss_spec_in_t *__restrict__ in, int nrow, int n,
-                                gss_spec_t *__restrict__ spec)
+   Dopplers per wave.
+   The rows and walks live in pinned host memory (gss_run), so the workgroup (8 rows x 8
+   segments) stages them in LDS: each row read once across the link in 8-byte words instead of
+   by each of its 8 lanes, and the walks written back whole (16-byte stores, 272 B per row)
+   instead of field by field -- the walks' link traffic had slowed the slot downloads beside
+   them by a tenth (tools/d2h_overlap.py).  Segments past a row's k are written as zeros. */
+constexpr int SPEC_ROWS = 64 / GSS_SPEC_K;               /* rows per workgroup */
+static_assert(sizeof(gss_spec_in_t) % 8 == 0 && sizeof(gss_spec_t) % 16 == 0, "row sizes");
+
+__device__ inline int spec_row_of(int u, int nrow)
 {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nrow * GSS_SPEC_K)
-        return;
-    const int u = t / GSS_SPEC_K, j = t % GSS_SPEC_K;
     const int nb = nrow / GSS_MAXCH;
-    const int i = nrow % GSS_MAXCH ? u : (u % nb) * GSS_MAXCH + u / nb;
-    gss_spec_in_t row = in[i];
-    if (row.k == 0) {
+    return nrow % GSS_MAXCH ? u : (u % nb) * GSS_MAXCH + u / nb;
+}
+
+__global__ __launch_bounds__(64) void gss_spec_kernel(gss_spec_in_t *__restrict__ in, int nrow,
+                                                      int n, gss_spec_t *__restrict__ spec)
+{
+    __shared__ gss_spec_in_t s_in[SPEC_ROWS];
+    __shared__ gss_spec_t s_out[SPEC_ROWS];
+    __shared__ int s_guessed[SPEC_ROWS];
+    constexpr int WI = sizeof(gss_spec_in_t) / 8, WO = sizeof(gss_spec_t) / 16;
+    const int lane = threadIdx.x, r = lane / GSS_SPEC_K, j = lane % GSS_SPEC_K;
+    const int u0 = blockIdx.x * SPEC_ROWS;
+    for (int q = lane; q < SPEC_ROWS * WI; q += 64) {    /* the rows in, 8 bytes a lane */
+        const int rr = q / WI, w = q % WI;
+        if (u0 + rr < nrow)
+            ((uint64_t *)&s_in[rr])[w] = ((const uint64_t *)&in[spec_row_of(u0 + rr, nrow)])[w];
+    }
+    for (int q = lane; q < SPEC_ROWS * WO; q += 64)      /* the walks zeroed */
+        ((uint4 *)s_out)[q] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    const bool live = u0 + r < nrow;
+    gss_spec_in_t row = s_in[r];
+    const bool guess = live && row.k == 0;
+    if (guess) {
         /* segment starts not guessed yet (gss_carr_chain_starts): every lane of the row makes
            the same guesses; its first lane writes them back for the host's chain */
         gss_spec_guess_row(row.g, row.s, n, &row);
-        if (j == 0) {
-            in[i].k = row.k;
-            for (int q = 1; q < GSS_SPEC_K; q++) {
-                in[i].P[q] = row.P[q];
-                in[i].W[q] = row.W[q];
-            }
-        }
     }
-    if (j >= row.k)
-        return;
-    gss_spec_seg_walk(&row, j, n, &spec[i]);
+    __syncthreads();                                     /* every lane has read s_in[r] */
+    if (j == 0) {
+        s_guessed[r] = guess;
+        if (guess)
+            s_in[r] = row;
+    }
+    if (live && j < row.k)
+        gss_spec_seg_walk(&row, j, n, &s_out[r]);
+    __syncthreads();
+    for (int q = lane; q < SPEC_ROWS * WO; q += 64) {    /* the walks out, 16 bytes a lane */
+        const int rr = q / WO, w = q % WO;
+        if (u0 + rr < nrow)
+            ((uint4 *)&spec[spec_row_of(u0 + rr, nrow)])[w] = ((const uint4 *)&s_out[rr])[w];
+    }
+    for (int q = lane; q < SPEC_ROWS * WI; q += 64) {    /* the walkers' guesses back */
+        const int rr = q / WI, w = q % WI;
+        if (u0 + rr < nrow && s_guessed[rr])
+            ((uint64_t *)&in[spec_row_of(u0 + rr, nrow)])[w] = ((const uint64_t *)&s_in[rr])[w];
+    }
 }
 
 extern "C" int gss_spec_device(gss_dev *d, gss_spec_in_t *in, int nrow, int n_per_blk,
                                gss_spec_t *spec, void *stream)
 {
-    if (!d || nrow < 0 || n_per_blk <= 0 || (nrow > 0 && (!in || !spec)))
-        return gss_fail(GSS_E_ARG, "invalid speculative-walk arguments");
+    if (!d || nrow < 0 || n_per_blk <= 0 || (nrow > 0 && (!in || !spec)) ||
+        ((uintptr_t)in & 7) || ((uintptr_t)spec & 15))
+        return gss_fail(GSS_E_ARG, "invalid speculative-walk arguments (rows 8-byte, walks "
+                        "16-byte aligned)");
     if (nrow == 0)
         return 0;
     if (hipSetDevice(gss_dev_ordinal(d)) != hipSuccess)
         return gss_fail(GSS_E_HIP, "hipSetDevice failed");
-    const long long lanes = (long long)nrow * GSS_SPEC_K;
-    hipLaunchKernelGGL(gss_spec_kernel, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0,
+    hipLaunchKernelGGL(gss_spec_kernel, dim3((unsigned)((nrow + SPEC_ROWS - 1) / SPEC_ROWS)),
+                       dim3(64), 0,
                        (hipStream_t)stream, in, nrow, n_per_blk, spec);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "spec kernel: %s", hipGetErrorString(e));

@@ -6,7 +6,8 @@ kernels of one 2048-block batch alone (DeviceWindow.step_batch); both at once on
 the D2H beside compute-bound GEMMs; the D2H while host threads plan rows (the planner's CPU
 load in gss_run); a 10 MB upload (a slot's inputs) alone and during the D2H ("_kern_ms" of the
 "up" modes is the upload's time); the D2H while 8 host threads copy 64 MB arrays (copy_mem); 16 back-to-back downloads into one
-buffer and cycling over four (gss_run's slots).  Prints one JSON line.   usage: python tools/d2h_overlap.py [reps]"""
+buffer and cycling over four (gss_run's slots); a slot's carrier walks (gss_spec_device on pinned
+rows, high-priority stream) alone, beside the download, and beside download and render.  Prints one JSON line.   usage: python tools/d2h_overlap.py [reps]"""
 import json
 import os
 import sys
@@ -64,6 +65,26 @@ def main():
         e1.record(st)
         return e0, e1
 
+    # a slot's carrier walks (gss_spec_device on pinned host rows, as gss_run launches them)
+    import numpy as np
+    sc = G.Scenario(B.NAV, llh=B.LOC, duration=410.0, samp_freq=2.6e6, data_format=1)
+    sb, sn, sch = sc.next_deferred(2048, 16)
+    gi = G.carr_chain_guess(sc.carrier(), sb, sn, sch, sc.n_per_blk, starts_only=True).reshape(-1)
+    nrow = gi.size
+    sp_in = torch.empty(nrow * G.SPEC_IN_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
+    sp_out = torch.empty(nrow * G.SPEC_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
+    h_in = sp_in.numpy().view(G.SPEC_IN_DTYPE)
+
+    def spec_on(st):
+        h_in[:] = gi                                   # fresh guesses (k = 0 rows) each time
+        e0, e1 = ev(), ev()
+        e0.record(st)
+        dev.spec_device(sp_in.data_ptr(), nrow, sc.n_per_blk, sp_out.data_ptr(),
+                        stream=st.cuda_stream)
+        e1.record(st)
+        return e0, e1
+
+    ss = torch.cuda.Stream(dev_t, priority=-1)
     busy = [False]
 
     import numpy as np
@@ -89,8 +110,9 @@ def main():
         e1.record(cp)
         torch.cuda.synchronize(dev_t)
         out["cycle%d_ms_per_copy" % nbuf] = round(e0.elapsed_time(e1) / 16, 3)
-    for mode in ("copy", "kern", "both", "copy_gemm", "copy_host", "both_host", "up", "copy_up", "copy_mem"):
-        tc, tk = [], []
+    for mode in ("copy", "kern", "both", "copy_gemm", "copy_host", "both_host", "up", "copy_up", "copy_mem",
+                 "spec", "copy_spec", "both_spec"):
+        tc, tk, tw = [], [], []
         for r in range(reps + 1):
             torch.cuda.synchronize(dev_t)
             th = None
@@ -110,9 +132,11 @@ def main():
                 with torch.cuda.stream(cs):
                     for _ in range(20):
                         torch.mm(a, a)
-            k = kern_on(cs) if mode in ("kern", "both", "both_host") else None
-            c = copy_on(cp) if mode not in ("kern", "up") else None
-            if mode in ("up", "copy_up", "copy_mem"):
+            w = spec_on(ss) if mode.endswith("spec") else None
+            k = kern_on(cs) if mode in ("kern", "both", "both_host", "both_spec") else None
+            c = copy_on(cp) if mode not in ("kern", "up", "spec") else None
+            if mode in ("up", "copy_up", "copy_mem",
+                 "spec", "copy_spec", "both_spec"):
                 time.sleep(0.0005)
                 k = up_on(cs)
             torch.cuda.synchronize(dev_t)
@@ -123,6 +147,8 @@ def main():
             for t in ths:
                 t.join()
             if r:
+                if w:
+                    tw.append(w[0].elapsed_time(w[1]))
                 if c:
                     tc.append(c[0].elapsed_time(c[1]))
                 if k:
@@ -131,6 +157,8 @@ def main():
             out[mode + "_copy_ms"] = round(sorted(tc)[len(tc) // 2], 3)
         if tk:
             out[mode + "_kern_ms"] = round(sorted(tk)[len(tk) // 2], 3)
+        if tw:
+            out[mode + "_walks_ms"] = round(sorted(tw)[len(tw) // 2], 3)
     print(json.dumps(out), flush=True)
     res.free()
     dev.close()
