@@ -560,6 +560,9 @@ __device__ uint64_t g_lin_stamp[LIN_STAMP_WAVES][4];
    the loop reads them back by broadcast LDS reads.
    LIN_SWIN 1 (measurement): the same table by compiler-visible s_loads: they share lgkmcnt with
    the LUT reads, so each pair's load is waited for with every LDS read drained (+16 %). */
+#ifndef LIN_ALDS
+#define LIN_ALDS 1      /* 1: the pair MFMA's gain operand read from the records (no VALU masks) */
+#endif
 #ifndef LIN_SWIN
 #if LIN_MFMA
 #define LIN_SWIN 3
@@ -633,6 +636,13 @@ struct alignas(16) lin_ct {
 #if !LIN_SWIN
     uint32_t W[LIN_CH];          /* the steps' chip windows (16-byte aligned: ds_read_b128)     */
 #endif
+#if LIN_ALDS
+    uint32_t na, nb;             /* (as below; first here: one 8-byte read)                      */
+    uint32_t wn;
+    uint32_t g2;
+    uint32_t A[5][2];            /* A[0..3] as below; A[4] zeros: the pair MFMA's gain operand   */
+                                 /* half of each lane is A[its class] (lin_pair_cls)            */
+#else
 #if LIN_MFMA
     uint32_t A[4][2];            /* the MFMA gain operand of lane 4b + i: g (f16) at slot i      */
     uint32_t g2;                 /* g as an f16 pair (both halves), the pair MFMA's gain         */
@@ -641,6 +651,7 @@ struct alignas(16) lin_ct {
                                     renders -- the next pair's, the lone last channel's (twice)
                                     or the next chunk's first pair's (lin_sw_pair)              */
     uint32_t wn;                 /* LIN_SWIN 3: ... of the next chunk's (its first pair preloads) */
+#endif
 };
 /* the broadcast reads of the record assume these alignments (a misaligned ds_read_b128 is split
    by the hardware and cost the round-4 LDS-window build 3x) */
@@ -1053,6 +1064,14 @@ __device__ __forceinline__ lin_half8 lin_pair_gains(uint32_t ga2, uint32_t gb2, 
     return __builtin_bit_cast(lin_half8, v);
 }
 
+/* LIN_ALDS: the lane's row of lin_ct.A for the pair operand: r = lane mod 4 on lanes 20q + r,
+   4 (zeros) elsewhere (the same placement as lin_pair_sel's masks) */
+__device__ __forceinline__ uint32_t lin_pair_cls(int lane)
+{
+    const int q = lane >> 4, r = lane & 3;
+    return ((lane & 15) >> 2) == q ? (uint32_t)r : 4u;
+}
+
 __device__ __forceinline__ void lin_pair_sel(int lane, uint32_t &sel0, uint32_t &sel1)
 {
     const int q = lane >> 4, r = lane & 3;
@@ -1077,7 +1096,13 @@ __device__ __forceinline__ void lin_sw_pair(lin_f4 (&cq)[LIN_CH / 2], lin_f4 c0,
     const lin_ct &ta = T[k0], &tb = T[k0 + 1];
     uint64_t Pa = s_lane[k0 * 64 + lane] + ta.B, Pb = s_lane[(k0 + 1) * 64 + lane] + tb.B;
     const uint64_t Da = ta.D, Db = tb.D;
+#if LIN_ALDS
+    const uint2 ga = *(const uint2 *)ta.A[psel0], gb = *(const uint2 *)tb.A[psel0];
+    const lin_half8 A = __builtin_bit_cast(lin_half8, make_uint4(ga.x, ga.y, gb.x, gb.y));
+    (void)psel1;
+#else
     const lin_half8 A = lin_pair_gains(ta.g2, tb.g2, psel0, psel1);
+#endif
     /* the rows to load while this pair renders (the record's na, nb): the next pair's (or the
        lone last channel's), or after the last pair the next chunk's first pair (more: there is a
        next chunk) */
@@ -1429,6 +1454,9 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
 #if LIN_MFMA == 2
     uint32_t psel0, psel1;                                /* the pair MFMA's A-operand masks */
     lin_pair_sel(lane, psel0, psel1);
+#if LIN_ALDS
+    psel0 = lin_pair_cls(lane);                           /* ... or the lane's class */
+#endif
 #endif
 #if LIN_MFMA
     lin_f4 c0 = lin_f4{LIN_MAGF, LIN_MAGF, LIN_MAGF, LIN_MAGF};   /* the accumulators' bias */
@@ -1480,6 +1508,10 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
         t.pos1 = sk.pos1;
         t.dq = ck.dq;
         t.tab = ck.tab;
+#if LIN_ALDS
+        t.A[4][0] = 0;
+        t.A[4][1] = 0;
+#endif
 #if LIN_SWIN
         /* a chunk's row of the window table: its C/A row and code base chip E (clamped to the
            table; gss_lin_win16_ok keeps a certified channel inside it) */
@@ -1543,8 +1575,14 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
         {
             /* the rows each pair (k, k + 1) loads ahead (gather from lanes k + 2, k + 3, 0, 1:
                once per chunk in parallel, instead of selects per pair) */
-            const uint32_t wa2 = __shfl_down(my_wa, 2), wa3 = __shfl_down(my_wa, 3);
-            const uint32_t wn0 = __shfl(my_wn, 0), wn1 = __shfl(my_wn, nc > 1 ? 1 : 0);
+            /* the channels are lanes 0..15, one DPP row: lane k takes lane k + 2's / k + 3's
+               by a row shift (row_shl), the first pair's by readlane -- no LDS permutes */
+            const uint32_t wa2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)my_wa, 0x102, 0xF,
+                                                                       0xF, true);
+            const uint32_t wa3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)my_wa, 0x103, 0xF,
+                                                                       0xF, true);
+            const uint32_t wn0 = (uint32_t)__builtin_amdgcn_readlane((int)my_wn, 0);
+            const uint32_t wn1 = (uint32_t)__builtin_amdgcn_readlane((int)my_wn, nc > 1 ? 1 : 0);
             if (lane < nc) {
                 const bool in2 = lane + 2 < nc, in3 = lane + 3 < nc;
                 T[lane].na = in2 ? wa2 : wn0;
