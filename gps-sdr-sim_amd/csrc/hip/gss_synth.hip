@@ -560,6 +560,9 @@ __device__ uint64_t g_lin_stamp[LIN_STAMP_WAVES][4];
    the loop reads them back by broadcast LDS reads.
    LIN_SWIN 1 (measurement): the same table by compiler-visible s_loads: they share lgkmcnt with
    the LUT reads, so each pair's load is waited for with every LDS read drained (+16 %). */
+#ifndef LIN_NCRE
+#define LIN_NCRE 1      /* 1: nc opaque per chunk (no hoisted, spilled channel-count masks) */
+#endif
 #ifndef LIN_ALDS
 #define LIN_ALDS 1      /* 1: the pair MFMA's gain operand read from the records (no VALU masks) */
 #endif
@@ -1521,7 +1524,17 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
 #endif
     }
 
+    const int nc_blk = nc;
     for (int c = 0; c < LIN_STEPS / LIN_CH; c++) {
+#if LIN_NCRE
+        /* the channel count made opaque per chunk: its conditions (nc > 1, lane + 2 < nc, ...)
+           are recomputed by the scalar unit and one compare each, instead of being hoisted out
+           of the loop, spilled to VGPR lanes and read back with 12 v_readlane per chunk */
+        int nc = nc_blk;
+        asm volatile("" : "+s"(nc));
+#else
+        const int nc = nc_blk;
+#endif
         const int nb0 = n0 + c * (64 * LIN_CH);           /* first sample of the chunk */
         if (nb0 >= n_per_blk)
             break;
