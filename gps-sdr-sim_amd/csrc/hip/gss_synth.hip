@@ -560,6 +560,9 @@ __device__ uint64_t g_lin_stamp[LIN_STAMP_WAVES][4];
    the loop reads them back by broadcast LDS reads.
    LIN_SWIN 1 (measurement): the same table by compiler-visible s_loads: they share lgkmcnt with
    the LUT reads, so each pair's load is waited for with every LDS read drained (+16 %). */
+#ifndef LIN_PUNROLL
+#define LIN_PUNROLL 1   /* 1: the channel-pair loop unrolled (immediate record offsets) */
+#endif
 #ifndef LIN_NCRE
 #define LIN_NCRE 1      /* 1: nc opaque per chunk (no hoisted, spilled channel-count masks) */
 #endif
@@ -1649,8 +1652,20 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
                 acc[s] = v;
             }
         }
+#if LIN_PUNROLL
+        /* unrolled: each pair's record and lane-table addresses are immediate offsets */
+#pragma unroll
+        for (int p = 1; p < GSS_MAXCH / 2; p++) {
+            if (2 * p + 1 >= nc)
+                break;
+            lin_sw_pair<false>(acc, c0, T, 2 * p, nc, lane, s_lane, M, s_lut, tw, psel0, psel1,
+                               more);
+            k0 = 2 * p + 2;
+        }
+#else
         for (; k0 + 1 < nc; k0 += 2)                      /* uniform loop over channel pairs */
             lin_sw_pair<false>(acc, c0, T, k0, nc, lane, s_lane, M, s_lut, tw, psel0, psel1, more);
+#endif
         if (k0 < nc) {                                    /* the lone last channel: s[68:83] */
             uint32_t ws[LIN_CH], wb[LIN_CH];
             lin_sw_take_a(ws);
