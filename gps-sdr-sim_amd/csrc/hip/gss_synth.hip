@@ -1541,34 +1541,29 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
         const int nb0 = n0 + c * (64 * LIN_CH);           /* first sample of the chunk */
         if (nb0 >= n_per_blk)
             break;
-        /* ---- the chunk's parameters, lane k for channel k ---- */
-        uint32_t my_flags = 0;
-#if LIN_SWIN == 3
-        uint32_t my_wa = 0, my_wn = 0;
+        /* ---- the chunk's parameters, lane k for channel k: computed on every lane (the
+           lanes past nc hold zero rows and flags, their values unused), stored by the first nc
+           (no phi moves for the lanes outside) ---- */
+        const bool after = pos1 <= nb0;                    /* the data bit changed before it */
+        const bool chg = pos1 < nb0 + 64 * LIN_CH;         /* ... or changes inside it      */
+        const uint32_t my_flags = (chg && !after ? 1u : 0u) | pflag;
+        const uint64_t zn = zb + zs10;                     /* the next chunk's code base */
+#if LIN_SWIN
+        const uint32_t my_wa = wa_next;
+        const uint32_t my_wn = (trow + min((uint32_t)(zn >> 50), (uint32_t)(GSS_LIN_TWE - 1))) *
+                               (uint32_t)(LIN_CH * sizeof(uint32_t));
 #endif
         if (lane < nc) {
             lin_ct &t = T[lane];
             /* the chunk's base B (gss_lin.h): the segment's lines plus c chunks */
             t.B = (xb & ~0xFFFFFFFFull) | (uint32_t)(zb >> GSS_LIN_CSH);
-            const bool after = pos1 <= nb0;                /* the data bit changed before it */
-            const bool chg = pos1 < nb0 + 64 * LIN_CH;     /* ... or changes inside it      */
-            t.flags = (chg && !after ? 1u : 0u) | pflag;
-            my_flags = t.flags;
+            t.flags = my_flags;
 #if !LIN_SWIN
             /* 1/16 chip below lane 0's first chip, plus CBW_PRE chips */
             t.q0 = (uint32_t)(zb >> 46) + (16 * CBW_PRE - 1);
-#endif
-            const uint64_t zn = zb + zs10;                 /* the next chunk's code base */
-#if LIN_SWIN
-            const uint32_t wn = (trow + min((uint32_t)(zn >> 50), (uint32_t)(GSS_LIN_TWE - 1))) *
-                                (uint32_t)(LIN_CH * sizeof(uint32_t));
-            t.wa = wa_next;
-            t.wn = wn;
-#if LIN_SWIN == 3
-            my_wa = wa_next;
-            my_wn = wn;
-#endif
-            wa_next = wn;
+#else
+            t.wa = my_wa;
+            t.wn = my_wn;
 #endif
             if ((int)after != g_after) {                   /* the gain the chunk starts with */
                 g_after = (int)after;
@@ -1583,22 +1578,29 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
                 t.g = (int32_t)gh;
 #endif
             }
-            xb += xs10;
-            zb = zn;
         }
+#if LIN_SWIN
+        wa_next = my_wn;
+#endif
+        xb += xs10;
+        zb = zn;
         /* the channels with a gain change or patches in this chunk (wave-uniform) */
 #if LIN_SWIN == 3 && LIN_MFMA == 2
+        /* the first two channels' rows of this chunk and the next (scalar: readlane) */
+        const uint32_t wa0 = (uint32_t)__builtin_amdgcn_readlane((int)my_wa, 0);
+        const uint32_t wa1r = (uint32_t)__builtin_amdgcn_readlane((int)my_wa, 1);
+        const uint32_t wn0 = (uint32_t)__builtin_amdgcn_readlane((int)my_wn, 0);
+        const uint32_t wn1r = (uint32_t)__builtin_amdgcn_readlane((int)my_wn, 1);
+        const uint32_t wa1 = nc > 1 ? wa1r : wa0, wn1 = nc > 1 ? wn1r : wn0;
         {
             /* the rows each pair (k, k + 1) loads ahead (gather from lanes k + 2, k + 3, 0, 1:
-               once per chunk in parallel, instead of selects per pair) */
-            /* the channels are lanes 0..15, one DPP row: lane k takes lane k + 2's / k + 3's
-               by a row shift (row_shl), the first pair's by readlane -- no LDS permutes */
+               once per chunk in parallel, instead of selects per pair); the channels are lanes
+               0..15, one DPP row: lane k takes lane k + 2's / k + 3's by a row shift (row_shl),
+               the first pair's by readlane -- no LDS permutes */
             const uint32_t wa2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)my_wa, 0x102, 0xF,
                                                                        0xF, true);
             const uint32_t wa3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)my_wa, 0x103, 0xF,
                                                                        0xF, true);
-            const uint32_t wn0 = (uint32_t)__builtin_amdgcn_readlane((int)my_wn, 0);
-            const uint32_t wn1 = (uint32_t)__builtin_amdgcn_readlane((int)my_wn, nc > 1 ? 1 : 0);
             if (lane < nc) {
                 const bool in2 = lane + 2 < nc, in3 = lane + 3 < nc;
                 T[lane].na = in2 ? wa2 : wn0;
@@ -1637,7 +1639,7 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
 #if LIN_MFMA == 2 && LIN_SWIN == 3
         /* the first pair's rows: loaded during the chunk before, or now */
         if (nc > 0 && !sw_ahead)
-            lin_sw_load2(tw, T[0].wa, T[nc > 1 ? 1 : 0].wa);
+            lin_sw_load2(tw, wa0, wa1);
         const bool more = c + 1 < LIN_STEPS / LIN_CH && nb0 + 64 * LIN_CH < n_per_blk;
         int k0 = 0;
         if (nc >= 2) {                                    /* the first pair sets acc = bias + ... */
@@ -1672,7 +1674,7 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
             lin_sw_take(wb);                              /* (its duplicate, unused) */
             (void)wb;
             if (more)                                     /* the next chunk's first pair */
-                lin_sw_load2(tw, T[0].wn, T[nc > 1 ? 1 : 0].wn);
+                lin_sw_load2(tw, wn0, wn1);
             lin_sw_steps(acc, T[k0], k0, lane, s_lane, M, s_lut, ws);
             k0 = nc;
         }
