@@ -1228,6 +1228,29 @@ int drain(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, int
     return 0;
 }
 
+/* GSS_RUN_SPEC_CUS=N (measurement): the walks' stream on N of the device's CUs, spread over
+   them (every (ncu / N)-th), and with GSS_RUN_RENDER_REST=1 the render stream on the others */
+int spec_cus()
+{
+    const char *e = getenv("GSS_RUN_SPEC_CUS");
+    return e && *e ? atoi(e) : 0;
+}
+
+hipError_t cu_mask_stream(hipStream_t *st, int n_sel, bool rest)
+{
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0 || n_sel <= 0 || n_sel >= ncu)
+        return hipErrorInvalidValue;
+    const int every = ncu / n_sel;
+    std::vector<uint32_t> m((size_t)(ncu + 31) / 32, 0u);
+    for (int i = 0; i < ncu; i++)
+        if ((i % every == 0) != rest)
+            m[(size_t)i / 32] |= 1u << (i % 32);
+    return hipExtStreamCreateWithCUMask(st, (uint32_t)m.size(), m.data());
+}
+
 bool make_streams(hipStream_t *cp)
 {
     for (int k = 0; k < NCOPY; k++)
@@ -1364,7 +1387,9 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
     {
         gss_ca_table(r.ca);                            /* the proofs' copy, on the host */
         if (hipMalloc((void **)&d_ca, sizeof r.ca) != hipSuccess ||
-            hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+            (spec_cus() > 0 && getenv("GSS_RUN_RENDER_REST")
+                 ? cu_mask_stream(&st, spec_cus(), true)
+                 : hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess ||
             !make_streams(cp) ||
             (trace_on() && (hipEventCreate(&r.t_base) != hipSuccess ||
                             hipEventRecord(r.t_base, st) != hipSuccess)))
@@ -1417,7 +1442,9 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             /* high priority: the walks wait for free CUs behind the render kernels otherwise */
             int lo_pri = 0, hi_pri = 0;
             (void)hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri);
-            if (hipStreamCreateWithPriority(&r.spec_st, hipStreamNonBlocking, hi_pri) !=
+            if ((spec_cus() > 0
+                     ? cu_mask_stream(&r.spec_st, spec_cus(), false)
+                     : hipStreamCreateWithPriority(&r.spec_st, hipStreamNonBlocking, hi_pri)) !=
                     hipSuccess ||
                 hipMalloc((void **)&r.spec_warm, 1024) != hipSuccess)
                 err = gss_fail(GSS_E_HIP, "run carrier-chain stream");
