@@ -1,5 +1,5 @@
 """gss_run over one of bench.py's per-config workloads (configs[2..4]) with the run's own trace
-(GSS_RUN_TRACE=1 on stderr, summarised by tools/e2e_trace_sum.py): where the end-to-end time of a
+(GSS_RUN_TRACE=1 on stderr, summarised by tools/e2e_trace_summary.py): where the end-to-end time of a
 non-headline config goes.  Usage: python tools/e2e_cfg_probe.py <config index 2-4> [window s]
 [threads].  GPU box only."""
 import os
