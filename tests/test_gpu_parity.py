@@ -532,15 +532,20 @@ def test_streaming_run_sink_error_stops_cleanly(dev, golden):
     ("0", "1", "1", "host", 57), ("1", "0", "1", "host", 57), ("1", "1", "0", "host", 57),
     ("1", "1", "1", "host", 57), ("1", "1", "1", "host", 1),
     ("0", "1", "1", "gpu", 57), ("1", "0", "1", "gpu", 57), ("1", "1", "1", "gpu", 57),
-    ("1", "1", "1", "gpu", 1), ("1", "1", "1", "split", 57), ("1", "0", "1", "split", 1)])
+    ("1", "1", "1", "gpu", 1), ("1", "1", "1", "split", 57), ("1", "0", "1", "split", 1),
+    ("1", "1", "1", "host-dma", 57), ("0", "0", "1", "gpu-dma", 57)])
 def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec, ahead, prover, proof, batch):
     """gss_run with the carrier chain walked on the host (GSS_RUN_SPEC=0) and run ahead on the
     GPU (the default), with the rows produced on the planner thread (GSS_RUN_ROWS_AHEAD=0) or
     ahead on their own (the default; one-block batches too), and the proofs on the planner thread
-    (GSS_RUN_PROVER=0) or their own, or on the GPU (GSS_RUN_PROOF=gpu; split: every other slot): a 65 s run
+    (GSS_RUN_PROVER=0) or their own, or on the GPU (GSS_RUN_PROOF=gpu; split: every other slot),
+    the slots' inputs uploaded by kernel (the default) or by the copy engine (-dma): a 65 s run
     across two 30 s updates, whole and from a mid-run block, against the reference's golden
     hashes."""
     monkeypatch.setenv("GSS_RUN_SPEC", spec)
+    if proof.endswith("-dma"):                # the slots' uploads by the copy engine
+        proof = proof[:-4]
+        monkeypatch.setenv("GSS_RUN_UPLOAD", "dma")
     monkeypatch.setenv("GSS_RUN_PROOF", proof)
     monkeypatch.setenv("GSS_RUN_ROWS_AHEAD", ahead)
     monkeypatch.setenv("GSS_RUN_PROVER", prover)
