@@ -498,6 +498,12 @@ def test_spec_walks_on_device(dev):
         for r in np.flatnonzero(live):
             k = gi.reshape(-1)["k"][r]
             assert got2["seg"][r][:k].tobytes() == got["seg"][r][:k].tobytes(), (kw, r)
+    # the kernel stages rows and walks through LDS in 8- and 16-byte words: misaligned buffers
+    # are refused, not read or written across their ends
+    with pytest.raises(G.GssError, match="aligned"):
+        dev.spec_device(d_in.data_ptr() + 4, 16, n, d_spec.data_ptr())
+    with pytest.raises(G.GssError, match="aligned"):
+        dev.spec_device(d_in.data_ptr(), 16, n, d_spec.data_ptr() + 8)
 
 
 def test_streaming_run_sink_error_stops_cleanly(dev, golden):
