@@ -463,16 +463,18 @@ GATHER_FS, GATHER_WINDOW_S = 2.0e7, 450.0   # configs[3]: 3600 s at 20 MS/s over
 
 
 def gather_leg(G, torch, td, dev, dev_t, rank, world, coll_t, walker, threads, window_s,
-               host_wire):
+               host_wire, layout="stripe"):
     """BASELINE configs[3] as a whole-node run (N > 1 only): static -s 20000000 -b 16, each rank
     owning window_s seconds of one world * window_s run (weak scaling: 450 s per rank is
-    configs[3]'s 3600 s at 8 GPUs), each rank's window planned (baton, chain run ahead) and
-    resident, then rendered chunk by chunk and gathered in run order to rank 0 over RCCL point to
-    point (gpssim_amd.node: render_chunks, chunk_source, ordered_gather) into a discarding sink.
-    Timed from the first render launch to the last byte at rank 0 (max over ranks): the
-    node's data path, xGMI included, file system excluded."""
-    from gpssim_amd.node import chunk_plan, chunk_source, ordered_gather, rank_blocks, \
-        render_chunks
+    configs[3]'s 3600 s at 8 GPUs), each rank's window planned (baton, chain run ahead); with the
+    "stripe" layout (gpssim_amd.node.chunk_plan) the chunks' rows are handed round-robin to the
+    ranks that render them (exchange_rows), so that rank 0 receives from every peer at once; the
+    chunks are rendered and gathered in run order to rank 0 over RCCL point to point
+    (render_chunks, chunk_source, ordered_gather) into a discarding sink.  Timed from the first
+    render launch to the last byte at rank 0 (max over ranks): the node's data path, xGMI
+    included, file system excluded."""
+    from gpssim_amd.node import chunk_plan, chunk_source, exchange_rows, ordered_gather, \
+        rank_blocks, render_chunks
     from gpssim_amd.render import DeviceWindow
     from gpssim_amd.shard import Baton, plan_window
     t0 = time.perf_counter()
@@ -484,8 +486,17 @@ def gather_leg(G, torch, td, dev, dev_t, rank, world, coll_t, walker, threads, w
     b0, b1 = rank_blocks(nb_all, rank, world)
     blk, nch, ck, pt = plan_window(scn, b0, b1 - b0, baton=Baton(td, rank, world, device=coll_t),
                                    threads=threads, walker=walker)
-    win = DeviceWindow(torch, dev, dev_t, blk, nch, scn.nav_table(), npb, 16, ck=ck,
-                       threads=threads, batch=chunk)
+    plan = chunk_plan(nb_all, world, chunk, layout)
+    nav = scn.nav_table()
+    if layout == "stripe":
+        blk, nch, nav, firsts = exchange_rows(plan, nb_all, rank, world, td, blk, nch, nav,
+                                              device=coll_t)
+        ck = None
+    else:
+        firsts = [c for r, c, nb in plan if r == rank]
+    sizes = [nb for r, c, nb in plan if r == rank]
+    win = DeviceWindow(torch, dev, dev_t, blk, nch, nav, npb, 16, ck=ck, threads=threads,
+                       sizes=sizes or None)
     plan_s = time.perf_counter() - t0
     got = {"bytes": 0}
 
@@ -495,14 +506,15 @@ def gather_leg(G, torch, td, dev, dev_t, rank, world, coll_t, walker, threads, w
     def make_buf(nb):
         return torch.empty(nb * bb, dtype=torch.uint8, device="cpu" if host_wire else dev_t)
 
-    plan = chunk_plan(nb_all, world, chunk)
+    stats = {}
     td.barrier()
     torch.cuda.synchronize(dev_t)
     t1 = time.perf_counter()
     _, evs = render_chunks(torch, win, dev_t)
-    get_chunk = chunk_source(torch, win, b0, chunk, evs, dev_t,
+    get_chunk = chunk_source(torch, win, firsts, evs, dev_t,
                              host_wire=host_wire and rank != 0)
-    ordered_gather(plan, rank, td, get_chunk, make_buf, sink if rank == 0 else None)
+    ordered_gather(plan, rank, td, get_chunk, make_buf, sink if rank == 0 else None,
+                   stats=stats)
     torch.cuda.synchronize(dev_t)
     el = time.perf_counter() - t1
     t = torch.tensor([el, plan_s], dtype=torch.float64, device=coll_t)
@@ -511,12 +523,16 @@ def gather_leg(G, torch, td, dev, dev_t, rank, world, coll_t, walker, threads, w
     total = nb_all * bb
     win.free()
     return {"workload": f"static -s 20000000 -b 16, {window_s * world:g} s over {world} ranks "
-                        f"({window_s:g} s = {b1 - b0} blocks per rank), rendered and gathered "
-                        f"in run order to rank 0 (chunks of {chunk} blocks), discarding sink",
+                        f"({window_s:g} s = {b1 - b0} blocks planned per rank), rendered "
+                        f"({layout} layout) and gathered in run order to rank 0 (chunks of "
+                        f"{chunk} blocks), discarding sink",
             "wire": "gloo via host memory (rehearsal)" if host_wire else "RCCL point to point",
-            "bytes": total, "bytes_at_rank0": got["bytes"] if rank == 0 else None,
+            "layout": layout, "bytes": total,
+            "bytes_at_rank0": got["bytes"] if rank == 0 else None,
             "wall_s": round(el, 3), "GBps_at_rank0": round(total / el / 1e9, 2),
             "MSps": round(nb_all * npb / el / 1e6, 1), "host_plan_s_max": round(plan_s, 3),
+            "recv_outstanding_max": stats.get("max_outstanding") if rank == 0 else None,
+            "peers_outstanding_max": stats.get("max_peers_outstanding") if rank == 0 else None,
             "spec_rows_translated_rank": pt.get("spec_hits")}
 
 
@@ -540,6 +556,9 @@ def main():
     ap.add_argument("--threads", type=int, default=BOX_CORES)
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the whole-node gather leg (N > 1: configs[3] to rank 0)")
+    ap.add_argument("--gather-layout", default="stripe", choices=["stripe", "block"],
+                    help="gather leg: chunks rendered round-robin over the ranks (stripe, every "
+                         "xGMI link into rank 0 at once) or each rank its own window (block)")
     ap.add_argument("--gather-window", type=float, default=GATHER_WINDOW_S,
                     help="seconds per rank of the gather leg's 20 MS/s run")
     args = ap.parse_args()
@@ -689,7 +708,7 @@ def main():
     gather = None
     if dist and not args.no_gather:
         gather = gather_leg(G, torch, td, dev, dev_t, rank, world, coll_t, walker, args.threads,
-                            args.gather_window, host_wire=rehearse)
+                            args.gather_window, host_wire=rehearse, layout=args.gather_layout)
         progress(f"gather: {gather['GBps_at_rank0']} GB/s at rank 0")
     configs = e2e = None
     # the headline's end-to-end leg first, then the per-config legs (each after its own kernel

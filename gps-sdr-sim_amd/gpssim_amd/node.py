@@ -22,7 +22,9 @@ import os
 import sys
 import time
 
-from . import Device, Scenario, block_bytes
+import numpy as np
+
+from . import MAXCH, NAV_WORDS, Device, Scenario, block_bytes
 
 
 def rank_blocks(n_blocks, rank, world):
@@ -49,63 +51,198 @@ def render_chunks(torch, win, dev_t):
     return st, evs
 
 
-def chunk_source(torch, win, first_block, chunk_blocks, evs, dev_t, host_wire):
+def chunk_source(torch, win, firsts, evs, dev_t, host_wire):
     """get_chunk(first, nb) for ordered_gather: the chunk's bytes in HBM once its render event
     has passed (the caller's stream waits for it, so a send or copy queued behind runs after it,
-    while later chunks still render); host_wire: a host copy (gloo)"""
+    while later chunks still render); firsts: the first block of each of win's batches, in batch
+    order (one batch = one gather chunk); host_wire: a host copy (gloo)"""
     bb = win.bb
+    at = {f: i for i, f in enumerate(firsts)}
 
     def get_chunk(first, nb):
-        i = (first - first_block) // chunk_blocks
+        i = at[first]
+        b0, b1 = win.batches[i][:2]
+        assert b1 - b0 == nb, "a gather chunk is one render batch"
         torch.cuda.current_stream(dev_t).wait_event(evs[i])
-        t = win.out[(first - first_block) * bb:(first - first_block + nb) * bb]
+        t = win.out[b0 * bb:b1 * bb]
         return t.cpu() if host_wire else t
     return get_chunk
 
 
-def chunk_plan(n_blocks, world, chunk_blocks):
-    """The run's chunks in run order: [(owner rank, first block, blocks)]."""
+def chunk_plan(n_blocks, world, chunk_blocks, layout="block"):
+    """The run's chunks in run order: [(render rank, first block, blocks)].  Chunks never cross
+    a planning window (rank_blocks: rank r plans [B r/N, B (r+1)/N)).  layout "block": each rank
+    renders the chunks of its own window, so rank 0 takes rank 1's whole window, then rank 2's,
+    ... -- one peer, one xGMI link, at a time.  "stripe": chunk i of the run is rendered by rank
+    i mod N (its rows handed over by exchange_rows), so any N consecutive chunks come from N
+    different ranks and rank 0 receives over every link at once."""
     plan = []
     for r in range(world):
         b0, b1 = rank_blocks(n_blocks, r, world)
         for c in range(b0, b1, chunk_blocks):
             plan.append((r, c, min(chunk_blocks, b1 - c)))
+    if layout == "stripe":
+        plan = [(i % world, c, nb) for i, (_, c, nb) in enumerate(plan)]
+    elif layout != "block":
+        raise ValueError(f"unknown layout {layout!r}")
     return plan
 
 
-def ordered_gather(plan, rank, dist, get_chunk, make_buf, sink):
-    """Rank 0 hands every chunk of `plan` to sink(tensor) in plan order: its own from
-    get_chunk(first, blocks), the others received from their owner (dist.irecv into one of two
-    buffers from make_buf(blocks), the next receive posted before the current chunk is written).
-    Every other rank sends its own chunks, in order (dist.send).  Point-to-point only: with
-    RCCL each chunk crosses xGMI once, GPU to GPU."""
+def planner_of(first, n_blocks, world):
+    """the rank whose planning window holds block `first`"""
+    r = first * world // n_blocks
+    while rank_blocks(n_blocks, r, world)[0] > first:
+        r -= 1
+    while rank_blocks(n_blocks, r, world)[1] <= first:
+        r += 1
+    return r
+
+
+def exchange_rows(plan, n_blocks, rank, world, dist, blk, nch, nav, device="cpu"):
+    """Hand each chunk's rows from the rank that planned it (its window: blk[n, 16], nch[n], its
+    nav table) to the rank that renders it (plan from chunk_plan(layout="stripe")).  Returns this
+    rank's render input: (blk, nch, nav, firsts) over the chunks it renders, in run order, with
+    every row's nav_tbl moved into the returned table (the planners' tables concatenated in rank
+    order); firsts: each chunk's first block.  Point to point only: per pair of ranks one message
+    of the nav-table size, then one of the table and the rows (torch.distributed; `device`
+    "cuda" for RCCL).  The carriers are already exact in the rows (plan_window's chain), so a
+    chunk renders the same bytes on any rank."""
+    import torch
+    from . import CHAN_DTYPE
+    my0, _ = rank_blocks(n_blocks, rank, world)
+    row_b = CHAN_DTYPE.itemsize * MAXCH
+    nav = np.ascontiguousarray(nav, np.uint32)
+    # chunks by (planner, renderer), in run order
+    pairs = {}
+    for r, c, nb in plan:
+        pairs.setdefault((planner_of(c, n_blocks, world), r), []).append((c, nb))
+
+    def payload(q):
+        parts = [nav.view(np.uint8).reshape(-1)]
+        for c, nb in pairs.get((rank, q), []):
+            parts.append(np.ascontiguousarray(blk[c - my0:c - my0 + nb]).view(np.uint8).reshape(-1))
+            parts.append(np.ascontiguousarray(nch[c - my0:c - my0 + nb], np.int32)
+                         .view(np.uint8).reshape(-1))
+        return np.concatenate(parts)
+
+    # phase 1: nav-table sizes to every renderer this rank plans for (and from every planner)
+    sends = [q for q in range(world) if q != rank and (rank, q) in pairs]
+    recvs = [p for p in range(world) if p != rank and (p, rank) in pairs]
+    ops, sizes = [], {}
+    for q in sends:
+        ops.append(dist.isend(torch.tensor([len(nav)], dtype=torch.int64, device=device), dst=q))
+    for p in recvs:
+        sizes[p] = torch.empty(1, dtype=torch.int64, device=device)
+        ops.append(dist.irecv(sizes[p], src=p))
+    for w in ops:
+        w.wait()
+    # phase 2: the tables and rows
+    ops, bufs, keep = [], {}, []
+    for q in sends:
+        t = torch.from_numpy(payload(q)).to(device)
+        keep.append(t)
+        ops.append(dist.isend(t, dst=q))
+    for p in recvs:
+        n_nav = int(sizes[p].item())
+        nbytes = n_nav * NAV_WORDS * 4 + sum(nb for c, nb in pairs[(p, rank)]) * (row_b + 4)
+        bufs[p] = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        ops.append(dist.irecv(bufs[p], src=p))
+    for w in ops:
+        w.wait()
+    # assemble: the planners' nav tables in rank order, rows re-pointed into them
+    tables, rows = {}, {}
+    for p in range(world):
+        if p == rank:
+            if (rank, rank) in pairs:
+                tables[p] = nav
+                for c, nb in pairs[(rank, rank)]:
+                    rows[c] = (blk[c - my0:c - my0 + nb], np.asarray(nch[c - my0:c - my0 + nb],
+                                                                     np.int32), p)
+            continue
+        if p not in bufs:
+            continue
+        raw = bufs[p].cpu().numpy()
+        n_nav = int(sizes[p].item())
+        o = n_nav * NAV_WORDS * 4
+        tables[p] = raw[:o].view(np.uint32).reshape(n_nav, NAV_WORDS)
+        for c, nb in pairs[(p, rank)]:
+            b = raw[o:o + nb * row_b].view(CHAN_DTYPE).reshape(nb, MAXCH)
+            o += nb * row_b
+            n = raw[o:o + nb * 4].view(np.int32)
+            o += nb * 4
+            rows[c] = (b, n, p)
+    base, off = {}, 0
+    for p in sorted(tables):
+        base[p] = off
+        off += len(tables[p])
+    mine = [(c, nb) for r, c, nb in plan if r == rank]
+    out_blk = np.zeros((sum(nb for _, nb in mine), MAXCH), CHAN_DTYPE)
+    out_nch = np.zeros(len(out_blk), np.int32)
+    o = 0
+    for c, nb in mine:
+        b, n, p = rows[c]
+        out_blk[o:o + nb] = b
+        out_blk[o:o + nb]["nav_tbl"] += base[p]
+        out_nch[o:o + nb] = n
+        o += nb
+    out_nav = (np.concatenate([tables[p] for p in sorted(tables)]) if tables
+               else np.zeros((1, NAV_WORDS), np.uint32))
+    return out_blk, out_nch, out_nav, [c for c, _ in mine]
+
+
+def ordered_gather(plan, rank, dist, get_chunk, make_buf, sink, depth=2, stats=None):
+    """Rank 0 hands every chunk of `plan` ([(render rank, first, blocks)], run order) to
+    sink(tensor) in plan order: its own from get_chunk(first, blocks), every other rank's
+    received from it.  Every other rank sends its own chunks in order (dist.send).  Rank 0 keeps
+    up to `depth` receives in flight from EVERY peer at once, each into one of that peer's
+    `depth` buffers (make_buf(blocks), sliced for a short chunk), re-posted as soon as the sink
+    has taken the chunk it held; so with a layout whose consecutive chunks come from different
+    ranks (chunk_plan "stripe") the peers' links all carry data together.  Point to point only:
+    with RCCL each chunk crosses xGMI once, GPU to GPU.  stats (a dict, rank 0): the most
+    receives and the most distinct peers that were outstanding at once."""
     if rank != 0:
         for r, b0, nb in plan:
             if r == rank:
                 dist.send(get_chunk(b0, nb), dst=0)
         return
-    bufs = {}
-
-    def post(i):
-        r, b0, nb = plan[i]
-        if r == 0:
-            return None, None
-        key = i % 2
-        buf = bufs.get((key, nb))
-        if buf is None:
-            buf = make_buf(nb)
-            bufs[(key, nb)] = buf
-        return dist.irecv(buf, src=r), buf
-
-    nxt = post(0) if plan else None
+    from collections import deque
+    queues, cap = {}, {}
     for i, (r, b0, nb) in enumerate(plan):
-        work, buf = nxt
-        nxt = post(i + 1) if i + 1 < len(plan) else None
+        if r != 0:
+            queues.setdefault(r, deque()).append(i)
+            cap[r] = max(cap.get(r, 0), nb)
+    free = {r: deque(make_buf(cap[r]) for _ in range(min(depth, len(q))))
+            for r, q in queues.items()}
+    inflight = {}                         # plan index -> (work, buffer, its view)
+    out = {r: 0 for r in queues}
+    most, most_peers = 0, 0
+
+    def fill(r):
+        nonlocal most, most_peers
+        q = queues[r]
+        while q and free[r]:
+            i = q.popleft()
+            buf = free[r].popleft()
+            view = buf[:plan[i][2] * (buf.numel() // cap[r])]
+            inflight[i] = (dist.irecv(view, src=r), buf, view)
+            out[r] += 1
+        most = max(most, len(inflight))
+        most_peers = max(most_peers, sum(1 for v in out.values() if v))
+
+    for r in queues:
+        fill(r)
+    for i, (r, b0, nb) in enumerate(plan):
         if r == 0:
             sink(get_chunk(b0, nb))
-        else:
-            work.wait()
-            sink(buf)
+            continue
+        work, buf, view = inflight.pop(i)
+        work.wait()
+        sink(view)
+        out[r] -= 1
+        free[r].append(buf)
+        fill(r)
+    if stats is not None:
+        stats.update(max_outstanding=most, max_peers_outstanding=most_peers, depth=depth)
 
 
 class FileSink:
@@ -131,8 +268,11 @@ class FileSink:
         self.bytes += n
 
 
-def run_node(argv, rank, world, local, backend="nccl", chunk_blocks=None, threads=16):
-    """The whole-node run of one gps-sdr-sim command line; returns rank 0's byte count."""
+def run_node(argv, rank, world, local, backend="nccl", chunk_blocks=None, threads=16,
+             layout="stripe", stats=None):
+    """The whole-node run of one gps-sdr-sim command line; returns rank 0's byte count.  layout:
+    chunk_plan's ("stripe": planned by window, rendered round-robin by chunk, gathered over every
+    link at once; "block": every rank renders its own window)."""
     import torch
     import torch.distributed as dist
     from .render import DeviceWindow
@@ -146,26 +286,35 @@ def run_node(argv, rank, world, local, backend="nccl", chunk_blocks=None, thread
     dev_t = torch.device("cuda", local)
     dev = Device(local)
     b0, b1 = rank_blocks(n_blocks, rank, world)
-    baton = Baton(dist, rank, world, device=dev_t if backend == "nccl" else "cpu")
+    wire = dev_t if backend == "nccl" else "cpu"
+    baton = Baton(dist, rank, world, device=wire)
     blk, nch, ck, _ = plan_window(scn, b0, b1 - b0, baton=baton, threads=threads,
                                   walker=device_walker(dev, torch))
-    win = DeviceWindow(torch, dev, dev_t, blk, nch, scn.nav_table(), npb, fmt, ck=ck,
-                       threads=threads, batch=chunk_blocks)
+    plan = chunk_plan(n_blocks, world, chunk_blocks, layout)
+    nav = scn.nav_table()
+    if layout == "stripe":
+        blk, nch, nav, firsts = exchange_rows(plan, n_blocks, rank, world, dist, blk, nch, nav,
+                                              device=wire)
+        ck = None
+    else:
+        firsts = [c for r, c, nb in plan if r == rank]
+    sizes = [nb for r, c, nb in plan if r == rank]
+    win = DeviceWindow(torch, dev, dev_t, blk, nch, nav, npb, fmt, ck=ck, threads=threads,
+                       sizes=sizes or None)
     wire_gpu = backend == "nccl"
     _, evs = render_chunks(torch, win, dev_t)
-    get_chunk = chunk_source(torch, win, b0, chunk_blocks, evs, dev_t,
+    get_chunk = chunk_source(torch, win, firsts, evs, dev_t,
                              host_wire=not (wire_gpu or rank == 0))
 
     def make_buf(nb):
         return torch.empty(nb * bb, dtype=torch.uint8, device=dev_t if wire_gpu else "cpu")
 
-    plan = chunk_plan(n_blocks, world, chunk_blocks)
     total = 0
     if rank == 0:
         fd = 1 if out_file == "-" else os.open(out_file, os.O_WRONLY | os.O_CREAT | os.O_TRUNC,
                                                0o644)
         sink = FileSink(torch, fd, chunk_blocks * bb)
-        ordered_gather(plan, rank, dist, get_chunk, make_buf, sink)
+        ordered_gather(plan, rank, dist, get_chunk, make_buf, sink, stats=stats)
         total = sink.bytes
         if fd != 1:
             os.close(fd)
@@ -191,7 +340,8 @@ def main(argv=None):
     backend = os.environ.get("GSS_BACKEND", "nccl")
     dist.init_process_group(backend)
     t0 = time.perf_counter()
-    n = run_node(argv, rank, world, local, backend=backend)
+    n = run_node(argv, rank, world, local, backend=backend,
+                 layout=os.environ.get("GSS_GATHER_LAYOUT", "stripe"))
     if rank == 0:
         dt = time.perf_counter() - t0
         print(f"\nDone! {n} bytes from {world} ranks in {dt:.1f} s", file=sys.stderr)

@@ -27,10 +27,11 @@ def block_checkpoints(blk, nch, n_per_blk, blocks=None):
 
 class DeviceWindow:
     """One window of blocks, proven and resident in HBM, rendered in calls of at most `batch`
-    blocks (each call's fast-path scratch rows scale with its block count)."""
+    blocks (each call's fast-path scratch rows scale with its block count), or in the calls
+    `sizes` gives (block counts in row order: gpssim_amd.node's gather chunks)."""
 
     def __init__(self, torch, dev, dev_t, blk, nch, nav, n_per_blk, fmt, ck=None, threads=8,
-                 batch=3000, out=None, proof="gpu"):
+                 batch=3000, out=None, proof="gpu", sizes=None):
         self.torch, self.dev, self.fmt, self.npb = torch, dev, fmt, n_per_blk
 
         def up(a):
@@ -79,13 +80,17 @@ class DeviceWindow:
                                                            device=dev_t)
         assert self.out.numel() >= self.nblk * self.bb
         self.batches = []
-        for b0 in range(0, self.nblk, batch):
-            b1 = min(self.nblk, b0 + batch)
+        if sizes is None:
+            sizes = [min(batch, self.nblk - b0) for b0 in range(0, self.nblk, batch)]
+        assert sum(sizes) == self.nblk and all(n > 0 for n in sizes)
+        b1 = 0
+        for n in sizes:
+            b0, b1 = b1, b1 + n
             fb = np.nonzero(fast[b0:b1] == 0)[0].astype(np.int32)
             d_fb = torch.from_numpy(fb if len(fb) else np.zeros(1, np.int32)).to(dev_t)
             self.batches.append((b0, b1, d_fb, len(fb)))
         if self.nblk:
-            dev.reserve(min(batch, self.nblk), n_per_blk)
+            dev.reserve(max(sizes), n_per_blk)
 
     def step(self, stream=0):
         """Render every block of the window into self.out (stream-ordered)."""

@@ -1,11 +1,18 @@
 """Whole-node single-sink output (gpssim_amd.node): the ordered chunked gather of the ranks' time
 shards to rank 0.
 
-* CPU, gloo, world sizes 2 and 3: ordered_gather over synthetic byte chunks whose content
-  encodes (block, byte) -- rank 0's sink must see the run's bytes in run order, whatever the
-  partition and chunk size (uneven ranks, a last short chunk, more ranks than chunks of a rank);
-* GPU (-m gpu), gloo, two ranks on the one GPU: run_node renders the two halves of the static
-  -d 3 -b 16 run and rank 0 writes the file; its blocks carry the reference's golden hashes.
+* CPU, gloo, world sizes 2-4: ordered_gather over synthetic byte chunks whose content encodes
+  (block, byte) -- rank 0's sink must see the run's bytes in run order, whatever the partition,
+  chunk size and layout (uneven ranks, a last short chunk, more ranks than chunks of a rank,
+  "block" and "stripe"); with every layout rank 0 must have had receives outstanding from
+  min(world - 1, 2) or more peers at once (the per-peer receive windows), and with "stripe"
+  from every peer;
+* CPU, gloo, world sizes 3 and 4: exchange_rows hands each chunk's rows from its planner to its
+  renderer byte for byte, with the nav rows re-pointed into the merged table;
+* GPU (-m gpu), two ranks on the one GPU, backend GSS_TEST_BACKEND (default gloo: RCCL needs a
+  GPU per rank, so a whole-node driver run sets nccl and exercises the same test unchanged):
+  run_node renders the static -d 3 -b 16 run in both layouts and rank 0 writes the file; its
+  blocks carry the reference's golden hashes.
 """
 import hashlib
 import os
@@ -32,42 +39,143 @@ def _block_bytes(b, bb):
     return ((np.arange(bb, dtype=np.int64) * 7 + b * 131) % 251).astype(np.uint8)
 
 
-def _gather_worker(rank, world, port, n_blocks, bb, chunk_blocks, out_path):
+def _gather_worker(rank, world, port, n_blocks, bb, chunk_blocks, layout, out_path):
     sys.path.insert(0, os.path.join(REPO, "gps-sdr-sim_amd"))
+    import json
     import numpy as np
     import torch
     import torch.distributed as dist
-    from gpssim_amd.node import chunk_plan, ordered_gather, rank_blocks
+    from gpssim_amd.node import chunk_plan, ordered_gather
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    b0, b1 = rank_blocks(n_blocks, rank, world)
-    mine = torch.from_numpy(np.concatenate([_block_bytes(b, bb) for b in range(b0, b1)])
-                            if b1 > b0 else np.zeros(0, np.uint8))
+    plan = chunk_plan(n_blocks, world, chunk_blocks, layout)
 
-    def get_chunk(first, nb):
-        return mine[(first - b0) * bb:(first - b0 + nb) * bb].clone()
+    def get_chunk(first, nb):             # this rank "renders" the chunks the plan gives it
+        assert any(r == rank and c == first and n == nb for r, c, n in plan)
+        return torch.from_numpy(np.concatenate([_block_bytes(b, bb)
+                                                for b in range(first, first + nb)]))
 
-    got = []
-    ordered_gather(chunk_plan(n_blocks, world, chunk_blocks), rank, dist, get_chunk,
+    got, stats = [], {}
+    ordered_gather(plan, rank, dist, get_chunk,
                    lambda nb: torch.empty(nb * bb, dtype=torch.uint8),
-                   (lambda t: got.append(t.numpy().tobytes())) if rank == 0 else None)
+                   (lambda t: got.append(t.numpy().tobytes())) if rank == 0 else None,
+                   stats=stats)
     if rank == 0:
         open(out_path, "wb").write(b"".join(got))
+        open(out_path + ".json", "w").write(json.dumps(stats))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_blocks,chunk", [(2, 29, 4), (3, 10, 3), (3, 5, 8), (2, 1, 4)])
-def test_ordered_gather_gloo(tmp_path, world, n_blocks, chunk):
+@pytest.mark.parametrize("layout", ["block", "stripe"])
+@pytest.mark.parametrize("world,n_blocks,chunk", [(2, 29, 4), (3, 10, 3), (3, 5, 8), (2, 1, 4),
+                                                  (4, 23, 2), (4, 41, 5)])
+def test_ordered_gather_gloo(tmp_path, world, n_blocks, chunk, layout):
+    import json
     import numpy as np
     import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(REPO, "gps-sdr-sim_amd"))
+    from gpssim_amd.node import chunk_plan
     bb = 40
     out = tmp_path / "run.bin"
-    mp.spawn(_gather_worker, args=(world, _free_port(), n_blocks, bb, chunk, str(out)),
+    mp.spawn(_gather_worker, args=(world, _free_port(), n_blocks, bb, chunk, layout, str(out)),
              nprocs=world, join=True)
     want = np.concatenate([_block_bytes(b, bb) for b in range(n_blocks)]).tobytes()
     assert out.read_bytes() == want
+    st = json.loads((tmp_path / "run.bin.json").read_text())
+    plan = chunk_plan(n_blocks, world, chunk, layout)
+    peers = {r for r, c, nb in plan if r != 0}
+    # every peer with chunks had its first receive posted before rank 0's sink took anything
+    assert st["max_peers_outstanding"] == len(peers)
+    assert st["max_peers_outstanding"] >= min(len(peers), 2)
+    assert st["max_outstanding"] >= min(len(peers), 2)
+    if layout == "stripe":
+        assert {r for r, c, nb in plan[:world]} == set(range(min(world, len(plan))))
+
+
+def _exchange_worker(rank, world, port, n_blocks, chunk, out_dir):
+    sys.path.insert(0, os.path.join(REPO, "gps-sdr-sim_amd"))
+    import numpy as np
+    import torch.distributed as dist
+    from gpssim_amd import CHAN_DTYPE, MAXCH, NAV_WORDS
+    from gpssim_amd.node import chunk_plan, exchange_rows, rank_blocks
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b0, b1 = rank_blocks(n_blocks, rank, world)
+    blk, nch, nav = _rows(b0, b1, rank)
+    plan = chunk_plan(n_blocks, world, chunk, "stripe")
+    ob, on, onav, firsts = exchange_rows(plan, n_blocks, rank, world, dist, blk, nch, nav)
+    np.save(os.path.join(out_dir, f"blk{rank}.npy"), ob.view(np.uint8))
+    np.save(os.path.join(out_dir, f"nch{rank}.npy"), on)
+    np.save(os.path.join(out_dir, f"nav{rank}.npy"), onav)
+    np.save(os.path.join(out_dir, f"first{rank}.npy"), np.asarray(firsts, np.int64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _rows(b0, b1, planner):
+    """synthetic rows of blocks [b0, b1) as planner `planner` would hold them: every field a
+    function of (block, channel), nav_tbl into a planner-sized table of distinct rows"""
+    import numpy as np
+    from gpssim_amd import CHAN_DTYPE, MAXCH, NAV_WORDS
+    n_nav = 3 + planner * 2
+    nav = (np.arange(n_nav * NAV_WORDS, dtype=np.uint32).reshape(n_nav, NAV_WORDS) +
+           np.uint32(1000 * (planner + 1)))
+    blk = np.zeros((b1 - b0, MAXCH), CHAN_DTYPE)
+    for i, b in enumerate(range(b0, b1)):
+        for k in range(MAXCH):
+            blk[i, k]["carr0"] = b + k / 64
+            blk[i, k]["gain"] = b * 16 + k
+            blk[i, k]["ca_tbl"] = (b + k) % 32
+            blk[i, k]["nav_tbl"] = (b * 7 + k) % n_nav
+    nch = np.array([(b % 12) + 1 for b in range(b0, b1)], np.int32)
+    return blk, nch, nav
+
+
+@pytest.mark.parametrize("world,n_blocks,chunk", [(3, 20, 3), (4, 23, 2), (4, 3, 2)])
+def test_exchange_rows_gloo(tmp_path, world, n_blocks, chunk):
+    import numpy as np
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(REPO, "gps-sdr-sim_amd"))
+    from gpssim_amd import CHAN_DTYPE
+    from gpssim_amd.node import chunk_plan, planner_of, rank_blocks
+    mp.spawn(_exchange_worker, args=(world, _free_port(), n_blocks, chunk, str(tmp_path)),
+             nprocs=world, join=True)
+    plan = chunk_plan(n_blocks, world, chunk, "stripe")
+    for r in range(world):
+        ob = np.load(tmp_path / f"blk{r}.npy").view(CHAN_DTYPE).reshape(-1, 16)
+        on = np.load(tmp_path / f"nch{r}.npy")
+        onav = np.load(tmp_path / f"nav{r}.npy")
+        firsts = list(np.load(tmp_path / f"first{r}.npy"))
+        mine = [(c, nb) for q, c, nb in plan if q == r]
+        assert firsts == [c for c, _ in mine]
+        o = 0
+        for c, nb in mine:
+            p = planner_of(c, n_blocks, world)
+            pb0, pb1 = rank_blocks(n_blocks, p, world)
+            assert pb0 <= c and c + nb <= pb1              # a chunk never crosses a window
+            wb, wn, wnav = _rows(pb0, pb1, p)
+            got, want = ob[o:o + nb], wb[c - pb0:c - pb0 + nb]
+            for f in ("carr0", "gain", "ca_tbl"):
+                assert np.array_equal(got[f], want[f])
+            assert np.array_equal(on[o:o + nb], wn[c - pb0:c - pb0 + nb])
+            # the re-pointed nav rows are the planner's rows
+            assert np.array_equal(onav[got["nav_tbl"].reshape(-1)],
+                                  wnav[want["nav_tbl"].reshape(-1)])
+            o += nb
+        assert o == len(ob) == len(on)
+
+
+def test_planner_of():
+    sys.path.insert(0, os.path.join(REPO, "gps-sdr-sim_amd"))
+    from gpssim_amd.node import planner_of, rank_blocks
+    for n, w in [(863999, 8), (29, 3), (3, 4), (100, 7)]:
+        for b in list(range(min(n, 60))) + [n - 1]:
+            r = planner_of(b, n, w)
+            lo, hi = rank_blocks(n, r, w)
+            assert lo <= b < hi
 
 
 def test_chunk_plan_partition():
@@ -80,24 +188,37 @@ def test_chunk_plan_partition():
     assert sorted({p[0] for p in plan}) == list(range(8))
 
 
-def _node_worker(rank, world, port, out_path):
+def _node_worker(rank, world, port, out_path, backend, layout):
     sys.path.insert(0, os.path.join(REPO, "gps-sdr-sim_amd"))
+    import json
     import torch.distributed as dist
     from gpssim_amd.node import run_node
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    stats = {}
+    # nccl: one GPU per rank (a whole-node run); gloo: both ranks on GPU 0
     run_node(["-e", NAV, "-l", "30.286502,120.032669,100", "-d", "3", "-b", "16", "-o",
-              out_path], rank, world, 0, backend="gloo", chunk_blocks=5, threads=4)
+              out_path], rank, world, rank if backend == "nccl" else 0, backend=backend,
+             chunk_blocks=5, threads=4, layout=layout, stats=stats)
+    if rank == 0:
+        open(out_path + ".json", "w").write(json.dumps(stats))
     dist.destroy_process_group()
 
 
 @pytest.mark.gpu
-def test_node_run_two_ranks_one_sink(tmp_path, golden):
+@pytest.mark.parametrize("layout", ["block", "stripe"])
+def test_node_run_two_ranks_one_sink(tmp_path, golden, layout):
+    import json
     import torch.multiprocessing as mp
+    backend = os.environ.get("GSS_TEST_BACKEND", "gloo")
+    world = int(os.environ.get("GSS_TEST_WORLD", "2"))
     out = tmp_path / "gpssim.bin"
-    mp.spawn(_node_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    mp.spawn(_node_worker, args=(world, _free_port(), str(out), backend, layout), nprocs=world,
+             join=True)
     data = out.read_bytes()
     bb = 1040000
     assert len(data) == 29 * bb
     hs = [hashlib.sha256(data[i * bb:(i + 1) * bb]).hexdigest()[:16] for i in range(29)]
     assert hs == golden["static_d30_b16"]["block_sha16"][:29]
+    st = json.loads(open(str(out) + ".json").read())
+    assert st["max_peers_outstanding"] == world - 1
