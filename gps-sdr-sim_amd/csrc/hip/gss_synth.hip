@@ -20,7 +20,7 @@
  *                               SC16/SC08/SC01 packing.  Output is staged per lane in LDS
  *                               (128 B) and stored by the wave as whole 128-B lines.
  * gss_lin_kernel (the fast path, below) renders the blocks the host proof certifies: integer
- * phase lines, LDS LUT reads, and the gain x LUT sums on the matrix cores (LIN_MFMA).
+ * phase lines, LDS LUT reads, and the gain x LUT sums on the matrix cores.
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -483,36 +483,57 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
    walk.  Lanes are consecutive samples: one wave step renders 64 consecutive samples, so the LUT
    reads of a wave hit a few neighbouring cells and the output leaves as one contiguous 256-B
    (-b 16) store per step.
-   A wave renders one 4096-sample segment in chunks of LIN_CH steps.  Per chunk, the wave's
-   lanes first build every channel's parameters in parallel (lin_ct in LDS: the chunk base, the
-   step, the gain, and the 16 chip windows from vector loads of the window table); then, channel
-   by channel, each lane forms its anchor P (code in the low word, carrier in the high word,
-   gss_lin.h) with one 64-bit add of the base to its entry of the workgroup's lane table (LDS),
-   and per 64-sample step
-       t = W_s >> byte3(P.lo)  chip sign at bit 0, from the step's window       v_lshrrev_b32_sdwa
+   A workgroup of 4 waves renders 4 consecutive 4096-sample segments of one block; a wave
+   renders its segment in 4 chunks of LIN_CH = 16 steps of 64 samples.  Per chunk the wave's
+   lanes first write every channel's record in parallel (lin_ct in LDS: the chunk base, the step,
+   the gain operands, the window-table rows to load next); then, two channels at a time, each
+   lane forms its anchors P (code in the low word, carrier in the high word, gss_lin.h) with one
+   64-bit add of the chunk base to its entry of the workgroup's lane table (LDS), and per
+   64-sample step and channel
+       t = W_s >> byte3(P.lo)  chip sign at bit 0, from the step's window        v_lshrrev_b32_sdwa
        a = alignbit(t, P.hi, 21) & M   LUT byte address: cell (carrier bits 23..31) at bits
                                     2..10, chip sign at bit 11 (second half of the LUT negated)
-       acc += g * LUT[a]       packed I/Q                                       v_mad_i64_i32
-       P += D                  carrier and code together                        v_lshl_add_u64
-   5 VALU + 1 LDS per channel-sample; with LIN_MFMA (the default build) the accumulate is one
-   v_mfma_f32_4x4x4_16b_f16 per channel and two steps instead (4 VALU + 1 LDS + 1/2 MFMA).
-   Measured on the int64 build (profiles/round2/ablate_b1.log, ablate_b2.log):
-   without any memory access the kernel still takes 75-80 % of its time, and the scalar unit,
-   one per CU for four SIMDs, was the next limit once the loop lost its 64-bit code add (the
-   per-channel scalar work of a chunk, ~90 instructions, cost more than the steps' VALU).  So the
-   code is a 32-bit word beside the carrier (a carry out of the code word adds 2^-32 cycle to the
-   carrier, which the render model counts), and everything wave-uniform that used to be scalar per channel is built
-   once per chunk by the lanes in parallel.
+       e = LUT[a]              (cos, sin) as an f16 pair                          ds_read_b32
+       P += D                  carrier and code together                          v_lshl_add_u64
+   and per two steps and two channels one v_mfma_f32_16x16x32_f16 accumulates gain x (cos, sin)
+   into the four I/Q sums of the lane's two samples: 4 VALU + 1 LDS + 1/4 MFMA per
+   channel-sample.  The code is a 32-bit word beside the carrier (a carry out of the code word
+   adds 2^-32 cycle to the carrier, which the render model counts).
    Chip windows: the window of extended chip E holds the 32 chips from E on, rotated (bit e mod 32
    = sign of chip e mod 1023, 1 = negative), so that any lane whose chip e lies in [E, E + 32)
-   takes its sign with a shift by e mod 32 = byte 3 of the code word mod 32.  Lanes build them in
-   the chunk's parameter pass from the channel's sign bit-stream (table cab: one row of CAB_W words
-   per C/A table row, bit j = sign of extended chip j - 32, copied to LDS per workgroup): two LDS
-   words and two alignbits (extract the 32 bits at E, rotate by E mod 32).  Step s reads entry floor(Q_s/4), Q_s = Q_0 + s dq
-   in 1/16 chip (Q_0 1/16 below lane 0's first chip, dq = floor(64 zs / 2^46)).  The window then
-   starts at most two chips below lane 0's chip and every lane's chip of the step lies inside it
-   when 63 zs + 3 chips <= 31 (GSS_LIN_WIN_OK, checked by gss_linearize); the index is clamped to
-   the row, which a certified channel never needs. */
+   takes its sign with a shift by e mod 32 = byte 3 of the code word mod 32.  Step s of a chunk
+   whose code base has chip E uses entry [row][E][s] of the chunk window table (gss_tw16_kernel,
+   per C/A row one 64-byte row of the 16 steps' windows per start chip, 5.2 MB, rebuilt per call
+   because the sample rate sets the window advance); the window then starts at most two chips
+   below lane 0's chip and every lane's chip of the step lies inside it when 63 zs + 3 chips <= 31
+   (GSS_LIN_WIN_OK, checked by the proof, gss_lin_win16_ok).
+   The rows are loaded into SGPRs by an s_load_dwordx16 the compiler does not see, into 16
+   registers it never allocates (the kernel is limited to LIN_SW_SGPRS by amdgpu_num_sgpr; the
+   buffers s[68:83] and s[84:99] sit above that), issued one pair ahead (while the pair before
+   renders; the last pair of a chunk loads the next chunk's first); at the pair's start an
+   explicit s_waitcnt and s_mov_b64s hand the windows to ordinary SGPRs, which the chip-sign shift
+   takes directly.  Hidden from the compiler, a load in flight leaves the LDS waits counted (a
+   pending load only makes one of them wait for one more LDS read), so the LUT reads stay
+   pipelined (1.62-1.64 ms per 300 s launch against 1.76 for windows built in LDS, round 4;
+   compiler-visible scalar loads share lgkmcnt with the LUT reads and cost +16 %, round 3).
+   Accumulation on the matrix cores: channels in pairs on v_mfma_f32_16x16x32_f16.  Lane l holds
+   B[8 (l>>4) + j][l & 15] (j = 0..7) and C[4 (l>>4) + r][l & 15] (r = 0..3), so a lane's four
+   outputs depend only on its own eight B values when A row 4q + r is zero outside K columns
+   8q .. 8q+7 (tools/ubench/mfma16_probe.hip checks the map and the exact sums on gfx950).  B is
+   the lane's four LUT words -- channel a at steps s, s+1, channel b at steps s, s+1 -- and A puts
+   g_a at column 8q + r and g_b at 8q + 4 + r of row 4q + r: the lanes 20q + r hold those two
+   gains (elements r and 4 + r), every other lane zeros.  A lone last channel, and the rare
+   gain-change reruns, take one v_mfma_f32_4x4x4_16b_f16 per channel and two steps instead: lane
+   4b + i holds row i of block b's A (the gain at slot i) and lane 4b + j column j of B (its own
+   two LUT words: K = cos_s, sin_s, cos_s+1, sin_s+1) and of C (I_s, Q_s, I_s+1, Q_s+1)
+   (tools/ubench/mfma_probe.hip).
+   Exactness: the LUT values (|v| <= 250) and the doubled gains (|2 g| <= 2048, their data-bit
+   differences <= 4096 and even; the proof admits |g| <= 1024, sum |g| <= 8000) are exact f16
+   integers, products are exact in f32, and the accumulators start at 1.5 2^23 + 128, so that
+   each sum holds 2 (sum + 64), an even integer below 2^23 in magnitude: exact in any order, and
+   its IEEE bits 0x4B400000 + 2 (sum + 64) put (sum + 64) >> 7 + 2^14 in bits 8..23.  The -b 16
+   sample word is then one byte permutation of the I and Q bits and one packed 16-bit add of
+   0xC000; -b 8 takes bits 12..; -b 1 compares with 0x4B400000 + 256. */
 #define LIN_THREADS 256
 #define LIN_WAVES   (LIN_THREADS / 64)
 #define LIN_STEPS   (GSS_LIN_SEG / 64)     /* 64-sample steps per wave segment: 4096 samples    */
@@ -522,109 +543,13 @@ __global__ __launch_bounds__(SYNTH_THREADS) __attribute__((amdgpu_waves_per_eu(S
                                               reach (4160 samples * 0.46 chip) plus a window     */
 #define CAB_W       ((CBW_CHIPS + 96) / 32)    /* sign words per row: chips -32 .. CBW_CHIPS + 63 */
 static_assert(LIN_STEPS % LIN_CH == 0 && (LIN_CH & (LIN_CH - 1)) == 0, "whole chunks");
-/* LIN_ABLATE (measurement builds only, tools/ablate.sh; wrong output): 1 no output stores,
-   2 no chip-window loads, 4 no LUT reads, 8 every block stores into one of 8 blocks (L2),
-   32 no alignbit (VALU work), 64 no window reads in the render loop (LDS work), 128 the LUT
-   address without the chip sign (no bank conflicts between a cell's two signs), 256 windows
-   made by the scalar unit in SGPRs (no window pass, no LDS window reads), 512 no window pass
-   (the loop still reads the records' windows from LDS) */
-#ifndef LIN_ABLATE
-#define LIN_ABLATE 0
-#endif
-/* LIN_STAMP (diagnostic builds only, tools/clock_stamp.py; MI355X_MICROARCH.md "DVFS give-back"
-   item 6): each wave of gss_lin_kernel reads the shader-clock counter (s_memtime) and the
-   constant 100 MHz counter (s_memrealtime) once before and once after its chunk loop and lane 0
-   writes the four values with a vector store into g_lin_stamp[wave of the launch], a buffer of
-   their own that nothing else reads.  Cycles per wave and the clock the launch held
-   (cycles / ticks x 100 MHz) then come apart; the product kernel executes no stamp. */
-#ifndef LIN_STAMP
-#define LIN_STAMP 0
-#endif
-#if LIN_STAMP
-#define LIN_STAMP_WAVES (1 << 20)
-__device__ uint64_t g_lin_stamp[LIN_STAMP_WAVES][4];
-#endif
-/* Where a step's 32-chip window comes from.
-   LIN_SWIN 3 (the default, round 4): from the chunk window table (gss_lin.h, gss_tw16_kernel,
-   per C/A row and chunk start chip E one 64-byte row of the 16 steps' windows, 5.2 MB, rebuilt
-   per call).  Each channel's row is loaded by an s_load_dwordx16 the compiler does not see, into
-   16 SGPRs it never allocates (the kernel is limited to LIN_SW_SGPRS by amdgpu_num_sgpr; the
-   buffers s[68:83] and s[84:99] sit above that), issued one pair ahead (while the pair before
-   renders; the last pair of a chunk loads the next chunk's first); at the pair's start an
-   explicit s_waitcnt and s_mov_b64s hand the windows to ordinary SGPRs, which the chip-sign
-   shift takes directly.  Hidden from the compiler, a load in flight leaves the LDS waits counted
-   (a pending load only makes one of them wait for one more LDS read), so the LUT reads stay
-   pipelined.  No window pass, no broadcast window reads, no bit-streams in LDS.  Interleaved on
-   one box: 1.62-1.64 ms per 300 s launch against 1.76 for LIN_SWIN 0 (profiles/round4/).
-   LIN_SWIN 0 (rounds 2-3): the lanes build each chunk's windows from the bit-streams in LDS and
-   the loop reads them back by broadcast LDS reads.
-   LIN_SWIN 1 (measurement): the same table by compiler-visible s_loads: they share lgkmcnt with
-   the LUT reads, so each pair's load is waited for with every LDS read drained (+16 %). */
-#ifndef LIN_PUNROLL
-#define LIN_PUNROLL 1   /* 1: the channel-pair loop unrolled (immediate record offsets) */
-#endif
-#ifndef LIN_NCRE
-#define LIN_NCRE 1      /* 1: nc opaque per chunk (no hoisted, spilled channel-count masks) */
-#endif
-#ifndef LIN_ALDS
-#define LIN_ALDS 1      /* 1: the pair MFMA's gain operand read from the records (no VALU masks) */
-#endif
-#ifndef LIN_SWIN
-#if LIN_MFMA
-#define LIN_SWIN 3
-#else
-#define LIN_SWIN 0
-#endif
-#endif
-#if LIN_SWIN == 3
-#define LIN_SW_SGPRS (LIN_MFMA == 2 ? 68 : 84)     /* hidden: s[84:99], pairs also s[68:83] */
-static_assert(LIN_MFMA >= 1, "LIN_SWIN 3 accumulates on the matrix cores");
-#endif
-#if LIN_SWIN || (LIN_ABLATE & 256)
-#define LIN_WCON "s"                       /* the shift takes the window from an SGPR            */
-#else
-#define LIN_WCON "v"
-#endif
-/* LIN_MFMA 1: the gain x LUT accumulation runs on the matrix cores instead of v_mad_i64_i32.
-   The LUT holds (cos, sin) as an f16 pair (exact integers, |v| <= 250); per channel and pair of
-   steps one v_mfma_f32_4x4x4_16b_f16 takes B = the lane's two LUT words (K = cos_s, sin_s,
-   cos_s+1, sin_s+1) and A = the gain placed at slot i of lane 4b + i (f16, exact for
-   |g| <= 2048; the proof certifies |g| <= 1024 so that gain differences stay exact too), so
-   block b's column j -- lane 4b + j's own sample -- receives rows (I_s, Q_s, I_s+1, Q_s+1).
-   The f32 accumulators start at 1.5 2^23 + 64: every partial sum is an integer below 2^24 in
-   magnitude, so the matrix core's sums are exact in any order, and the IEEE bits of the result
-   are 0x4B400000 + (sum + 64), from which (sum + 64) >> 7 is a shift
-   (tools/ubench/mfma_probe.hip: operand layout and exactness on gfx950). */
-/* LIN_MFMA 2 (the default build): channels in pairs on v_mfma_f32_16x16x32_f16.  Lane l holds
-   B[8 (l>>4) + j][l & 15] (j = 0..7) and C[4 (l>>4) + r][l & 15] (r = 0..3), so a lane's four
-   outputs depend only on its own eight B values when A row 4q + r is zero outside K columns
-   8q .. 8q+7 (tools/ubench/mfma16_probe.hip checks the map and the exact sums on gfx950).  B is
-   the lane's four LUT words -- channel a at steps s, s+1, channel b at steps s, s+1 -- and A
-   puts g_a at column 8q + r and g_b at 8q + 4 + r of row 4q + r: the lanes 20q + r hold those
-   two gains (elements r and 4 + r), every other lane zeros.  One MFMA per two channels and two
-   steps instead of one per channel and two steps: the 4x4x4 MFMA holds the SIMD's vector issue
-   about 9 cycles, the 16x16x32 one about 11 (tools/ubench/mfma_issue_ubench.hip), so the
-   accumulate costs ~2.8 instead of ~4.6 issue cycles per channel-step.  A lone last channel, and
-   the rare gain-change reruns, keep the 4x4x4 form. */
-#ifndef LIN_MFMA
-#define LIN_MFMA 0
-#endif
+#define LIN_SW_SGPRS 68                    /* hidden window buffers: s[68:83] and s[84:99]       */
 typedef _Float16 lin_half4 __attribute__((ext_vector_type(4)));
 typedef _Float16 lin_half8 __attribute__((ext_vector_type(8)));
 typedef float lin_f4 __attribute__((ext_vector_type(4)));
-/* LIN_PK2 (the default with the MFMA accumulation): the gains enter the matrix cores doubled
-   (2 g, still exact f16 integers: |2 g| <= 2048, their data-bit differences |2 (g1 - g0)| <=
-   4096 and even) and the accumulators start at 1.5 2^23 + 128, so that each sum holds
-   2 (sum + 64), an even integer below 2^23 in magnitude: exact, and its IEEE bits
-   0x4B400000 + 2 (sum + 64) put (sum + 64) >> 7 + 2^14 in bits 8..23.  The -b 16 sample word is
-   then one byte permutation of the I and Q bits and one packed 16-bit add of 0xC000 (2 VALU
-   instead of 3); -b 8 takes bits 12.., -b 1 compares with 0x4B400000 + 256. */
-#ifndef LIN_PK2
-#define LIN_PK2 1
-#endif
-#define LIN_GS    (LIN_PK2 ? 2 : 1)             /* the gain scale on the matrix cores     */
-#define LIN_MAGF  (12582912.0f + 64.0f * LIN_GS)   /* 1.5 2^23 + 64 LIN_GS               */
-#define LIN_MAGB  0x4B400000u                   /* IEEE bits of 1.5 2^23                  */
+#define LIN_GS    2                        /* the gain scale on the matrix cores                 */
+#define LIN_MAGF  (12582912.0f + 64.0f * LIN_GS)   /* 1.5 2^23 + 64 LIN_GS                       */
+#define LIN_MAGB  0x4B400000u              /* IEEE bits of 1.5 2^23                              */
 
 /* per (block, segment wave, chunk, channel): the chunk's render parameters, built by the wave's
    lanes in parallel (vector loads and VALU) and read back by the render loop with broadcast LDS
@@ -633,41 +558,24 @@ typedef float lin_f4 __attribute__((ext_vector_type(4)));
 struct alignas(16) lin_ct {
     uint64_t B;                  /* the chunk's base (gss_lin.h)                                */
     uint64_t D;                  /* the 64-sample step dC : dX                                  */
-    int32_t g;                   /* signed gain at the chunk start                              */
+    int32_t g;                   /* (unused)                                                    */
     int32_t gd;                  /* gain change inside the chunk (g1 - g0), from sample pos1 on */
     int32_t pos1;
     uint32_t flags;              /* 1: a gain change inside the chunk, 2: patched samples       */
-    uint32_t q0, dq, tab;        /* first window offset (1/16 chip), its step, the row          */
-    uint32_t wa;                 /* LIN_SWIN: byte offset of the chunk's window-table row       */
-#if !LIN_SWIN
-    uint32_t W[LIN_CH];          /* the steps' chip windows (16-byte aligned: ds_read_b128)     */
-#endif
-#if LIN_ALDS
-    uint32_t na, nb;             /* (as below; first here: one 8-byte read)                      */
-    uint32_t wn;
-    uint32_t g2;
-    uint32_t A[5][2];            /* A[0..3] as below; A[4] zeros: the pair MFMA's gain operand   */
-                                 /* half of each lane is A[its class] (lin_pair_cls)            */
-#else
-#if LIN_MFMA
-    uint32_t A[4][2];            /* the MFMA gain operand of lane 4b + i: g (f16) at slot i      */
-    uint32_t g2;                 /* g as an f16 pair (both halves), the pair MFMA's gain         */
-#endif
-    uint32_t na, nb;             /* LIN_SWIN 3, pairs: the rows to load while the pair (k, k + 1)
-                                    renders -- the next pair's, the lone last channel's (twice)
-                                    or the next chunk's first pair's (lin_sw_pair)              */
-    uint32_t wn;                 /* LIN_SWIN 3: ... of the next chunk's (its first pair preloads) */
-#endif
+    uint32_t q0, dq, tab;        /* (dq, tab: the channel's window step and C/A row)            */
+    uint32_t wa;                 /* byte offset of the chunk's window-table row                 */
+    uint32_t na, nb;             /* the rows to load while the pair (k, k + 1) renders -- the
+                                    next pair's, the lone last channel's (twice) or the next
+                                    chunk's first pair's (lin_sw_pair); one 8-byte read         */
+    uint32_t wn;                 /* the next chunk's row                                        */
+    uint32_t g2;                 /* the gain as an f16 pair                                     */
+    uint32_t A[5][2];            /* A[i]: the 4x4x4 MFMA's gain operand of lane 4b + i (the gain
+                                    at f16 slot i); A[4] zeros.  The pair MFMA's operand half of
+                                    each lane is A[its class] (lin_pair_cls)                    */
 };
 /* the broadcast reads of the record assume these alignments (a misaligned ds_read_b128 is split
    by the hardware and cost the round-4 LDS-window build 3x) */
-#if !LIN_SWIN
-static_assert(offsetof(lin_ct, W) % 16 == 0 && sizeof(lin_ct) % 16 == 0,
-              "lin_ct.W: 16-byte broadcast reads");
-#endif
-#if LIN_MFMA
 static_assert(offsetof(lin_ct, A) % 8 == 0, "lin_ct.A: 8-byte reads");
-#endif
 
 /* per (block, channel): the render constants of gss_lin.h (written by gss_linseg_kernel) */
 struct lin_chan {
@@ -771,71 +679,37 @@ __global__ void gss_tw16_kernel(const uint32_t *__restrict__ cab, int n_ca, uint
     tw[i] = __builtin_amdgcn_alignbit(lin, lin, (32u - j) & 31u);
 }
 
-/* where a channel's chunk windows come from: the wave's LDS record (W = its W[]) or, with
-   LIN_SWIN, the chunk window table (W = the row of the channel's chunk, wave-uniform) */
+/* a channel's chunk windows: the row of its chunk in the chunk window table (wave-uniform) */
 struct lin_wsrc {
     const uint32_t *W;
 };
 
-/* step s's window; w4 caches four LDS windows (one broadcast read per four steps) */
-__device__ __forceinline__ uint32_t lin_wget(const lin_wsrc &w, int s, uint4 &w4, uint32_t M,
-                                             int salt)
-{
-#if LIN_SWIN
-    (void)w4; (void)M; (void)salt;
-    return w.W[s];                                  /* uniform: one s_load_dwordx16 for all 16 */
-#else
-    if (LIN_ABLATE & 256)          /* measurement: SGPR windows, no LDS window reads or pass */
-        return __builtin_amdgcn_readfirstlane(M) * (uint32_t)(s + 1 + salt);
-    if (s % 4 == 0) {                                     /* four windows per broadcast read */
-        if (LIN_ABLATE & 64)
-            w4 = make_uint4(M * (s + 1 + salt), M * (s + 3 + salt), M * (s + 5 + salt),
-                            M * (s + 7 + salt));
-        else
-            w4 = ((const uint4 *)w.W)[s / 4];
-    }
-    return s % 4 == 0 ? w4.x : s % 4 == 1 ? w4.y : s % 4 == 2 ? w4.z : w4.w;
-#endif
-}
-
-/* LIN_SWIN: all LIN_CH windows of a chunk as one scalar load, waited for before the steps (the
-   scalar and LDS loads share one counter, so a window load left in flight would turn every LUT
-   read's wait into a full drain) */
+/* all LIN_CH windows of a chunk by compiler-visible scalar loads (the rare gain-change reruns),
+   waited for before the steps (the scalar and LDS loads share one counter, so a window load left
+   in flight would turn every LUT read's wait into a full drain) */
 __device__ __forceinline__ void lin_wissue(const lin_wsrc &w, uint32_t (&ws)[LIN_CH])
 {
 #pragma unroll
-    for (int s = 0; s < LIN_CH; s++) {
-        uint4 unused;
-        ws[s] = lin_wget(w, s, unused, 0u, 0);
-    }
+    for (int s = 0; s < LIN_CH; s++)
+        ws[s] = w.W[s];                               /* uniform: one s_load_dwordx16 for all 16 */
 }
 
 /* ... and the fence that needs them all (one wait, after every load of the chunk is issued) */
 __device__ __forceinline__ void lin_wfence(const uint32_t (&ws)[LIN_CH])
 {
-#if LIN_SWIN
     static_assert(LIN_CH == 16, "the fence below names 16 windows");
     asm volatile("" :: "s"(ws[0]), "s"(ws[1]), "s"(ws[2]), "s"(ws[3]), "s"(ws[4]), "s"(ws[5]),
                  "s"(ws[6]), "s"(ws[7]), "s"(ws[8]), "s"(ws[9]), "s"(ws[10]), "s"(ws[11]),
                  "s"(ws[12]), "s"(ws[13]), "s"(ws[14]), "s"(ws[15]));
-#else
-    (void)ws;
-#endif
 }
 
 __device__ __forceinline__ lin_wsrc lin_wsrc_of(const lin_ct &t, const uint32_t *__restrict__ tw)
 {
-#if LIN_SWIN
     const uint32_t off = __builtin_amdgcn_readfirstlane(t.wa);
     return lin_wsrc{(const uint32_t *)__builtin_assume_aligned(
         (const char *)tw + off, 64)};
-#else
-    (void)tw;
-    return lin_wsrc{t.W};
-#endif
 }
 
-#if LIN_SWIN == 3
 #define LIN_SW_CLOBB "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", \
                      "s95", "s96", "s97", "s98", "s99"
 #define LIN_SW_CLOBA "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", \
@@ -897,59 +771,27 @@ __device__ __forceinline__ void lin_sw_take_a(uint32_t (&ws)[LIN_CH])        /* 
     LIN_SW_TAKE(68, w);
     lin_sw_split(w, ws);
 }
-#endif
 
-/* one channel's contribution to the chunk's LIN_CH steps: the lane's anchor P (carrier : code,
-   high : low word, gss_lin.h) and its 64-sample step D, the steps' chip windows (LDS, the same for every lane),
-   the LUT mask M, the signed gain (with LANE_GAIN: the gain difference, applied from sample
-   pos1 on) */
-#define LIN_ACC0 (64 + (1 << 21) + ((int64_t)64 << 22))   /* (0 + 64 + 2^21) + 2^22 (0 + 64) */
-
-template <bool LANE_GAIN>
-__device__ __forceinline__ void lin_channel_chunk(int64_t (&acc)[LIN_CH], uint64_t P, uint64_t D,
-                                                  lin_wsrc W, uint32_t M, int g, int pos1,
-                                                  int p0, const int32_t *__restrict__ s_lut)
-{
-    uint4 w4;
-#pragma unroll
-    for (int s = 0; s < LIN_CH; s++) {
-        const uint32_t ws = lin_wget(W, s, w4, M, 0);
-        uint32_t t;
-        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
-            "src1_sel:DWORD" : "=v"(t) : "v"((uint32_t)P), LIN_WCON(ws));             /* bit 0: sign */
-        const uint32_t a = ((LIN_ABLATE & 32) ? t : __builtin_amdgcn_alignbit(t, (uint32_t)(P >> 32), 21)) & M;
-        const int32_t e = (LIN_ABLATE & 4) ? (int32_t)a : *(const int32_t *)((const char *)s_lut + a);
-        const int gg = LANE_GAIN ? (p0 + s * 64 >= pos1 ? g : 0) : g;
-        acc[s] += (int64_t)gg * (int64_t)e;
-        P += D;
-    }
-}
-
-/* LIN_MFMA: the same steps, the accumulation on the matrix cores (one MFMA per two steps; with
-   LANE_GAIN the LUT words of samples before pos1 are zeroed and A carries the gain difference) */
+/* one channel's LIN_CH steps on one v_mfma_f32_4x4x4_16b_f16 per two steps: the lane's anchor P
+   (carrier : code, high : low word, gss_lin.h), its 64-sample step D, the steps' windows W, the
+   LUT mask M and the gain operand A (lin_gain_operand); with LANE_GAIN (a gain-change rerun) the
+   LUT words of samples before pos1 are zeroed and A carries the gain difference */
 template <bool LANE_GAIN, bool FIRST = false>
 __device__ __forceinline__ void lin_channel_chunk_m(lin_f4 (&cq)[LIN_CH / 2], lin_f4 c0, uint64_t P,
                                                     uint64_t D, lin_wsrc W, uint32_t M,
                                                     lin_half4 A, int pos1, int p0,
                                                     const int32_t *__restrict__ s_lut)
 {
-    uint4 w4;
     uint32_t e0 = 0;
-#if LIN_SWIN
     uint32_t sw[LIN_CH];
     lin_wissue(W, sw);
     lin_wfence(sw);
-#endif
 #pragma unroll
     for (int s = 0; s < LIN_CH; s++) {
-#if LIN_SWIN
         const uint32_t ws = sw[s];
-#else
-        const uint32_t ws = lin_wget(W, s, w4, M, 0);
-#endif
         uint32_t t;
         asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
-            "src1_sel:DWORD" : "=v"(t) : "v"((uint32_t)P), LIN_WCON(ws));             /* bit 0: sign */
+            "src1_sel:DWORD" : "=v"(t) : "v"((uint32_t)P), "s"(ws));                  /* bit 0: sign */
         const uint32_t a = __builtin_amdgcn_alignbit(t, (uint32_t)(P >> 32), 21) & M;
         uint32_t e = *(const uint32_t *)((const char *)s_lut + a);
         if (LANE_GAIN)
@@ -965,8 +807,8 @@ __device__ __forceinline__ void lin_channel_chunk_m(lin_f4 (&cq)[LIN_CH / 2], li
     }
 }
 
-#if LIN_SWIN == 3
-/* LIN_SWIN 3: channel k's 16 steps from windows ws (SGPRs), one 4x4x4 MFMA per two steps */
+/* the lone last channel k of a chunk: its 16 steps from windows ws (SGPRs), one 4x4x4 MFMA per
+   two steps */
 __device__ __forceinline__ void lin_sw_steps(lin_f4 (&cq)[LIN_CH / 2], const lin_ct &t, int k,
                                              int lane, const uint64_t *s_lane, uint32_t M,
                                              const int32_t *__restrict__ s_lut,
@@ -994,101 +836,14 @@ __device__ __forceinline__ void lin_sw_steps(lin_f4 (&cq)[LIN_CH / 2], const lin
     }
 }
 
-/* channel k, its windows taken from the hidden buffer (loaded while channel k - 1 rendered);
-   the next channel's row goes into the buffer while this one renders (LIN_MFMA 1) */
-__device__ __forceinline__ void lin_sw_channel(lin_f4 (&cq)[LIN_CH / 2], const lin_ct *T, int k,
-                                               int nc, int lane, const uint64_t *s_lane,
-                                               uint32_t M, const int32_t *__restrict__ s_lut,
-                                               const uint32_t *__restrict__ tw)
-{
-    const uint32_t wn = k + 1 < nc ? T[k + 1].wa : 0u;
-    uint32_t ws[LIN_CH];
-    lin_sw_take(ws);                                 /* this channel's windows */
-    if (k + 1 < nc)
-        lin_sw_load(tw, wn);                         /* the next channel's, meanwhile */
-    lin_sw_steps(cq, T[k], k, lane, s_lane, M, s_lut, ws);
-}
-
-#endif
-
-/* LIN_MFMA 2: two channels' steps, one v_mfma_f32_16x16x32_f16 per two steps (B = channel a's
-   words of steps s, s+1 and channel b's; A = the pair's gains, lin_pair_gains).  FIRST: the
-   chunk's first pair, whose MFMAs take C = the bias c0 instead of the accumulators (no
-   per-chunk initialisation) */
-template <bool FIRST>
-__device__ __forceinline__ void lin_pair_chunk(lin_f4 (&cq)[LIN_CH / 2], lin_f4 c0, uint64_t Pa, uint64_t Da,
-                                               lin_wsrc Wa, uint64_t Pb, uint64_t Db,
-                                               lin_wsrc Wb, uint32_t M, lin_half8 A,
-                                               const int32_t *__restrict__ s_lut)
-{
-    uint4 wa4, wb4;
-    uint32_t ea0 = 0, eb0 = 0;
-#if LIN_SWIN
-    uint32_t swa[LIN_CH], swb[LIN_CH];
-    lin_wissue(Wa, swa);
-    lin_wissue(Wb, swb);
-    lin_wfence(swa);
-    lin_wfence(swb);
-#endif
-#pragma unroll
-    for (int s = 0; s < LIN_CH; s++) {
-#if LIN_SWIN
-        const uint32_t wa = swa[s], wb = swb[s];
-#else
-        const uint32_t wa = lin_wget(Wa, s, wa4, M, 0);
-        const uint32_t wb = lin_wget(Wb, s, wb4, M, 1);
-#endif
-        uint32_t ta, tb;
-        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
-            "src1_sel:DWORD" : "=v"(ta) : "v"((uint32_t)Pa), LIN_WCON(wa));
-        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 "
-            "src1_sel:DWORD" : "=v"(tb) : "v"((uint32_t)Pb), LIN_WCON(wb));
-        const uint32_t aa = __builtin_amdgcn_alignbit(ta, (uint32_t)(Pa >> 32), 21) & M;
-        const uint32_t ab = __builtin_amdgcn_alignbit(tb, (uint32_t)(Pb >> 32), 21) & M;
-        const uint32_t ea = *(const uint32_t *)((const char *)s_lut + aa);
-        const uint32_t eb = *(const uint32_t *)((const char *)s_lut + ab);
-        if (s & 1) {
-            const uint4 bb = make_uint4(ea0, ea, eb0, eb);
-            cq[s / 2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, __builtin_bit_cast(lin_half8, bb),
-                                                              FIRST ? c0 : cq[s / 2], 0, 0, 0);
-        } else {
-            ea0 = ea;
-            eb0 = eb;
-        }
-        Pa += Da;
-        Pb += Db;
-    }
-}
-
-/* the pair MFMA's A operand: lanes 20q + r (q, r = 0..3) hold g_a at element r and g_b at 4 + r,
-   every other lane zeros; sel0 / sel1 (per lane, from lin_pair_sel) mask the f16 half of
-   elements 0..3 (dword 0, 1) that is this lane's element r */
-__device__ __forceinline__ lin_half8 lin_pair_gains(uint32_t ga2, uint32_t gb2, uint32_t sel0,
-                                                    uint32_t sel1)
-{
-    const uint4 v = make_uint4(ga2 & sel0, ga2 & sel1, gb2 & sel0, gb2 & sel1);
-    return __builtin_bit_cast(lin_half8, v);
-}
-
-/* LIN_ALDS: the lane's row of lin_ct.A for the pair operand: r = lane mod 4 on lanes 20q + r,
-   4 (zeros) elsewhere (the same placement as lin_pair_sel's masks) */
+/* the lane's row of lin_ct.A for the pair MFMA's gain operand: r = lane mod 4 on lanes 20q + r
+   (q, r = 0..3), which hold g_a at element r and g_b at 4 + r; 4 (zeros) elsewhere */
 __device__ __forceinline__ uint32_t lin_pair_cls(int lane)
 {
     const int q = lane >> 4, r = lane & 3;
     return ((lane & 15) >> 2) == q ? (uint32_t)r : 4u;
 }
 
-__device__ __forceinline__ void lin_pair_sel(int lane, uint32_t &sel0, uint32_t &sel1)
-{
-    const int q = lane >> 4, r = lane & 3;
-    const bool act = ((lane & 15) >> 2) == q;
-    const uint32_t half = (r & 1) ? 0xFFFF0000u : 0x0000FFFFu;
-    sel0 = act && r < 2 ? half : 0u;
-    sel1 = act && r >= 2 ? half : 0u;
-}
-
-#if LIN_SWIN == 3
-#if LIN_MFMA == 2
 /* channels k0, k0 + 1 from the hidden buffers s[68:83], s[84:99] (loaded while the pair before
    rendered); the next pair's rows (or the lone last channel's) load meanwhile.  FIRST: the
    chunk's first pair, whose MFMAs take the bias c0 as C (no initialisation moves) */
@@ -1096,19 +851,14 @@ template <bool FIRST>
 __device__ __forceinline__ void lin_sw_pair(lin_f4 (&cq)[LIN_CH / 2], lin_f4 c0, const lin_ct *T, int k0,
                                             int nc, int lane, const uint64_t *s_lane, uint32_t M,
                                             const int32_t *__restrict__ s_lut,
-                                            const uint32_t *__restrict__ tw, uint32_t psel0,
-                                            uint32_t psel1, bool more)
+                                            const uint32_t *__restrict__ tw, uint32_t cls,
+                                            bool more)
 {
     const lin_ct &ta = T[k0], &tb = T[k0 + 1];
     uint64_t Pa = s_lane[k0 * 64 + lane] + ta.B, Pb = s_lane[(k0 + 1) * 64 + lane] + tb.B;
     const uint64_t Da = ta.D, Db = tb.D;
-#if LIN_ALDS
-    const uint2 ga = *(const uint2 *)ta.A[psel0], gb = *(const uint2 *)tb.A[psel0];
+    const uint2 ga = *(const uint2 *)ta.A[cls], gb = *(const uint2 *)tb.A[cls];
     const lin_half8 A = __builtin_bit_cast(lin_half8, make_uint4(ga.x, ga.y, gb.x, gb.y));
-    (void)psel1;
-#else
-    const lin_half8 A = lin_pair_gains(ta.g2, tb.g2, psel0, psel1);
-#endif
     /* the rows to load while this pair renders (the record's na, nb): the next pair's (or the
        lone last channel's), or after the last pair the next chunk's first pair (more: there is a
        next chunk) */
@@ -1143,8 +893,6 @@ __device__ __forceinline__ void lin_sw_pair(lin_f4 (&cq)[LIN_CH / 2], lin_f4 c0,
         Pb += Db;
     }
 }
-#endif
-#endif
 
 /* the MFMA gain operand of this lane (g at slot lane mod 4, f16 bits gh) */
 __device__ __forceinline__ lin_half4 lin_gain_operand(uint32_t gh, int lane)
@@ -1160,68 +908,19 @@ __device__ __forceinline__ uint32_t lin_f16_bits(int g)
 }
 
 /* output stores: the stream is written once and never read back by this kernel, while each
-   XCD's L2 must keep the chip-window table warm.  LIN_STORE_POLICY: 0 plain,
-   1 nt, 2 sc1 (drops the line from L2), 3 sc0 sc1 */
-#ifndef LIN_STORE_POLICY
-#define LIN_STORE_POLICY 1
-#endif
+   XCD's L2 must keep the chip-window table warm: non-temporal */
 __device__ __forceinline__ void lin_put(uint32_t *p, uint32_t v)
 {
-    if (LIN_STORE_POLICY == 1)
-        __builtin_nontemporal_store(v, p);
-    else if (LIN_STORE_POLICY == 2)
-        asm volatile("global_store_dword %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
-    else if (LIN_STORE_POLICY == 3)
-        asm volatile("global_store_dword %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
-    else
-        *p = v;
+    __builtin_nontemporal_store(v, p);
 }
 
-#if LIN_STORE_POLICY == 1
-#define LIN_ST_MOD "nt"
-#elif LIN_STORE_POLICY == 2
-#define LIN_ST_MOD "sc1"
-#elif LIN_STORE_POLICY == 3
-#define LIN_ST_MOD "sc0 sc1"
-#else
-#define LIN_ST_MOD ""
-#endif
-#ifndef LIN_SADDR
-#define LIN_SADDR 1
-#endif
 /* v_writelane_b32: a wave-uniform value into one lane (no clang builtin in this toolchain) */
 extern "C" __device__ int gss_writelane(int, int, int) __asm("llvm.amdgcn.writelane.i32");
 
-/* Per step s of a chunk, from either accumulator: the -b 16 sample word (I16 | Q16 << 16), the
-   -b 8 halfword (I8 | Q8 << 8) and the -b 1 signs (I16 > 0, Q16 > 0), gpssim.c:2257-2287.
-   Packed int64: acc = (sum I + 64 + 2^21) + 2^22 (sum Q + 64); the 2^21 bias keeps the I field
-   non-negative, so (sum Q + 64) >> 7 is bits 29.. of acc and (sum I + 64) >> 7 is the 15-bit
-   field at bit 7 with its top bit flipped.
-   MFMA f32 (LIN_MFMA): the IEEE bits of 1.5 2^23 + (sum + 64) are 0x4B400000 + (sum + 64), so
-   (sum + 64) >> n is the word shifted by n, offset by 0x4B400000 >> n (whose low 16 bits are
-   0x8000 for n = 7 and whose low byte is 0 for n = 11). */
-__device__ __forceinline__ uint32_t lin_w16(const int64_t (&acc)[LIN_CH], int s)
-{
-    const uint32_t lo = (uint32_t)acc[s], hi = (uint32_t)(acc[s] >> 32);
-    const int i16 = __builtin_amdgcn_sbfe((int)(lo ^ (1u << 21)), 7, 15);
-    const uint32_t q16 = __builtin_amdgcn_alignbit(hi, lo, 29);
-    return __builtin_amdgcn_perm(q16, (uint32_t)i16, 0x05040100u);
-}
-__device__ __forceinline__ uint32_t lin_w8(const int64_t (&acc)[LIN_CH], int s)
-{
-    const uint32_t lo = (uint32_t)acc[s], hi = (uint32_t)(acc[s] >> 32);
-    const int i8 = __builtin_amdgcn_sbfe((int)(lo ^ (1u << 21)), 11, 11);
-    const uint32_t q8 = (uint32_t)((int)hi >> 1);
-    return __builtin_amdgcn_perm(q8, (uint32_t)i8, 0x0c0c0400u);
-}
-__device__ __forceinline__ bool lin_ipos(const int64_t (&acc)[LIN_CH], int s)
-{
-    return ((uint32_t)acc[s] & 0x3FFFFFu) >= (1u << 21) + 128u;
-}
-__device__ __forceinline__ bool lin_qpos(const int64_t (&acc)[LIN_CH], int s)
-{
-    return acc[s] >= ((int64_t)1 << 29);
-}
+/* Per step s of a chunk, from the accumulators: the -b 16 sample word (I16 | Q16 << 16), the
+   -b 8 halfword (I8 | Q8 << 8) and the -b 1 signs (I16 > 0, Q16 > 0), gpssim.c:2257-2287.  The
+   IEEE bits of 1.5 2^23 + 2 (sum + 64) are 0x4B400000 + 2 (sum + 64), so (sum + 64) >> n is the
+   word shifted by n + 1, offset by 0x4B400000 >> (n + 1). */
 __device__ __forceinline__ uint32_t lin_ib(const lin_f4 (&cq)[LIN_CH / 2], int s)
 {
     return __float_as_uint(cq[s / 2][2 * (s & 1)]);
@@ -1230,27 +929,20 @@ __device__ __forceinline__ uint32_t lin_qb(const lin_f4 (&cq)[LIN_CH / 2], int s
 {
     return __float_as_uint(cq[s / 2][2 * (s & 1) + 1]);
 }
-/* the Q half (byte) is shifted straight into place by an SDWA shift that preserves the rest of
-   the destination: two shifts, no perm */
 __device__ __forceinline__ uint32_t lin_w16(const lin_f4 (&cq)[LIN_CH / 2], int s)
 {
-#if LIN_PK2
     /* bytes 1, 2 of the I bits (low half) and of the Q bits (high half): 2^14 + (sum + 64) >> 7
        each, then + 0xC000 per half = (sum + 64) >> 7 mod 2^16 */
     const uint32_t pq = __builtin_amdgcn_perm(lin_qb(cq, s), lin_ib(cq, s), 0x06050201u);
     uint32_t r;
     asm("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(pq), "s"(0xC000C000u));
     return r;
-#else
-    uint32_t d = lin_ib(cq, s) >> 7;
-    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "
-        "src1_sel:DWORD" : "+v"(d) : "v"(7u), "v"(lin_qb(cq, s)));
-    return d ^ 0x80008000u;
-#endif
 }
 __device__ __forceinline__ uint32_t lin_w8(const lin_f4 (&cq)[LIN_CH / 2], int s)
 {
-    constexpr uint32_t sh = LIN_PK2 ? 12u : 11u;
+    /* the Q byte is shifted straight into place by an SDWA shift that preserves the rest of the
+       destination: two shifts, no perm */
+    constexpr uint32_t sh = 12u;
     uint32_t d = lin_ib(cq, s) >> sh;                 /* bytes 2, 3: not stored */
     asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "
         "src1_sel:DWORD" : "+v"(d) : "v"(sh), "v"(lin_qb(cq, s)));
@@ -1265,8 +957,8 @@ __device__ __forceinline__ bool lin_qpos(const lin_f4 (&cq)[LIN_CH / 2], int s)
     return lin_qb(cq, s) >= LIN_MAGB + 128u * LIN_GS;
 }
 
-template <int FMT, bool TAIL, class ACC>
-__device__ __forceinline__ void lin_store(const ACC &acc, uint8_t *__restrict__ ob,
+template <int FMT, bool TAIL>
+__device__ __forceinline__ void lin_store(const lin_f4 (&acc)[LIN_CH / 2], uint8_t *__restrict__ ob,
                                           int nb0, int lane, int n_per_blk)
 {
     /* the -b 1 epilogue hands lane 4 s + j the 16 samples 64 s + 16 j .. + 15: 4 LIN_CH lanes */
@@ -1283,7 +975,7 @@ __device__ __forceinline__ void lin_store(const ACC &acc, uint8_t *__restrict__ 
             pk[s] = lin_w16(acc, s);
         } else if (FMT == 8) {                            /* iq_buff >> 4 → signed char */
             const uint32_t v = lin_w8(acc, s);
-            if (!TAIL && LIN_SADDR)               /* SGPR base, 32-bit lane offset, as -b 16 */
+            if (!TAIL)                            /* SGPR base, 32-bit lane offset, as -b 16 */
                 asm volatile("global_store_short %0, %1, %2 offset:%3"
                              : : "v"((uint32_t)lane * 2u), "v"(v),
                                "s"((uint16_t *)ob + nb0 + (s >> 4) * 2048), "i"((s & 15) * 128)
@@ -1291,8 +983,8 @@ __device__ __forceinline__ void lin_store(const ACC &acc, uint8_t *__restrict__ 
             else if (in)
                 ((uint16_t *)ob)[p] = (uint16_t)v;
         } else {                                          /* {I0 Q0 I1 Q1 ...} MSB first */
-            /* I16 > 0 <=> sum I + 64 >= 128 <=> the I field (low 22 bits) >= 2^21 + 128;
-               Q16 > 0 <=> acc >= 2^29 (gpssim.c:2266-2276: bit = iq_buff[] > 0) */
+            /* I16 > 0 <=> sum I + 64 >= 128 <=> the I word >= 0x4B400000 + 256, the same for
+               Q (gpssim.c:2266-2276: bit = iq_buff[] > 0) */
             const uint64_t mi = __builtin_amdgcn_ballot_w64(lin_ipos(acc, s));
             const uint64_t mq = __builtin_amdgcn_ballot_w64(lin_qpos(acc, s));
             /* lane 4s + j collects the I (low half) and Q (high half) sign bits of samples
@@ -1331,13 +1023,13 @@ __device__ __forceinline__ void lin_store(const ACC &acc, uint8_t *__restrict__ 
     }
     if (FMT == 16) {
         __builtin_amdgcn_sched_barrier(0);
-        if (!TAIL && LIN_SADDR) {
+        if (!TAIL) {
             /* uniform base in SGPRs, 32-bit lane offset: no 64-bit address VGPRs per store */
             uint32_t *base = (uint32_t *)ob + nb0;
             const uint32_t off = (uint32_t)lane * 4u;
 #pragma unroll
             for (int s = 0; s < LIN_CH; s++)
-                asm volatile("global_store_dword %0, %1, %2 offset:%3 " LIN_ST_MOD  /* 13-bit offset */
+                asm volatile("global_store_dword %0, %1, %2 offset:%3 nt"  /* 13-bit offset */
                              : : "v"(off), "v"(pk[s]), "s"(base + (s >> 4) * 1024),
                                "i"((s & 15) * 256) : "memory");
         } else {
@@ -1352,27 +1044,8 @@ __device__ __forceinline__ void lin_store(const ACC &acc, uint8_t *__restrict__ 
 }
 
 /* The chunk holds samples where the render arithmetic does not give the exact term (gss_lin_t
-   ppos/pdelta, rare): add the correction to that lane and step. */
-__device__ __forceinline__ void lin_patch_fix(int64_t (&acc)[LIN_CH],
-                                              const gss_lin_t *__restrict__ Lk, int nb0, int lane)
-{
-    for (int j = 0; j < GSS_NPATCH; j++) {
-        const int pp = Lk->ppos[j];                   /* ascending, unused = INT32_MAX */
-        if (pp >= nb0 + 64 * LIN_CH)
-            break;
-        if (pp < nb0)
-            continue;
-        const int q = pp - nb0;
-        const int64_t add = lane == (q & 63) ? Lk->pdelta[j] : 0;
-        const int sq = q >> 6;
-#pragma unroll
-        for (int s = 0; s < LIN_CH; s++)
-            acc[s] += add & -(int64_t)(s == sq);
-    }
-}
-
-/* ... the same on the MFMA accumulators: the packed delta dI + 2^22 dQ split into its two exact
-   integers, added in f32 (exact: integers below 2^24) */
+   ppos/pdelta, rare): add the correction to that lane and step, the packed delta dI + 2^22 dQ
+   split into its two exact integers and added in f32 (exact: integers below 2^24) */
 __device__ __forceinline__ void lin_patch_fix(lin_f4 (&cq)[LIN_CH / 2],
                                               const gss_lin_t *__restrict__ Lk, int nb0, int lane)
 {
@@ -1399,33 +1072,21 @@ __device__ __forceinline__ void lin_patch_fix(lin_f4 (&cq)[LIN_CH / 2],
 }
 
 
+/* workgroups per CU the register budget aims at: the window loads pipeline deeper at 5-6 waves
+   per SIMD (8 would spill; 3, 4 and 5 measured the same, round 4) */
+#define LIN_MINB 4
 template <int FMT>
-#ifndef LIN_MINB                           /* workgroups per CU the register budget aims at:   */
-#define LIN_MINB (LIN_SWIN == 3 ? 4 : 8)   /* with SGPR windows the loads pipeline deeper at 5-6
-                                              waves per SIMD (8 would spill)                   */
-#endif
-#if LIN_SWIN == 3
-#define LIN_KATTR __attribute__((amdgpu_num_sgpr(LIN_SW_SGPRS)))
-#else
-#define LIN_KATTR
-#endif
-__global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kernel(
+__global__ __launch_bounds__(LIN_THREADS, LIN_MINB) __attribute__((amdgpu_num_sgpr(LIN_SW_SGPRS)))
+void gss_lin_kernel(
     const gss_lin_t *__restrict__ lin, const lin_seg *__restrict__ segs,
     const lin_chan *__restrict__ chans, const int32_t *__restrict__ nch,
     const int32_t *__restrict__ fast, const uint32_t *__restrict__ cab,
     const uint32_t *__restrict__ tw, lut_arg lut, int n_per_blk, int nseg, int wg_per_blk,
     uint8_t *__restrict__ out, size_t block_bytes)
 {
-    __shared__ int32_t s_lut[1024];                       /* cos + 2^22 sin; [512+i] = -[i] */
+    __shared__ int32_t s_lut[1024];                       /* (cos, sin) f16; [512+i] = -[i] */
     __shared__ uint64_t s_lane[GSS_MAXCH * 64];           /* lane offsets L(l) per channel    */
     __shared__ lin_ct s_ct[LIN_WAVES][GSS_MAXCH];         /* the current chunk, per wave      */
-#if !LIN_SWIN
-    __shared__ uint32_t s_cab[GSS_MAXCH][CAB_W];          /* the channels' sign bit-streams   */
-#endif
-#ifdef LIN_LDS_PAD                                        /* occupancy measurements only      */
-    __shared__ uint32_t s_pad[LIN_LDS_PAD];
-    if (threadIdx.x == 1023) s_pad[blockIdx.x % LIN_LDS_PAD] = 0;
-#endif
     const int b = blockIdx.x / wg_per_blk;
     const int w = blockIdx.x - b * wg_per_blk;
     if (!fast[b])
@@ -1433,41 +1094,21 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);    /* wave-uniform: scalar */
     for (int i = tid; i < 512; i += LIN_THREADS) {
-        if (LIN_MFMA) {                                   /* (cos, sin) f16; [512+i] negated */
-            const uint32_t v = lin_f16_bits(lut.cos512[i]) | (lin_f16_bits(lut.sin512[i]) << 16);
-            s_lut[i] = (int32_t)v;
-            s_lut[512 + i] = (int32_t)(v ^ 0x80008000u);
-        } else {
-            const int32_t v = (int32_t)lut.cos512[i] + (int32_t)lut.sin512[i] * (1 << 22);
-            s_lut[i] = v;
-            s_lut[512 + i] = -v;
-        }
+        const uint32_t v = lin_f16_bits(lut.cos512[i]) | (lin_f16_bits(lut.sin512[i]) << 16);
+        s_lut[i] = (int32_t)v;
+        s_lut[512 + i] = (int32_t)(v ^ 0x80008000u);
     }
     const lin_chan *CH = chans + (size_t)b * GSS_MAXCH;
     const int nc = nch[b];
     for (int i = tid; i < nc * 64; i += LIN_THREADS)
         s_lane[i] = gss_lin_lane(CH[i >> 6].xs, CH[i >> 6].zs, (uint32_t)(i & 63));
-#if LIN_SWIN
     (void)cab;
-#else
-    (void)tw;
-    for (int i = tid; i < nc * CAB_W; i += LIN_THREADS)
-        s_cab[i / CAB_W][i % CAB_W] = cab[(size_t)CH[i / CAB_W].tab * CAB_W + i % CAB_W];
-#endif
     __syncthreads();
-    uint32_t M = (LIN_ABLATE & 128) ? 0x7FCu : 0xFFCu;   /* LUT address mask, in a VGPR */
+    uint32_t M = 0xFFCu;                                  /* LUT address mask, in a VGPR */
     asm volatile("" : "+v"(M));
-#if LIN_MFMA == 2
-    uint32_t psel0, psel1;                                /* the pair MFMA's A-operand masks */
-    lin_pair_sel(lane, psel0, psel1);
-#if LIN_ALDS
-    psel0 = lin_pair_cls(lane);                           /* ... or the lane's class */
-#endif
-#endif
-#if LIN_MFMA
+    const uint32_t cls = lin_pair_cls(lane);              /* the pair MFMA's gain operand row */
     lin_f4 c0 = lin_f4{LIN_MAGF, LIN_MAGF, LIN_MAGF, LIN_MAGF};   /* the accumulators' bias */
     asm volatile("" : "+v"(c0));
-#endif
     const int sg = w * LIN_WAVES + wave;
     const int n0 = sg * (64 * LIN_STEPS);
     if (n0 >= n_per_blk)
@@ -1475,21 +1116,14 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
     const gss_lin_t *L = lin + (size_t)b * GSS_MAXCH;
     const lin_seg *S = segs + (size_t)b * GSS_MAXCH * nseg + sg;
     lin_ct *T = s_ct[wave];
-    uint8_t *ob = out + ((LIN_ABLATE & 8) ? (size_t)(b & 7) : (size_t)b) * block_bytes;
-#if LIN_STAMP
-    const uint64_t st_t0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
-#if LIN_SWIN == 3
+    uint8_t *ob = out + (size_t)b * block_bytes;
     bool sw_ahead = false;                 /* the chunk's first pair is already loading */
-#endif
     /* ---- lane k: channel k's rows, the same for every chunk of the wave: loaded once, the
        record's constant fields written once, the lines advanced by one chunk per chunk ---- */
     uint64_t xb = 0, zb = 0, xs10 = 0, zs10 = 0;       /* chunk bases, per-chunk advances     */
     int32_t pos1 = INT32_MAX;
     uint32_t pflag = 0, gh0 = 0, gh1 = 0;
-#if LIN_SWIN
     uint32_t trow = 0, wa_next = 0;                    /* table row base, this chunk's row     */
-#endif
     int g_after = -1;                                  /* the gain the record holds (none yet) */
     if (lane < nc) {
         const lin_chan ck = CH[lane];
@@ -1502,42 +1136,30 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
         pos1 = sk.pos1;
         pflag = sk.npatch != 0 ? 2u : 0u;
         const int g0 = (int)(int16_t)(sk.g01 & 0xFFFF), g1 = sk.g01 >> 16;
-        gh0 = (uint32_t)g0;
-        gh1 = (uint32_t)g1;
-#if LIN_MFMA
         gh0 = lin_f16_bits(g0 * LIN_GS);
         gh1 = lin_f16_bits(g1 * LIN_GS);
-#endif
         lin_ct &t = T[lane];
         t.D = ck.d;
         t.gd = g1 - g0;
         t.pos1 = sk.pos1;
         t.dq = ck.dq;
         t.tab = ck.tab;
-#if LIN_ALDS
         t.A[4][0] = 0;
         t.A[4][1] = 0;
-#endif
-#if LIN_SWIN
         /* a chunk's row of the window table: its C/A row and code base chip E (clamped to the
            table; gss_lin_win16_ok keeps a certified channel inside it) */
         trow = ck.tab * GSS_LIN_TWE;
         wa_next = (trow + min((uint32_t)(zb >> 50), (uint32_t)(GSS_LIN_TWE - 1))) *
                   (uint32_t)(LIN_CH * sizeof(uint32_t));
-#endif
     }
 
     const int nc_blk = nc;
     for (int c = 0; c < LIN_STEPS / LIN_CH; c++) {
-#if LIN_NCRE
         /* the channel count made opaque per chunk: its conditions (nc > 1, lane + 2 < nc, ...)
            are recomputed by the scalar unit and one compare each, instead of being hoisted out
            of the loop, spilled to VGPR lanes and read back with 12 v_readlane per chunk */
         int nc = nc_blk;
         asm volatile("" : "+s"(nc));
-#else
-        const int nc = nc_blk;
-#endif
         const int nb0 = n0 + c * (64 * LIN_CH);           /* first sample of the chunk */
         if (nb0 >= n_per_blk)
             break;
@@ -1548,44 +1170,30 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
         const bool chg = pos1 < nb0 + 64 * LIN_CH;         /* ... or changes inside it      */
         const uint32_t my_flags = (chg && !after ? 1u : 0u) | pflag;
         const uint64_t zn = zb + zs10;                     /* the next chunk's code base */
-#if LIN_SWIN
         const uint32_t my_wa = wa_next;
         const uint32_t my_wn = (trow + min((uint32_t)(zn >> 50), (uint32_t)(GSS_LIN_TWE - 1))) *
                                (uint32_t)(LIN_CH * sizeof(uint32_t));
-#endif
         if (lane < nc) {
             lin_ct &t = T[lane];
             /* the chunk's base B (gss_lin.h): the segment's lines plus c chunks */
             t.B = (xb & ~0xFFFFFFFFull) | (uint32_t)(zb >> GSS_LIN_CSH);
             t.flags = my_flags;
-#if !LIN_SWIN
-            /* 1/16 chip below lane 0's first chip, plus CBW_PRE chips */
-            t.q0 = (uint32_t)(zb >> 46) + (16 * CBW_PRE - 1);
-#else
             t.wa = my_wa;
             t.wn = my_wn;
-#endif
             if ((int)after != g_after) {                   /* the gain the chunk starts with */
                 g_after = (int)after;
                 const uint32_t gh = after ? gh1 : gh0;
-#if LIN_MFMA
                 t.A[0][0] = gh;         t.A[0][1] = 0;     /* lane 4b + i's gain operand */
                 t.A[1][0] = gh << 16;   t.A[1][1] = 0;
                 t.A[2][0] = 0;          t.A[2][1] = gh;
                 t.A[3][0] = 0;          t.A[3][1] = gh << 16;
                 t.g2 = gh | (gh << 16);
-#else
-                t.g = (int32_t)gh;
-#endif
             }
         }
-#if LIN_SWIN
         wa_next = my_wn;
-#endif
         xb += xs10;
         zb = zn;
         /* the channels with a gain change or patches in this chunk (wave-uniform) */
-#if LIN_SWIN == 3 && LIN_MFMA == 2
         /* the first two channels' rows of this chunk and the next (scalar: readlane) */
         const uint32_t wa0 = (uint32_t)__builtin_amdgcn_readlane((int)my_wa, 0);
         const uint32_t wa1r = (uint32_t)__builtin_amdgcn_readlane((int)my_wa, 1);
@@ -1607,43 +1215,16 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
                 T[lane].nb = in3 ? wa3 : in2 ? wa2 : wn1;
             }
         }
-#endif
         const uint64_t fmask = __builtin_amdgcn_ballot_w64(my_flags != 0);
         wave_sync_lds();
-#if !LIN_SWIN && !(LIN_ABLATE & (256 | 512))
-        /* ---- the chip windows, lane (k, s) ---- */
-        for (int i = lane; i < nc * LIN_CH; i += 64) {
-            const int k = i / LIN_CH;
-            const lin_ct &t = T[k];
-            /* the window's first extended chip E (1/16 chip offsets, CBW_PRE chips below 0) and
-               its bit in the row, j = E + 32 */
-            const uint32_t j = min(((t.q0 + (uint32_t)(i % LIN_CH) * t.dq) >> 4) + (32 - CBW_PRE),
-                                   (uint32_t)(32 * CAB_W - 64));
-            uint32_t wv;
-            if (LIN_ABLATE & 2) {
-                wv = j * 0x9E3779B9u;
-            } else {
-                const uint32_t lin = __builtin_amdgcn_alignbit(s_cab[k][(j >> 5) + 1],
-                                                              s_cab[k][j >> 5], j & 31);
-                wv = __builtin_amdgcn_alignbit(lin, lin, (32u - j) & 31u);   /* rotl by E mod 32 */
-            }
-            T[k].W[i % LIN_CH] = wv;
-        }
-        wave_sync_lds();
-#endif
-#if LIN_MFMA
         lin_f4 acc[LIN_CH / 2];
-#ifndef LIN_C0
-#define LIN_C0 1        /* the first channel (pair)'s MFMAs take the bias as C, no init moves */
-#endif
-#if LIN_MFMA == 2 && LIN_SWIN == 3
         /* the first pair's rows: loaded during the chunk before, or now */
         if (nc > 0 && !sw_ahead)
             lin_sw_load2(tw, wa0, wa1);
         const bool more = c + 1 < LIN_STEPS / LIN_CH && nb0 + 64 * LIN_CH < n_per_blk;
         int k0 = 0;
         if (nc >= 2) {                                    /* the first pair sets acc = bias + ... */
-            lin_sw_pair<true>(acc, c0, T, 0, nc, lane, s_lane, M, s_lut, tw, psel0, psel1, more);
+            lin_sw_pair<true>(acc, c0, T, 0, nc, lane, s_lane, M, s_lut, tw, cls, more);
             k0 = 2;
         } else {
             /* (the copies pinned inside this branch: hoisted, they cost 32 moves every chunk) */
@@ -1654,20 +1235,14 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
                 acc[s] = v;
             }
         }
-#if LIN_PUNROLL
         /* unrolled: each pair's record and lane-table addresses are immediate offsets */
 #pragma unroll
         for (int p = 1; p < GSS_MAXCH / 2; p++) {
             if (2 * p + 1 >= nc)
                 break;
-            lin_sw_pair<false>(acc, c0, T, 2 * p, nc, lane, s_lane, M, s_lut, tw, psel0, psel1,
-                               more);
+            lin_sw_pair<false>(acc, c0, T, 2 * p, nc, lane, s_lane, M, s_lut, tw, cls, more);
             k0 = 2 * p + 2;
         }
-#else
-        for (; k0 + 1 < nc; k0 += 2)                      /* uniform loop over channel pairs */
-            lin_sw_pair<false>(acc, c0, T, k0, nc, lane, s_lane, M, s_lut, tw, psel0, psel1, more);
-#endif
         if (k0 < nc) {                                    /* the lone last channel: s[68:83] */
             uint32_t ws[LIN_CH], wb[LIN_CH];
             lin_sw_take_a(ws);
@@ -1679,51 +1254,7 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
             k0 = nc;
         }
         sw_ahead = nc > 0 && more;
-#elif LIN_MFMA == 2
-        int k0 = 0;
-        if (LIN_C0 && nc >= 2) {                          /* the first pair sets acc = bias + ... */
-            const lin_ct &ta = T[0], &tb = T[1];
-            lin_pair_chunk<true>(acc, c0, s_lane[lane] + ta.B, ta.D, lin_wsrc_of(ta, tw),
-                                 s_lane[64 + lane] + tb.B, tb.D, lin_wsrc_of(tb, tw), M,
-                                 lin_pair_gains(ta.g2, tb.g2, psel0, psel1), s_lut);
-            k0 = 2;
-        } else {
-#pragma unroll
-            for (int s = 0; s < LIN_CH / 2; s++)
-                acc[s] = c0;
-        }
-        for (; k0 + 1 < nc; k0 += 2) {                    /* uniform loop over channel pairs */
-            const lin_ct &ta = T[k0], &tb = T[k0 + 1];
-            lin_pair_chunk<false>(acc, c0, s_lane[k0 * 64 + lane] + ta.B, ta.D,
-                                  lin_wsrc_of(ta, tw), s_lane[(k0 + 1) * 64 + lane] + tb.B, tb.D,
-                                  lin_wsrc_of(tb, tw), M,
-                                  lin_pair_gains(ta.g2, tb.g2, psel0, psel1), s_lut);
-        }
-#elif LIN_SWIN == 3
-#pragma unroll
-        for (int s = 0; s < LIN_CH / 2; s++)
-            acc[s] = c0;
-        if (nc > 0)
-            lin_sw_load(tw, T[0].wa);
-        for (int k = 0; k < nc; k++)                      /* uniform channel loop */
-            lin_sw_channel(acc, T, k, nc, lane, s_lane, M, s_lut, tw);
-        const int k0 = nc;
-#else
-        int k0 = 0;
-        if (LIN_C0 && nc >= 1) {                          /* the first channel sets acc = bias + ... */
-            const lin_ct &t = T[0];
-            const uint2 a2 = *(const uint2 *)t.A[lane & 3];
-            lin_channel_chunk_m<false, true>(acc, c0, s_lane[lane] + t.B, t.D, lin_wsrc_of(t, tw), M,
-                                             __builtin_bit_cast(lin_half4, a2), 0, 0, s_lut);
-            k0 = 1;
-        } else {
-#pragma unroll
-            for (int s = 0; s < LIN_CH / 2; s++)
-                acc[s] = c0;
-        }
-#endif
-        for (int k = k0; k < nc; k++) {                   /* uniform channel loop (mode 1), or
-                                                             the lone last channel (mode 2) */
+        for (int k = k0; k < nc; k++) {                   /* (none left: k0 == nc) */
             const lin_ct &t = T[k];
             const uint64_t B = t.B, D = t.D;
             const uint2 a2 = *(const uint2 *)t.A[lane & 3];
@@ -1746,68 +1277,14 @@ __global__ __launch_bounds__(LIN_THREADS, LIN_MINB) LIN_KATTR void gss_lin_kerne
             if (__builtin_expect(fl & 2u, 0))
                 lin_patch_fix(acc, L + k, nb0, lane);
         }
-#else
-        int64_t acc[LIN_CH];
-#pragma unroll
-        for (int s = 0; s < LIN_CH; s++) {
-            acc[s] = LIN_ACC0;
-            asm volatile("" : "+v"(acc[s]));              /* one move each, no copies */
-        }
-        for (int k = 0; k < nc; k++) {                    /* uniform channel loop */
-            const lin_ct &t = T[k];                       /* broadcast LDS reads */
-            const uint64_t B = t.B, D = t.D;
-            const uint32_t fl = __builtin_amdgcn_readfirstlane(t.flags);
-            lin_channel_chunk<false>(acc, s_lane[k * 64 + lane] + B, D, lin_wsrc_of(t, tw), M, t.g,
-                                     0, 0, s_lut);
-            /* ... inside it: add (g1 - g0) e from sample pos1 on */
-            if (__builtin_expect(fl & 1u, 0)) {
-                uint32_t l2 = (uint32_t)lane;
-                asm volatile("" : "+v"(l2));               /* recomputed: nothing stays live */
-                lin_channel_chunk<true>(acc, s_lane[k * 64 + l2] + B, D, lin_wsrc_of(t, tw), M, t.gd,
-                                        t.pos1,
-                                        nb0 + (int)l2, s_lut);
-            }
-            if (__builtin_expect(fl & 2u, 0))
-                lin_patch_fix(acc, L + k, nb0, lane);
-        }
-#endif
         wave_sync_lds();                                  /* T is rewritten by the next chunk */
-        if (LIN_ABLATE & 1) {
-            uint32_t x = 0;
-#pragma unroll
-            for (int s = 0; s < LIN_CH; s++)
-                x ^= lin_w16(acc, s);
-            if (x == 0x12345678u)
-                ob[lane] = 1;
-        } else if (nb0 + 64 * LIN_CH <= n_per_blk)
+        if (nb0 + 64 * LIN_CH <= n_per_blk)
             lin_store<FMT, false>(acc, ob, nb0, lane, n_per_blk);
         else
             lin_store<FMT, true>(acc, ob, nb0, lane, n_per_blk);
     }
-#if LIN_STAMP
-    const uint64_t st_t1 = __builtin_amdgcn_s_memtime(), st_r1 = __builtin_amdgcn_s_memrealtime();
-    const size_t sw = (size_t)blockIdx.x * LIN_WAVES + wave;
-    if (lane == 0 && sw < LIN_STAMP_WAVES) {
-        uint64_t *d = g_lin_stamp[sw];
-        d[0] = st_t0;
-        d[1] = st_t1;
-        d[2] = st_r0;
-        d[3] = st_r1;
-    }
-#endif
 }
 
-#if LIN_STAMP
-/* the stamps of the last gss_lin_kernel launch: n waves x {memtime0, memtime1, realtime0,
-   realtime1} (diagnostic builds only; not in include/gpssim_amd.h) */
-extern "C" int gss_diag_lin_stamps(uint64_t *out, size_t n_waves)
-{
-    if (n_waves > LIN_STAMP_WAVES)
-        n_waves = LIN_STAMP_WAVES;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lin_stamp), n_waves * 4 * sizeof(uint64_t), 0,
-                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif
 
 /* ======================================================================================== */
 /* C ABI                                                                                    */
@@ -1854,8 +1331,7 @@ extern "C" int gss_dev_ordinal(const gss_dev *d) { return d->ordinal; }
 
 extern "C" const char *gss_build_info(void)
 {
-    return "lin_mfma=" GSS_STR(LIN_MFMA) " lin_ch=" GSS_STR(LIN_CH) " lin_swin=" GSS_STR(LIN_SWIN)
-           " arch=gfx950";
+    return "lin_mfma=2 lin_ch=" GSS_STR(LIN_CH) " lin_swin=3 arch=gfx950";
 }
 
 extern "C" size_t gss_block_bytes(int n, int fmt)
@@ -2117,10 +1593,9 @@ extern "C" int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const
     HIP_TRY(hipSetDevice(d->ordinal));
     hipStream_t st = (hipStream_t)stream;
     /* chip-sign bit-streams of every C/A table row (32 x 99 x 4 B) and, after them, the chunk
-       window table of LIN_SWIN (32 x 2560 x 64 B); rebuilt per call (the sample rate sets its
-       window advance): a few µs */
-    const size_t ncbw = (size_t)n_ca * CAB_W,
-                 ntw = LIN_SWIN ? (size_t)n_ca * GSS_LIN_TWE * LIN_CH : 0;
+       window table (32 x 2560 x 64 B); rebuilt per call (the sample rate sets its window
+       advance): a few µs */
+    const size_t ncbw = (size_t)n_ca * CAB_W, ntw = (size_t)n_ca * GSS_LIN_TWE * LIN_CH;
     const size_t tw_off = (ncbw + 63) & ~(size_t)63;
     if ((tw_off + ntw) * sizeof(uint32_t) > d->d_cbw_cap) {
         (void)hipFree(d->d_cbw);
@@ -2132,12 +1607,10 @@ extern "C" int gss_synth_lin_device(gss_dev *d, const gss_chan_blk_t *blk, const
     hipLaunchKernelGGL(gss_cab_kernel, dim3((unsigned)((ncbw + 255) / 256)), dim3(256), 0, st,
                        ca_bits, n_ca, d->d_cbw);
     HIP_TRY(hipGetLastError());
-    if (ntw) {
-        hipLaunchKernelGGL(gss_tw16_kernel, dim3((unsigned)((ntw + 255) / 256)), dim3(256), 0,
-                           st, (const uint32_t *)d->d_cbw, n_ca, gss_lin_wstep16(n_per_blk),
-                           d->d_cbw + tw_off);
-        HIP_TRY(hipGetLastError());
-    }
+    hipLaunchKernelGGL(gss_tw16_kernel, dim3((unsigned)((ntw + 255) / 256)), dim3(256), 0, st,
+                       (const uint32_t *)d->d_cbw, n_ca, gss_lin_wstep16(n_per_blk),
+                       d->d_cbw + tw_off);
+    HIP_TRY(hipGetLastError());
     const int segs = (n_per_blk + 64 * LIN_STEPS - 1) / (64 * LIN_STEPS);
     const int wg_per_blk = (segs + LIN_WAVES - 1) / LIN_WAVES;
     const size_t nsegrows = (size_t)nblk * GSS_MAXCH * segs;

@@ -1,12 +1,14 @@
 #!/bin/bash
-# Build measurement variants of the library into _var/<name>/ (ablations of the fast-path kernel,
-# or other LIN_CH): usage  [HOSTFLAGS="-D..."] bash tools/ablate.sh name "EXTRA_HIPFLAGS"
-# SYNTH_SRC=<file> builds another version of gss_synth.hip (e.g. a previous commit's, next to it).
+# Build measurement variants of the library into _var/<name>/ (another LIN_CH, or a variant
+# source of the fast-path kernel): usage  [HOSTFLAGS="-D..."] bash tools/ablate.sh name "EXTRA_HIPFLAGS"
+# SYNTH_SRC=<file> builds another version of gss_synth.hip (a measurement variant kept outside
+# the product source, or a previous commit's: git show <rev>:gps-sdr-sim_amd/csrc/hip/gss_synth.hip;
+# the ablation switches of rounds 2-4 -- LIN_ABLATE, LIN_STAMP, LIN_SWIN, LIN_MFMA, ... -- are in
+# the source of commit 898e226).
 # The variant is loaded by bench.py through GSS_LIB_PATH=_var/<name>/libgpssim_amd.so.
 set -e
 cd "$(dirname "$0")/.."
 name=$1; flags=$2
-case "$flags" in *LIN_MFMA=*) ;; *) flags="-DLIN_MFMA=2 $flags" ;; esac   # the Makefile's default
 mkdir -p _var/$name/obj
 HIPCC=/opt/rocm/bin/hipcc
 F="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Iinclude -Wno-unused-result -mllvm -amdgpu-mfma-vgpr-form=1 $flags"

@@ -2,7 +2,9 @@
 """In-kernel clock of gss_lin_kernel (MI355X_MICROARCH.md, "DVFS give-back" item 6).
 
 Runs the bench workload (BASELINE configs[1]: static 300 s, 2.6 MS/s, -b 16) through a
-diagnostic build of the library (gss_synth.hip built with -DLIN_STAMP=1, tools/ablate.sh), first
+diagnostic build of the library (a stamp variant of gss_synth.hip built by tools/ablate.sh with
+SYNTH_SRC: the product source carries no stamps; the LIN_STAMP=1 build of commit 898e226 is
+one), first
 back to back for --hold seconds so that the clock has settled, then --steps timed launches.  Each
 wave stamps s_memtime (shader cycles) and s_memrealtime (100 MHz) around its chunk loop; the
 stamps of the last launch give, per wave, the cycles it took and the clock it ran at
