@@ -39,7 +39,11 @@ Extra JSON fields besides the driver contract:
   cpu_baseline  the reference program built from its own sources (oracle/_ref/gps-sdr-sim) on a
                 bounded sample, on 1 core and as C concurrent processes on C host cores, rank 0
                 only, before the GPU is initialised;
-  exact_path    the same resident batch through the exact walking path alone.
+  exact_path    the same resident batch through the exact walking path alone;
+  window        the fast path including its proofs on the device, per step: gss_linearize_device
+                over the window's resident rows (the proof kernel) and then the render
+                (gss_synth_lin_device: window tables, segment rows, gss_lin_kernel) -- the cost of
+                a window that is proven once and rendered once, beside the kernel-only headline.
 """
 import argparse
 import json
@@ -264,7 +268,7 @@ def live_traffic(fmt, window, threads, kern_ms, steps, warmup, timeout=150):
     child = [sys.executable, os.path.abspath(__file__), "--steps", str(steps), "--warmup",
              str(warmup), "--fmt", str(fmt), "--window", str(window), "--threads", str(threads),
              "--no-cpu-baseline", "--no-exact", "--no-configs", "--no-e2e", "--no-pmc",
-             "--no-sustained"]
+             "--no-sustained", "--no-window"]
     env = dict(os.environ, TMPDIR="/tmp")
     env.pop("GSS_PROF_SAVE", None)
     passes = [("kt", ["--kernel-trace", "--stats"]),
@@ -338,6 +342,43 @@ def time_steps(torch, dev, dev_t, res, steps, warmup, stream):
     el = time.perf_counter() - t0
     n_lin, lin_ms = dev.timing_lin()
     return el, n_lin, lin_ms
+
+
+def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None):
+    """proof + render of the resident window per step (see the module docstring): the proof kernel
+    rewrites the window's rows and fast flags in place (byte-identical rows: tests/
+    test_gpu_proof.py), then the window renders from them; HIP events on the launch stream time
+    the proof apart"""
+    st = torch.cuda.current_stream(dev_t)
+
+    def prove():
+        dev.linearize_device(res.d_blk.data_ptr(), res.d_nch.data_ptr(), res.nblk, res.npb,
+                             res.d_ca.data_ptr(), res.n_ca, res.d_nav.data_ptr(), res.n_nav,
+                             res.d_lin.data_ptr(), res.d_fast.data_ptr(), stream)
+    for _ in range(warmup):
+        prove()
+        res.step(stream)
+    torch.cuda.synchronize(dev_t)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(st)
+        prove()
+        ev[i][1].record(st)
+        res.step(stream)
+    torch.cuda.synchronize(dev_t)
+    el = time.perf_counter() - t0
+    proof_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    samples = res.nblk * res.npb
+    out = {"value": round(samples * steps / el / 1e6, 2), "unit": "MS/s",
+           "ms_per_step": round(el / steps * 1e3, 3), "proof_ms": round(proof_ms, 3),
+           "steps": steps, "warmup": warmup,
+           "workload": "the headline window: proof kernel (gss_linearize_device) + render "
+                       "(gss_synth_lin_device) per step on resident rows"}
+    if exact:
+        out["vs_exact_path"] = round(out["value"] / exact["value"], 3)
+    return out
 
 
 def per_config(G, torch, dev, dev_t, stream, steps, warmup, threads, e2e=True):
@@ -547,6 +588,8 @@ def main():
     ap.add_argument("--no-exact", action="store_true",
                     help="skip the exact-path run on the same batch (exact_path)")
     ap.add_argument("--no-configs", action="store_true", help="skip per_config")
+    ap.add_argument("--no-window", action="store_true",
+                    help="skip the proof + render leg (window)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the gss_run end-to-end run")
     ap.add_argument("--e2e-window", type=float, default=1800.0)
     ap.add_argument("--no-sustained", action="store_true",
@@ -689,6 +732,10 @@ def main():
         el = time.perf_counter() - t1
         exact = {"value": round(samples_rank * args.steps / el / 1e6, 2),
                  "ms_per_step": round(el / args.steps * 1e3, 3)}
+    window = None
+    if single and not args.no_window and res.proof == "gpu":
+        window = window_leg(torch, dev, dev_t, res, args.steps, args.warmup, stream, exact)
+        progress(f"window (proof + render): {window['value']} MS/s, proof {window['proof_ms']} ms")
     ms_per_step = elapsed / args.steps * 1e3
     progress(f"timed {args.steps} steps: {ms_per_step:.3f} ms/step, kernel {lin_ms:.3f} ms")
     value = world * samples_rank * args.steps / elapsed / 1e6          # MS/s, whole job
@@ -717,7 +764,9 @@ def main():
         e2e = e2e_run(G, dev, args.threads, args.e2e_window, batch=128)
         progress(f"e2e: {e2e['value']} MS/s")
     if single and not args.no_configs:
-        configs = per_config(G, torch, dev, dev_t, stream, min(args.steps, 3), 1, args.threads,
+        # the headline's steps and warm-up: the shader clock ramps over the first ~25 launches
+        # after an idle spell, so a leg timed on fewer launches reads slower
+        configs = per_config(G, torch, dev, dev_t, stream, args.steps, args.warmup, args.threads,
                              e2e=not args.no_e2e)
     # the live PMC passes last: their processes' device memory is wiped when they exit (above)
     traffic, traffic_src, prof = None, "not measured (--no-pmc)", None
@@ -769,6 +818,7 @@ def main():
         "gather": gather,
         "e2e": e2e,
         "exact_path": exact,
+        "window": window,
         "lib": {"path": os.path.relpath(G.LIB_PATH, REPO), "version": version, "sha16": sha},
     }
     if rank == 0:

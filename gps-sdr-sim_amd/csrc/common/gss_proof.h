@@ -277,8 +277,8 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
     if (ZS <= 0 || Z0 >= per || !GSS_LIN_WIN_OK((uint64_t)ZS) ||
         !gss_lin_win16_ok((uint64_t)ZS, n))
         return 0;
-    const int nhz = ambiguous(Z0, ZS, 2 + (i128)n * (LIN_CODE_ERR + 1) + GSS_LIN_KDEV_CODE,
-                              LIN_CODE_LGB, n, hz, LIN_MAXHIT);
+    const i128 DZ1 = 2 + (i128)n * (LIN_CODE_ERR + 1);            /* line vs reference */
+    const int nhz = ambiguous(Z0, ZS, DZ1 + GSS_LIN_KDEV_CODE, LIN_CODE_LGB, n, hz, LIN_MAXHIT);
     if (nhz < 0)
         return 0;
     lin->x0 = (uint64_t)X0;
@@ -286,15 +286,27 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
     lin->z0 = (uint64_t)Z0;
     lin->zs = (uint64_t)ZS;
 
-    /* exact code state at the code's ambiguous samples */
+    /* exact code state at the code's ambiguous samples (the samples where the KERNEL's chip may
+       differ from the line's).  The reference's value lies within DZ1 of the line, so where the
+       line is farther than that from every chip boundary the reference has the line's chip and
+       the line's number of wraps: its state follows from the line, and only the samples whose
+       line is within DZ1 of a boundary take the exact walk (from the last walked state) */
     gss_code_state st = {c0, p->icode, p->ibit, p->iword};
     int64_t at = 0;
     for (int i = 0; i < nhz; i++) {
-#ifndef GSS_PF_ABLATE_CODE_WALK          /* (measurement builds only: wrong rows) */
-        gss_code_walk_cc(&st, cs, hz[i] - at);
-#endif
-        at = hz[i];
-        at_hz[i] = st;
+        const i128 zq = (i128)Z0 + (i128)hz[i] * ZS;
+        if (near_boundary(zq, DZ1, LIN_CODE_LGB)) {
+            gss_code_walk_cc(&st, cs, hz[i] - at);
+            at = hz[i];
+            at_hz[i] = st;
+        } else {
+            const int64_t chips = (int64_t)(zq >> LIN_CODE_LGB);   /* from chip 0 of the block */
+            const int64_t tot = p->icode + chips / GSS_CA_LEN, bits = p->ibit + tot / 20;
+            at_hz[i].ph = (double)(chips % GSS_CA_LEN) + 0.5;      /* (only its floor is read) */
+            at_hz[i].icode = (int)(tot % 20);
+            at_hz[i].ibit = (int)(bits % 30);
+            at_hz[i].iword = p->iword + (int)(bits / 30);
+        }
     }
 
     /* ---- code wraps, data bits and the signed-gain schedule ---- */

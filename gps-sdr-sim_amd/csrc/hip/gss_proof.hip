@@ -40,7 +40,11 @@ const proof_lut &host_lut()
     return L;
 }
 
-__device__ void lin_row_init(gss_lin_t *l)
+}  // namespace
+
+/* (outside the anonymous namespace, so that profiles name the kernel: rocprofv3 prints
+   "(anonymous namespace)::..." for the others) */
+__device__ static void lin_row_init(gss_lin_t *l)
 {
     memset(l, 0, sizeof *l);
     for (int i = 0; i < GSS_NGC; i++)
@@ -49,7 +53,7 @@ __device__ void lin_row_init(gss_lin_t *l)
         l->ppos[i] = INT32_MAX;
 }
 
-constexpr int PF_BLOCKS = 16;          /* blocks per workgroup, one lane per channel slot */
+static constexpr int PF_BLOCKS = 16;          /* blocks per workgroup, one lane per channel slot */
 
 /* force_exact > 0 (gss_run's test hook GSS_RUN_FORCE_EXACT): blocks first + b with
    (first + b) % force_exact == 0 are sent to the exact path as well */
@@ -113,8 +117,6 @@ __global__ __launch_bounds__(PF_BLOCKS * GSS_MAXCH) void gss_proof_kernel(
         }
     }
 }
-
-}  // namespace
 
 /* gss_run's launch (force_exact: its test hook); not exported (exports.map) */
 int run_proof_launch(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,

@@ -58,7 +58,7 @@ for s in "$@"; do
                 [ "$v" != cur ] && lib=_var/$v/libgpssim_amd.so
                 line=$(GSS_ALLOW_LIB_OVERRIDE=1 GSS_LIB_PATH=$lib timeout -k 10 200 python bench.py \
                     --steps ${STEPS:-20} --warmup ${WARMUP:-5} --no-configs --no-e2e \
-                    --no-cpu-baseline --no-exact --no-pmc --no-sustained 2>>$OUT/ablate.err | tail -1)
+                    --no-cpu-baseline --no-exact --no-pmc --no-sustained --no-window 2>>$OUT/ablate.err | tail -1)
                 step "ablate $v" $?
                 echo "$v $(echo "$line" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["stages_ms"]["fast_path"], d["value"])')" >> $OUT/ablate.log
             done
@@ -97,7 +97,7 @@ for s in "$@"; do
         step "rehearse $n$t" $? ;;
     pmcclk:*)
         vs=${s#pmcclk:}
-        BA="--steps 20 --warmup 5 --no-exact --no-configs --no-e2e --no-cpu-baseline --no-pmc"
+        BA="--steps 20 --warmup 5 --no-exact --no-configs --no-e2e --no-cpu-baseline --no-pmc --no-window"
         for v in cur ${vs//,/ }; do
             lib=gps-sdr-sim_amd/lib/libgpssim_amd.so
             [ "$v" != cur ] && lib=_var/$v/libgpssim_amd.so

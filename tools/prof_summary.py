@@ -12,7 +12,10 @@ import sys
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "")
+    """the kernel's name without its parameter list: 'void gss_lin_kernel<16>(...)' ->
+    'gss_lin_kernel<16>', '(anonymous namespace)::k(...)' -> 'k'"""
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return name.split("(")[0]
 
 
 def kernel_stats(d):
@@ -54,12 +57,21 @@ def timed_avg_ns(durs, steps, warmup=0):
 
 
 def counters(d):
+    """per kernel: each counter averaged over its dispatches, and "_clk": the clock the dispatches
+    with GRBM_GUI_ACTIVE ran at, their per-XCD cycles summed over their own durations (the
+    counter pass's timestamps of the same dispatches, not another pass's averages)"""
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     meta = {}
+    clk = collections.defaultdict(lambda: [0.0, 0.0])       # kernel -> [cycles, ns]
     for f in glob.glob(os.path.join(d, "pmc_*", "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             k = short(r["Kernel_Name"])
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if r["Counter_Name"] == "GRBM_GUI_ACTIVE" and r.get("End_Timestamp"):
+                ns = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                if ns > 0:
+                    clk[k][0] += float(r["Counter_Value"]) / 8
+                    clk[k][1] += ns
             meta[k] = {"vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"]),
                        "lds": int(r["LDS_Block_Size"]), "scratch": int(r["Scratch_Size"]),
                        "grid": int(r["Grid_Size"]), "wg": int(r["Workgroup_Size"])}
@@ -67,6 +79,8 @@ def counters(d):
     for k, cs in acc.items():
         res[k] = {c: sum(v) / len(v) for c, v in cs.items()}
         res[k]["_meta"] = meta[k]
+        if clk[k][1] > 0:
+            res[k]["_clk"] = clk[k][0] / clk[k][1]
     return res
 
 
@@ -87,15 +101,15 @@ def main():
                 e["timed_launches"] = min(steps, len(kd[k]))
         c = cs.get(k, {})
         e.update({"meta": c.get("_meta")})
-        e["counters"] = {n: v for n, v in c.items() if n != "_meta"}
+        e["counters"] = {n: v for n, v in c.items() if not n.startswith("_")}
         if "WRITE_SIZE" in c:
             e["hbm_write_bytes"] = c["WRITE_SIZE"] * 1024
         if "FETCH_SIZE" in c:
             e["hbm_read_bytes_corrected"] = c["FETCH_SIZE"] * 1024 * 2
         if "SQ_INSTS_VALU" in c and "SQ_WAVES" in c:
             e["valu_insts_per_wave"] = c["SQ_INSTS_VALU"] / max(c["SQ_WAVES"], 1)
-        if "GRBM_GUI_ACTIVE" in c and "avg_ns" in e:
-            e["eff_clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / e["avg_ns"]
+        if "_clk" in c:
+            e["eff_clock_ghz"] = c["_clk"]
         if "GRBM_GUI_ACTIVE" in c:
             cyc = c["GRBM_GUI_ACTIVE"] / 8                 # per-XCD GPU cycles of the dispatch
             if "SQ_ACTIVE_INST_VALU" in c:                 # 4 issue cycles per wave64 VALU op

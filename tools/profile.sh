@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 TAG=${1:-r2}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BA="${PROF_BENCH_ARGS:---steps 3 --warmup 1 --no-exact --no-configs --no-e2e} --no-cpu-baseline --no-pmc"
+BA="${PROF_BENCH_ARGS:---steps 3 --warmup 1 --no-exact --no-configs --no-e2e} --no-cpu-baseline --no-pmc --no-window"
 # the counter passes only need the headline kernel: without the per-config and e2e legs
 PA="$BA --no-configs --no-e2e"
 run() {  # name, rocprofv3 args...
