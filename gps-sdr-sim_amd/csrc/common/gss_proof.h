@@ -28,18 +28,34 @@
 typedef unsigned __int128 u128;
 typedef __int128 i128;
 
-/* floor(a / b) for a quotient below 2^53 (b > 0): a 64-bit division when a fits 64 bits, else
-   a double estimate (relative error 2^-52: off by at most one here) corrected by exact products;
-   no 128-bit division (none on the GPU, a slow library call on the host) */
+/* floor(a / b) for b > 0 and a quotient below 2^64: a 64-bit division when a fits 64 bits; for a
+   quotient below 2^53 a double estimate (a's two halves converted apart: relative error below
+   2^-51, so off by at most two here) corrected by exact products; above, an exact shift-subtract
+   long division (no caller reaches it: the proofs' quotients stay far below 2^53).  No 128-bit
+   division (none on the GPU, a slow library call on the host). */
 GSS_PF uint64_t gss_pf_udiv(u128 a, uint64_t b)
 {
-    if ((uint64_t)(a >> 64) == 0)
-        return (uint64_t)a / b;
-    uint64_t q = (uint64_t)((double)a / (double)b);
-    while ((u128)q * b > a)
-        q--;
-    while ((u128)(q + 1) * b <= a)
-        q++;
+    const uint64_t hi = (uint64_t)(a >> 64), lo = (uint64_t)a;
+    if (hi == 0)
+        return lo / b;
+    if (a < ((u128)b << 53)) {
+        uint64_t q = (uint64_t)(((double)hi * 0x1p64 + (double)lo) / (double)b);
+        while ((u128)q * b > a)
+            q--;
+        while ((u128)(q + 1) * b <= a)
+            q++;
+        return q;
+    }
+    u128 r = 0;                                      /* r < 2^65 throughout */
+    uint64_t q = 0;
+    for (int i = 127; i >= 0; i--) {
+        r = (r << 1) | (uint64_t)((a >> i) & 1u);
+        if (r >= b) {
+            r -= b;
+            if (i < 64)
+                q |= (uint64_t)1 << i;
+        }
+    }
     return q;
 }
 

@@ -205,6 +205,8 @@ struct Run {
     int force_exact;                 /* GSS_RUN_FORCE_EXACT=k: every k-th block to the exact
                                         path (tests of the mixed batch), 0 = off */
     int64_t first, last;             /* [first, last) block range of the run */
+    int64_t start = 0;               /* the handle's next block when the run began (an earlier
+                                        run, a seek): the planner's and rows thread's cursor   */
     const gss_run_opts_t *opts;      /* carrier hand-off (gss_run_ex), or null */
     /* with opts->carr_in: the whole range planned up front (rows, carriers, checkpoints) */
     std::vector<gss_chan_blk_t> pre_blk;
@@ -548,7 +550,7 @@ void rows_thread(Run *r)
         const char *e = getenv("GSS_RUN_ROWS_POOL");   /* 0: share the planner's workers */
         gss_pool_select(e && e[0] == '0' ? 0 : 1);
     }
-    int64_t cursor = 0;
+    int64_t cursor = r->start;
     int nav_done = 0;
     for (int i = 0;; i++) {
         Run::RowBatch &q = r->rb[i & 1];
@@ -877,7 +879,7 @@ int proof_ahead(Run &r, Slot &sl);
 
 void planner(Run *r)
 {
-    int64_t cursor = 0;
+    int64_t cursor = r->start;
     int up_rc = (r->opts && r->opts->carr_in) ? plan_range_upfront(*r) : 0;
     for (int i = 0;; i++) {
         Slot &sl = r->slot[i % NSLOT];
@@ -948,6 +950,20 @@ void prover(Run *r)
         if (end)
             return;
     }
+}
+
+/* Nav-table rows a run can end with: the handle's rows so far (earlier runs, seeks, the
+   allocation) plus, per 30 s update the run can cross, the re-generated frame of every active
+   channel and a fresh one for every channel allocation, at most 2 GSS_MAXCH (scenario.c:
+   update_30s, allocate_channels) -- the reservations of the tables that must not move during
+   the run (the prover's host copy, the device table with GPU proofs) */
+size_t nav_rows_bound(const gss_scn *s, const gss_scn_info_t &info)
+{
+    const uint32_t *rows = nullptr;
+    int n = 0;
+    if (gss_scn_nav_table(s, &rows, &n) != 0 || n < 0)
+        n = 0;
+    return (size_t)n + ((size_t)info.n_blocks / 300 + 2) * 2 * GSS_MAXCH;
 }
 
 /* the device nav table holds at least `rows` rows (grown on the compute stream's order) */
@@ -1152,8 +1168,9 @@ int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, in
 }
 
 /* GPU proofs: the blocks they rejected (fast[b] == 0, rare: none in the bench runs) rendered
-   again, this time with the exact path for them (their checkpoints from the rows' exact
-   carriers), and the slot's bytes copied once more; synchronous */
+   again on the exact path alone (their checkpoints from the rows' exact carriers; the fast
+   flags zeroed on the device, so that the fast kernel renders nothing), and only their bytes
+   copied to the host again; synchronous */
 int redo_rejected(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_rows, int n_per_blk,
                   int fmt, size_t bb, hipStream_t st)
 {
@@ -1175,6 +1192,7 @@ int redo_rejected(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_rows
         }
     const SlotDev v = slot_dev(sl);
     RUN_H2D(v.ck, sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb, st);
+    RUN_TRY(hipMemsetAsync(v.fast, 0, sizeof(int32_t) * (size_t)sl.nb, st));
     RUN_H2D(v.fast + sl.nb, sl.fast + sl.nb, sizeof(int32_t) * (size_t)nf, st);
     RUN_TRY(hipMemsetAsync(sl.d_status, 0, sizeof(int32_t), st));
     int rc = gss_synth_lin_device(d, v.blk, v.nch, sl.nch_max, v.lin, v.fast, v.fast + sl.nb, nf,
@@ -1182,9 +1200,19 @@ int redo_rejected(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_rows
                                   sl.d_out, sl.d_status, st);
     if (rc)
         return rc;
-    RUN_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, bb * (size_t)sl.nb, hipMemcpyDeviceToHost, st));
+    for (int i = 0; i < nf;) {                        /* runs of consecutive rejected blocks */
+        const int b0 = sl.fast[sl.nb + i];
+        int j = i + 1;
+        while (j < nf && sl.fast[sl.nb + j] == b0 + (j - i))
+            j++;
+        RUN_TRY(hipMemcpyAsync(sl.h_out + bb * (size_t)b0, sl.d_out + bb * (size_t)b0,
+                               bb * (size_t)(j - i), hipMemcpyDeviceToHost, st));
+        i = j;
+    }
     RUN_TRY(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     RUN_TRY(hipStreamSynchronize(st));
+    for (int i = 0; i < nf; i++)                      /* (the verdicts stay on the host copy) */
+        sl.fast[sl.fast[sl.nb + i]] = 0;
     if (trace_on())
         fprintf(stderr, "trace redo first %lld blocks %d\n", (long long)sl.first, nf);
     return 0;
@@ -1334,6 +1362,12 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         r.batch = (int)(SLOT_OUT_MAX / bb) > 0 ? (int)(SLOT_OUT_MAX / bb) : 1;
     r.first = first_block;
     r.last = n_blocks < 0 ? INT64_MAX : first_block + n_blocks;
+    /* the handle may have produced blocks already (an earlier run or seek): the run continues
+       from there; blocks before first_block are planned (the carrier chain) and dropped */
+    r.start = info.next_block;
+    if (first_block < r.start)
+        return gss_fail(GSS_E_STATE, "run from block %lld, but the scenario is at block %lld",
+                        (long long)first_block, (long long)r.start);
 
     int ordinal = 0;
     RUN_TRY(hipGetDevice(&ordinal));
@@ -1487,9 +1521,9 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                 r.prover = 0;
         }
         if (!err && r.rows_ahead) {
-            /* the nav table's host copy never moves while the prover reads it: room for the
-               allocation's rows and up to GSS_MAXCH new rows per 30 s update */
-            r.nav_rows_h.reserve(((size_t)info.n_blocks / 300 + 4) * GSS_MAXCH * GSS_NAV_WORDS);
+            /* the nav table's host copy never moves while the prover reads it (take_rows
+               still grows it safely if the bound were passed) */
+            r.nav_rows_h.reserve(nav_rows_bound(s, info) * GSS_NAV_WORDS);
             for (Run::RowBatch &q : r.rb) {
                 q.blk.resize(nb * GSS_MAXCH);
                 q.nch.resize(nb);
@@ -1501,7 +1535,7 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             err = gss_dev_reserve(d, r.batch, info.n_per_blk);
         if (!err && r.gpu_proof) {
             /* proofs run ahead on the slots' own streams (proof_ahead); the device nav table
-               reserved for the whole run (at most GSS_MAXCH new rows per 30 s update) */
+               reserved for the whole run (nav_rows_bound) */
             r.dev = d;
             r.d_ca = d_ca;
             int lo_pri = 0, hi_pri = 0;
@@ -1517,7 +1551,7 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                     err = gss_fail(GSS_E_HIP, "run proof streams");
             }
             if (!err)
-                err = nav_reserve(r, ((size_t)info.n_blocks / 300 + 4) * GSS_MAXCH, st);
+                err = nav_reserve(r, nav_rows_bound(s, info), st);
             /* the C/A table (built on st above) before any proof stream reads it */
             if (!err && hipStreamSynchronize(st) != hipSuccess)
                 err = gss_fail(GSS_E_HIP, "run set-up");

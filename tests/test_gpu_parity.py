@@ -574,3 +574,40 @@ def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec, ahead, prover
     dev.run(s, sink, first_block=333, n_blocks=150, batch=64 if batch > 1 else 1)
     assert [b for b, _ in blocks] == list(range(333, 483))
     assert [x for _, x in blocks] == g["block_sha16"][333:483]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proof", ["gpu", "split"])
+def test_streaming_run_twice_on_one_handle_gpu_proofs(dev, golden, monkeypatch, proof):
+    """Two gss_run calls on one scenario handle with the proofs on the GPU: the second run starts
+    where the first stopped, after the first run's nav rows (and its 30 s updates) are already in
+    the handle's table, so the second run's device nav table must be sized from the rows the
+    handle holds, not from the run length alone (nav_rows_bound).  65 s across two 30 s updates
+    against the reference's golden hashes."""
+    monkeypatch.setenv("GSS_RUN_PROOF", proof)
+    g = golden["static_d65_b8_noiono"]
+    s, _ = G.Scenario.from_cli(["-e", NAV, "-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8",
+                                "-i"])
+    bb = G.block_bytes(s.n_per_blk, 8)
+    blocks = []
+
+    def sink(buf, first, nb):
+        for i in range(nb):
+            blocks.append((first + i, hashlib.sha256(buf[i * bb:(i + 1) * bb]).hexdigest()[:16]))
+
+    dev.run(s, sink, first_block=0, n_blocks=310, batch=64, threads=4)
+    dev.run(s, sink, first_block=310, n_blocks=-1, batch=64, threads=4)
+    assert [b for b, _ in blocks] == list(range(len(g["block_sha16"])))
+    assert [x for _, x in blocks] == g["block_sha16"]
+    # a run cannot start before the handle's position
+    s, _ = G.Scenario.from_cli(["-e", NAV, "-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8",
+                                "-i"])
+    blocks.clear()
+    dev.run(s, sink, first_block=0, n_blocks=100, batch=64, threads=4)
+    with pytest.raises(Exception):
+        dev.run(s, sink, first_block=50, n_blocks=10, batch=64, threads=4)
+    # ... and a later start skips ahead (planned, dropped), as from a fresh handle
+    dev.run(s, sink, first_block=400, n_blocks=60, batch=64, threads=4)
+    assert [b for b, _ in blocks] == list(range(100)) + list(range(400, 460))
+    assert [x for _, x in blocks] == g["block_sha16"][:100] + g["block_sha16"][400:460]
+

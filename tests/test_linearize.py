@@ -115,6 +115,51 @@ def test_first_below_small_vs_brute():
         assert G.first_below(n, m, a, s, w) == brute_first_below(n, m, a, s, w), (n, m, a, s, w)
 
 
+def _first_below_ref(n, m, a, s, w):
+    """smallest p in [0, n) with (a + p s) mod m < w, or n: an independent Python restatement by
+    the classic reduction of the modular inequality (exact integers, any size)"""
+    a, s = a % m, s % m
+    if n <= 0:
+        return 0
+    if a < w:
+        return 0
+
+    def first_in(s, m, lo, hi):              # least x >= 0 with (s x) mod m in [lo, hi], lo > 0
+        if s == 0:
+            return None
+        x = -(-lo // s)
+        if s * x <= hi:
+            return x
+        y = first_in(m % s, s, (-hi) % s, (-lo) % s)   # least y: (m y) mod s in [s - hi%s, ..]
+        if y is None:
+            return None
+        return -(-(lo + m * y) // s)
+
+    x = first_in(s, m, m - a, m - a + w - 1)
+    return n if x is None or x >= n else x
+
+
+def test_first_below_any_n():
+    """first_below with run lengths and moduli far beyond a block's (up to 2^62): it ends at
+    once, agrees with an independent restatement, and the sample it returns lies in the window
+    with no earlier one (checked against the restatement's minimality).  The division on its way
+    back up (gss_pf_udiv) then meets quotients of up to ~2^62; it must stay exact there."""
+    rng = np.random.default_rng(11)
+    for _ in range(300):
+        lgm = int(rng.integers(20, 62))
+        m = int(rng.integers(1 << (lgm - 1), 1 << lgm))
+        n = int(rng.integers(1, 1 << 62)) if rng.random() < 0.7 else int(rng.integers(1, 10**6))
+        a, s = int(rng.integers(0, m)), int(rng.integers(1, m))
+        w = int(rng.integers(1, max(2, m >> int(rng.integers(1, lgm)))))
+        got = G.first_below(n, m, a, s, w)
+        want = _first_below_ref(n, m, a, s, w)
+        if got == (1 << 64) - 2:             # GSS_PF_GIVE_UP: a descent deeper than 64 levels
+            continue
+        assert got == want, (n, m, a, s, w)
+        if got < n:
+            assert (a + got * s) % m < w
+
+
 @pytest.mark.parametrize("lgm", [50, 55])
 def test_first_below_pow2_vs_numpy(lgm):
     """The proof's moduli and window widths (2 D of 2^-34 cycle / 2^-25 chip and wider), runs of a
