@@ -526,7 +526,8 @@ def gather_leg(G, torch, td, dev, dev_t, rank, world, coll_t, walker, threads, w
     chunk = max(1, (256 << 20) // bb)
     b0, b1 = rank_blocks(nb_all, rank, world)
     blk, nch, ck, pt = plan_window(scn, b0, b1 - b0, baton=Baton(td, rank, world, device=coll_t),
-                                   threads=threads, walker=walker)
+                                   threads=threads, walker=walker,
+                                   chain_threads=max(threads, BOX_CORES))
     plan = chunk_plan(nb_all, world, chunk, layout)
     nav = scn.nav_table()
     if layout == "stripe":
@@ -597,6 +598,9 @@ def main():
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the live rocprofv3 traffic passes (roofline.traffic)")
     ap.add_argument("--threads", type=int, default=BOX_CORES)
+    ap.add_argument("--chain-threads", type=int, default=BOX_CORES,
+                    help="threads of each rank's carrier-chain walk (the ranks' chains run one "
+                         "after another: the baton)")
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the whole-node gather leg (N > 1: configs[3] to rank 0)")
     ap.add_argument("--gather-layout", default="stripe", choices=["stripe", "block"],
@@ -645,9 +649,15 @@ def main():
     t_plan0 = time.perf_counter()
     blk, nch, ck, nav, npb, plan_t = plan_rank(NAV, rank, world, args.window, llh=LOC,
                                                samp_freq=FS, data_format=args.fmt,
-                                               threads=args.threads, baton=baton, walker=walker)
+                                               threads=args.threads, baton=baton, walker=walker,
+                                               chain_threads=args.chain_threads)
     host_plan_s = time.perf_counter() - t_plan0
     progress(f"planned {len(nch)} blocks in {host_plan_s:.2f} s")
+    if dist:
+        # every rank's window planned before any renders: a rank's carrier chain (run ahead on
+        # its GPU) then never shares the GPU with the proofs and renders of ranks planned before
+        # it, which only happens in a one-GPU rehearsal (GSS_BENCH_REHEARSE)
+        td.barrier()
 
     stream = torch.cuda.current_stream(dev_t).cuda_stream
     res = DeviceWindow(torch, dev, dev_t, blk, nch, nav, npb, args.fmt, ck=ck,

@@ -161,3 +161,52 @@ extern "C" int gss_spec_device(gss_dev *d, gss_spec_in_t *in, int nrow, int n_pe
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "spec kernel: %s", hipGetErrorString(e));
 }
+
+/* gss_run's uploads of its slots' inputs (gss_run.hip, dev_copy): 16-byte vector loads, four in
+   flight per lane; the tail bytes (and unaligned buffers) byte by byte */
+__global__ __launch_bounds__(256) void upload_kernel(const uint4 *__restrict__ src,
+                                                     uint4 *__restrict__ dst, size_t n16,
+                                                     int tail)
+{
+    const size_t stride = (size_t)gridDim.x * 256;
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride],
+                    d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n16; i += stride)
+        dst[i] = src[i];
+    if (blockIdx.x == 0 && (int)threadIdx.x < tail)
+        ((uint8_t *)(dst + n16))[threadIdx.x] = ((const uint8_t *)(src + n16))[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void upload_bytes_kernel(const uint8_t *__restrict__ src,
+                                                           uint8_t *__restrict__ dst, size_t n)
+{
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        dst[i] = src[i];
+}
+
+/* n bytes from src to dst by a kernel on st: pinned host (hipHostMalloc) or device memory on
+   either side (gss_run's uploads; not exported) */
+int run_copy_launch(void *dst, const void *src, size_t n, hipStream_t st)
+{
+    if (n == 0)
+        return 0;
+    if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
+        const size_t n16 = n >> 4;
+        const size_t g = (n16 + 1023) / 1024;
+        hipLaunchKernelGGL(upload_kernel, dim3((unsigned)(g < 1 ? 1 : g > 2048 ? 2048 : g)),
+                           dim3(256), 0, st, (const uint4 *)src, (uint4 *)dst, n16,
+                           (int)(n & 15));
+    } else {
+        const size_t g = (n + 255) / 256;
+        hipLaunchKernelGGL(upload_bytes_kernel, dim3((unsigned)(g > 2048 ? 2048 : g)), dim3(256),
+                           0, st, (const uint8_t *)src, (uint8_t *)dst, n);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "copy kernel launch");
+}

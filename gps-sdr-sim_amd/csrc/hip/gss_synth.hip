@@ -1334,16 +1334,6 @@ extern "C" const char *gss_build_info(void)
     return "lin_mfma=2 lin_ch=" GSS_STR(LIN_CH) " lin_swin=3 arch=gfx950";
 }
 
-extern "C" size_t gss_block_bytes(int n, int fmt)
-{
-    if (n <= 0) return 0;
-    switch (fmt) {
-    case GSS_FMT_SC16: return (size_t)n * 4;
-    case GSS_FMT_SC08: return (size_t)n * 2;
-    case GSS_FMT_SC01: return (n % 4) ? 0 : (size_t)n / 4;
-    default: return 0;
-    }
-}
 
 extern "C" int gss_dev_open(gss_dev **out, int ordinal)
 {

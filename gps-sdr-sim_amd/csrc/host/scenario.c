@@ -1139,3 +1139,17 @@ int gss_lut(int32_t *sin512, int32_t *cos512)
 }
 
 const char *gss_version(void) { return "gpssim_amd 0.1 (gfx950)"; }
+
+/* the bytes the reference writes per block (gpssim.c:2276, 2283, 2287): 4, 2 or 1/4 per sample;
+   0 for an invalid format or a -b 1 block of samples not a multiple of 4 */
+size_t gss_block_bytes(int n, int fmt)
+{
+    if (n <= 0) return 0;
+    switch (fmt) {
+    case GSS_FMT_SC16: return (size_t)n * 4;
+    case GSS_FMT_SC08: return (size_t)n * 2;
+    case GSS_FMT_SC01: return (n % 4) ? 0 : (size_t)n / 4;
+    default: return 0;
+    }
+}
+

@@ -115,10 +115,15 @@ class Baton:
             self.dist.send(t, dst=self.rank + 1)
 
 
-def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=True, walker=None):
+def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=True, walker=None,
+                chain_threads=None):
     """Rows of blocks [first, first + count) of Scenario scn (count < 0: to the end), planned
     without the blocks before `first` when a baton supplies the carriers there (rank > 0).
     Returns (blk, nch, ck or None, timings {seek_s, rows_s, wait_s, chain_s, spec_hits}).
+    chain_threads (default: threads): the threads of the carrier chain's walk.  The ranks' rows
+    are produced at the same time, each on its `threads`; their chains run one after another
+    (each waits for the carriers of the rank before it), so on a box whose CPUs the ranks share
+    the chain can take them all.
     Without a baton and first > 0 the prefix's carrier chain is planned here (a lone process).
     With a walker (host_walker / device_walker) the window's chain is run ahead
     (chain_run_ahead) and ck is None: the exact path walks the few uncertified blocks from their
@@ -162,13 +167,14 @@ def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=Tr
         blk = np.zeros((0, MAXCH), CHAN_DTYPE)
         nch = np.zeros(0, np.int32)
         chain = np.zeros((0, MAXCH), CHAIN_DTYPE)
+    ct = chain_threads or threads
     if walker is not None and len(nch):
         end, t["spec_hits"] = chain_run_ahead(carr, blk, nch, chain, scn.n_per_blk, walker,
-                                              threads=threads)
+                                              threads=ct)
         ck = None
     else:
         end, ck = carr_chain(carr, blk, nch, chain, scn.n_per_blk, carrier_int=scn.carrier_int,
-                             with_ck=with_ck, threads=threads)
+                             with_ck=with_ck, threads=ct)
     t["chain_s"] = time.perf_counter() - t0
     if baton is not None:
         baton.send(end)
@@ -176,7 +182,7 @@ def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=Tr
 
 
 def plan_rank(nav_file, rank, world, window_s, *, llh, samp_freq=2.6e6, data_format=16,
-              threads=8, batch=2000, baton=None, walker=None):
+              threads=8, batch=2000, baton=None, walker=None, chain_threads=None):
     """Host plane for one rank: (blk[n, 16], nch[n], ck[n, 16, NCK] or None, nav rows,
     n_per_blk, timings) of its block range (ck: the carrier checkpoints).  With world > 1 pass a
     Baton: the rank then plans only its own window (module docstring)."""
@@ -184,7 +190,7 @@ def plan_rank(nav_file, rank, world, window_s, *, llh, samp_freq=2.6e6, data_for
     scn = Scenario(nav_file, llh=llh, duration=window_s * world if world > 1 else window_s,
                    samp_freq=samp_freq, data_format=data_format)
     blk, nch, ck, t = plan_window(scn, first, count, baton=baton, threads=threads, batch=batch,
-                                  walker=walker)
+                                  walker=walker, chain_threads=chain_threads)
     if len(nch) != count:
         raise RuntimeError(f"rank {rank}: planned {len(nch)} of {count} blocks")
     t["rows_out"] = int(scn.position()[1])

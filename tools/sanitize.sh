@@ -1,21 +1,53 @@
 #!/bin/bash
-# The host plane under the sanitizers (CPU only): the C sources of
-# gps-sdr-sim_amd/csrc/host (scenario, chains, proofs, worker pools) and the CLI parser, linked
-# with tests/helpers/run_harness.c -- gss_run's rows / planner / prover threads on their own
-# pools, walks by gss_spec_host -- once with -fsanitize=thread and once with
-# -fsanitize=address,undefined.  Any sanitizer report or row mismatch fails.  Logs go to $OUT
-# (default profiles/round4/sanitize).
+# The host side under the sanitizers (CPU only), once with -fsanitize=thread and
+# once with -fsanitize=address,undefined; any sanitizer report, row or byte mismatch fails.
+#  * gss_run itself (gps-sdr-sim_amd/csrc/hip/gss_run.hip, unchanged: its planner, rows and
+#    prover threads, slot state machine, buffer pool, uploads, streams and events) built against
+#    the CPU stand-in of the HIP runtime (tests/helpers/fake_hip) and the CPU fakes of its device
+#    functions (tests/helpers/fake_dev.cpp), driven through every mode of the run by
+#    tests/helpers/run_fake.cpp, which checks every byte the sink gets against independently
+#    produced rows;
+#  * the host plane alone (scenario, chains, proofs, worker pools, the CLI parser) in
+#    tests/helpers/run_harness.c's arrangement of the same threads.
+# Logs go to $OUT (default profiles/round5/sanitize).
 set -o pipefail
 cd "$(dirname "$0")/.."
-OUT=${OUT:-profiles/round4/sanitize}
+OUT=${OUT:-profiles/round5/sanitize}
 SECS=${SECS:-300}
 mkdir -p $OUT /tmp/gss_san
 SRC="gps-sdr-sim_amd/csrc/host/*.c gps-sdr-sim_amd/csrc/cli/cli_args.c tests/helpers/run_harness.c"
 CF="-O1 -g -fno-omit-frame-pointer -ffp-contract=off -fno-fast-math -D_FILE_OFFSET_BITS=64 -Iinclude"
 NAV=tests/golden/data/brdc3540.14n
 rc=0
+FK="tests/helpers/fake_hip/fake_hip.cpp tests/helpers/fake_dev.cpp tests/helpers/run_fake.cpp"
 for san in thread address,undefined; do
     tag=${san%%,*}
+    # gss_run on the fake device: C host sources by gcc, the C++ ones by g++
+    d=/tmp/gss_san/fake_$tag
+    mkdir -p $d
+    for f in gps-sdr-sim_amd/csrc/host/*.c gps-sdr-sim_amd/csrc/cli/cli_args.c; do
+        gcc $CF -fsanitize=$san -c $f -o $d/$(basename ${f%.c}).o || exit 1
+    done
+    g++ -std=c++17 $CF -Itests/helpers -Itests/helpers/fake_hip -fsanitize=$san -x c++ \
+        -c gps-sdr-sim_amd/csrc/hip/gss_run.hip -o $d/gss_run.o || exit 1
+    for f in $FK; do
+        g++ -std=c++17 $CF -Itests/helpers -Itests/helpers/fake_hip -fsanitize=$san -c $f \
+            -o $d/$(basename ${f%.cpp}).o || exit 1
+    done
+    g++ -fsanitize=$san -o $d/run_fake $d/*.o -lm -lpthread || exit 1
+    for args in "70 64 1" "40 16 8" "300 512 1"; do
+        log=$OUT/gss_run_${tag}_$(echo $args | tr ' ' _).log
+        echo "== -fsanitize=$san, gss_run on the fake device: run_fake $args" > $log
+        TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" \
+        ASAN_OPTIONS="detect_leaks=1 halt_on_error=1" UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1" \
+            timeout -k 10 1800 $d/run_fake $NAV $args >> $log 2>&1
+        r=$?
+        echo "exit $r" >> $log
+        grep -c "WARNING: ThreadSanitizer\|ERROR: AddressSanitizer\|runtime error\|LeakSanitizer" $log \
+            | sed 's/^/sanitizer reports: /' >> $log
+        tail -3 $log
+        [ $r -eq 0 ] || rc=1
+    done
     exe=/tmp/gss_san/run_harness_$tag
     gcc $CF -fsanitize=$san $SRC -o $exe -lm -lpthread || exit 1
     for args in "$SECS 512 1" "60 64 16"; do
