@@ -1204,40 +1204,92 @@ GSS_HD void gss_spec_seg_walk(const gss_spec_in_t *in, int j, int64_t n, gss_spe
     sg->wrap_end = we;
 }
 
-/* The block's exact end from its true start x and the row's speculative walk (*hit = 1 where the
-   translation carried through every segment). */
-GSS_HD double gss_spec_fix(double x, int64_t n, const gss_spec_in_t *in, const gss_spec_t *o,
-                           int *hit)
+/* From the row's exact post-wrap value v at its first wrap (pos = o->p1): the segments'
+   translations while they hold, then the exact walk.  *hit = 1 where every segment translated;
+   *dlast = the translation of the last segment (the row's end is its end + *dlast). */
+GSS_HD double gss_spec_fix_at(double v, int64_t n, const gss_spec_in_t *in, const gss_spec_t *o,
+                              int *hit, double *dlast)
 {
     const double s = in->s;
     const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
+    int64_t pos = o->p1;
+    double d = v - o->w1;                       /* exact: both on the post-wrap lattice */
+    int j = 0;
+    *hit = 0;
+    for (; j < k; j++) {
+        const gss_spec_seg_t *sg = &o->seg[j];
+        if (!(d >= sg->dlo && d <= sg->dhi))
+            break;                              /* v is still the exact value at pos */
+        v = sg->end + d;
+        pos = j + 1 < k ? in->P[j + 1] : n;
+        if (j + 1 < k) {
+            if (!sg->wrap_end) { j++; break; }   /* exact at pos, but not post-wrap */
+            d = v - in->W[j + 1];
+        }
+    }
+    if (j == k && pos == n) {
+        *hit = 1;
+        *dlast = d;
+        return v;
+    }
+    return gss_carr_walk_cc(v, s, n - pos);
+}
+
+/* The block's exact end from its true start x and the row's speculative walk: x to its first
+   wrap exactly (one partial cycle), then gss_spec_fix_at where that wrap is the guess's. */
+GSS_HD double gss_spec_fix_d(double x, int64_t n, const gss_spec_in_t *in, const gss_spec_t *o,
+                             int *hit, double *dlast)
+{
+    const double s = in->s;
     *hit = 0;
     double v = x;
     int wr = 0;
     const int64_t t = gss_carr_to_wrap(&v, s, n, &wr);
     if (!wr || t >= n)
         return v;                               /* no wrap: v is the end, walked exactly */
-    int64_t pos = t;
-    if (t == o->p1) {
-        double d = v - o->w1;                   /* exact: both on the post-wrap lattice */
-        int j = 0;
-        for (; j < k; j++) {
-            const gss_spec_seg_t *sg = &o->seg[j];
-            if (!(d >= sg->dlo && d <= sg->dhi))
-                break;                          /* v is still the exact value at pos */
-            v = sg->end + d;
-            pos = j + 1 < k ? in->P[j + 1] : n;
-            if (j + 1 < k) {
-                if (!sg->wrap_end) { j++; break; }   /* exact at pos, but not post-wrap */
-                d = v - in->W[j + 1];
-            }
+    if (t == o->p1)
+        return gss_spec_fix_at(v, n, in, o, hit, dlast);
+    return gss_carr_walk_cc(v, s, n - t);
+}
+
+GSS_HD double gss_spec_fix(double x, int64_t n, const gss_spec_in_t *in, const gss_spec_t *o,
+                           int *hit)
+{
+    double d;
+    return gss_spec_fix_d(x, n, in, o, hit, &d);
+}
+
+/* gss_carr_to_wrap with the admissible translations [*dlo, *dhi] of the start (lattice 2^-52
+   ascending, 2^-53 descending: the chain's translations), for a start anywhere in [0, 1): the
+   link from a row's speculative end to the next row's first wrap (gss_spec_links). */
+GSS_HD int64_t gss_carr_to_wrap_margins(double *x, double s, int64_t n, int *wr, double *dlo,
+                                        double *dhi)
+{
+    *wr = 0;
+    if (s > 0.0)
+        return gss_asc_to_wrap(x, s, 1.0, n, wr, dlo, dhi);
+    const double T = gss_pow2(gss_exp2i(-s) + 2);
+    const double dunit = gss_pow2(-53);
+    double v = *x;
+    int st = 0;
+    int64_t taken = gss_desc_head(&v, s, T, n, &st, dlo, dhi);
+    while (st && taken < n) {                   /* below T: real steps to the wrap */
+        gss_margin_step(v, s, dunit, dlo, dhi);
+        const double r = v + s;
+        taken++;
+        if (r < 0.0) {
+            const double lim = -r - 2.0 * dunit;
+            if (lim < *dhi) *dhi = lim;
+            gss_margin_step(r, 1.0, dunit, dlo, dhi);
+            v = r + 1.0;
+            *wr = 1;
+            break;
         }
-        if (j == k && pos == n) {
-            *hit = 1;
-            return v;
-        }
+        if (-r > *dlo) *dlo = -r;
+        v = r;
     }
-    return gss_carr_walk_cc(v, s, n - pos);
+    *x = v;
+    return taken;
 }
 
 /* ---- code iterator ---------------------------------------------------------------------- */

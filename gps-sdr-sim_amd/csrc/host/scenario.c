@@ -655,6 +655,167 @@ int gss_carr_chain_spec(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
     return 0;
 }
 
+/* ---- links between a slot's consecutive rows (gss_spec_links / gss_carr_chain_linked) --------
+ * Where row e' of a slot translated by d (its end = its last segment's end + d), the next row e of
+ * the slot starts at y + d, y = that segment's end: known before the chain runs.  So e's partial
+ * cycle to its first wrap is walked from y ahead of time with the admissible translations of y,
+ * and e's whole walk folds into one record: e translates iff d is in [lo, hi], and then its own
+ * last translation is d + dd and its end is end + (d + dd).  Exact: every translation the record
+ * chains (d_0 = d + (w1' - w1), d_j+1 = d_j + (end_j - W_j+1)) is a sum of post-wrap lattice
+ * values (multiples of 2^-52 ascending, 2^-53 descending, below 2 in magnitude), so the double
+ * arithmetic carries it exactly, and the bounds lo_j - c_j are rounded inward. */
+typedef struct {
+    const int32_t *nch;
+    const gss_chain_t *chain;
+    const gss_spec_in_t *in;
+    const gss_spec_t *spec;
+    gss_spec_link_t *link;
+    int nblk, n_per_blk;
+} link_job;
+
+/* the record of row e entered from y (the previous row's last segment end); 0: none */
+static int link_row(double y, const gss_spec_in_t *in, const gss_spec_t *o, int64_t n,
+                    gss_spec_link_t *L)
+{
+    const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
+    double a = -GSS_BIG, b = GSS_BIG;
+    int wr = 0;
+    double x = y;
+    const int64_t t = gss_carr_to_wrap_margins(&x, in->s, n, &wr, &a, &b);
+    if (!wr || t >= n || t != o->p1 || !(a <= b))
+        return 0;
+    double c = x - o->w1;                        /* d_0 = d + c */
+    double lo = a, hi = b;
+    for (int j = 0; j < k; j++) {
+        const gss_spec_seg_t *sg = &o->seg[j];
+        if (!(sg->dlo <= sg->dhi))
+            return 0;
+        const double l = nextafter(sg->dlo - c, GSS_BIG), h = nextafter(sg->dhi - c, -GSS_BIG);
+        if (l > lo) lo = l;
+        if (h < hi) hi = h;
+        if (j + 1 < k) {
+            if (!sg->wrap_end)
+                return 0;                        /* the walk goes on exactly: no record */
+            c += sg->end - in->W[j + 1];
+        }
+    }
+    if (!(lo <= hi))
+        return 0;
+    L->lo = lo;
+    L->hi = hi;
+    L->dd = c;
+    L->end = o->seg[k - 1].end;
+    return 1;
+}
+
+static void link_slot_part(void *arg, int slot)
+{
+    const link_job *j = arg;
+    int64_t prev = -1;
+    for (int b = 0; b < j->nblk; b++)
+        for (int k = 0; k < j->nch[b]; k++) {
+            const size_t e = (size_t)b * GSS_MAXCH + k;
+            if (j->chain[e].slot != slot)
+                continue;
+            gss_spec_link_t *L = &j->link[e];
+            L->lo = 1.0;                          /* an empty interval: no record */
+            L->hi = 0.0;
+            L->dd = L->end = 0.0;
+            if (prev >= 0 && !j->chain[e].reset && j->in[e].s != 0.0 && j->in[prev].s != 0.0) {
+                const gss_spec_in_t *pi = &j->in[prev];
+                const int kp = pi->k < 1 ? 1 : (pi->k > GSS_SPEC_K ? GSS_SPEC_K : pi->k);
+                if (!link_row(j->spec[prev].seg[kp - 1].end, &j->in[e], &j->spec[e],
+                              j->n_per_blk, L)) {
+                    L->lo = 1.0;
+                    L->hi = 0.0;
+                }
+            }
+            prev = (int64_t)e;
+            break;
+        }
+}
+
+int gss_spec_links(const int32_t *nch, const gss_chain_t *chain, int nblk, int n_per_blk,
+                   const gss_spec_in_t *in, const gss_spec_t *spec, gss_spec_link_t *link,
+                   int threads)
+{
+    if (nblk < 0 || n_per_blk <= 0 ||
+        (nblk > 0 && (nch == NULL || chain == NULL || in == NULL || spec == NULL || link == NULL)))
+        return gss_fail(GSS_E_ARG, "invalid spec-link arguments");
+    for (size_t e = 0; e < (size_t)nblk * GSS_MAXCH; e++) {
+        link[e].lo = 1.0;
+        link[e].hi = 0.0;
+        link[e].dd = link[e].end = 0.0;
+    }
+    const link_job j = {nch, chain, in, spec, link, nblk, n_per_blk};
+    gss_pool_run(threads, K_MAX_CHAN, link_slot_part, (void *)&j);      /* one part per slot */
+    return 0;
+}
+
+typedef struct {
+    double *carr;
+    gss_chan_blk_t *blk;
+    const int32_t *nch;
+    const gss_chain_t *chain;
+    const gss_spec_in_t *in;
+    const gss_spec_t *spec;
+    const gss_spec_link_t *link;
+    int nblk, n_per_blk;
+    int hits[K_MAX_CHAN];
+} linked_job;
+
+static void linked_slot_part(void *arg, int slot)
+{
+    linked_job *j = arg;
+    double x = j->carr[slot], d = 0.0;
+    int hits = 0, held = 0;
+    for (int b = 0; b < j->nblk; b++)
+        for (int k = 0; k < j->nch[b]; k++) {
+            const size_t e = (size_t)b * GSS_MAXCH + k;
+            if (j->chain[e].slot != slot)
+                continue;
+            if (j->chain[e].reset) {
+                x = j->chain[e].init;
+                held = 0;
+            }
+            j->blk[e].carr0 = x;
+            const gss_spec_link_t *L = &j->link[e];
+            int hit = 0;
+            if (held && d >= L->lo && d <= L->hi) {
+                d += L->dd;
+                x = L->end + d;
+                hit = 1;
+            } else {
+                x = gss_spec_fix_d(x, j->n_per_blk, &j->in[e], &j->spec[e], &hit, &d);
+            }
+            held = hit;
+            hits += hit;
+            break;
+        }
+    j->carr[slot] = x;
+    j->hits[slot] = hits;
+}
+
+int gss_carr_chain_linked(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
+                          const gss_chain_t *chain, int nblk, int n_per_blk,
+                          const gss_spec_in_t *in, const gss_spec_t *spec,
+                          const gss_spec_link_t *link, int threads, int *n_hit)
+{
+    if (carr == NULL || nblk < 0 || n_per_blk <= 0 ||
+        (nblk > 0 && (blk == NULL || nch == NULL || chain == NULL || in == NULL || spec == NULL ||
+                      link == NULL)))
+        return gss_fail(GSS_E_ARG, "invalid carrier-chain arguments");
+    linked_job j = {carr, blk, nch, chain, in, spec, link, nblk, n_per_blk, {0}};
+    gss_pool_run(threads, K_MAX_CHAN, linked_slot_part, (void *)&j);
+    if (n_hit) {
+        int h = 0;
+        for (int i = 0; i < K_MAX_CHAN; i++)
+            h += j.hits[i];
+        *n_hit = h;
+    }
+    return 0;
+}
+
 /* ---- per-block ranges in parallel --------------------------------------------------------------
  * The per-block refresh (gpssim.c:2156-2188) needs computeRange for every active channel of
  * every block, and block b only uses its own range and block b-1's.  Between two 30 s updates the

@@ -59,6 +59,8 @@ assert SPEC_IN_DTYPE.itemsize == 152
 SPEC_SEG_DTYPE = np.dtype([("end", "<f8"), ("dlo", "<f8"), ("dhi", "<f8"), ("wrap_end", "<i8")])
 SPEC_DTYPE = np.dtype([("p1", "<i8"), ("w1", "<f8"), ("seg", SPEC_SEG_DTYPE, (SPEC_K,))])
 assert SPEC_DTYPE.itemsize == 272
+SPEC_LINK_DTYPE = np.dtype([("lo", "<f8"), ("hi", "<f8"), ("dd", "<f8"), ("end", "<f8")])
+assert SPEC_LINK_DTYPE.itemsize == 32
 # gss_nav_src_t: one nav-table row's source for the GPU producer (include/gpssim_amd.h)
 NAV_SRC_DTYPE = np.dtype([("sbf", "<u4", (5, 10)), ("tow", "<u4"), ("wn", "<u4"), ("prev", "<i4"),
                           ("next", "<i4"), ("head", "<u4", (10,))])
@@ -142,6 +144,9 @@ _SIGS = {
     "gss_spec_device": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, _P]),
     "gss_carr_chain_spec": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P, C.c_int,
                                       C.POINTER(C.c_int)]),
+    "gss_spec_links": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, _P, _P, C.c_int]),
+    "gss_carr_chain_linked": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P, _P, C.c_int,
+                                        C.POINTER(C.c_int)]),
     "gss_scn_seek": (C.c_int, [_P, C.c_int64, C.c_int]),
     "gss_scn_carrier": (C.c_int, [_P, _P]),
     "gss_scn_set_carrier": (C.c_int, [_P, _P]),
@@ -509,6 +514,37 @@ def carr_chain_spec(carr, blk, nch, chain, n_per_blk, gi, spec, threads=8):
     _check(lib().gss_carr_chain_spec(_ptr(c), _ptr(blk), _ptr(nch), _ptr(chain), len(nch),
                                      int(n_per_blk), _ptr(gi), _ptr(spec), threads,
                                      C.byref(hit)))
+    return c, hit.value
+
+
+def spec_links(nch, chain, n_per_blk, gi, spec, threads=8):
+    """Each row's link from its slot's previous row (gss_spec_links): SPEC_LINK_DTYPE [nb, 16]."""
+    nch = np.ascontiguousarray(nch, np.int32)
+    chain = np.ascontiguousarray(chain, CHAIN_DTYPE)
+    gi = np.ascontiguousarray(gi, SPEC_IN_DTYPE)
+    spec = np.ascontiguousarray(spec, SPEC_DTYPE)
+    assert spec.size == gi.size == len(nch) * MAXCH
+    link = np.zeros((len(nch), MAXCH), SPEC_LINK_DTYPE)
+    _check(lib().gss_spec_links(_ptr(nch), _ptr(chain), len(nch), int(n_per_blk), _ptr(gi),
+                                _ptr(spec), _ptr(link), threads))
+    return link
+
+
+def carr_chain_linked(carr, blk, nch, chain, n_per_blk, gi, spec, link, threads=8):
+    """carr_chain_spec's result with the rows' links (gss_carr_chain_linked): fills blk["carr0"]
+    in place; returns (carrier after the last block, blocks where the translation held)."""
+    c = np.array(carr, np.float64, copy=True)
+    assert c.shape == (MAXCH,) and blk.flags.c_contiguous and blk.dtype == CHAN_DTYPE
+    nch = np.ascontiguousarray(nch, np.int32)
+    chain = np.ascontiguousarray(chain, CHAIN_DTYPE)
+    gi = np.ascontiguousarray(gi, SPEC_IN_DTYPE)
+    spec = np.ascontiguousarray(spec, SPEC_DTYPE)
+    link = np.ascontiguousarray(link, SPEC_LINK_DTYPE)
+    assert spec.size == gi.size == link.size == len(nch) * MAXCH
+    hit = C.c_int(0)
+    _check(lib().gss_carr_chain_linked(_ptr(c), _ptr(blk), _ptr(nch), _ptr(chain), len(nch),
+                                       int(n_per_blk), _ptr(gi), _ptr(spec), _ptr(link), threads,
+                                       C.byref(hit)))
     return c, hit.value
 
 

@@ -30,7 +30,7 @@ import time
 import numpy as np
 
 from . import (MAXCH, SPEC_DTYPE, SPEC_IN_DTYPE, Scenario, carr_chain, carr_chain_guess,
-               carr_chain_spec, spec_host)
+               carr_chain_linked, carr_chain_spec, carr_line_end, spec_host, spec_links)
 
 SPEC_CHUNK = 4096                # blocks per run-ahead chunk (gss_run.hip chain_upfront_spec)
 
@@ -103,6 +103,7 @@ class Baton:
     def __init__(self, dist, rank, world, device="cpu"):
         import torch
         self.torch, self.dist, self.rank, self.world, self.device = torch, dist, rank, world, device
+        self._pending = None
 
     def recv(self):
         t = self.torch.empty(MAXCH, dtype=self.torch.float64, device=self.device)
@@ -114,9 +115,159 @@ class Baton:
             t = self.torch.from_numpy(np.ascontiguousarray(carr, np.float64)).to(self.device)
             self.dist.send(t, dst=self.rank + 1)
 
+    def isend(self, carr):
+        """send without waiting for rank r+1 to take it (it may still be in a collective);
+        finish() completes it"""
+        if self.rank + 1 < self.world:
+            t = self.torch.from_numpy(np.ascontiguousarray(carr, np.float64)).to(self.device)
+            self._pending = (t, self.dist.isend(t, dst=self.rank + 1))
+
+    def finish(self):
+        if self._pending is not None:
+            self._pending[1].wait()
+            self._pending = None
+
+    def all_gather(self, vec):
+        """every rank's float64 vector (same length on all ranks), in rank order"""
+        t = self.torch.from_numpy(np.ascontiguousarray(vec, np.float64)).to(self.device)
+        parts = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t)
+        return [p.cpu().numpy() for p in parts]
+
+
+# ---- the chain speculated across ranks -----------------------------------------------------------
+# A rank's window acts on the 16 slot carriers as x -> x + a (mod 1) per slot, or as a constant
+# where allocateChannel re-initialises the slot inside the window (gpssim.c:1615-1626).  Every rank
+# publishes that map (all_gather, 48 doubles) and composes the maps of the ranks before it into a
+# prediction of its start, so its guesses and walks run before the baton arrives:
+#   1. the lines' map (gss_carr_line_end): a start off by ~1e-13 cycle per block before it;
+#   2. walks from that start, the chain from them (gss_carr_chain_spec, exact for that start) and
+#      its map: exact but for the rounding differences where the start's error crossed a margin,
+#      so the second prediction is off by ~1e-13 cycle in all;
+#   3. the rows walked again from the first chain's carriers moved by the correction (rows after
+#      a re-initialisation keep their walks: they do not depend on the start);
+#   4. every row's walk folded with its predecessor's into a link record (gss_spec_links);
+#   5. the baton: the exact start, and gss_carr_chain_linked from it -- a compare and two adds per
+#      row where the translation holds (almost every row) and the exact walk where it does not --
+#      whose end goes on to rank r+1 at once.  Exact in every case; only the time depends on the
+#      guesses.
+SPEC_WALK_ROWS = 1 << 18         # rows per walker call (bounds the pinned buffers)
+
+
+def _live(nch):
+    return np.arange(MAXCH)[None, :] < np.asarray(nch)[:, None]
+
+
+def slot_resets(nch, chain):
+    """[16] bool: slots the window re-initialises (their carrier after it is a constant)"""
+    live = _live(nch)
+    sl = chain["slot"][live].astype(np.int64)
+    ok = (chain["reset"][live] != 0) & (sl >= 0) & (sl < MAXCH)
+    out = np.zeros(MAXCH, bool)
+    out[sl[ok]] = True
+    return out
+
+
+def _start_dependent(nch, chain):
+    """[nb, 16] bool: live rows whose carrier depends on the window's start (no re-initialisation
+    of their slot at or before their block)"""
+    live = _live(nch)
+    nb = len(nch)
+    sl = np.where(live, chain["slot"], -1).astype(np.int64)
+    rs = live & (chain["reset"] != 0) & (sl >= 0)
+    bi = np.broadcast_to(np.arange(nb, dtype=np.int64)[:, None], sl.shape)
+    first = np.full(MAXCH, nb, np.int64)
+    np.minimum.at(first, sl[rs], bi[rs])
+    return live & (sl >= 0) & (bi < first[np.clip(sl, 0, MAXCH - 1)])
+
+
+def map_vec(start, end, resets):
+    """this rank's published map: [start (rank 0's is the run's), add, reset flags]"""
+    add = np.where(resets, end, np.mod(end - start, 1.0))
+    return np.concatenate([np.asarray(start, np.float64), add, resets.astype(np.float64)])
+
+
+def compose_start(maps, rank):
+    """the predicted slot carriers at rank `rank`'s first block from the ranks' maps"""
+    x = np.array(maps[0][:MAXCH], np.float64)
+    for m in maps[:rank]:
+        add, rs = m[MAXCH:2 * MAXCH], m[2 * MAXCH:] != 0
+        x = np.where(rs, add, np.mod(x + add, 1.0))
+    return x
+
+
+def _walk_rows(gi_rows, n_per_blk, walker):
+    """the walker over a 1-D array of rows, SPEC_WALK_ROWS at a time (gi_rows written back)"""
+    spec = np.zeros(len(gi_rows), SPEC_DTYPE)
+    for i in range(0, len(gi_rows), SPEC_WALK_ROWS):
+        part = gi_rows[i:i + SPEC_WALK_ROWS]
+        spec[i:i + len(part)] = walker(part, n_per_blk).reshape(-1)
+    return spec
+
+
+def chain_speculated(scn_carr, blk, nch, chain, n_per_blk, walker, baton, threads=8):
+    """The window's chain with the walks run before the baton (steps 1-4 above): fills
+    blk["carr0"]; returns (end carriers, timings).  Every rank of the baton's group calls it (two
+    all_gathers); rank 0 passes the run's initial carriers as scn_carr."""
+    t = {}
+    t0 = time.perf_counter()
+    rank = baton.rank
+    resets = slot_resets(nch, chain)
+    nb = len(nch)
+    zero = np.zeros(MAXCH)
+    line_end = (carr_line_end(zero, blk, nch, chain, n_per_blk) if nb else zero)
+    start0 = scn_carr if rank == 0 else zero
+    maps = baton.all_gather(map_vec(start0, line_end, resets))
+    x0 = np.array(scn_carr, np.float64) if rank == 0 else compose_start(maps, rank)
+    gi = carr_chain_guess(x0, blk, nch, chain, n_per_blk, starts_only=True)
+    spec = _walk_rows(gi.reshape(-1), n_per_blk, walker).reshape(gi.shape)
+    first = blk if rank == 0 else blk.copy()
+    e0, hits = carr_chain_spec(x0, first, nch, chain, n_per_blk, gi, spec, threads=threads)
+    if rank == 0:                            # the exact chain: on to rank 1 at once
+        baton.isend(e0)
+        t["fix_s"] = time.perf_counter() - t0
+    maps = baton.all_gather(map_vec(x0 if rank else scn_carr, e0, resets))
+    rewalked = 0
+    if rank > 0:
+        x1 = compose_start(maps, rank)
+        d = np.mod(x1 - x0 + 0.5, 1.0) - 0.5
+        dep = _start_dependent(nch, chain) & (d[np.clip(chain["slot"], 0, MAXCH - 1)] != 0.0)
+        if dep.any():
+            gi2 = gi[dep]
+            sl = chain["slot"][dep].astype(np.int64)
+            gi2["g"] = np.mod(first["carr0"][dep] + d[sl], 1.0)
+            gi2["k"] = 0
+            spec[dep] = _walk_rows(gi2, n_per_blk, walker)
+            gi[dep] = gi2
+            rewalked = int(dep.sum())
+        link = spec_links(nch, chain, n_per_blk, gi, spec, threads=threads)
+        t["pre_s"] = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        x = baton.recv()
+        t["wait_s"] = time.perf_counter() - t1
+        t1 = time.perf_counter()
+        e0, hits = carr_chain_linked(x, blk, nch, chain, n_per_blk, gi, spec, link,
+                                     threads=threads)
+        baton.isend(e0)
+        t["fix_s"] = time.perf_counter() - t1
+    baton.finish()
+    t["chain_s"] = time.perf_counter() - t0 - t.get("wait_s", 0.0)
+    t["spec_hits"] = hits
+    t["spec_rewalked"] = rewalked
+    return e0, t
+
+
+def _concat(parts):
+    if parts:
+        return (np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]),
+                np.concatenate([p[2] for p in parts]))
+    from . import CHAIN_DTYPE, CHAN_DTYPE
+    return (np.zeros((0, MAXCH), CHAN_DTYPE), np.zeros(0, np.int32),
+            np.zeros((0, MAXCH), CHAIN_DTYPE))
+
 
 def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=True, walker=None,
-                chain_threads=None):
+                chain_threads=None, speculate=True):
     """Rows of blocks [first, first + count) of Scenario scn (count < 0: to the end), planned
     without the blocks before `first` when a baton supplies the carriers there (rank > 0).
     Returns (blk, nch, ck or None, timings {seek_s, rows_s, wait_s, chain_s, spec_hits}).
@@ -127,7 +278,9 @@ def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=Tr
     Without a baton and first > 0 the prefix's carrier chain is planned here (a lone process).
     With a walker (host_walker / device_walker) the window's chain is run ahead
     (chain_run_ahead) and ck is None: the exact path walks the few uncertified blocks from their
-    carr0 (DeviceWindow computes their checkpoints)."""
+    carr0 (DeviceWindow computes their checkpoints).  With a walker and a baton over more than one
+    rank the chain is speculated across ranks (chain_speculated; speculate=False: the baton
+    first, then the chain run ahead)."""
     t = {}
     t0 = time.perf_counter()
     carr = None
@@ -153,20 +306,21 @@ def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=Tr
         parts.append((b, n, c))
         done += len(n)
     t["rows_s"] = time.perf_counter() - t0
+    speculate = (carr is None and walker is not None and baton is not None and baton.world > 1
+                 and speculate)
+    if speculate:
+        blk, nch, chain = _concat(parts)
+        end, tc = chain_speculated(scn.carrier() if baton.rank == 0 else None, blk, nch, chain,
+                                   scn.n_per_blk, walker, baton, threads=chain_threads or threads)
+        t.update(tc)
+        t.setdefault("wait_s", 0.0)
+        return blk, nch, None, t
     t0 = time.perf_counter()
     if carr is None:
         carr = baton.recv() if (baton is not None and baton.rank > 0) else scn.carrier()
     t["wait_s"] = time.perf_counter() - t0
     t0 = time.perf_counter()
-    if parts:
-        blk = np.concatenate([p[0] for p in parts])
-        nch = np.concatenate([p[1] for p in parts])
-        chain = np.concatenate([p[2] for p in parts])
-    else:
-        from . import CHAIN_DTYPE, CHAN_DTYPE
-        blk = np.zeros((0, MAXCH), CHAN_DTYPE)
-        nch = np.zeros(0, np.int32)
-        chain = np.zeros((0, MAXCH), CHAIN_DTYPE)
+    blk, nch, chain = _concat(parts)
     ct = chain_threads or threads
     if walker is not None and len(nch):
         end, t["spec_hits"] = chain_run_ahead(carr, blk, nch, chain, scn.n_per_blk, walker,
@@ -182,7 +336,7 @@ def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=Tr
 
 
 def plan_rank(nav_file, rank, world, window_s, *, llh, samp_freq=2.6e6, data_format=16,
-              threads=8, batch=2000, baton=None, walker=None, chain_threads=None):
+              threads=8, batch=2000, baton=None, walker=None, chain_threads=None, speculate=True):
     """Host plane for one rank: (blk[n, 16], nch[n], ck[n, 16, NCK] or None, nav rows,
     n_per_blk, timings) of its block range (ck: the carrier checkpoints).  With world > 1 pass a
     Baton: the rank then plans only its own window (module docstring)."""
@@ -190,7 +344,8 @@ def plan_rank(nav_file, rank, world, window_s, *, llh, samp_freq=2.6e6, data_for
     scn = Scenario(nav_file, llh=llh, duration=window_s * world if world > 1 else window_s,
                    samp_freq=samp_freq, data_format=data_format)
     blk, nch, ck, t = plan_window(scn, first, count, baton=baton, threads=threads, batch=batch,
-                                  walker=walker, chain_threads=chain_threads)
+                                  walker=walker, chain_threads=chain_threads,
+                                  speculate=speculate)
     if len(nch) != count:
         raise RuntimeError(f"rank {rank}: planned {len(nch)} of {count} blocks")
     t["rows_out"] = int(scn.position()[1])

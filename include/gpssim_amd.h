@@ -339,6 +339,27 @@ int gss_carr_chain_spec(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
                         const gss_chain_t *chain, int nblk, int n_per_blk,
                         const gss_spec_in_t *in, const gss_spec_t *spec, int threads,
                         int *n_hit);
+/* Links between a slot's consecutive rows, computed before the chain's start is known (the
+   multi-rank planner runs them ahead of the baton; gpssim_amd/shard.py chain_speculated):
+     gss_spec_links         for every row that continues its slot's chain in the batch, its
+                            whole walk folded into one record from the previous row's
+                            speculative end (its partial cycle to the first wrap walked from
+                            there ahead of time, with the admissible translations)
+     gss_carr_chain_linked  gss_carr_chain_spec's result, where a row whose predecessor's
+                            translation held is one compare and two adds: the serial part is then
+                            a few ns per row, plus the exact walks where a translation fails. */
+typedef struct gss_spec_link {
+    double lo, hi;                     /* the previous row translated by d in [lo, hi] (lo > hi:
+                                          no record): this row translates too ...               */
+    double dd, end;                    /* ... by d + dd, and ends at end + (d + dd)             */
+} gss_spec_link_t;                     /* 32 bytes */
+int gss_spec_links(const int32_t *nch, const gss_chain_t *chain, int nblk, int n_per_blk,
+                   const gss_spec_in_t *in, const gss_spec_t *spec, gss_spec_link_t *link,
+                   int threads);
+int gss_carr_chain_linked(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
+                          const gss_chain_t *chain, int nblk, int n_per_blk,
+                          const gss_spec_in_t *in, const gss_spec_t *spec,
+                          const gss_spec_link_t *link, int threads, int *n_hit);
 /* Move to run block `block` (>= the next block) without producing the blocks in between: only the
    30 s updates are replayed (nav frames, ephemeris steps, allocation), and the ranges of the
    block before the target (rho0 of computeCodePhase).  The slot carriers are unknown afterwards:

@@ -220,6 +220,41 @@ def test_speculative_chain_exact_with_wrong_guesses():
             assert hit < 0.05 * int(nch.sum()), (mode, hit)
 
 
+@pytest.mark.parametrize("kind,pert", [("static", 0.0), ("static", 3e-10), ("circle", 1e-9),
+                                       ("static", 1e-4)])
+def test_linked_chain_equals_exact_chain(kind, pert):
+    """gss_spec_links + gss_carr_chain_linked (the multi-rank planner's chain after the baton,
+    shard.chain_speculated): each row's walk folded with its predecessor's into one record ahead
+    of time, the chain then a compare and two adds per row where the translation holds.  Bit
+    for bit the exact chain's carr0 and end carriers, over a whole window guessed from a start
+    off by `pert` (1e-4: no translation holds, every row walked exactly), with the same blocks
+    translated as gss_carr_chain_spec."""
+    if kind == "static":
+        s = G.Scenario(NAV, llh=LOC, duration=300.0)
+    else:
+        s = G.Scenario(NAV, motion_file=CIRCLE, duration=300.0)
+    n = s.n_per_blk
+    b0, n0, c0 = s.next_deferred(100, threads=8)        # the slots' first rows are resets:
+    carr, _ = G.carr_chain(s.carrier(), b0, n0, c0, n, with_ck=False)   # start after them
+    blk, nch, chain = s.next_deferred(2900, threads=8)
+    ref = blk.copy()
+    end_ref, _ = G.carr_chain(carr, ref, nch, chain, n, with_ck=False)
+    gi = G.carr_chain_guess(np.mod(carr + pert, 1.0), blk, nch, chain, n, starts_only=True)
+    spec = G.spec_host(gi, n, threads=8)
+    link = G.spec_links(nch, chain, n, gi, spec, threads=8)
+    b1, b2 = blk.copy(), blk.copy()
+    end1, hit1 = G.carr_chain_spec(carr, b1, nch, chain, n, gi, spec)
+    end2, hit2 = G.carr_chain_linked(carr, b2, nch, chain, n, gi, spec, link)
+    assert b2["carr0"].tobytes() == ref["carr0"].tobytes()
+    assert end2.tobytes() == end_ref.tobytes()
+    assert hit2 == hit1
+    rows = int(nch.sum())
+    if pert < 1e-6:
+        assert hit2 >= 0.97 * rows and (link["lo"] <= link["hi"]).sum() >= 0.95 * rows
+    else:
+        assert hit2 < 0.05 * rows, (hit2, rows)
+
+
 def test_worker_pool_after_fork():
     """The host plane's persistent worker threads do not survive fork(): a child that plans
     (gss_pool_run on 8 threads) after the parent has grown its pools must still finish, with the
@@ -269,14 +304,15 @@ def test_plan_window_chain_run_ahead(fmt, fs, dur, first, count):
 
 
 def test_host_threads_under_sanitizers(tmp_path):
-    """gss_run's host threads (rows / planner / prover, each on its own worker pool) over the host
-    plane's C sources, built with ThreadSanitizer and with AddressSanitizer + UBSan
-    (tools/sanitize.sh, tests/helpers/run_harness.c): no report, rows equal the serial chain."""
+    """gss_run itself on the CPU fake of the HIP runtime (tests/helpers/run_fake.cpp, every run
+    mode) and the host plane's threads (tests/helpers/run_harness.c), built with ThreadSanitizer
+    and with AddressSanitizer + UBSan (tools/sanitize.sh, shortened here; the committed logs under
+    profiles/round5/sanitize are the full runs): no report, every byte as expected."""
     import os
     import subprocess
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run(["bash", os.path.join(repo, "tools", "sanitize.sh")],
-                       env=dict(os.environ, SECS="60", OUT=str(tmp_path)),
+                       env=dict(os.environ, SECS="60", FAKE_ARGS="30 32 8", OUT=str(tmp_path)),
                        capture_output=True, text=True, timeout=900)
     logs = "".join(open(os.path.join(tmp_path, f)).read() for f in sorted(os.listdir(tmp_path)))
     assert r.returncode == 0, logs[-3000:]

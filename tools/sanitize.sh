@@ -9,7 +9,8 @@
 #    produced rows;
 #  * the host plane alone (scenario, chains, proofs, worker pools, the CLI parser) in
 #    tests/helpers/run_harness.c's arrangement of the same threads.
-# Logs go to $OUT (default profiles/round5/sanitize).
+# Logs go to $OUT (default profiles/round5/sanitize).  FAKE_ARGS: the run_fake argument sets
+# (";"-separated "seconds batch fmt"), SECS: run_harness's long run.
 set -o pipefail
 cd "$(dirname "$0")/.."
 OUT=${OUT:-profiles/round5/sanitize}
@@ -35,7 +36,8 @@ for san in thread address,undefined; do
             -o $d/$(basename ${f%.cpp}).o || exit 1
     done
     g++ -fsanitize=$san -o $d/run_fake $d/*.o -lm -lpthread || exit 1
-    for args in "70 64 1" "40 16 8" "300 512 1"; do
+    IFS=';' read -ra fargs <<< "${FAKE_ARGS:-70 64 1;40 16 8;300 512 1}"
+    for args in "${fargs[@]}"; do
         log=$OUT/gss_run_${tag}_$(echo $args | tr ' ' _).log
         echo "== -fsanitize=$san, gss_run on the fake device: run_fake $args" > $log
         TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" \
