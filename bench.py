@@ -707,7 +707,8 @@ def main():
         sustained_ms = round(dev.timing_lin()[1], 3)
     mine = [host_plan_s, plan_t["seek_s"], plan_t["rows_s"], plan_t["wait_s"],
             plan_t["chain_s"], host_lin_s, float(plan_t["rows_out"]),
-            float(plan_t.get("spec_hits", -1))]
+            float(plan_t.get("spec_hits", -1)), plan_t.get("fix_s", -1.0),
+            float(plan_t.get("spec_rewalked", -1))]
     per_rank = [mine]
     if dist:
         t = torch.tensor([elapsed, ck_ms, syn_ms, host_plan_s, lin_ms, host_lin_s],
@@ -723,8 +724,12 @@ def main():
          "rows_s": round(v[2], 3), "baton_wait_s": round(v[3], 3),
          "carrier_chain_s": round(v[4], 3), "host_linearize_s": round(v[5], 3),
          "rows_produced": int(v[6]),
-         "carrier_chain": "run ahead on the GPU" if v[7] >= 0 else "host walk",
-         "spec_rows_translated": int(v[7]) if v[7] >= 0 else None}
+         "carrier_chain": ("speculated across ranks (walks on the GPU)" if v[9] >= 0 else
+                           "run ahead on the GPU" if v[7] >= 0 else "host walk"),
+         "spec_rows_translated": int(v[7]) if v[7] >= 0 else None,
+         # the chain from the baton's arrival to the hand-off to rank r+1 (rank 0: its whole chain)
+         "handoff_s": round(v[8], 3) if v[8] >= 0 else None,
+         "spec_rows_rewalked": int(v[9]) if v[9] >= 0 else None}
         for r, v in enumerate(per_rank)]
 
     samples_rank = nblk * npb
