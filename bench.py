@@ -344,17 +344,22 @@ def time_steps(torch, dev, dev_t, res, steps, warmup, stream):
     return el, n_lin, lin_ms
 
 
-def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None):
+def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None, anch=None):
     """proof + render of the resident window per step (see the module docstring): the proof kernel
     rewrites the window's rows and fast flags in place (byte-identical rows: tests/
     test_gpu_proof.py), then the window renders from them; HIP events on the launch stream time
-    the proof apart"""
+    the proof apart.  anch: the planner's chain anchors (resident like the rows), where the
+    proofs' carrier walks start (gss_linearize_device_ex)"""
     st = torch.cuda.current_stream(dev_t)
+    d_anch = None
+    if anch is not None:
+        d_anch = torch.from_numpy(anch.view("u1").reshape(-1).copy()).to(dev_t)
 
     def prove():
         dev.linearize_device(res.d_blk.data_ptr(), res.d_nch.data_ptr(), res.nblk, res.npb,
                              res.d_ca.data_ptr(), res.n_ca, res.d_nav.data_ptr(), res.n_nav,
-                             res.d_lin.data_ptr(), res.d_fast.data_ptr(), stream)
+                             res.d_lin.data_ptr(), res.d_fast.data_ptr(), stream,
+                             anch_ptr=d_anch.data_ptr() if d_anch is not None else None)
     for _ in range(warmup):
         prove()
         res.step(stream)
@@ -375,7 +380,8 @@ def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None):
            "ms_per_step": round(el / steps * 1e3, 3), "proof_ms": round(proof_ms, 3),
            "steps": steps, "warmup": warmup,
            "workload": "the headline window: proof kernel (gss_linearize_device) + render "
-                       "(gss_synth_lin_device) per step on resident rows"}
+                       "(gss_synth_lin_device) per step on resident rows",
+           "anchors": d_anch is not None}
     if exact:
         out["vs_exact_path"] = round(out["value"] / exact["value"], 3)
     return out
@@ -650,7 +656,8 @@ def main():
     blk, nch, ck, nav, npb, plan_t = plan_rank(NAV, rank, world, args.window, llh=LOC,
                                                samp_freq=FS, data_format=args.fmt,
                                                threads=args.threads, baton=baton, walker=walker,
-                                               chain_threads=args.chain_threads)
+                                               chain_threads=args.chain_threads,
+                                               anchors=single and not args.no_window)
     host_plan_s = time.perf_counter() - t_plan0
     progress(f"planned {len(nch)} blocks in {host_plan_s:.2f} s")
     if dist:
@@ -749,7 +756,8 @@ def main():
                  "ms_per_step": round(el / args.steps * 1e3, 3)}
     window = None
     if single and not args.no_window and res.proof == "gpu":
-        window = window_leg(torch, dev, dev_t, res, args.steps, args.warmup, stream, exact)
+        window = window_leg(torch, dev, dev_t, res, args.steps, args.warmup, stream, exact,
+                            anch=plan_t.get("anch"))
         progress(f"window (proof + render): {window['value']} MS/s, proof {window['proof_ms']} ms")
     ms_per_step = elapsed / args.steps * 1e3
     progress(f"timed {args.steps} steps: {ms_per_step:.3f} ms/step, kernel {lin_ms:.3f} ms")

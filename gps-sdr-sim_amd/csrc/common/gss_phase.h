@@ -1204,13 +1204,31 @@ GSS_HD void gss_spec_seg_walk(const gss_spec_in_t *in, int j, int64_t n, gss_spe
     sg->wrap_end = we;
 }
 
-/* From the row's exact post-wrap value v at its first wrap (pos = o->p1): the segments'
-   translations while they hold, then the exact walk.  *hit = 1 where every segment translated;
-   *dlast = the translation of the last segment (the row's end is its end + *dlast). */
-GSS_HD double gss_spec_fix_at(double v, int64_t n, const gss_spec_in_t *in, const gss_spec_t *o,
-                              int *hit, double *dlast)
+/* The exact walk from v at sample pos to the block end, through the segment starts P[j] (j >= j0)
+   past pos: with av != NULL, av[j] = the exact value at P[j] (the chain's anchors). */
+GSS_HD double gss_spec_walk_rest(double v, int64_t pos, int64_t n, const gss_spec_in_t *in, int k,
+                                 int j0, double *av)
 {
     const double s = in->s;
+    if (av) {
+        for (int j = j0 < 1 ? 1 : j0; j < k; j++) {
+            if (in->P[j] <= pos)
+                continue;
+            v = gss_carr_walk_cc(v, s, in->P[j] - pos);
+            pos = in->P[j];
+            av[j] = v;
+        }
+    }
+    return gss_carr_walk_cc(v, s, n - pos);
+}
+
+/* From the row's exact post-wrap value v at its first wrap (pos = o->p1): the segments'
+   translations while they hold, then the exact walk.  *hit = 1 where every segment translated;
+   *dlast = the translation of the last segment (the row's end is its end + *dlast); av (NULL:
+   none) gets the exact value at every segment start P[j], j >= 1 (gss_spec_walk_rest). */
+GSS_HD double gss_spec_fix_at(double v, int64_t n, const gss_spec_in_t *in, const gss_spec_t *o,
+                              int *hit, double *dlast, double *av)
+{
     const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
     int64_t pos = o->p1;
     double d = v - o->w1;                       /* exact: both on the post-wrap lattice */
@@ -1223,6 +1241,8 @@ GSS_HD double gss_spec_fix_at(double v, int64_t n, const gss_spec_in_t *in, cons
         v = sg->end + d;
         pos = j + 1 < k ? in->P[j + 1] : n;
         if (j + 1 < k) {
+            if (av)
+                av[j + 1] = v;
             if (!sg->wrap_end) { j++; break; }   /* exact at pos, but not post-wrap */
             d = v - in->W[j + 1];
         }
@@ -1232,31 +1252,36 @@ GSS_HD double gss_spec_fix_at(double v, int64_t n, const gss_spec_in_t *in, cons
         *dlast = d;
         return v;
     }
-    return gss_carr_walk_cc(v, s, n - pos);
+    return gss_spec_walk_rest(v, pos, n, in, k, j + 1, av);
 }
 
 /* The block's exact end from its true start x and the row's speculative walk: x to its first
    wrap exactly (one partial cycle), then gss_spec_fix_at where that wrap is the guess's. */
 GSS_HD double gss_spec_fix_d(double x, int64_t n, const gss_spec_in_t *in, const gss_spec_t *o,
-                             int *hit, double *dlast)
+                             int *hit, double *dlast, double *av)
 {
     const double s = in->s;
+    const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
     *hit = 0;
     double v = x;
     int wr = 0;
     const int64_t t = gss_carr_to_wrap(&v, s, n, &wr);
-    if (!wr || t >= n)
-        return v;                               /* no wrap: v is the end, walked exactly */
+    if (!wr || t >= n) {                        /* no wrap: v is the end, walked exactly */
+        if (av && s != 0.0) {                   /* (anchors: walked again, to each P[j]) */
+            return gss_spec_walk_rest(x, 0, n, in, k, 1, av);
+        }
+        return v;
+    }
     if (t == o->p1)
-        return gss_spec_fix_at(v, n, in, o, hit, dlast);
-    return gss_carr_walk_cc(v, s, n - t);
+        return gss_spec_fix_at(v, n, in, o, hit, dlast, av);
+    return gss_spec_walk_rest(v, t, n, in, k, 1, av);
 }
 
 GSS_HD double gss_spec_fix(double x, int64_t n, const gss_spec_in_t *in, const gss_spec_t *o,
                            int *hit)
 {
     double d;
-    return gss_spec_fix_d(x, n, in, o, hit, &d);
+    return gss_spec_fix_d(x, n, in, o, hit, &d, NULL);
 }
 
 /* gss_carr_to_wrap with the admissible translations [*dlo, *dhi] of the start (lattice 2^-52

@@ -251,9 +251,12 @@ GSS_PF int merge_hits(const int64_t *a, int na, const int64_t *b, int nb, int64_
     return n;
 }
 
-/* 1 if certified (lin filled), 0 if this channel needs the exact path */
+/* 1 if certified (lin filled), 0 if this channel needs the exact path.  an (NULL: none): the
+   chain's exact carrier values inside the block (gss_carr_anchor_t), where the carrier walks to
+   the ambiguous samples start instead of at the block start; the rows are the same either way. */
 GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, const uint32_t *ca,
-                       const int32_t *lcos, const int32_t *lsin, gss_lin_t *lin)
+                       const int32_t *lcos, const int32_t *lsin, const gss_carr_anchor_t *an,
+                       gss_lin_t *lin)
 {
     int inexact = 0;
     int64_t hx[LIN_MAXHIT], hz[LIN_MAXHIT], hq[2 * LIN_MAXHIT + 1];
@@ -379,9 +382,14 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
         if (q == 0) {
             cell = (int)floor(x0 * 512.0);
         } else if (near_boundary(X0 + (i128)q * XS, DX1, LIN_CARR_LGB)) {
-#ifndef GSS_PF_ABLATE_CARR_WALK
+            if (an)                                  /* from the last anchor past the walk */
+                for (int a = GSS_SPEC_K - 1; a >= 1; a--)
+                    if (an->pos[a] > xat && an->pos[a] <= q) {
+                        x = an->val[a];
+                        xat = an->pos[a];
+                        break;
+                    }
             x = gss_carr_walk_cc(x, s, q - xat);     /* the reference may differ from the line */
-#endif
             xat = q;
             cell = (int)floor(x * 512.0);
             if (cell > 511)      /* carr += 1.0 rounded to 1.0: the reference reads cosTable512[512]

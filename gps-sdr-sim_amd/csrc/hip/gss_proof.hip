@@ -60,8 +60,8 @@ static constexpr int PF_BLOCKS = 16;          /* blocks per workgroup, one lane 
 __global__ __launch_bounds__(PF_BLOCKS * GSS_MAXCH) void gss_proof_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch, int nblk,
     int n_per_blk, const uint32_t *__restrict__ ca, int n_ca, const uint32_t *__restrict__ nav,
-    int n_nav, proof_lut lut, gss_lin_t *__restrict__ lin, int32_t *__restrict__ fast,
-    int64_t first, int force_exact)
+    int n_nav, proof_lut lut, const gss_carr_anchor_t *__restrict__ anch,
+    gss_lin_t *__restrict__ lin, int32_t *__restrict__ fast, int64_t first, int force_exact)
 {
     __shared__ int32_t lcos[512], lsin[512];
     __shared__ int fail_k[PF_BLOCKS * GSS_MAXCH];
@@ -88,7 +88,8 @@ __global__ __launch_bounds__(PF_BLOCKS * GSS_MAXCH) void gss_proof_kernel(
                 failed = 1;
             } else {
                 int ok = lin_channel(p, n_per_blk, nav + (size_t)p->nav_tbl * GSS_NAV_WORDS,
-                                     ca + (size_t)p->ca_tbl * GSS_CA_WORDS, lcos, lsin, l);
+                                     ca + (size_t)p->ca_tbl * GSS_CA_WORDS, lcos, lsin,
+                                     anch ? anch + (size_t)b * GSS_MAXCH + k : nullptr, l);
                 if (p->gain > 1024 || p->gain < -1024)
                     ok = 0;
                 failed = !ok;
@@ -121,14 +122,14 @@ __global__ __launch_bounds__(PF_BLOCKS * GSS_MAXCH) void gss_proof_kernel(
 /* gss_run's launch (force_exact: its test hook); not exported (exports.map) */
 int run_proof_launch(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
                      const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
-                     gss_lin_t *lin, int32_t *fast, int64_t first, int force_exact,
-                     hipStream_t st)
+                     const gss_carr_anchor_t *anch, gss_lin_t *lin, int32_t *fast,
+                     int64_t first, int force_exact, hipStream_t st)
 {
     if (nblk <= 0)
         return 0;
     hipLaunchKernelGGL(gss_proof_kernel, dim3((unsigned)((nblk + PF_BLOCKS - 1) / PF_BLOCKS)),
                        dim3(PF_BLOCKS * GSS_MAXCH), 0, st, blk, nch, nblk, n_per_blk, ca_bits,
-                       n_ca, nav, n_nav, host_lut(), lin, fast, first, force_exact);
+                       n_ca, nav, n_nav, host_lut(), anch, lin, fast, first, force_exact);
     return hipGetLastError() == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "proof kernel launch");
 }
 
@@ -137,11 +138,21 @@ extern "C" int gss_linearize_device(gss_dev *d, const gss_chan_blk_t *blk, const
                                     const uint32_t *nav, int n_nav, gss_lin_t *lin, int32_t *fast,
                                     void *stream)
 {
+    return gss_linearize_device_ex(d, blk, nch, nblk, n_per_blk, ca_bits, n_ca, nav, n_nav, NULL,
+                                   lin, fast, stream);
+}
+
+extern "C" int gss_linearize_device_ex(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch,
+                                       int nblk, int n_per_blk, const uint32_t *ca_bits, int n_ca,
+                                       const uint32_t *nav, int n_nav,
+                                       const gss_carr_anchor_t *anch, gss_lin_t *lin,
+                                       int32_t *fast, void *stream)
+{
     if (!d || !blk || !nch || !lin || !fast || nblk < 0 || n_per_blk <= 0 ||
         (n_nav > 0 && !nav) || (n_ca > 0 && !ca_bits) || n_ca < 0)
         return gss_fail(GSS_E_ARG, "invalid linearize_device arguments");
     if (hipSetDevice(gss_dev_ordinal(d)) != hipSuccess)
         return gss_fail(GSS_E_HIP, "hipSetDevice");
-    return run_proof_launch(blk, nch, nblk, n_per_blk, ca_bits, n_ca, nav, n_nav, lin, fast, 0, 0,
-                            (hipStream_t)stream);
+    return run_proof_launch(blk, nch, nblk, n_per_blk, ca_bits, n_ca, nav, n_nav, anch, lin, fast,
+                            0, 0, (hipStream_t)stream);
 }

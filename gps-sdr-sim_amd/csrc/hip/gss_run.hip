@@ -170,6 +170,8 @@ struct Slot {
     int nav_first = 0;               /* global row index of the first of them                 */
     gss_lin_t *lin = nullptr;        /* certified lines [nb][GSS_MAXCH] (fast path)      */
     int32_t *fast = nullptr;         /* fast[nb], then the exact-path block list [n_fb] */
+    gss_carr_anchor_t *anch = nullptr;   /* the chain's anchors [nb][GSS_MAXCH] (proofs)   */
+    int has_anch = 0;                /* ... filled for this use of the slot               */
     int n_fb = 0;
     int nb = 0, nch_max = 1;
     int64_t first = 0;               /* run index of the slot's first block */
@@ -308,8 +310,8 @@ static int h2d(const Run &r, void *dst, const void *src, size_t n, hipStream_t s
 }  // namespace
 int run_proof_launch(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
                      const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
-                     gss_lin_t *lin, int32_t *fast, int64_t first, int force_exact,
-                     hipStream_t st);                  /* gss_proof.hip */
+                     const gss_carr_anchor_t *anch, gss_lin_t *lin, int32_t *fast,
+                     int64_t first, int force_exact, hipStream_t st);   /* gss_proof.hip */
 namespace {
 
 static void fill_fb_ck(const Run &r, Slot &sl)
@@ -655,7 +657,9 @@ int spec_launch(Run &r, Run::SpecBatch &b, int ask)
     return 0;
 }
 
-int spec_finish(Run &r, Run::SpecBatch &b, gss_chan_blk_t *blk, int32_t *nch, int *nb_out)
+/* the batch's chain; anch (NULL: none): its anchors for the slot's proofs */
+int spec_finish(Run &r, Run::SpecBatch &b, gss_chan_blk_t *blk, int32_t *nch, int *nb_out,
+                gss_carr_anchor_t *anch)
 {
     b.launched = 0;
     *nb_out = 0;
@@ -669,8 +673,8 @@ int spec_finish(Run &r, Run::SpecBatch &b, gss_chan_blk_t *blk, int32_t *nch, in
     double carr[GSS_MAXCH];                          /* exact: the batches before are done */
     memcpy(carr, r.rows_ahead ? r.carr : b.carr, sizeof carr);
     int hit = 0;
-    int rc = gss_carr_chain_spec(carr, b.blk.data(), b.nch.data(), b.chain.data(), nb,
-                                 r.n_per_blk, b.h_in, b.h_spec, r.threads, &hit);
+    int rc = gss_carr_chain_anchored(carr, b.blk.data(), b.nch.data(), b.chain.data(), nb,
+                                     r.n_per_blk, b.h_in, b.h_spec, r.threads, &hit, anch);
     if (rc)
         return rc;
     if (r.rows_ahead)
@@ -709,6 +713,7 @@ int next_ask(const Run &r, int64_t cursor)
    hand-off, blocks before `first` are planned (the carrier chain is serial) and dropped. */
 int plan_into(Run &r, Slot &sl, int64_t *cursor)
 {
+    sl.has_anch = 0;
     if (r.opts && r.opts->carr_in) {
         int nb = 0;
         int rc = take_upfront(r, sl, &nb);
@@ -763,7 +768,7 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
                     r.fly_end = 1;                     /* the scenario's end */
             }
             if (!rc && r.n_fly > 0) {
-                rc = spec_finish(r, r.sb[r.sb_head], sl.blk, sl.nch, &nb);
+                rc = spec_finish(r, r.sb[r.sb_head], sl.blk, sl.nch, &nb, sl.anch);
                 r.sb_head = (r.sb_head + 1) % 3;
                 r.n_fly--;
             }
@@ -772,7 +777,7 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
             if (!b.launched && ask > 0)
                 rc = spec_launch(r, b, ask);
             if (!rc && b.launched)                     /* else the range is done: nb stays 0 */
-                rc = spec_finish(r, b, sl.blk, sl.nch, &nb);
+                rc = spec_finish(r, b, sl.blk, sl.nch, &nb, sl.anch);
             if (!rc && nb > 0) {                       /* the next batch's walks, on the GPU now */
                 const int ask2 = next_ask(r, *cursor + nb);
                 r.sb_cur ^= 1;
@@ -797,6 +802,7 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
             continue;                                  /* before the range: planned, dropped */
         sl.first = b0;
         sl.nb = nb;
+        sl.has_anch = sl.anch != nullptr && r.spec;
         int m = 1;
         for (int i = 0; i < nb; i++)
             m = sl.nch[i] > m ? sl.nch[i] : m;
@@ -821,8 +827,8 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
         if (r.use_lin && !sl.gpu_proven) {             /* the proofs, on the planner thread */
             if (trace_on())
                 fprintf(stderr, "trace scn_done %.6f\n", tnow());
-            rc = gss_linearize(sl.blk, sl.nch, nb, r.n_per_blk, r.ca, 32, rows, n_rows, sl.lin,
-                               sl.fast, r.threads);
+            rc = gss_linearize_ex(sl.blk, sl.nch, nb, r.n_per_blk, r.ca, 32, rows, n_rows,
+                                  sl.has_anch ? sl.anch : nullptr, sl.lin, sl.fast, r.threads);
             if (rc)
                 return rc;
             int nf = 0;
@@ -886,8 +892,9 @@ void prover(Run *r)
         }
         const double t0 = trace_on() ? tnow() : 0.0;
         if (!sl.end && !sl.err && !sl.gpu_proven) {
-            int rc = gss_linearize(sl.blk, sl.nch, sl.nb, r->n_per_blk, r->ca, 32, sl.lin_nav,
-                                   sl.lin_n_nav, sl.lin, sl.fast, r->threads);
+            int rc = gss_linearize_ex(sl.blk, sl.nch, sl.nb, r->n_per_blk, r->ca, 32, sl.lin_nav,
+                                      sl.lin_n_nav, sl.has_anch ? sl.anch : nullptr, sl.lin,
+                                      sl.fast, r->threads);
             if (rc) {
                 sl.err = rc;
                 sl.end = 1;
@@ -956,6 +963,7 @@ struct SlotDev {
     gss_nav_src_t *src;
     gss_lin_t *lin;
     int32_t *fast;                   /* fast[nb], then the exact-path block list */
+    gss_carr_anchor_t *anch;         /* the chain's anchors (GPU proofs), or null */
     size_t need;
 };
 
@@ -967,9 +975,11 @@ SlotDev slot_dev(const Slot &sl)
     const size_t s_nav = sizeof(gss_nav_src_t) * (size_t)(sl.n_nav > 0 ? sl.n_nav : 1);
     const size_t s_lin = sl.lin ? sizeof(gss_lin_t) * GSS_MAXCH * (size_t)sl.nb : 0;
     const size_t s_fast = sl.lin ? sizeof(int32_t) * 2 * (size_t)sl.nb : 0;
+    const int anch = sl.has_anch && sl.gpu_proven;
+    const size_t s_anch = anch ? sizeof(gss_carr_anchor_t) * GSS_MAXCH * (size_t)sl.nb : 0;
     SlotDev v;
     v.need = al256(s_blk) + al256(s_nch) + al256(s_ck) + al256(s_nav) + al256(s_lin) +
-             al256(s_fast);
+             al256(s_fast) + al256(s_anch);
     uint8_t *p = sl.d_in;
     v.blk = (gss_chan_blk_t *)p;
     v.nch = (int32_t *)(p + al256(s_blk));
@@ -977,6 +987,7 @@ SlotDev slot_dev(const Slot &sl)
     v.src = (gss_nav_src_t *)(p + al256(s_blk) + al256(s_nch) + al256(s_ck));
     v.lin = (gss_lin_t *)((uint8_t *)v.src + al256(s_nav));
     v.fast = (int32_t *)((uint8_t *)v.lin + al256(s_lin));
+    v.anch = anch ? (gss_carr_anchor_t *)((uint8_t *)v.fast + al256(s_fast)) : nullptr;
     return v;
 }
 
@@ -1016,10 +1027,12 @@ int proof_ahead(Run &r, Slot &sl)
     RUN_H2D(v.nch, sl.nch, sizeof(int32_t) * (size_t)sl.nb, sl.pst);
     if (!lazy_ck(r))               /* (with lazy checkpoints only a rejected block needs them) */
         RUN_H2D(v.ck, sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb, sl.pst);
+    if (v.anch)
+        RUN_H2D(v.anch, sl.anch, sizeof(gss_carr_anchor_t) * GSS_MAXCH * (size_t)sl.nb, sl.pst);
     RUN_TRY(hipStreamWaitEvent(sl.pst, sl.navd, 0));
     int rc = run_proof_launch(v.blk, v.nch, sl.nb, r.n_per_blk, r.d_ca, 32, r.d_nav,
-                              n_rows > 0 ? n_rows : 1, v.lin, v.fast, sl.first, r.force_exact,
-                              sl.pst);
+                              n_rows > 0 ? n_rows : 1, v.anch, v.lin, v.fast, sl.first,
+                              r.force_exact, sl.pst);
     if (rc)
         return rc;
     RUN_TRY(hipEventRecord(sl.proved, sl.pst));
@@ -1347,7 +1360,7 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             (void)hipHostFree(sl.nav); (void)hipHostFree(sl.h_status);
             pool_put(sl.h_out, sl.h_out_bytes, true, ordinal);
             pool_put(sl.d_out, sl.d_out_bytes, false, ordinal);
-            (void)hipHostFree(sl.lin); (void)hipHostFree(sl.fast);
+            (void)hipHostFree(sl.lin); (void)hipHostFree(sl.fast); (void)hipHostFree(sl.anch);
             (void)hipFree(sl.d_in); (void)hipFree(sl.d_status);
             if (sl.done) (void)hipEventDestroy(sl.done);
             if (sl.rendered) (void)hipEventDestroy(sl.rendered);
@@ -1455,6 +1468,15 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                                   hipHostMallocDefault) != hipSuccess)
                     err = gss_fail(GSS_E_NOMEM, "run carrier-chain buffers (%zu rows)", rows);
             }
+            /* the chain's anchors for the proofs' carrier walks (GSS_RUN_ANCHORS=0: none) */
+            const char *ea = getenv("GSS_RUN_ANCHORS");
+            if (r.use_lin && !(opts && opts->carr_in) && !(ea && ea[0] == '0'))
+                for (Slot &sl : r.slot) {
+                    if (err) break;
+                    if (hipHostMalloc((void **)&sl.anch, sizeof(gss_carr_anchor_t) * rows,
+                                      hipHostMallocDefault) != hipSuccess)
+                        err = gss_fail(GSS_E_NOMEM, "run anchors (%zu rows)", rows);
+                }
         }
         /* the rows and prover threads where the planner is the limit: slots of >= 1024 blocks
            (-b 1 at 2.6 MS/s: 2,048).  The D2H-bound formats gain nothing from them, and inside

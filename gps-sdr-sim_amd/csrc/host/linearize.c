@@ -113,6 +113,7 @@ typedef struct {
     int n_nav, n_ca, n_per_blk, b_lo, b_hi;
     gss_lin_t *lin;
     int32_t *fast;
+    const gss_carr_anchor_t *anch;
 } lin_job;
 
 static void *lin_run(void *arg)
@@ -141,6 +142,7 @@ static void *lin_run(void *arg)
             }
             ok = lin_channel(p, j->n_per_blk, j->nav + (size_t)p->nav_tbl * GSS_NAV_WORDS,
                              j->ca + (size_t)p->ca_tbl * GSS_CA_WORDS, lut_cosT, lut_sinT,
+                             j->anch ? &j->anch[(size_t)b * GSS_MAXCH + k] : NULL,
                              &j->lin[(size_t)b * GSS_MAXCH + k]);
             if (p->gain > 1024 || p->gain < -1024)    /* an exact f16 MFMA operand, and so is
                                                          its doubled data-bit difference */
@@ -167,13 +169,21 @@ int gss_linearize(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n
                   const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
                   gss_lin_t *lin, int32_t *fast, int threads)
 {
+    return gss_linearize_ex(blk, nch, nblk, n_per_blk, ca_bits, n_ca, nav, n_nav, NULL, lin, fast,
+                            threads);
+}
+
+int gss_linearize_ex(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
+                     const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
+                     const gss_carr_anchor_t *anch, gss_lin_t *lin, int32_t *fast, int threads)
+{
     if (!blk || !nch || !lin || !fast || nblk < 0 || n_per_blk <= 0 || (n_nav > 0 && !nav) ||
         (n_ca > 0 && !ca_bits) || n_ca < 0)
         return gss_fail(GSS_E_ARG, "invalid linearize arguments");
     if (nblk == 0)
         return 0;
     pthread_once(&lut_once, lut_fill);                /* before any worker thread starts */
-    const lin_job all = {blk, nch, nav, ca_bits, n_nav, n_ca, n_per_blk, 0, nblk, lin, fast};
+    const lin_job all = {blk, nch, nav, ca_bits, n_nav, n_ca, n_per_blk, 0, nblk, lin, fast, anch};
     /* one part per block on the pooled workers (blocks differ in their ambiguous samples) */
     gss_pool_run(threads, nblk, lin_part, (void *)&all);
     return 0;

@@ -610,14 +610,37 @@ typedef struct {
     const gss_chain_t *chain;
     const gss_spec_in_t *in;
     const gss_spec_t *spec;
+    gss_carr_anchor_t *anch;
     int nblk, n_per_blk;
     int hits[K_MAX_CHAN];
 } spec_chain_job;
 
+/* one row's end from its true start x; with a != NULL its anchors: the start, and the exact value
+   at every segment start the fix-up passed or walked */
+static double fix_row(double x, int n, const gss_spec_in_t *in, const gss_spec_t *o, int *hit,
+                      double *d, gss_carr_anchor_t *a)
+{
+    if (a == NULL)
+        return gss_spec_fix_d(x, n, in, o, hit, d, NULL);
+    double av[GSS_SPEC_K];
+    for (int j = 0; j < GSS_SPEC_K; j++)
+        av[j] = -1.0;                                /* a carrier value is never negative */
+    const double end = gss_spec_fix_d(x, n, in, o, hit, d, av);
+    const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
+    a->pos[0] = 0;
+    a->val[0] = x;
+    for (int j = 1; j < GSS_SPEC_K; j++) {
+        const int ok = j < k && av[j] >= 0.0 && in->P[j] > 0 && in->P[j] < n;
+        a->pos[j] = ok ? (int32_t)in->P[j] : -1;
+        a->val[j] = ok ? av[j] : 0.0;
+    }
+    return end;
+}
+
 static void spec_slot_part(void *arg, int slot)
 {
     spec_chain_job *j = arg;
-    double x = j->carr[slot];
+    double x = j->carr[slot], d = 0.0;
     int hits = 0;
     for (int b = 0; b < j->nblk; b++)
         for (int k = 0; k < j->nch[b]; k++) {
@@ -628,7 +651,8 @@ static void spec_slot_part(void *arg, int slot)
                 x = j->chain[e].init;
             j->blk[e].carr0 = x;
             int hit = 0;
-            x = gss_spec_fix(x, j->n_per_blk, &j->in[e], &j->spec[e], &hit);
+            x = fix_row(x, j->n_per_blk, &j->in[e], &j->spec[e], &hit, &d,
+                        j->anch ? &j->anch[e] : NULL);
             hits += hit;
             break;
         }
@@ -636,15 +660,30 @@ static void spec_slot_part(void *arg, int slot)
     j->hits[slot] = hits;
 }
 
-int gss_carr_chain_spec(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
-                        const gss_chain_t *chain, int nblk, int n_per_blk,
-                        const gss_spec_in_t *in, const gss_spec_t *spec, int threads,
-                        int *n_hit)
+static void anchors_none(gss_carr_anchor_t *anch, const int32_t *nch, int nblk)
+{
+    for (int b = 0; b < nblk; b++)
+        for (int k = 0; k < GSS_MAXCH; k++) {
+            gss_carr_anchor_t *a = &anch[(size_t)b * GSS_MAXCH + k];
+            for (int j = 0; j < GSS_SPEC_K; j++) {
+                a->pos[j] = -1;
+                a->val[j] = 0.0;
+            }
+        }
+    (void)nch;
+}
+
+int gss_carr_chain_anchored(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
+                            const gss_chain_t *chain, int nblk, int n_per_blk,
+                            const gss_spec_in_t *in, const gss_spec_t *spec, int threads,
+                            int *n_hit, gss_carr_anchor_t *anch)
 {
     if (carr == NULL || nblk < 0 || n_per_blk <= 0 ||
         (nblk > 0 && (blk == NULL || nch == NULL || chain == NULL || in == NULL || spec == NULL)))
         return gss_fail(GSS_E_ARG, "invalid carrier-chain arguments");
-    spec_chain_job j = {carr, blk, nch, chain, in, spec, nblk, n_per_blk, {0}};
+    if (anch)
+        anchors_none(anch, nch, nblk);                /* padding rows: none */
+    spec_chain_job j = {carr, blk, nch, chain, in, spec, anch, nblk, n_per_blk, {0}};
     gss_pool_run(threads, K_MAX_CHAN, spec_slot_part, (void *)&j);   /* one part per slot */
     if (n_hit) {
         int h = 0;
@@ -652,6 +691,50 @@ int gss_carr_chain_spec(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
             h += j.hits[i];
         *n_hit = h;
     }
+    return 0;
+}
+
+int gss_carr_chain_spec(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
+                        const gss_chain_t *chain, int nblk, int n_per_blk,
+                        const gss_spec_in_t *in, const gss_spec_t *spec, int threads,
+                        int *n_hit)
+{
+    return gss_carr_chain_anchored(carr, blk, nch, chain, nblk, n_per_blk, in, spec, threads,
+                                   n_hit, NULL);
+}
+
+/* anchors of rows whose carr0 the chain has set (any chain): in parallel over blocks */
+typedef struct {
+    const gss_chan_blk_t *blk;
+    const int32_t *nch;
+    const gss_spec_in_t *in;
+    const gss_spec_t *spec;
+    gss_carr_anchor_t *anch;
+    int n_per_blk;
+} anchor_job;
+
+static void anchor_part(void *arg, int b)
+{
+    const anchor_job *j = arg;
+    for (int k = 0; k < j->nch[b] && k < GSS_MAXCH; k++) {
+        const size_t e = (size_t)b * GSS_MAXCH + k;
+        int hit = 0;
+        double d = 0.0;
+        (void)fix_row(j->blk[e].carr0, j->n_per_blk, &j->in[e], &j->spec[e], &hit, &d,
+                      &j->anch[e]);
+    }
+}
+
+int gss_carr_anchors(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
+                     const gss_spec_in_t *in, const gss_spec_t *spec, gss_carr_anchor_t *anch,
+                     int threads)
+{
+    if (nblk < 0 || n_per_blk <= 0 ||
+        (nblk > 0 && (blk == NULL || nch == NULL || in == NULL || spec == NULL || anch == NULL)))
+        return gss_fail(GSS_E_ARG, "invalid carrier-anchor arguments");
+    anchors_none(anch, nch, nblk);
+    const anchor_job j = {blk, nch, in, spec, anch, n_per_blk};
+    gss_pool_run(threads, nblk, anchor_part, (void *)&j);
     return 0;
 }
 
@@ -786,7 +869,7 @@ static void linked_slot_part(void *arg, int slot)
                 x = L->end + d;
                 hit = 1;
             } else {
-                x = gss_spec_fix_d(x, j->n_per_blk, &j->in[e], &j->spec[e], &hit, &d);
+                x = gss_spec_fix_d(x, j->n_per_blk, &j->in[e], &j->spec[e], &hit, &d, NULL);
             }
             held = hit;
             hits += hit;

@@ -61,6 +61,9 @@ SPEC_DTYPE = np.dtype([("p1", "<i8"), ("w1", "<f8"), ("seg", SPEC_SEG_DTYPE, (SP
 assert SPEC_DTYPE.itemsize == 272
 SPEC_LINK_DTYPE = np.dtype([("lo", "<f8"), ("hi", "<f8"), ("dd", "<f8"), ("end", "<f8")])
 assert SPEC_LINK_DTYPE.itemsize == 32
+# gss_carr_anchor_t: the chain's exact carrier values inside a block (the proofs' walk starts)
+ANCHOR_DTYPE = np.dtype([("pos", "<i4", (SPEC_K,)), ("val", "<f8", (SPEC_K,))])
+assert ANCHOR_DTYPE.itemsize == 96
 # gss_nav_src_t: one nav-table row's source for the GPU producer (include/gpssim_amd.h)
 NAV_SRC_DTYPE = np.dtype([("sbf", "<u4", (5, 10)), ("tow", "<u4"), ("wn", "<u4"), ("prev", "<i4"),
                           ("next", "<i4"), ("head", "<u4", (10,))])
@@ -145,6 +148,13 @@ _SIGS = {
     "gss_carr_chain_spec": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P, C.c_int,
                                       C.POINTER(C.c_int)]),
     "gss_spec_links": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, _P, _P, C.c_int]),
+    "gss_carr_chain_anchored": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P, C.c_int,
+                                          C.POINTER(C.c_int), _P]),
+    "gss_carr_anchors": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, _P, _P, C.c_int]),
+    "gss_linearize_ex": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_int, _P, C.c_int, _P, _P, _P,
+                                   C.c_int]),
+    "gss_linearize_device_ex": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, _P, C.c_int, _P, C.c_int,
+                                          _P, _P, _P, _P]),
     "gss_carr_chain_linked": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P, _P, C.c_int,
                                         C.POINTER(C.c_int)]),
     "gss_scn_seek": (C.c_int, [_P, C.c_int64, C.c_int]),
@@ -242,18 +252,26 @@ def lut():
     return s, c
 
 
-def linearize(blk, nch, nav, n_per_blk, threads=8, ca=None):
+def linearize(blk, nch, nav, n_per_blk, threads=8, ca=None, anch=None):
     """(lin[nblk, 16] LIN_DTYPE, fast[nblk] int32): the certified integer lines of every block
     (gss_linearize); fast[b] == 1 where the fast path renders block b exactly.  ca: the C/A
-    table the blocks' ca_tbl index (default: ca_table(), PRN 1..32)."""
+    table the blocks' ca_tbl index (default: ca_table(), PRN 1..32).  anch: the chain's anchors
+    (ANCHOR_DTYPE [nblk, 16], gss_linearize_ex): the same rows, shorter carrier walks."""
     blk = np.ascontiguousarray(blk, CHAN_DTYPE)
     nch = np.ascontiguousarray(nch, np.int32)
     nav = np.ascontiguousarray(nav, np.uint32)
     ca = np.ascontiguousarray(ca_table() if ca is None else ca, np.uint32)
     lin = np.zeros((len(nch), MAXCH), LIN_DTYPE)
     fast = np.zeros(len(nch), np.int32)
-    _check(lib().gss_linearize(_ptr(blk), _ptr(nch), len(nch), n_per_blk, _ptr(ca), len(ca),
-                               _ptr(nav), len(nav), _ptr(lin), _ptr(fast), threads))
+    if anch is None:
+        _check(lib().gss_linearize(_ptr(blk), _ptr(nch), len(nch), n_per_blk, _ptr(ca), len(ca),
+                                   _ptr(nav), len(nav), _ptr(lin), _ptr(fast), threads))
+    else:
+        anch = np.ascontiguousarray(anch, ANCHOR_DTYPE)
+        assert anch.size == len(nch) * MAXCH
+        _check(lib().gss_linearize_ex(_ptr(blk), _ptr(nch), len(nch), n_per_blk, _ptr(ca),
+                                      len(ca), _ptr(nav), len(nav), _ptr(anch), _ptr(lin),
+                                      _ptr(fast), threads))
     return lin, fast
 
 
@@ -517,6 +535,37 @@ def carr_chain_spec(carr, blk, nch, chain, n_per_blk, gi, spec, threads=8):
     return c, hit.value
 
 
+def carr_chain_anchored(carr, blk, nch, chain, n_per_blk, gi, spec, threads=8):
+    """carr_chain_spec, also returning the chain's anchors (gss_carr_chain_anchored):
+    (end carriers, hits, ANCHOR_DTYPE [nb, 16])."""
+    c = np.array(carr, np.float64, copy=True)
+    assert c.shape == (MAXCH,) and blk.flags.c_contiguous and blk.dtype == CHAN_DTYPE
+    nch = np.ascontiguousarray(nch, np.int32)
+    chain = np.ascontiguousarray(chain, CHAIN_DTYPE)
+    gi = np.ascontiguousarray(gi, SPEC_IN_DTYPE)
+    spec = np.ascontiguousarray(spec, SPEC_DTYPE)
+    assert spec.size == gi.size == len(nch) * MAXCH
+    anch = np.zeros((len(nch), MAXCH), ANCHOR_DTYPE)
+    hit = C.c_int(0)
+    _check(lib().gss_carr_chain_anchored(_ptr(c), _ptr(blk), _ptr(nch), _ptr(chain), len(nch),
+                                         int(n_per_blk), _ptr(gi), _ptr(spec), threads,
+                                         C.byref(hit), _ptr(anch)))
+    return c, hit.value, anch
+
+
+def carr_anchors(blk, nch, n_per_blk, gi, spec, threads=8):
+    """The anchors of rows whose carr0 a chain has set (gss_carr_anchors): ANCHOR_DTYPE [nb, 16]."""
+    blk = np.ascontiguousarray(blk, CHAN_DTYPE)
+    nch = np.ascontiguousarray(nch, np.int32)
+    gi = np.ascontiguousarray(gi, SPEC_IN_DTYPE)
+    spec = np.ascontiguousarray(spec, SPEC_DTYPE)
+    assert spec.size == gi.size == len(nch) * MAXCH
+    anch = np.zeros((len(nch), MAXCH), ANCHOR_DTYPE)
+    _check(lib().gss_carr_anchors(_ptr(blk), _ptr(nch), len(nch), int(n_per_blk), _ptr(gi),
+                                  _ptr(spec), _ptr(anch), threads))
+    return anch
+
+
 def spec_links(nch, chain, n_per_blk, gi, spec, threads=8):
     """Each row's link from its slot's previous row (gss_spec_links): SPEC_LINK_DTYPE [nb, 16]."""
     nch = np.ascontiguousarray(nch, np.int32)
@@ -650,13 +699,21 @@ class Device:
         return n.value, a.value, b.value
 
     def linearize_device(self, blk_ptr, nch_ptr, nblk, n_per_blk, ca_ptr, n_ca, nav_ptr, n_nav,
-                         lin_ptr, fast_ptr, stream=0):
+                         lin_ptr, fast_ptr, stream=0, anch_ptr=None):
         """gss_linearize_device: the fast path's proofs on the GPU (device pointers, rows as
-        gss_linearize's, async on stream)."""
-        _check(lib().gss_linearize_device(self._h, C.c_void_p(blk_ptr), C.c_void_p(nch_ptr), nblk,
-                                          n_per_blk, C.c_void_p(ca_ptr), n_ca,
-                                          C.c_void_p(nav_ptr), n_nav, C.c_void_p(lin_ptr),
-                                          C.c_void_p(fast_ptr), C.c_void_p(stream)))
+        gss_linearize's, async on stream); anch_ptr: the chain's anchors on the device
+        (gss_linearize_device_ex)."""
+        if anch_ptr is None:
+            _check(lib().gss_linearize_device(self._h, C.c_void_p(blk_ptr), C.c_void_p(nch_ptr),
+                                              nblk, n_per_blk, C.c_void_p(ca_ptr), n_ca,
+                                              C.c_void_p(nav_ptr), n_nav, C.c_void_p(lin_ptr),
+                                              C.c_void_p(fast_ptr), C.c_void_p(stream)))
+        else:
+            _check(lib().gss_linearize_device_ex(self._h, C.c_void_p(blk_ptr),
+                                                 C.c_void_p(nch_ptr), nblk, n_per_blk,
+                                                 C.c_void_p(ca_ptr), n_ca, C.c_void_p(nav_ptr),
+                                                 n_nav, C.c_void_p(anch_ptr), C.c_void_p(lin_ptr),
+                                                 C.c_void_p(fast_ptr), C.c_void_p(stream)))
 
     def spec_device(self, in_ptr, nrow, n_per_blk, spec_ptr, stream=0):
         """gss_spec_device on raw device pointers (nrow SPEC_IN_DTYPE rows in, SPEC_DTYPE rows

@@ -29,8 +29,9 @@ import time
 
 import numpy as np
 
-from . import (MAXCH, SPEC_DTYPE, SPEC_IN_DTYPE, Scenario, carr_chain, carr_chain_guess,
-               carr_chain_linked, carr_chain_spec, carr_line_end, spec_host, spec_links)
+from . import (ANCHOR_DTYPE, MAXCH, SPEC_DTYPE, SPEC_IN_DTYPE, Scenario, carr_anchors,
+               carr_chain, carr_chain_anchored, carr_chain_guess, carr_chain_linked,
+               carr_chain_spec, carr_line_end, spec_host, spec_links)
 
 SPEC_CHUNK = 4096                # blocks per run-ahead chunk (gss_run.hip chain_upfront_spec)
 
@@ -68,18 +69,26 @@ def device_walker(dev, torch):
     return walk
 
 
-def chain_run_ahead(carr, blk, nch, chain, n_per_blk, walker, threads=8, chunk=SPEC_CHUNK):
+def chain_run_ahead(carr, blk, nch, chain, n_per_blk, walker, threads=8, chunk=SPEC_CHUNK,
+                    anch=None):
     """gss_carr_chain's result (blk["carr0"] filled in place, the carriers after the last block)
-    from speculative walks: returns (end carriers, rows whose translation held)"""
+    from speculative walks: returns (end carriers, rows whose translation held).  anch
+    (ANCHOR_DTYPE [nb, 16], optional): filled with the chain's anchors (the proofs' walk starts)."""
     c = np.array(carr, np.float64, copy=True)
     hits = 0
     for b0 in range(0, len(nch), chunk):
         b1 = min(len(nch), b0 + chunk)
         gi = carr_chain_guess(c, blk[b0:b1], nch[b0:b1], chain[b0:b1], n_per_blk,
                               starts_only=True)
-        spec = walker(gi, n_per_blk)
-        c, h = carr_chain_spec(c, blk[b0:b1], nch[b0:b1], chain[b0:b1], n_per_blk, gi, spec,
-                               threads=threads)
+        spec = walker(gi, n_per_blk).reshape(gi.shape)
+        if anch is None:
+            c, h = carr_chain_spec(c, blk[b0:b1], nch[b0:b1], chain[b0:b1], n_per_blk, gi, spec,
+                                   threads=threads)
+        else:
+            sub = blk[b0:b1]                 # a contiguous view: filled in place
+            c, h, a = carr_chain_anchored(c, sub, nch[b0:b1], chain[b0:b1], n_per_blk, gi, spec,
+                                          threads=threads)
+            anch[b0:b1] = a
         hits += h
     return c, hits
 
@@ -205,7 +214,8 @@ def _walk_rows(gi_rows, n_per_blk, walker):
     return spec
 
 
-def chain_speculated(scn_carr, blk, nch, chain, n_per_blk, walker, baton, threads=8):
+def chain_speculated(scn_carr, blk, nch, chain, n_per_blk, walker, baton, threads=8,
+                     anchors=False):
     """The window's chain with the walks run before the baton (steps 1-4 above): fills
     blk["carr0"]; returns (end carriers, timings).  Every rank of the baton's group calls it (two
     all_gathers); rank 0 passes the run's initial carriers as scn_carr."""
@@ -251,6 +261,8 @@ def chain_speculated(scn_carr, blk, nch, chain, n_per_blk, walker, baton, thread
         baton.isend(e0)
         t["fix_s"] = time.perf_counter() - t1
     baton.finish()
+    if anchors:                              # after the hand-off: off the ranks' serial path
+        t["anch"] = carr_anchors(blk, nch, n_per_blk, gi, spec, threads=threads)
     t["chain_s"] = time.perf_counter() - t0 - t.get("wait_s", 0.0)
     t["spec_hits"] = hits
     t["spec_rewalked"] = rewalked
@@ -267,7 +279,7 @@ def _concat(parts):
 
 
 def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=True, walker=None,
-                chain_threads=None, speculate=True):
+                chain_threads=None, speculate=True, anchors=False):
     """Rows of blocks [first, first + count) of Scenario scn (count < 0: to the end), planned
     without the blocks before `first` when a baton supplies the carriers there (rank > 0).
     Returns (blk, nch, ck or None, timings {seek_s, rows_s, wait_s, chain_s, spec_hits}).
@@ -280,7 +292,8 @@ def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=Tr
     (chain_run_ahead) and ck is None: the exact path walks the few uncertified blocks from their
     carr0 (DeviceWindow computes their checkpoints).  With a walker and a baton over more than one
     rank the chain is speculated across ranks (chain_speculated; speculate=False: the baton
-    first, then the chain run ahead)."""
+    first, then the chain run ahead).  anchors (with a walker): the chain's anchors in
+    timings["anch"] (ANCHOR_DTYPE [count, 16]) for the proofs (gss_linearize_ex)."""
     t = {}
     t0 = time.perf_counter()
     carr = None
@@ -311,7 +324,8 @@ def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=Tr
     if speculate:
         blk, nch, chain = _concat(parts)
         end, tc = chain_speculated(scn.carrier() if baton.rank == 0 else None, blk, nch, chain,
-                                   scn.n_per_blk, walker, baton, threads=chain_threads or threads)
+                                   scn.n_per_blk, walker, baton, threads=chain_threads or threads,
+                                   anchors=anchors)
         t.update(tc)
         t.setdefault("wait_s", 0.0)
         return blk, nch, None, t
@@ -323,8 +337,11 @@ def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=Tr
     blk, nch, chain = _concat(parts)
     ct = chain_threads or threads
     if walker is not None and len(nch):
+        anch = np.zeros((len(nch), MAXCH), ANCHOR_DTYPE) if anchors else None
         end, t["spec_hits"] = chain_run_ahead(carr, blk, nch, chain, scn.n_per_blk, walker,
-                                              threads=ct)
+                                              threads=ct, anch=anch)
+        if anchors:
+            t["anch"] = anch
         ck = None
     else:
         end, ck = carr_chain(carr, blk, nch, chain, scn.n_per_blk, carrier_int=scn.carrier_int,
@@ -336,7 +353,8 @@ def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=Tr
 
 
 def plan_rank(nav_file, rank, world, window_s, *, llh, samp_freq=2.6e6, data_format=16,
-              threads=8, batch=2000, baton=None, walker=None, chain_threads=None, speculate=True):
+              threads=8, batch=2000, baton=None, walker=None, chain_threads=None, speculate=True,
+              anchors=False):
     """Host plane for one rank: (blk[n, 16], nch[n], ck[n, 16, NCK] or None, nav rows,
     n_per_blk, timings) of its block range (ck: the carrier checkpoints).  With world > 1 pass a
     Baton: the rank then plans only its own window (module docstring)."""
@@ -345,7 +363,7 @@ def plan_rank(nav_file, rank, world, window_s, *, llh, samp_freq=2.6e6, data_for
                    samp_freq=samp_freq, data_format=data_format)
     blk, nch, ck, t = plan_window(scn, first, count, baton=baton, threads=threads, batch=batch,
                                   walker=walker, chain_threads=chain_threads,
-                                  speculate=speculate)
+                                  speculate=speculate, anchors=anchors)
     if len(nch) != count:
         raise RuntimeError(f"rank {rank}: planned {len(nch)} of {count} blocks")
     t["rows_out"] = int(scn.position()[1])

@@ -339,6 +339,32 @@ int gss_carr_chain_spec(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
                         const gss_chain_t *chain, int nblk, int n_per_blk,
                         const gss_spec_in_t *in, const gss_spec_t *spec, int threads,
                         int *n_hit);
+/* Anchors: exact carrier values inside a block, by-products of the chain (the values at the
+   segment starts its fix-up passed or walked), which the proofs start their exact carrier walks
+   from (gss_linearize_ex / gss_linearize_device_ex) instead of from the block start.
+     gss_carr_chain_anchored  gss_carr_chain_spec, also filling anch[nblk][GSS_MAXCH]
+     gss_carr_anchors         the same anchors for rows whose carr0 any chain has set, in parallel
+                              over blocks (the speculative walks of those rows, gss_spec_*)   */
+typedef struct gss_carr_anchor {
+    int32_t pos[GSS_SPEC_K];           /* sample positions within the block (-1: none); pos[0] 0 */
+    double val[GSS_SPEC_K];            /* the reference's carr_phase at sample pos (val[0] carr0) */
+} gss_carr_anchor_t;                   /* 96 bytes */
+int gss_carr_chain_anchored(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
+                            const gss_chain_t *chain, int nblk, int n_per_blk,
+                            const gss_spec_in_t *in, const gss_spec_t *spec, int threads,
+                            int *n_hit, gss_carr_anchor_t *anch);
+int gss_carr_anchors(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
+                     const gss_spec_in_t *in, const gss_spec_t *spec, gss_carr_anchor_t *anch,
+                     int threads);
+/* gss_linearize / gss_linearize_device with the anchors (anch [nblk][GSS_MAXCH], NULL: none;
+   device memory for the _device form): the same rows, byte for byte, with shorter walks.      */
+int gss_linearize_ex(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
+                     const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
+                     const gss_carr_anchor_t *anch, gss_lin_t *lin, int32_t *fast, int threads);
+int gss_linearize_device_ex(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch, int nblk,
+                            int n_per_blk, const uint32_t *ca_bits, int n_ca,
+                            const uint32_t *nav, int n_nav, const gss_carr_anchor_t *anch,
+                            gss_lin_t *lin, int32_t *fast, void *stream);
 /* Links between a slot's consecutive rows, computed before the chain's start is known (the
    multi-rank planner runs them ahead of the baton; gpssim_amd/shard.py chain_speculated):
      gss_spec_links         for every row that continues its slot's chain in the batch, its

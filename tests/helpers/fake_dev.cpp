@@ -63,13 +63,14 @@ extern "C" int gss_spec_device(gss_dev *d, gss_spec_in_t *in, int nrow, int n_pe
 
 int run_proof_launch(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
                      const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
-                     gss_lin_t *lin, int32_t *fast, int64_t first, int force_exact,
-                     hipStream_t st)
+                     const gss_carr_anchor_t *anch, gss_lin_t *lin, int32_t *fast,
+                     int64_t first, int force_exact, hipStream_t st)
 {
     if (nblk <= 0)
         return 0;
     fake_enqueue(st, [=] {
-        (void)gss_linearize(blk, nch, nblk, n_per_blk, ca_bits, n_ca, nav, n_nav, lin, fast, 1);
+        (void)gss_linearize_ex(blk, nch, nblk, n_per_blk, ca_bits, n_ca, nav, n_nav, anch, lin,
+                               fast, 1);
         if (force_exact > 0)
             for (int b = 0; b < nblk; b++)
                 if ((first + b) % force_exact == 0)

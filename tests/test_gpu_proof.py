@@ -23,7 +23,7 @@ def dev():
     d.close()
 
 
-def device_proof(dev, blk, nch, nav, n):
+def device_proof(dev, blk, nch, nav, n, anch=None):
     t = torch.device("cuda", 0)
     ca = G.ca_table()
 
@@ -34,18 +34,20 @@ def device_proof(dev, blk, nch, nav, n):
     nb = len(nch)
     d_lin = torch.full((nb * G.MAXCH * G.LIN_DTYPE.itemsize,), 0xA5, dtype=torch.uint8, device=t)
     d_fast = torch.full((nb * 4,), 0x5A, dtype=torch.uint8, device=t)
+    d_anch = up(np.ascontiguousarray(anch, G.ANCHOR_DTYPE)) if anch is not None else None
     dev.linearize_device(d_blk.data_ptr(), d_nch.data_ptr(), nb, n, d_ca.data_ptr(), len(ca),
                          d_nav.data_ptr(), len(nav), d_lin.data_ptr(), d_fast.data_ptr(),
-                         torch.cuda.current_stream(t).cuda_stream)
+                         torch.cuda.current_stream(t).cuda_stream,
+                         anch_ptr=d_anch.data_ptr() if d_anch is not None else None)
     torch.cuda.synchronize(t)
     lin = d_lin.cpu().numpy().view(G.LIN_DTYPE).reshape(nb, G.MAXCH)
     fast = d_fast.cpu().numpy().view(np.int32)
     return lin, fast
 
 
-def check_same(dev, blk, nch, nav, n):
+def check_same(dev, blk, nch, nav, n, anch=None):
     want_lin, want_fast = G.linearize(blk, nch, nav, n)
-    got_lin, got_fast = device_proof(dev, blk, nch, nav, n)
+    got_lin, got_fast = device_proof(dev, blk, nch, nav, n, anch)
     assert np.array_equal(got_fast, want_fast), np.nonzero(got_fast != want_fast)[0][:10]
     a, b = want_lin.view(np.uint8).reshape(len(nch), -1), got_lin.view(np.uint8).reshape(len(nch), -1)
     bad = np.nonzero((a != b).any(axis=1))[0]
@@ -73,6 +75,26 @@ def test_proof_device_equals_host_scenarios(dev, case):
     else:
         blk, nch = s.all_blocks(batch=2000, threads=8)
     fast = check_same(dev, blk, nch, s.nav_table(), s.n_per_blk)
+    assert fast.sum() >= len(nch) * 0.95
+
+
+@pytest.mark.parametrize("fs,dur", [(2.6e6, 300.0), (2.0e7, 30.0)])
+def test_proof_device_with_anchors_equals_host(dev, fs, dur):
+    """gss_linearize_device_ex: the proofs' carrier walks start at the chain's anchors
+    (gss_carr_chain_anchored, exact values at the segment starts), on the device as on the host:
+    the same rows, byte for byte, as the host's proofs without them."""
+    s = G.Scenario(NAV, llh=LOC, duration=dur, samp_freq=fs)
+    n = s.n_per_blk
+    c0 = s.carrier()
+    blk, nch, chain = s.next_deferred(int(dur * 10), threads=8)
+    gi = G.carr_chain_guess(c0, blk, nch, chain, n, starts_only=True)
+    spec = G.spec_host(gi, n, threads=8)
+    _, _, anch = G.carr_chain_anchored(c0, blk, nch, chain, n, gi, spec)
+    nav = s.nav_table()
+    host_lin, host_fast = G.linearize(blk, nch, nav, n, anch=anch)
+    want_lin, want_fast = G.linearize(blk, nch, nav, n)
+    assert host_lin.tobytes() == want_lin.tobytes() and host_fast.tobytes() == want_fast.tobytes()
+    fast = check_same(dev, blk, nch, nav, n, anch)
     assert fast.sum() >= len(nch) * 0.95
 
 
