@@ -1135,7 +1135,7 @@ GSS_HD void gss_spec_guess_row(double g, double s, int64_t n, gss_spec_in_t *in)
     in->g = g0;
     in->s = s;
     in->k = 1;
-    in->pad = 0;
+    /* in->pad: the caller's (the previous row of the slot, gss_carr_chain_starts) */
     if (s == 0.0)
         return;
     const double as = s > 0.0 ? s : -s;
@@ -1315,6 +1315,88 @@ GSS_HD int64_t gss_carr_to_wrap_margins(double *x, double s, int64_t n, int *wr,
     }
     *x = v;
     return taken;
+}
+
+/* ---- a row's walk folded into one record (gss_spec_records*, gss_carr_chain_records) ----------
+ * gss_spec_fix_at's checks, d_j in [dlo_j, dhi_j] with d_0 = d + c and d_j+1 = d_j + (end_j -
+ * W_j+1), are one interval on d: [lo_j - c_j, hi_j - c_j] over j, rounded inward (the c_j are
+ * sums of post-wrap lattice values, exact in double; so is every translation the chain then
+ * forms).  0 where no translation can carry the row (an empty interval, or a segment that does
+ * not end on a wrap before the last). */
+#ifndef GSS_SPEC_REC_DEFINED
+#define GSS_SPEC_REC_DEFINED
+typedef struct gss_spec_rec {          /* a row's speculative walk folded (GPU or host)            */
+    double w1;                         /* post-wrap value at the guess's first wrap                */
+    double slo, shi, sdd;              /* self: d0 = (true post-wrap value at p1) - w1 in [slo,
+                                          shi] -> the row's last translation is d0 + sdd ...     */
+    double end;                        /* ... and its end is end + (d0 + sdd)                      */
+    double llo, lhi, ldd;              /* link: the previous row of the slot translated by d in
+                                          [llo, lhi] -> this one's last translation is d + ldd    */
+    int32_t p1;                        /* samples to the guess's first wrap                        */
+    int32_t ok;                        /* bit 0: self record, bit 1: link record                   */
+} gss_spec_rec_t;                      /* 72 bytes */
+#endif
+
+GSS_HD int gss_spec_fold(const gss_spec_in_t *in, const gss_spec_t *o, double c, double lo,
+                         double hi, double *olo, double *ohi, double *odd)
+{
+    const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
+    for (int j = 0; j < k; j++) {
+        const gss_spec_seg_t *sg = &o->seg[j];
+        if (!(sg->dlo <= sg->dhi))
+            return 0;
+        const double l = nextafter(sg->dlo - c, GSS_BIG), h = nextafter(sg->dhi - c, -GSS_BIG);
+        if (l > lo) lo = l;
+        if (h < hi) hi = h;
+        if (j + 1 < k) {
+            if (!sg->wrap_end)
+                return 0;                        /* the walk goes on exactly: no record */
+            c += sg->end - in->W[j + 1];
+        }
+    }
+    if (!(lo <= hi))
+        return 0;
+    *olo = lo;
+    *ohi = hi;
+    *odd = c;
+    return 1;
+}
+
+/* The link part: the row entered from y, the previous row's last segment end (that row
+   translated by d starts this one at y + d): its partial cycle walked from y with margins. */
+GSS_HD int gss_spec_link_fold(double y, const gss_spec_in_t *in, const gss_spec_t *o, int64_t n,
+                              double *olo, double *ohi, double *odd)
+{
+    double a = -GSS_BIG, b = GSS_BIG;
+    int wr = 0;
+    double x = y;
+    const int64_t t = gss_carr_to_wrap_margins(&x, in->s, n, &wr, &a, &b);
+    if (!wr || t >= n || t != o->p1 || !(a <= b))
+        return 0;
+    return gss_spec_fold(in, o, x - o->w1, a, b, olo, ohi, odd);
+}
+
+/* Row e's record; prev (NULL: none) the previous row of its slot within the batch. */
+GSS_HD void gss_spec_record(const gss_spec_in_t *in, const gss_spec_t *o,
+                            const gss_spec_in_t *pin, const gss_spec_t *po, int64_t n,
+                            gss_spec_rec_t *r)
+{
+    const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
+    r->w1 = o->w1;
+    r->p1 = (int32_t)(o->p1 < n ? o->p1 : n);
+    r->end = o->seg[k - 1].end;
+    r->slo = 1.0; r->shi = 0.0; r->sdd = 0.0;
+    r->llo = 1.0; r->lhi = 0.0; r->ldd = 0.0;
+    r->ok = 0;
+    if (in->s == 0.0 || o->p1 >= n)
+        return;
+    if (gss_spec_fold(in, o, 0.0, -GSS_BIG, GSS_BIG, &r->slo, &r->shi, &r->sdd))
+        r->ok |= 1;
+    if (pin && po && pin->s != 0.0) {
+        const int kp = pin->k < 1 ? 1 : (pin->k > GSS_SPEC_K ? GSS_SPEC_K : pin->k);
+        if (gss_spec_link_fold(po->seg[kp - 1].end, in, o, n, &r->llo, &r->lhi, &r->ldd))
+            r->ok |= 2;
+    }
 }
 
 /* ---- code iterator ---------------------------------------------------------------------- */

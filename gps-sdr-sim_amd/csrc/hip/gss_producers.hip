@@ -98,8 +98,12 @@ __device__ inline int spec_row_of(int u, int nrow)
     return nrow % GSS_MAXCH ? u : (u % nb) * GSS_MAXCH + u / nb;
 }
 
-__global__ __launch_bounds__(64) void gss_spec_kernel(gss_spec_in_t *__restrict__ in, int nrow,
-                                                      int n, gss_spec_t *__restrict__ spec)
+/* in: the rows (read); back: where the rows go back with the walkers' guesses (in itself for
+   gss_spec_device, only the rows guessed here; the device copy for gss_spec_records_device, every
+   row).  heads: read only each row's start, step, k and pad (the walkers guess the rest) */
+__global__ __launch_bounds__(64) void gss_spec_kernel(const gss_spec_in_t *in,
+                                                      gss_spec_in_t *back, int nrow, int n,
+                                                      gss_spec_t *__restrict__ spec, int heads)
 {
     __shared__ gss_spec_in_t s_in[SPEC_ROWS];
     __shared__ gss_spec_t s_out[SPEC_ROWS];
@@ -107,10 +111,12 @@ __global__ __launch_bounds__(64) void gss_spec_kernel(gss_spec_in_t *__restrict_
     constexpr int WI = sizeof(gss_spec_in_t) / 8, WO = sizeof(gss_spec_t) / 16;
     const int lane = threadIdx.x, r = lane / GSS_SPEC_K, j = lane % GSS_SPEC_K;
     const int u0 = blockIdx.x * SPEC_ROWS;
+    const int wr = heads ? 3 : WI;                       /* g, s, (k, pad): 3 words */
     for (int q = lane; q < SPEC_ROWS * WI; q += 64) {    /* the rows in, 8 bytes a lane */
         const int rr = q / WI, w = q % WI;
         if (u0 + rr < nrow)
-            ((uint64_t *)&s_in[rr])[w] = ((const uint64_t *)&in[spec_row_of(u0 + rr, nrow)])[w];
+            ((uint64_t *)&s_in[rr])[w] =
+                w < wr ? ((const uint64_t *)&in[spec_row_of(u0 + rr, nrow)])[w] : 0;
     }
     for (int q = lane; q < SPEC_ROWS * WO; q += 64)      /* the walks zeroed */
         ((uint4 *)s_out)[q] = make_uint4(0, 0, 0, 0);
@@ -139,9 +145,65 @@ __global__ __launch_bounds__(64) void gss_spec_kernel(gss_spec_in_t *__restrict_
     }
     for (int q = lane; q < SPEC_ROWS * WI; q += 64) {    /* the walkers' guesses back */
         const int rr = q / WI, w = q % WI;
-        if (u0 + rr < nrow && s_guessed[rr])
-            ((uint64_t *)&in[spec_row_of(u0 + rr, nrow)])[w] = ((const uint64_t *)&s_in[rr])[w];
+        if (u0 + rr < nrow && (s_guessed[rr] || back != in))
+            ((uint64_t *)&back[spec_row_of(u0 + rr, nrow)])[w] = ((const uint64_t *)&s_in[rr])[w];
     }
+}
+
+/* Each row's record (gss_phase.h gss_spec_record) from the walks in device memory: one lane per
+   row, the link from the previous row of its slot (in[].pad); the records staged in LDS and
+   written to host-visible memory in 16-byte stores (72 B per row instead of the walk's 272 and
+   the guesses' 152) */
+constexpr int REC_ROWS = 64;
+static_assert(sizeof(gss_spec_rec_t) == 72, "record size");
+
+__global__ __launch_bounds__(REC_ROWS) void gss_spec_rec_kernel(
+    const gss_spec_in_t *__restrict__ in, const gss_spec_t *__restrict__ spec, int nrow, int n,
+    gss_spec_rec_t *__restrict__ rec)
+{
+    __shared__ gss_spec_rec_t s_rec[REC_ROWS];
+    const int lane = threadIdx.x;
+    const int u0 = blockIdx.x * REC_ROWS, i = u0 + lane;
+    if (i < nrow) {
+        const int p = in[i].pad;
+        const bool ok = p >= 0 && p < i;
+        gss_spec_record(&in[i], &spec[i], ok ? &in[p] : nullptr, ok ? &spec[p] : nullptr, n,
+                        &s_rec[lane]);
+    }
+    __syncthreads();
+    constexpr int W = sizeof(gss_spec_rec_t) * REC_ROWS / 16;
+    const int rows = nrow - u0 < REC_ROWS ? nrow - u0 : REC_ROWS;
+    const int words = rows * (int)sizeof(gss_spec_rec_t) / 8;   /* 9 words a row */
+    if (rows == REC_ROWS) {
+        for (int q = lane; q < W; q += REC_ROWS)
+            ((uint4 *)&rec[u0])[q] = ((const uint4 *)s_rec)[q];
+    } else {
+        for (int q = lane; q < words; q += REC_ROWS)
+            ((uint64_t *)&rec[u0])[q] = ((const uint64_t *)s_rec)[q];
+    }
+}
+
+extern "C" int gss_spec_records_device(gss_dev *d, const gss_spec_in_t *in, int nrow,
+                                       int n_per_blk, gss_spec_in_t *d_in, gss_spec_t *d_spec,
+                                       gss_spec_rec_t *rec, void *stream)
+{
+    if (!d || nrow < 0 || n_per_blk <= 0 ||
+        (nrow > 0 && (!in || !d_in || !d_spec || !rec)) || ((uintptr_t)in & 7) ||
+        ((uintptr_t)d_in & 7) || ((uintptr_t)d_spec & 15) || ((uintptr_t)rec & 15) ||
+        (const void *)in == (const void *)d_in)
+        return gss_fail(GSS_E_ARG, "invalid speculative-record arguments (rows 8-byte, walks "
+                        "and records 16-byte aligned, in and d_in apart)");
+    if (nrow == 0)
+        return 0;
+    if (hipSetDevice(gss_dev_ordinal(d)) != hipSuccess)
+        return gss_fail(GSS_E_HIP, "hipSetDevice failed");
+    hipLaunchKernelGGL(gss_spec_kernel, dim3((unsigned)((nrow + SPEC_ROWS - 1) / SPEC_ROWS)),
+                       dim3(64), 0, (hipStream_t)stream, in, d_in, nrow, n_per_blk, d_spec, 1);
+    hipLaunchKernelGGL(gss_spec_rec_kernel, dim3((unsigned)((nrow + REC_ROWS - 1) / REC_ROWS)),
+                       dim3(REC_ROWS), 0, (hipStream_t)stream, d_in, d_spec, nrow, n_per_blk,
+                       rec);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "record kernels: %s", hipGetErrorString(e));
 }
 
 extern "C" int gss_spec_device(gss_dev *d, gss_spec_in_t *in, int nrow, int n_per_blk,
@@ -157,7 +219,7 @@ extern "C" int gss_spec_device(gss_dev *d, gss_spec_in_t *in, int nrow, int n_pe
         return gss_fail(GSS_E_HIP, "hipSetDevice failed");
     hipLaunchKernelGGL(gss_spec_kernel, dim3((unsigned)((nrow + SPEC_ROWS - 1) / SPEC_ROWS)),
                        dim3(64), 0,
-                       (hipStream_t)stream, in, nrow, n_per_blk, spec);
+                       (hipStream_t)stream, in, in, nrow, n_per_blk, spec, 0);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "spec kernel: %s", hipGetErrorString(e));
 }

@@ -233,6 +233,11 @@ struct Run {
         std::vector<gss_chain_t> chain;
         gss_spec_in_t *h_in = nullptr;        /* pinned host, read and written by the lanes */
         gss_spec_t *h_spec = nullptr;
+        /* records mode (r.rec): the walks and guesses stay on the device (d_in, d_spec) and
+           only each row's record comes back (h_rec, pinned) */
+        gss_spec_in_t *d_in = nullptr;
+        gss_spec_t *d_spec = nullptr;
+        gss_spec_rec_t *h_rec = nullptr;
         double carr[GSS_MAXCH];                              /* exact, at its first block */
         int nb = 0, launched = 0;
         double tg = 0.0, tk = 0.0;                           /* trace: guess start, launch end */
@@ -263,6 +268,8 @@ struct Run {
     std::vector<uint32_t> nav_rows_h;
     gss_dev *dev = nullptr;
     int spec = 0;                    /* per batch (gss_run), or over the range (hand-off)      */
+    int rec = 0;                     /* per batch: records, not walks, back from the GPU
+                                        (gss_spec_records_device; GSS_RUN_REC=0: the walks)    */
     hipStream_t spec_st = nullptr;
     uint64_t *spec_warm = nullptr;   /* device scratch of the walks' first launch (one row) */
     int64_t spec_rows = 0, spec_hits = 0;
@@ -649,7 +656,9 @@ int spec_launch(Run &r, Run::SpecBatch &b, int ask)
        16-byte copies each way) measured the same: the downloads beside them run at ~0.8 of the
        link either way, the walks' own traffic (~14 MB per 2048-block slot back to the host,
        with the 10 MB of uploads) sharing its device-to-host direction */
-    rc = gss_spec_device(r.dev, b.h_in, nrow, r.n_per_blk, b.h_spec, r.spec_st);
+    rc = r.rec ? gss_spec_records_device(r.dev, b.h_in, nrow, r.n_per_blk, b.d_in, b.d_spec,
+                                         b.h_rec, r.spec_st)
+               : gss_spec_device(r.dev, b.h_in, nrow, r.n_per_blk, b.h_spec, r.spec_st);
     if (rc)
         return rc;
     RUN_TRY(hipEventRecord(b.walked, r.spec_st));    /* not the stream: later batches queue */
@@ -673,8 +682,11 @@ int spec_finish(Run &r, Run::SpecBatch &b, gss_chan_blk_t *blk, int32_t *nch, in
     double carr[GSS_MAXCH];                          /* exact: the batches before are done */
     memcpy(carr, r.rows_ahead ? r.carr : b.carr, sizeof carr);
     int hit = 0;
-    int rc = gss_carr_chain_anchored(carr, b.blk.data(), b.nch.data(), b.chain.data(), nb,
-                                     r.n_per_blk, b.h_in, b.h_spec, r.threads, &hit, anch);
+    int rc = r.rec ? gss_carr_chain_records(carr, b.blk.data(), b.nch.data(), b.chain.data(), nb,
+                                            r.n_per_blk, b.h_rec, r.threads, &hit)
+                   : gss_carr_chain_anchored(carr, b.blk.data(), b.nch.data(), b.chain.data(),
+                                             nb, r.n_per_blk, b.h_in, b.h_spec, r.threads, &hit,
+                                             anch);
     if (rc)
         return rc;
     if (r.rows_ahead)
@@ -802,7 +814,7 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
             continue;                                  /* before the range: planned, dropped */
         sl.first = b0;
         sl.nb = nb;
-        sl.has_anch = sl.anch != nullptr && r.spec;
+        sl.has_anch = sl.anch != nullptr && r.spec && !r.rec;
         int m = 1;
         for (int i = 0; i < nb; i++)
             m = sl.nch[i] > m ? sl.nch[i] : m;
@@ -1378,7 +1390,8 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         (void)hipFree(r.d_nav);
         if (r.spec_st) (void)hipStreamSynchronize(r.spec_st);
         for (Run::SpecBatch &b : r.sb) {
-            (void)hipHostFree(b.h_in); (void)hipHostFree(b.h_spec);
+            (void)hipHostFree(b.h_in); (void)hipHostFree(b.h_spec); (void)hipHostFree(b.h_rec);
+            (void)hipFree(b.d_in); (void)hipFree(b.d_spec);
             if (b.walked) (void)hipEventDestroy(b.walked);
         }
         (void)hipFree(r.spec_warm);
@@ -1443,6 +1456,8 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         {
             const char *e = getenv("GSS_RUN_SPEC");
             r.spec = lazy_ck(r) && !(e && e[0] == '0');
+            const char *er = getenv("GSS_RUN_REC");
+            r.rec = r.spec && !(opts && opts->carr_in) && !(er && er[0] == '0');
         }
         if (!err && r.spec) {
             const size_t rows = nb * GSS_MAXCH;
@@ -1464,8 +1479,14 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                 if (hipEventCreateWithFlags(&b.walked, hipEventDisableTiming) != hipSuccess ||
                     hipHostMalloc((void **)&b.h_in, sizeof(gss_spec_in_t) * rows,
                                   hipHostMallocDefault) != hipSuccess ||
-                    hipHostMalloc((void **)&b.h_spec, sizeof(gss_spec_t) * rows,
-                                  hipHostMallocDefault) != hipSuccess)
+                    (r.rec ? hipMalloc((void **)&b.d_in, sizeof(gss_spec_in_t) * rows) !=
+                                     hipSuccess ||
+                                 hipMalloc((void **)&b.d_spec, sizeof(gss_spec_t) * rows) !=
+                                     hipSuccess ||
+                                 hipHostMalloc((void **)&b.h_rec, sizeof(gss_spec_rec_t) * rows,
+                                               hipHostMallocDefault) != hipSuccess
+                           : hipHostMalloc((void **)&b.h_spec, sizeof(gss_spec_t) * rows,
+                                           hipHostMallocDefault) != hipSuccess))
                     err = gss_fail(GSS_E_NOMEM, "run carrier-chain buffers (%zu rows)", rows);
             }
             /* the chain's anchors for the proofs' carrier walks (GSS_RUN_ANCHORS=0: none) */
@@ -1561,7 +1582,13 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         (void)hipMemsetAsync(r.spec_warm, 0, 1024, r.spec_st);
         (void)gss_spec_device(d, (gss_spec_in_t *)r.spec_warm, 1, info.n_per_blk,
                               (gss_spec_t *)((uint8_t *)r.spec_warm + 256), r.spec_st);
-
+        if (r.rec) {
+            uint8_t *w = (uint8_t *)r.spec_warm;
+            (void)hipMemsetAsync(r.spec_warm, 0, 1024, r.spec_st);
+            (void)gss_spec_records_device(d, (gss_spec_in_t *)w, 1, info.n_per_blk,
+                                          (gss_spec_in_t *)(w + 256), (gss_spec_t *)(w + 512),
+                                          (gss_spec_rec_t *)(w + 800), r.spec_st);
+        }
     }
     err = run_main(d, r, info.n_per_blk, info.data_format, bb, sink, user, st, cp, d_ca);
     {

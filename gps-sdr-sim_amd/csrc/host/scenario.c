@@ -499,24 +499,34 @@ static void guess_part(void *arg, int b)
 
 /* the starts, serially: the line of each slot from its exact start (in double: the drift over a
    batch, ~1e-13 per block, stays far inside the translation intervals); k = 0 on live rows (their
-   segment starts not guessed yet), 1 on padding rows */
+   segment starts not guessed yet), 1 on padding rows; pad = the index of the previous row of the
+   same slot chain in the batch (-1: the slot's first row here, or a re-initialisation), which the
+   records' links read (gss_spec_records*) */
 static void chain_starts(const double *carr, const gss_chan_blk_t *blk, const int32_t *nch,
                          const gss_chain_t *chain, int nblk, int n_per_blk, gss_spec_in_t *in)
 {
     double run[K_MAX_CHAN];
-    for (int i = 0; i < K_MAX_CHAN; i++)
+    int32_t last[K_MAX_CHAN];
+    for (int i = 0; i < K_MAX_CHAN; i++) {
         run[i] = carr[i];
+        last[i] = -1;
+    }
     for (int b = 0; b < nblk; b++)
         for (int k = 0; k < GSS_MAXCH; k++) {
             const size_t e = (size_t)b * GSS_MAXCH + k;
             const int slot = k < nch[b] ? chain[e].slot : -1;
             in[e].k = 1;
+            in[e].pad = -1;
             in[e].s = 0.0;
             in[e].g = 0.0;
             if (slot < 0 || slot >= K_MAX_CHAN)
                 continue;
-            if (chain[e].reset)
+            if (chain[e].reset) {
                 run[slot] = chain[e].init;
+                last[slot] = -1;
+            }
+            in[e].pad = last[slot];
+            last[slot] = (int32_t)e;
             const double g = run[slot];
             in[e].g = g >= 0.0 && g < 1.0 ? g : 0.0;
             in[e].s = blk[e].carr_step;
@@ -760,33 +770,13 @@ typedef struct {
 static int link_row(double y, const gss_spec_in_t *in, const gss_spec_t *o, int64_t n,
                     gss_spec_link_t *L)
 {
-    const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
-    double a = -GSS_BIG, b = GSS_BIG;
-    int wr = 0;
-    double x = y;
-    const int64_t t = gss_carr_to_wrap_margins(&x, in->s, n, &wr, &a, &b);
-    if (!wr || t >= n || t != o->p1 || !(a <= b))
-        return 0;
-    double c = x - o->w1;                        /* d_0 = d + c */
-    double lo = a, hi = b;
-    for (int j = 0; j < k; j++) {
-        const gss_spec_seg_t *sg = &o->seg[j];
-        if (!(sg->dlo <= sg->dhi))
-            return 0;
-        const double l = nextafter(sg->dlo - c, GSS_BIG), h = nextafter(sg->dhi - c, -GSS_BIG);
-        if (l > lo) lo = l;
-        if (h < hi) hi = h;
-        if (j + 1 < k) {
-            if (!sg->wrap_end)
-                return 0;                        /* the walk goes on exactly: no record */
-            c += sg->end - in->W[j + 1];
-        }
-    }
-    if (!(lo <= hi))
+    double lo, hi, dd;
+    if (!gss_spec_link_fold(y, in, o, n, &lo, &hi, &dd))
         return 0;
     L->lo = lo;
     L->hi = hi;
-    L->dd = c;
+    L->dd = dd;
+    const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
     L->end = o->seg[k - 1].end;
     return 1;
 }
@@ -890,6 +880,107 @@ int gss_carr_chain_linked(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
         return gss_fail(GSS_E_ARG, "invalid carrier-chain arguments");
     linked_job j = {carr, blk, nch, chain, in, spec, link, nblk, n_per_blk, {0}};
     gss_pool_run(threads, K_MAX_CHAN, linked_slot_part, (void *)&j);
+    if (n_hit) {
+        int h = 0;
+        for (int i = 0; i < K_MAX_CHAN; i++)
+            h += j.hits[i];
+        *n_hit = h;
+    }
+    return 0;
+}
+
+/* ---- records: each row's walk folded (gss_phase.h gss_spec_record), the chain from them ------- */
+typedef struct {
+    const gss_spec_in_t *in;
+    const gss_spec_t *spec;
+    gss_spec_rec_t *rec;
+    int nrow, n_per_blk;
+} rec_job;
+
+static void rec_part(void *arg, int part)
+{
+    const rec_job *j = arg;
+    for (int i = part * 64; i < j->nrow && i < part * 64 + 64; i++) {
+        const int p = j->in[i].pad;
+        const int ok = p >= 0 && p < i;
+        gss_spec_record(&j->in[i], &j->spec[i], ok ? &j->in[p] : NULL, ok ? &j->spec[p] : NULL,
+                        j->n_per_blk, &j->rec[i]);
+    }
+}
+
+int gss_spec_records(const gss_spec_in_t *in, const gss_spec_t *spec, int nrow, int n_per_blk,
+                     gss_spec_rec_t *rec, int threads)
+{
+    if (nrow < 0 || n_per_blk <= 0 || (nrow > 0 && (in == NULL || spec == NULL || rec == NULL)))
+        return gss_fail(GSS_E_ARG, "invalid spec-record arguments");
+    const rec_job j = {in, spec, rec, nrow, n_per_blk};
+    gss_pool_run(threads, (nrow + 63) / 64, rec_part, (void *)&j);
+    return 0;
+}
+
+typedef struct {
+    double *carr;
+    gss_chan_blk_t *blk;
+    const int32_t *nch;
+    const gss_chain_t *chain;
+    const gss_spec_rec_t *rec;
+    int nblk, n_per_blk;
+    int hits[K_MAX_CHAN];
+} rec_chain_job;
+
+static void rec_slot_part(void *arg, int slot)
+{
+    rec_chain_job *j = arg;
+    const int64_t n = j->n_per_blk;
+    double x = j->carr[slot], d = 0.0;
+    int hits = 0, held = 0;
+    for (int b = 0; b < j->nblk; b++)
+        for (int k = 0; k < j->nch[b]; k++) {
+            const size_t e = (size_t)b * GSS_MAXCH + k;
+            if (j->chain[e].slot != slot)
+                continue;
+            if (j->chain[e].reset) {
+                x = j->chain[e].init;
+                held = 0;
+            }
+            j->blk[e].carr0 = x;
+            const gss_spec_rec_t *R = &j->rec[e];
+            if (held && (R->ok & 2) && d >= R->llo && d <= R->lhi) {
+                d += R->ldd;                         /* the link: no walk at all */
+                x = R->end + d;
+                hits++;
+                break;
+            }
+            const double s = j->blk[e].carr_step;
+            double v = x;
+            int wr = 0;
+            const int64_t t = gss_carr_to_wrap(&v, s, n, &wr);
+            held = 0;
+            if (!wr || t >= n) {
+                x = v;                               /* no wrap: walked exactly */
+            } else if ((R->ok & 1) && t == R->p1 && v - R->w1 >= R->slo && v - R->w1 <= R->shi) {
+                d = (v - R->w1) + R->sdd;            /* the row's own record */
+                x = R->end + d;
+                held = 1;
+                hits++;
+            } else {
+                x = gss_carr_walk_cc(v, s, n - t);   /* a translation fails: the exact walk */
+            }
+            break;
+        }
+    j->carr[slot] = x;
+    j->hits[slot] = hits;
+}
+
+int gss_carr_chain_records(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
+                           const gss_chain_t *chain, int nblk, int n_per_blk,
+                           const gss_spec_rec_t *rec, int threads, int *n_hit)
+{
+    if (carr == NULL || nblk < 0 || n_per_blk <= 0 ||
+        (nblk > 0 && (blk == NULL || nch == NULL || chain == NULL || rec == NULL)))
+        return gss_fail(GSS_E_ARG, "invalid carrier-chain arguments");
+    rec_chain_job j = {carr, blk, nch, chain, rec, nblk, n_per_blk, {0}};
+    gss_pool_run(threads, K_MAX_CHAN, rec_slot_part, (void *)&j);
     if (n_hit) {
         int h = 0;
         for (int i = 0; i < K_MAX_CHAN; i++)

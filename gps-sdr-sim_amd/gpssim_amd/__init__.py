@@ -61,6 +61,11 @@ SPEC_DTYPE = np.dtype([("p1", "<i8"), ("w1", "<f8"), ("seg", SPEC_SEG_DTYPE, (SP
 assert SPEC_DTYPE.itemsize == 272
 SPEC_LINK_DTYPE = np.dtype([("lo", "<f8"), ("hi", "<f8"), ("dd", "<f8"), ("end", "<f8")])
 assert SPEC_LINK_DTYPE.itemsize == 32
+# gss_spec_rec_t: a row's speculative walk folded into one record (gss_spec_records*)
+SPEC_REC_DTYPE = np.dtype([("w1", "<f8"), ("slo", "<f8"), ("shi", "<f8"), ("sdd", "<f8"),
+                           ("end", "<f8"), ("llo", "<f8"), ("lhi", "<f8"), ("ldd", "<f8"),
+                           ("p1", "<i4"), ("ok", "<i4")])
+assert SPEC_REC_DTYPE.itemsize == 72
 # gss_carr_anchor_t: the chain's exact carrier values inside a block (the proofs' walk starts)
 ANCHOR_DTYPE = np.dtype([("pos", "<i4", (SPEC_K,)), ("val", "<f8", (SPEC_K,))])
 assert ANCHOR_DTYPE.itemsize == 96
@@ -151,6 +156,10 @@ _SIGS = {
     "gss_carr_chain_anchored": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P, C.c_int,
                                           C.POINTER(C.c_int), _P]),
     "gss_carr_anchors": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, _P, _P, C.c_int]),
+    "gss_spec_records": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_int]),
+    "gss_spec_records_device": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, _P, _P, _P]),
+    "gss_carr_chain_records": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, C.c_int,
+                                         C.POINTER(C.c_int)]),
     "gss_linearize_ex": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_int, _P, C.c_int, _P, _P, _P,
                                    C.c_int]),
     "gss_linearize_device_ex": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, _P, C.c_int, _P, C.c_int,
@@ -566,6 +575,33 @@ def carr_anchors(blk, nch, n_per_blk, gi, spec, threads=8):
     return anch
 
 
+def spec_records(gi, spec, n_per_blk, threads=8):
+    """Each row's record (gss_spec_records; the previous row of its slot from gi["pad"]):
+    SPEC_REC_DTYPE rows shaped like gi."""
+    gi = np.ascontiguousarray(gi, SPEC_IN_DTYPE)
+    spec = np.ascontiguousarray(spec, SPEC_DTYPE)
+    assert spec.size == gi.size
+    rec = np.zeros(gi.shape, SPEC_REC_DTYPE)
+    _check(lib().gss_spec_records(_ptr(gi), _ptr(spec), gi.size, int(n_per_blk), _ptr(rec),
+                                  threads))
+    return rec
+
+
+def carr_chain_records(carr, blk, nch, chain, n_per_blk, rec, threads=8):
+    """The chain from the rows' records (gss_carr_chain_records): fills blk["carr0"] in place;
+    returns (carrier after the last block, rows whose record held)."""
+    c = np.array(carr, np.float64, copy=True)
+    assert c.shape == (MAXCH,) and blk.flags.c_contiguous and blk.dtype == CHAN_DTYPE
+    nch = np.ascontiguousarray(nch, np.int32)
+    chain = np.ascontiguousarray(chain, CHAIN_DTYPE)
+    rec = np.ascontiguousarray(rec, SPEC_REC_DTYPE)
+    assert rec.size == len(nch) * MAXCH
+    hit = C.c_int(0)
+    _check(lib().gss_carr_chain_records(_ptr(c), _ptr(blk), _ptr(nch), _ptr(chain), len(nch),
+                                        int(n_per_blk), _ptr(rec), threads, C.byref(hit)))
+    return c, hit.value
+
+
 def spec_links(nch, chain, n_per_blk, gi, spec, threads=8):
     """Each row's link from its slot's previous row (gss_spec_links): SPEC_LINK_DTYPE [nb, 16]."""
     nch = np.ascontiguousarray(nch, np.int32)
@@ -714,6 +750,14 @@ class Device:
                                                  C.c_void_p(ca_ptr), n_ca, C.c_void_p(nav_ptr),
                                                  n_nav, C.c_void_p(anch_ptr), C.c_void_p(lin_ptr),
                                                  C.c_void_p(fast_ptr), C.c_void_p(stream)))
+
+    def spec_records_device(self, in_ptr, nrow, n_per_blk, d_in_ptr, d_spec_ptr, rec_ptr,
+                            stream=0):
+        """gss_spec_records_device: walks and records on the GPU (in / rec host-visible, d_in /
+        d_spec device scratch of nrow rows), async on stream."""
+        _check(lib().gss_spec_records_device(self._h, C.c_void_p(in_ptr), nrow, n_per_blk,
+                                             C.c_void_p(d_in_ptr), C.c_void_p(d_spec_ptr),
+                                             C.c_void_p(rec_ptr), C.c_void_p(stream)))
 
     def spec_device(self, in_ptr, nrow, n_per_blk, spec_ptr, stream=0):
         """gss_spec_device on raw device pointers (nrow SPEC_IN_DTYPE rows in, SPEC_DTYPE rows

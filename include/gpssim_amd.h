@@ -339,6 +339,38 @@ int gss_carr_chain_spec(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
                         const gss_chain_t *chain, int nblk, int n_per_blk,
                         const gss_spec_in_t *in, const gss_spec_t *spec, int threads,
                         int *n_hit);
+/* Records: each row's speculative walk folded into 72 bytes (gss_spec_rec_t: the interval of
+   translations of its first post-wrap value that carry it through every segment, and of its
+   predecessor's last translation that carry it from the predecessor's end), so that the chain
+   needs neither the walks (272 B) nor the segment guesses (152 B) on the host (gss_run: the
+   walks stay on the device and only the records cross the link).  The previous row of a row's
+   slot chain in the batch is in[].pad (gss_carr_chain_starts / _guess set it; -1: none).
+     gss_spec_records         the records from walks on the host
+     gss_spec_records_device  walks and records on the GPU: in (host-visible rows, their
+                              starts), d_in / d_spec (device scratch, nrow rows), rec
+                              (host-visible); async on stream
+     gss_carr_chain_records   the chain from the records (exact: a failed interval walks)   */
+#ifndef GSS_SPEC_REC_DEFINED
+#define GSS_SPEC_REC_DEFINED
+typedef struct gss_spec_rec {
+    double w1;                         /* post-wrap value at the guess's first wrap                */
+    double slo, shi, sdd;              /* self: d0 = (true post-wrap value at p1) - w1 in [slo,
+                                          shi] -> the row's last translation is d0 + sdd ...     */
+    double end;                        /* ... and its end is end + (d0 + sdd)                      */
+    double llo, lhi, ldd;              /* link: the previous row of the slot translated by d in
+                                          [llo, lhi] -> this one's last translation is d + ldd    */
+    int32_t p1;                        /* samples to the guess's first wrap                        */
+    int32_t ok;                        /* bit 0: self record, bit 1: link record                   */
+} gss_spec_rec_t;                      /* 72 bytes */
+#endif
+int gss_spec_records(const gss_spec_in_t *in, const gss_spec_t *spec, int nrow, int n_per_blk,
+                     gss_spec_rec_t *rec, int threads);
+int gss_spec_records_device(gss_dev *d, const gss_spec_in_t *in, int nrow, int n_per_blk,
+                            gss_spec_in_t *d_in, gss_spec_t *d_spec, gss_spec_rec_t *rec,
+                            void *stream);
+int gss_carr_chain_records(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
+                           const gss_chain_t *chain, int nblk, int n_per_blk,
+                           const gss_spec_rec_t *rec, int threads, int *n_hit);
 /* Anchors: exact carrier values inside a block, by-products of the chain (the values at the
    segment starts its fix-up passed or walked), which the proofs start their exact carrier walks
    from (gss_linearize_ex / gss_linearize_device_ex) instead of from the block start.

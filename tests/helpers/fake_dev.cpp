@@ -4,6 +4,7 @@
  * runtime (fake_hip/) and run there by host code:
  *   gss_ca_table_device / gss_nav_rows_device   the host producers (gss_ca_table, gss_nav_rows_host)
  *   gss_spec_device                             the walks on the host (gss_spec_host)
+ *   gss_spec_records_device                     walks and records on the host (gss_spec_records)
  *   run_proof_launch                            the proofs on the host (gss_linearize; the GPU proof
  *                                               writes the same rows, tests/test_gpu_proof.py)
  *   run_copy_launch                             memcpy
@@ -58,6 +59,27 @@ extern "C" int gss_spec_device(gss_dev *d, gss_spec_in_t *in, int nrow, int n_pe
 {
     (void)d;
     fake_enqueue((hipStream_t)stream, [=] { (void)gss_spec_host(in, nrow, n_per_blk, spec, 1); });
+    return 0;
+}
+
+extern "C" int gss_spec_records_device(gss_dev *d, const gss_spec_in_t *in, int nrow,
+                                       int n_per_blk, gss_spec_in_t *d_in, gss_spec_t *d_spec,
+                                       gss_spec_rec_t *rec, void *stream)
+{
+    if (!d || nrow < 0 || (nrow > 0 && (!in || !d_in || !d_spec || !rec)))
+        return GSS_E_ARG;
+    fake_enqueue((hipStream_t)stream, [=] {
+        for (int i = 0; i < nrow; i++) {              /* the heads only, as the kernel reads */
+            gss_spec_in_t r{};
+            r.g = in[i].g;
+            r.s = in[i].s;
+            r.k = in[i].k;
+            r.pad = in[i].pad;
+            d_in[i] = r;
+        }
+        (void)gss_spec_host(d_in, nrow, n_per_blk, d_spec, 1);
+        (void)gss_spec_records(d_in, d_spec, nrow, n_per_blk, rec, 1);
+    });
     return 0;
 }
 

@@ -10,6 +10,7 @@
  *   default (chain run ahead, rows ahead for large batches, host proofs), GSS_RUN_SPEC=0,
  *   GSS_RUN_ROWS_AHEAD=1 / 0 with GSS_RUN_PROVER=0 / 1, GSS_RUN_PROOF=gpu / split,
  *   GSS_RUN_FORCE_EXACT (blocks on the exact path, lazy checkpoints), GSS_RUN_UPLOAD=dma,
+ *   GSS_RUN_REC=0 (the walks back instead of records; the chain's anchors for the proofs),
  *   a range from a mid-run block, two runs on one handle, the carrier hand-off of gss_run_ex
  *   (two ranks in sequence), and a sink that stops the run.
  * Test infrastructure only (no GPU, nothing of it ships).
@@ -126,7 +127,7 @@ struct Mode {
 
 static const char *ENV_KEYS[] = {"GSS_RUN_SPEC", "GSS_RUN_ROWS_AHEAD", "GSS_RUN_PROVER",
                                  "GSS_RUN_PROOF", "GSS_RUN_FORCE_EXACT", "GSS_RUN_UPLOAD",
-                                 "GSS_RUN_ROWS_POOL"};
+                                 "GSS_RUN_ROWS_POOL", "GSS_RUN_REC", "GSS_RUN_ANCHORS"};
 
 static void set_env(const Mode &m)
 {
@@ -210,6 +211,10 @@ int main(int argc, char **argv)
         {"every 5th exact, device proofs", {{"GSS_RUN_FORCE_EXACT", "5"}, {"GSS_RUN_PROOF", "gpu"}}},
         {"every 3rd exact, rows ahead", {{"GSS_RUN_FORCE_EXACT", "3"}, {"GSS_RUN_ROWS_AHEAD", "1"}}},
         {"uploads by the copy engine", {{"GSS_RUN_UPLOAD", "dma"}}},
+        {"walks back, anchors (GSS_RUN_REC=0)", {{"GSS_RUN_REC", "0"}}},
+        {"walks back, anchors, rows ahead, device proofs",
+         {{"GSS_RUN_REC", "0"}, {"GSS_RUN_ROWS_AHEAD", "1"}, {"GSS_RUN_PROOF", "gpu"}}},
+        {"walks back, no anchors", {{"GSS_RUN_REC", "0"}, {"GSS_RUN_ANCHORS", "0"}}},
     };
     for (const Mode &m : modes) {
         set_env(m);

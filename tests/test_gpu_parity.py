@@ -506,6 +506,44 @@ def test_spec_walks_on_device(dev):
         dev.spec_device(d_in.data_ptr(), 16, n, d_spec.data_ptr() + 8)
 
 
+def test_spec_records_on_device(dev):
+    """gss_spec_records_device (gss_run's default): the walks stay on the device and only each
+    row's 72-byte record comes back; the records equal the host's (gss_spec_records over
+    gss_spec_host's walks) byte for byte, and the chain from them (gss_carr_chain_records) equals
+    the exact chain, for a static run across 30 s updates and the circle.csv run."""
+    import torch
+    for kw in (dict(llh=LOC, duration=400.0), dict(motion_file=CIRCLE, data_format=8)):
+        s = G.Scenario(NAV, **kw)
+        carr = s.carrier()
+        n = s.n_per_blk
+        b0, n0, c0 = s.next_deferred(50, threads=8)     # past the slots' first rows (resets)
+        carr, _ = G.carr_chain(carr, b0, n0, c0, n, with_ck=False)
+        blk, nch, chain = s.next_deferred(400, threads=8)
+        g0 = G.carr_chain_guess(carr, blk, nch, chain, n, starts_only=True)
+        gi = g0.copy()
+        want = G.spec_records(gi, G.spec_host(gi, n, threads=8).reshape(gi.shape), n)
+        nrow = g0.size
+        h_in = torch.from_numpy(g0.reshape(-1).view(np.uint8).copy()).pin_memory()
+        d_in = torch.zeros(nrow * G.SPEC_IN_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        d_spec = torch.zeros(nrow * G.SPEC_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        h_rec = torch.zeros(nrow * G.SPEC_REC_DTYPE.itemsize, dtype=torch.uint8).pin_memory()
+        dev.spec_records_device(h_in.data_ptr(), nrow, n, d_in.data_ptr(), d_spec.data_ptr(),
+                                h_rec.data_ptr())
+        torch.cuda.synchronize()
+        got = h_rec.numpy().view(G.SPEC_REC_DTYPE).reshape(g0.shape)
+        live = g0["s"] != 0
+        assert got[live].tobytes() == want[live].tobytes(), kw
+        assert (got["ok"][live] & 2).sum() >= 0.9 * 2 * live.sum(), kw     # linked rows
+        ref = blk.copy()
+        end_ref, _ = G.carr_chain(carr, ref, nch, chain, n, with_ck=False)
+        end, hit = G.carr_chain_records(carr, blk, nch, chain, n, got)
+        assert np.array_equal(blk["carr0"], ref["carr0"]) and np.array_equal(end, end_ref), kw
+        assert hit >= 0.95 * int(nch.sum()), (kw, hit)
+    with pytest.raises(G.GssError, match="aligned"):
+        dev.spec_records_device(h_in.data_ptr(), 16, n, d_in.data_ptr(), d_spec.data_ptr() + 8,
+                                h_rec.data_ptr())
+
+
 def test_streaming_run_sink_error_stops_cleanly(dev, golden):
     """A sink that raises mid-run stops gss_run (planner, rows thread and GPU streams wound down),
     the exception reaches the caller, and the next run on the same device is exact again."""
@@ -539,16 +577,22 @@ def test_streaming_run_sink_error_stops_cleanly(dev, golden):
     ("1", "1", "1", "host", 57), ("1", "1", "1", "host", 1),
     ("0", "1", "1", "gpu", 57), ("1", "0", "1", "gpu", 57), ("1", "1", "1", "gpu", 57),
     ("1", "1", "1", "gpu", 1), ("1", "1", "1", "split", 57), ("1", "0", "1", "split", 1),
-    ("1", "1", "1", "host-dma", 57), ("0", "0", "1", "gpu-dma", 57)])
+    ("1", "1", "1", "host-dma", 57), ("0", "0", "1", "gpu-dma", 57),
+    ("1", "1", "1", "host-walks", 57), ("1", "0", "1", "gpu-walks", 57),
+    ("1", "1", "1", "host-walks", 1)])
 def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec, ahead, prover, proof, batch):
     """gss_run with the carrier chain walked on the host (GSS_RUN_SPEC=0) and run ahead on the
     GPU (the default), with the rows produced on the planner thread (GSS_RUN_ROWS_AHEAD=0) or
     ahead on their own (the default; one-block batches too), and the proofs on the planner thread
     (GSS_RUN_PROVER=0) or their own, or on the GPU (GSS_RUN_PROOF=gpu; split: every other slot),
-    the slots' inputs uploaded by kernel (the default) or by the copy engine (-dma): a 65 s run
-    across two 30 s updates, whole and from a mid-run block, against the reference's golden
-    hashes."""
+    the slots' inputs uploaded by kernel (the default) or by the copy engine (-dma), and the
+    walks' records back from the GPU (the default) or the walks themselves (-walks,
+    GSS_RUN_REC=0, with the chain's anchors for the proofs): a 65 s run across two 30 s updates,
+    whole and from a mid-run block, against the reference's golden hashes."""
     monkeypatch.setenv("GSS_RUN_SPEC", spec)
+    if proof.endswith("-walks"):
+        proof = proof[:-6]
+        monkeypatch.setenv("GSS_RUN_REC", "0")
     if proof.endswith("-dma"):                # the slots' uploads by the copy engine
         proof = proof[:-4]
         monkeypatch.setenv("GSS_RUN_UPLOAD", "dma")

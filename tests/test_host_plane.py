@@ -255,6 +255,39 @@ def test_linked_chain_equals_exact_chain(kind, pert):
         assert hit2 < 0.05 * rows, (hit2, rows)
 
 
+@pytest.mark.parametrize("kind,pert", [("static", 0.0), ("static", 3e-10), ("circle", 1e-9),
+                                       ("static", 1e-4)])
+def test_records_chain_equals_exact_chain(kind, pert):
+    """gss_spec_records + gss_carr_chain_records (gss_run's default chain: the walks folded into
+    72-byte records, on the GPU there, only the records back): the exact chain's carr0 and end
+    carriers bit for bit from a start off by `pert`, the same rows translated as
+    gss_carr_chain_spec, and the links (gi["pad"]: the previous row of the slot) on nearly every
+    row."""
+    if kind == "static":
+        s = G.Scenario(NAV, llh=LOC, duration=290.0)
+    else:
+        s = G.Scenario(NAV, motion_file=CIRCLE, duration=290.0)
+    n = s.n_per_blk
+    b0, n0, c0 = s.next_deferred(100, threads=8)
+    carr, _ = G.carr_chain(s.carrier(), b0, n0, c0, n, with_ck=False)
+    blk, nch, chain = s.next_deferred(2790, threads=8)
+    ref = blk.copy()
+    end_ref, _ = G.carr_chain(carr, ref, nch, chain, n, with_ck=False)
+    gi = G.carr_chain_guess(np.mod(carr + pert, 1.0), blk, nch, chain, n, starts_only=True)
+    spec = G.spec_host(gi, n, threads=8).reshape(gi.shape)
+    rec = G.spec_records(gi, spec, n)
+    b1, b2 = blk.copy(), blk.copy()
+    _, hit1 = G.carr_chain_spec(carr, b1, nch, chain, n, gi, spec)
+    end2, hit2 = G.carr_chain_records(carr, b2, nch, chain, n, rec)
+    assert b2["carr0"].tobytes() == ref["carr0"].tobytes()
+    assert end2.tobytes() == end_ref.tobytes()
+    assert hit2 == hit1
+    rows = int(nch.sum())
+    assert ((rec["ok"] & 2) != 0).sum() >= 0.95 * rows
+    if pert < 1e-6:
+        assert hit2 >= 0.97 * rows
+
+
 def test_worker_pool_after_fork():
     """The host plane's persistent worker threads do not survive fork(): a child that plans
     (gss_pool_run on 8 threads) after the parent has grown its pools must still finish, with the
