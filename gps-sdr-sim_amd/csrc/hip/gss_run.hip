@@ -1509,13 +1509,18 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             r.rows_ahead = r.spec && !(opts && opts->carr_in) && want;
         }
         {
-            /* GSS_RUN_PROOF=gpu: the proofs on the GPU, run ahead by the planner (proof_ahead).
-               Not the default: one lane per channel-block leaves the proof kernel latency-bound
-               (2.3 ms per slot at 2.6 MS/s, 6.8 ms at 20 MS/s), more than a slot's download
-               takes, and the planner is not far enough ahead to hide it */
+            /* GSS_RUN_PROOF=gpu: the proofs on the GPU, run ahead by the planner (proof_ahead);
+               host: on the host threads; split: every other slot on the GPU.  The default (auto)
+               proves on the GPU only the planner-bound runs (rows ahead: slots of >= 1024
+               blocks, the -b 1 runs) with the walks' records (no walks on the host): there the
+               host's CPUs are the limit and the proofs take them off it (configs[4] e2e 0.85-0.86
+               against 0.80-0.82 of the D2H ceiling, profiles/round5/e2e/b_*_r5q).  Elsewhere one
+               lane per channel-block leaves the proof kernel latency-bound (6.8 ms per 20 MS/s
+               slot, more than its download) and host proofs win */
             const char *e = getenv("GSS_RUN_PROOF");
-            r.proof_mode = !r.use_lin || !e ? 0 : strcmp(e, "gpu") == 0 ? 1 :
-                           strcmp(e, "split") == 0 ? 2 : 0;
+            const int gpu_auto = r.rows_ahead && r.rec ? 1 : 0;
+            r.proof_mode = !r.use_lin ? 0 : !e || !*e || strcmp(e, "auto") == 0 ? gpu_auto :
+                           strcmp(e, "gpu") == 0 ? 1 : strcmp(e, "split") == 0 ? 2 : 0;
             r.gpu_proof = r.proof_mode != 0;
         }
         r.prover = r.rows_ahead && r.use_lin && r.proof_mode != 1;

@@ -200,9 +200,12 @@ int main(int argc, char **argv)
     const std::vector<Mode> modes = {
         {"default", {}},
         {"host chain (GSS_RUN_SPEC=0)", {{"GSS_RUN_SPEC", "0"}}},
-        {"rows ahead, prover thread", {{"GSS_RUN_ROWS_AHEAD", "1"}}},
-        {"rows ahead, proofs on the planner", {{"GSS_RUN_ROWS_AHEAD", "1"}, {"GSS_RUN_PROVER", "0"}}},
-        {"rows ahead, shared worker pool", {{"GSS_RUN_ROWS_AHEAD", "1"}, {"GSS_RUN_ROWS_POOL", "0"}}},
+        {"rows ahead, device proofs (auto)", {{"GSS_RUN_ROWS_AHEAD", "1"}}},
+        {"rows ahead, prover thread", {{"GSS_RUN_ROWS_AHEAD", "1"}, {"GSS_RUN_PROOF", "host"}}},
+        {"rows ahead, proofs on the planner",
+         {{"GSS_RUN_ROWS_AHEAD", "1"}, {"GSS_RUN_PROVER", "0"}, {"GSS_RUN_PROOF", "host"}}},
+        {"rows ahead, shared worker pool",
+         {{"GSS_RUN_ROWS_AHEAD", "1"}, {"GSS_RUN_ROWS_POOL", "0"}, {"GSS_RUN_PROOF", "host"}}},
         {"rows on the planner", {{"GSS_RUN_ROWS_AHEAD", "0"}}},
         {"device proofs (GSS_RUN_PROOF=gpu)", {{"GSS_RUN_PROOF", "gpu"}}},
         {"device proofs, rows ahead", {{"GSS_RUN_PROOF", "gpu"}, {"GSS_RUN_ROWS_AHEAD", "1"}}},
@@ -210,6 +213,8 @@ int main(int argc, char **argv)
         {"every 7th block exact", {{"GSS_RUN_FORCE_EXACT", "7"}}},
         {"every 5th exact, device proofs", {{"GSS_RUN_FORCE_EXACT", "5"}, {"GSS_RUN_PROOF", "gpu"}}},
         {"every 3rd exact, rows ahead", {{"GSS_RUN_FORCE_EXACT", "3"}, {"GSS_RUN_ROWS_AHEAD", "1"}}},
+        {"every 3rd exact, rows ahead, host proofs",
+         {{"GSS_RUN_FORCE_EXACT", "3"}, {"GSS_RUN_ROWS_AHEAD", "1"}, {"GSS_RUN_PROOF", "host"}}},
         {"uploads by the copy engine", {{"GSS_RUN_UPLOAD", "dma"}}},
         {"walks back, anchors (GSS_RUN_REC=0)", {{"GSS_RUN_REC", "0"}}},
         {"walks back, anchors, rows ahead, device proofs",
