@@ -1277,6 +1277,27 @@ GSS_HD double gss_spec_fix_d(double x, int64_t n, const gss_spec_in_t *in, const
     return gss_spec_walk_rest(v, t, n, in, k, 1, av);
 }
 
+/* A row's anchors from its exact start x and its walk: pos[0] = 0, val[0] = x, and at every
+   segment start P[j] the fix-up passed or walked, the exact carrier there (pos -1: none). */
+GSS_HD void gss_spec_anchors(double x, int64_t n, const gss_spec_in_t *in, const gss_spec_t *o,
+                             int32_t *pos, double *val)
+{
+    double av[GSS_SPEC_K];
+    for (int j = 0; j < GSS_SPEC_K; j++)
+        av[j] = -1.0;                                /* a carrier value is never negative */
+    int hit = 0;
+    double d = 0.0;
+    (void)gss_spec_fix_d(x, n, in, o, &hit, &d, av);
+    const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
+    pos[0] = 0;
+    val[0] = x;
+    for (int j = 1; j < GSS_SPEC_K; j++) {
+        const int ok = j < k && av[j] >= 0.0 && in->P[j] > 0 && in->P[j] < n;
+        pos[j] = ok ? (int32_t)in->P[j] : -1;
+        val[j] = ok ? av[j] : 0.0;
+    }
+}
+
 GSS_HD double gss_spec_fix(double x, int64_t n, const gss_spec_in_t *in, const gss_spec_t *o,
                            int *hit)
 {

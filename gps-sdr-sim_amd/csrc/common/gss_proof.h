@@ -253,11 +253,15 @@ GSS_PF int merge_hits(const int64_t *a, int na, const int64_t *b, int nb, int64_
 
 /* 1 if certified (lin filled), 0 if this channel needs the exact path.  an (NULL: none): the
    chain's exact carrier values inside the block (gss_carr_anchor_t), where the carrier walks to
-   the ambiguous samples start instead of at the block start; the rows are the same either way. */
+   the ambiguous samples start instead of at the block start; or, without them, sin / sspec (NULL:
+   none): the row's speculative walk, from which the anchors are made the first time a walk is
+   needed (gss_spec_anchors; gss_run's GPU proofs over the walks it keeps on the device).  The
+   rows are the same either way. */
 GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, const uint32_t *ca,
                        const int32_t *lcos, const int32_t *lsin, const gss_carr_anchor_t *an,
-                       gss_lin_t *lin)
+                       const gss_spec_in_t *sin, const gss_spec_t *sspec, gss_lin_t *lin)
 {
+    gss_carr_anchor_t la;
     int inexact = 0;
     int64_t hx[LIN_MAXHIT], hz[LIN_MAXHIT], hq[2 * LIN_MAXHIT + 1];
     gss_code_state at_hz[LIN_MAXHIT];
@@ -382,6 +386,10 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
         if (q == 0) {
             cell = (int)floor(x0 * 512.0);
         } else if (near_boundary(X0 + (i128)q * XS, DX1, LIN_CARR_LGB)) {
+            if (!an && sin && sspec && sin->s == s) {  /* the anchors, once, from the walk */
+                gss_spec_anchors(x0, n, sin, sspec, la.pos, la.val);
+                an = &la;
+            }
             if (an)                                  /* from the last anchor past the walk */
                 for (int a = GSS_SPEC_K - 1; a >= 1; a--)
                     if (an->pos[a] > xat && an->pos[a] <= q) {

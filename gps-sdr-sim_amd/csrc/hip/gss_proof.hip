@@ -61,6 +61,7 @@ __global__ __launch_bounds__(PF_BLOCKS * GSS_MAXCH) void gss_proof_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch, int nblk,
     int n_per_blk, const uint32_t *__restrict__ ca, int n_ca, const uint32_t *__restrict__ nav,
     int n_nav, proof_lut lut, const gss_carr_anchor_t *__restrict__ anch,
+    const gss_spec_in_t *__restrict__ sin, const gss_spec_t *__restrict__ sspec,
     gss_lin_t *__restrict__ lin, int32_t *__restrict__ fast, int64_t first, int force_exact)
 {
     __shared__ int32_t lcos[512], lsin[512];
@@ -89,7 +90,9 @@ __global__ __launch_bounds__(PF_BLOCKS * GSS_MAXCH) void gss_proof_kernel(
             } else {
                 int ok = lin_channel(p, n_per_blk, nav + (size_t)p->nav_tbl * GSS_NAV_WORDS,
                                      ca + (size_t)p->ca_tbl * GSS_CA_WORDS, lcos, lsin,
-                                     anch ? anch + (size_t)b * GSS_MAXCH + k : nullptr, l);
+                                     anch ? anch + (size_t)b * GSS_MAXCH + k : nullptr,
+                                     sin ? sin + (size_t)b * GSS_MAXCH + k : nullptr,
+                                     sspec ? sspec + (size_t)b * GSS_MAXCH + k : nullptr, l);
                 if (p->gain > 1024 || p->gain < -1024)
                     ok = 0;
                 failed = !ok;
@@ -119,17 +122,20 @@ __global__ __launch_bounds__(PF_BLOCKS * GSS_MAXCH) void gss_proof_kernel(
     }
 }
 
-/* gss_run's launch (force_exact: its test hook); not exported (exports.map) */
+/* gss_run's launch (force_exact: its test hook; sin / sspec: the batch's walks on the device,
+   the anchors' source in records mode); not exported (exports.map) */
 int run_proof_launch(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
                      const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
-                     const gss_carr_anchor_t *anch, gss_lin_t *lin, int32_t *fast,
-                     int64_t first, int force_exact, hipStream_t st)
+                     const gss_carr_anchor_t *anch, const gss_spec_in_t *sin,
+                     const gss_spec_t *sspec, gss_lin_t *lin, int32_t *fast, int64_t first,
+                     int force_exact, hipStream_t st)
 {
     if (nblk <= 0)
         return 0;
     hipLaunchKernelGGL(gss_proof_kernel, dim3((unsigned)((nblk + PF_BLOCKS - 1) / PF_BLOCKS)),
                        dim3(PF_BLOCKS * GSS_MAXCH), 0, st, blk, nch, nblk, n_per_blk, ca_bits,
-                       n_ca, nav, n_nav, host_lut(), anch, lin, fast, first, force_exact);
+                       n_ca, nav, n_nav, host_lut(), anch, sin, sspec, lin, fast, first,
+                       force_exact);
     return hipGetLastError() == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "proof kernel launch");
 }
 
@@ -153,6 +159,6 @@ extern "C" int gss_linearize_device_ex(gss_dev *d, const gss_chan_blk_t *blk, co
         return gss_fail(GSS_E_ARG, "invalid linearize_device arguments");
     if (hipSetDevice(gss_dev_ordinal(d)) != hipSuccess)
         return gss_fail(GSS_E_HIP, "hipSetDevice");
-    return run_proof_launch(blk, nch, nblk, n_per_blk, ca_bits, n_ca, nav, n_nav, anch, lin, fast,
-                            0, 0, (hipStream_t)stream);
+    return run_proof_launch(blk, nch, nblk, n_per_blk, ca_bits, n_ca, nav, n_nav, anch, nullptr,
+                            nullptr, lin, fast, 0, 0, (hipStream_t)stream);
 }

@@ -172,6 +172,8 @@ struct Slot {
     int32_t *fast = nullptr;         /* fast[nb], then the exact-path block list [n_fb] */
     gss_carr_anchor_t *anch = nullptr;   /* the chain's anchors [nb][GSS_MAXCH] (proofs)   */
     int has_anch = 0;                /* ... filled for this use of the slot               */
+    int sb_idx = -1;                 /* records mode: the walk batch it came from (its device
+                                        walks are the GPU proofs' anchors)                  */
     int n_fb = 0;
     int nb = 0, nch_max = 1;
     int64_t first = 0;               /* run index of the slot's first block */
@@ -238,6 +240,8 @@ struct Run {
         gss_spec_in_t *d_in = nullptr;
         gss_spec_t *d_spec = nullptr;
         gss_spec_rec_t *h_rec = nullptr;
+        hipEvent_t consumed = nullptr;        /* a slot's GPU proof has read d_in / d_spec */
+        int consumed_pending = 0;
         double carr[GSS_MAXCH];                              /* exact, at its first block */
         int nb = 0, launched = 0;
         double tg = 0.0, tk = 0.0;                           /* trace: guess start, launch end */
@@ -317,8 +321,9 @@ static int h2d(const Run &r, void *dst, const void *src, size_t n, hipStream_t s
 }  // namespace
 int run_proof_launch(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
                      const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
-                     const gss_carr_anchor_t *anch, gss_lin_t *lin, int32_t *fast,
-                     int64_t first, int force_exact, hipStream_t st);   /* gss_proof.hip */
+                     const gss_carr_anchor_t *anch, const gss_spec_in_t *sin,
+                     const gss_spec_t *sspec, gss_lin_t *lin, int32_t *fast, int64_t first,
+                     int force_exact, hipStream_t st);            /* gss_proof.hip */
 namespace {
 
 static void fill_fb_ck(const Run &r, Slot &sl)
@@ -656,6 +661,10 @@ int spec_launch(Run &r, Run::SpecBatch &b, int ask)
        16-byte copies each way) measured the same: the downloads beside them run at ~0.8 of the
        link either way, the walks' own traffic (~14 MB per 2048-block slot back to the host,
        with the 10 MB of uploads) sharing its device-to-host direction */
+    if (b.consumed_pending) {            /* a GPU proof still reads the batch's device walks */
+        RUN_TRY(hipStreamWaitEvent(r.spec_st, b.consumed, 0));
+        b.consumed_pending = 0;
+    }
     rc = r.rec ? gss_spec_records_device(r.dev, b.h_in, nrow, r.n_per_blk, b.d_in, b.d_spec,
                                          b.h_rec, r.spec_st)
                : gss_spec_device(r.dev, b.h_in, nrow, r.n_per_blk, b.h_spec, r.spec_st);
@@ -726,6 +735,7 @@ int next_ask(const Run &r, int64_t cursor)
 int plan_into(Run &r, Slot &sl, int64_t *cursor)
 {
     sl.has_anch = 0;
+    sl.sb_idx = -1;
     if (r.opts && r.opts->carr_in) {
         int nb = 0;
         int rc = take_upfront(r, sl, &nb);
@@ -781,6 +791,7 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
             }
             if (!rc && r.n_fly > 0) {
                 rc = spec_finish(r, r.sb[r.sb_head], sl.blk, sl.nch, &nb, sl.anch);
+                sl.sb_idx = r.sb_head;
                 r.sb_head = (r.sb_head + 1) % 3;
                 r.n_fly--;
             }
@@ -790,6 +801,7 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
                 rc = spec_launch(r, b, ask);
             if (!rc && b.launched)                     /* else the range is done: nb stays 0 */
                 rc = spec_finish(r, b, sl.blk, sl.nch, &nb, sl.anch);
+                sl.sb_idx = r.sb_cur;
             if (!rc && nb > 0) {                       /* the next batch's walks, on the GPU now */
                 const int ask2 = next_ask(r, *cursor + nb);
                 r.sb_cur ^= 1;
@@ -1042,11 +1054,17 @@ int proof_ahead(Run &r, Slot &sl)
     if (v.anch)
         RUN_H2D(v.anch, sl.anch, sizeof(gss_carr_anchor_t) * GSS_MAXCH * (size_t)sl.nb, sl.pst);
     RUN_TRY(hipStreamWaitEvent(sl.pst, sl.navd, 0));
+    Run::SpecBatch *sb = r.rec && sl.sb_idx >= 0 && !v.anch ? &r.sb[sl.sb_idx] : nullptr;
     int rc = run_proof_launch(v.blk, v.nch, sl.nb, r.n_per_blk, r.d_ca, 32, r.d_nav,
-                              n_rows > 0 ? n_rows : 1, v.anch, v.lin, v.fast, sl.first,
-                              r.force_exact, sl.pst);
+                              n_rows > 0 ? n_rows : 1, v.anch, sb ? sb->d_in : nullptr,
+                              sb ? sb->d_spec : nullptr, v.lin, v.fast, sl.first, r.force_exact,
+                              sl.pst);
     if (rc)
         return rc;
+    if (sb) {                                /* the batch's next walks wait for this proof */
+        RUN_TRY(hipEventRecord(sb->consumed, sl.pst));
+        sb->consumed_pending = 1;
+    }
     RUN_TRY(hipEventRecord(sl.proved, sl.pst));
     return 0;
 }
@@ -1393,6 +1411,7 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             (void)hipHostFree(b.h_in); (void)hipHostFree(b.h_spec); (void)hipHostFree(b.h_rec);
             (void)hipFree(b.d_in); (void)hipFree(b.d_spec);
             if (b.walked) (void)hipEventDestroy(b.walked);
+            if (b.consumed) (void)hipEventDestroy(b.consumed);
         }
         (void)hipFree(r.spec_warm);
         if (r.spec_st) (void)hipStreamDestroy(r.spec_st);
@@ -1477,6 +1496,7 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                 b.nch.resize(nb);
                 b.chain.resize(rows);
                 if (hipEventCreateWithFlags(&b.walked, hipEventDisableTiming) != hipSuccess ||
+                    hipEventCreateWithFlags(&b.consumed, hipEventDisableTiming) != hipSuccess ||
                     hipHostMalloc((void **)&b.h_in, sizeof(gss_spec_in_t) * rows,
                                   hipHostMallocDefault) != hipSuccess ||
                     (r.rec ? hipMalloc((void **)&b.d_in, sizeof(gss_spec_in_t) * rows) !=

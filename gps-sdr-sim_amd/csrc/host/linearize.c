@@ -142,7 +142,7 @@ static void *lin_run(void *arg)
             }
             ok = lin_channel(p, j->n_per_blk, j->nav + (size_t)p->nav_tbl * GSS_NAV_WORDS,
                              j->ca + (size_t)p->ca_tbl * GSS_CA_WORDS, lut_cosT, lut_sinT,
-                             j->anch ? &j->anch[(size_t)b * GSS_MAXCH + k] : NULL,
+                             j->anch ? &j->anch[(size_t)b * GSS_MAXCH + k] : NULL, NULL, NULL,
                              &j->lin[(size_t)b * GSS_MAXCH + k]);
             if (p->gain > 1024 || p->gain < -1024)    /* an exact f16 MFMA operand, and so is
                                                          its doubled data-bit difference */

@@ -728,10 +728,8 @@ static void anchor_part(void *arg, int b)
     const anchor_job *j = arg;
     for (int k = 0; k < j->nch[b] && k < GSS_MAXCH; k++) {
         const size_t e = (size_t)b * GSS_MAXCH + k;
-        int hit = 0;
-        double d = 0.0;
-        (void)fix_row(j->blk[e].carr0, j->n_per_blk, &j->in[e], &j->spec[e], &hit, &d,
-                      &j->anch[e]);
+        gss_spec_anchors(j->blk[e].carr0, j->n_per_blk, &j->in[e], &j->spec[e],
+                         j->anch[e].pos, j->anch[e].val);
     }
 }
 

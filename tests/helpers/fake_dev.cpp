@@ -85,12 +85,20 @@ extern "C" int gss_spec_records_device(gss_dev *d, const gss_spec_in_t *in, int 
 
 int run_proof_launch(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n_per_blk,
                      const uint32_t *ca_bits, int n_ca, const uint32_t *nav, int n_nav,
-                     const gss_carr_anchor_t *anch, gss_lin_t *lin, int32_t *fast,
-                     int64_t first, int force_exact, hipStream_t st)
+                     const gss_carr_anchor_t *anch, const gss_spec_in_t *sin,
+                     const gss_spec_t *sspec, gss_lin_t *lin, int32_t *fast, int64_t first,
+                     int force_exact, hipStream_t st)
 {
     if (nblk <= 0)
         return 0;
     fake_enqueue(st, [=] {
+        /* the walks the anchors would come from are read here (their lifetime is what the run
+           must keep: a reused batch must wait for this proof), then the host proof */
+        volatile double sink = 0.0;
+        if (sin && sspec)
+            for (int i = 0; i < nblk * GSS_MAXCH; i++)
+                sink = sink + sin[i].g + sspec[i].w1;
+        (void)sink;
         (void)gss_linearize_ex(blk, nch, nblk, n_per_blk, ca_bits, n_ca, nav, n_nav, anch, lin,
                                fast, 1);
         if (force_exact > 0)
