@@ -274,6 +274,10 @@ struct Run {
     int spec = 0;                    /* per batch (gss_run), or over the range (hand-off)      */
     int rec = 0;                     /* per batch: records, not walks, back from the GPU
                                         (gss_spec_records_device; GSS_RUN_REC=0: the walks)    */
+    int dev_anch = 0;                /* records mode: GPU proofs take their anchors from the
+                                        batch's device walks (GSS_RUN_DEV_ANCHORS=1).  Off: the
+                                        configs[4] run measured 43.2-43.4 GB/s with them against
+                                        43.8-44.8 without (profiles/round5/e2e/probe_r5s)      */
     hipStream_t spec_st = nullptr;
     uint64_t *spec_warm = nullptr;   /* device scratch of the walks' first launch (one row) */
     int64_t spec_rows = 0, spec_hits = 0;
@@ -1054,7 +1058,8 @@ int proof_ahead(Run &r, Slot &sl)
     if (v.anch)
         RUN_H2D(v.anch, sl.anch, sizeof(gss_carr_anchor_t) * GSS_MAXCH * (size_t)sl.nb, sl.pst);
     RUN_TRY(hipStreamWaitEvent(sl.pst, sl.navd, 0));
-    Run::SpecBatch *sb = r.rec && sl.sb_idx >= 0 && !v.anch ? &r.sb[sl.sb_idx] : nullptr;
+    Run::SpecBatch *sb = r.rec && r.dev_anch && sl.sb_idx >= 0 && !v.anch ? &r.sb[sl.sb_idx]
+                                                                          : nullptr;
     int rc = run_proof_launch(v.blk, v.nch, sl.nb, r.n_per_blk, r.d_ca, 32, r.d_nav,
                               n_rows > 0 ? n_rows : 1, v.anch, sb ? sb->d_in : nullptr,
                               sb ? sb->d_spec : nullptr, v.lin, v.fast, sl.first, r.force_exact,
@@ -1477,6 +1482,8 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             r.spec = lazy_ck(r) && !(e && e[0] == '0');
             const char *er = getenv("GSS_RUN_REC");
             r.rec = r.spec && !(opts && opts->carr_in) && !(er && er[0] == '0');
+            const char *ed = getenv("GSS_RUN_DEV_ANCHORS");
+            r.dev_anch = ed && ed[0] == '1';
         }
         if (!err && r.spec) {
             const size_t rows = nb * GSS_MAXCH;

@@ -127,7 +127,8 @@ struct Mode {
 
 static const char *ENV_KEYS[] = {"GSS_RUN_SPEC", "GSS_RUN_ROWS_AHEAD", "GSS_RUN_PROVER",
                                  "GSS_RUN_PROOF", "GSS_RUN_FORCE_EXACT", "GSS_RUN_UPLOAD",
-                                 "GSS_RUN_ROWS_POOL", "GSS_RUN_REC", "GSS_RUN_ANCHORS"};
+                                 "GSS_RUN_ROWS_POOL", "GSS_RUN_REC", "GSS_RUN_ANCHORS",
+                                 "GSS_RUN_DEV_ANCHORS"};
 
 static void set_env(const Mode &m)
 {
@@ -201,6 +202,8 @@ int main(int argc, char **argv)
         {"default", {}},
         {"host chain (GSS_RUN_SPEC=0)", {{"GSS_RUN_SPEC", "0"}}},
         {"rows ahead, device proofs (auto)", {{"GSS_RUN_ROWS_AHEAD", "1"}}},
+        {"rows ahead, device proofs, anchors from the device walks",
+         {{"GSS_RUN_ROWS_AHEAD", "1"}, {"GSS_RUN_DEV_ANCHORS", "1"}}},
         {"rows ahead, prover thread", {{"GSS_RUN_ROWS_AHEAD", "1"}, {"GSS_RUN_PROOF", "host"}}},
         {"rows ahead, proofs on the planner",
          {{"GSS_RUN_ROWS_AHEAD", "1"}, {"GSS_RUN_PROVER", "0"}, {"GSS_RUN_PROOF", "host"}}},

@@ -579,7 +579,8 @@ def test_streaming_run_sink_error_stops_cleanly(dev, golden):
     ("1", "1", "1", "gpu", 1), ("1", "1", "1", "split", 57), ("1", "0", "1", "split", 1),
     ("1", "1", "1", "host-dma", 57), ("0", "0", "1", "gpu-dma", 57),
     ("1", "1", "1", "host-walks", 57), ("1", "0", "1", "gpu-walks", 57),
-    ("1", "1", "1", "host-walks", 1)])
+    ("1", "1", "1", "host-walks", 1), ("1", "1", "1", "gpu-devanch", 57),
+    ("1", "1", "1", "gpu-devanch", 1)])
 def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec, ahead, prover, proof, batch):
     """gss_run with the carrier chain walked on the host (GSS_RUN_SPEC=0) and run ahead on the
     GPU (the default), with the rows produced on the planner thread (GSS_RUN_ROWS_AHEAD=0) or
@@ -593,6 +594,9 @@ def test_streaming_run_chain_modes(dev, golden, monkeypatch, spec, ahead, prover
     if proof.endswith("-walks"):
         proof = proof[:-6]
         monkeypatch.setenv("GSS_RUN_REC", "0")
+    if proof.endswith("-devanch"):            # GPU proofs anchored on the batch's device walks
+        proof = proof[:-8]
+        monkeypatch.setenv("GSS_RUN_DEV_ANCHORS", "1")
     if proof.endswith("-dma"):                # the slots' uploads by the copy engine
         proof = proof[:-4]
         monkeypatch.setenv("GSS_RUN_UPLOAD", "dma")
