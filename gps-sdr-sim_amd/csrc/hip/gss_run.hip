@@ -40,6 +40,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 #include "gpssim_amd.h"
 
@@ -140,6 +141,105 @@ static void pool_put(void *p, size_t n, bool host, int dev)
     (void)(host ? hipHostFree(p) : hipFree(p));
 }
 
+/* The run's other buffers and its streams outlive it the same way (a run creates a dozen
+   streams and pins ~75 MB of rows, lines and walk buffers at 2,048-block slots: most of a short
+   run's start-up): pin_alloc / dev_alloc take from the buffer pool and record the
+   size they got, so that pin_free / dev_free (any pointer, null included) give it back;
+   stream_get / stream_put keep idle non-blocking streams per device and priority. */
+namespace {
+std::unordered_map<void *, PoolBuf> pool_out;          /* pooled buffers in use, by pointer */
+struct PoolStream { hipStream_t s; int dev; int hi; };
+std::vector<PoolStream> spool;                         /* idle streams */
+std::vector<PoolStream> spool_out;                     /* pooled streams in use */
+}  // namespace
+
+static hipError_t pooled_alloc(void **p, size_t n, bool host)
+{
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    size_t got = 0;
+    *p = nullptr;
+    const hipError_t e = pool_get(p, n, host, dev, &got);
+    if (e == hipSuccess && *p) {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        pool_out[*p] = {*p, got, dev, host};
+    }
+    return e;
+}
+
+static void pooled_free(void *p)
+{
+    if (!p)
+        return;
+    PoolBuf b;
+    {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        const auto it = pool_out.find(p);
+        if (it == pool_out.end())
+            return;                                    /* not a pooled buffer */
+        b = it->second;
+        pool_out.erase(it);
+    }
+    pool_put(b.p, b.n, b.host, b.dev);
+}
+
+static hipError_t pin_alloc(void **p, size_t n) { return pooled_alloc(p, n, true); }
+static hipError_t dev_alloc(void **p, size_t n) { return pooled_alloc(p, n, false); }
+static void pin_free(void *p) { pooled_free(p); }
+static void dev_free(void *p) { pooled_free(p); }
+
+/* a non-blocking stream of the current device (hi: the highest priority) */
+static hipError_t stream_get(hipStream_t *s, bool hi)
+{
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        for (size_t i = 0; i < spool.size(); i++)
+            if (spool[i].dev == dev && spool[i].hi == (int)hi) {
+                *s = spool[i].s;
+                spool_out.push_back(spool[i]);
+                spool.erase(spool.begin() + (long)i);
+                return hipSuccess;
+            }
+    }
+    hipError_t e;
+    if (hi) {
+        int lo_pri = 0, hi_pri = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri);
+        e = hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi_pri);
+    } else {
+        e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    }
+    if (e == hipSuccess) {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        spool_out.push_back({*s, dev, (int)hi});
+    }
+    return e;
+}
+
+/* back to the pool when it came from stream_get (the caller has synchronised it), else
+   destroyed (the CU-masked streams) */
+static void stream_put(hipStream_t s)
+{
+    if (!s)
+        return;
+    {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        for (size_t i = 0; i < spool_out.size(); i++)
+            if (spool_out[i].s == s) {
+                if (spool.size() < 64) {
+                    spool.push_back(spool_out[i]);
+                    spool_out.erase(spool_out.begin() + (long)i);
+                    return;
+                }
+                spool_out.erase(spool_out.begin() + (long)i);
+                break;
+            }
+    }
+    (void)hipStreamDestroy(s);
+}
+
 /* free the pooled buffers of device `dev` (gss_dev_close; -1: every device) */
 extern "C" void gss_run_pool_drain(int dev)
 {
@@ -156,8 +256,22 @@ extern "C" void gss_run_pool_drain(int dev)
             }
         }
     }
+    std::vector<PoolStream> sout;
+    {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        for (size_t i = 0; i < spool.size();) {
+            if (dev < 0 || spool[i].dev == dev) {
+                sout.push_back(spool[i]);
+                spool.erase(spool.begin() + (long)i);
+            } else {
+                i++;
+            }
+        }
+    }
     for (const PoolBuf &b : out)
         (void)(b.host ? hipHostFree(b.p) : hipFree(b.p));
+    for (const PoolStream &q : sout)
+        (void)hipStreamDestroy(q.s);
 }
 
 struct Slot {
@@ -363,9 +477,9 @@ int chain_upfront_spec(Run &r, double *carr, const gss_chain_t *chain)
     gss_spec_in_t *h_in = nullptr;                     /* pinned: the lanes use them directly */
     gss_spec_t *h_spec = nullptr;
     int rc = 0;
-    if (hipHostMalloc((void **)&h_in, sizeof(gss_spec_in_t) * rows_max, hipHostMallocDefault) !=
+    if (pin_alloc((void **)&h_in, sizeof(gss_spec_in_t) * rows_max) !=
             hipSuccess ||
-        hipHostMalloc((void **)&h_spec, sizeof(gss_spec_t) * rows_max, hipHostMallocDefault) !=
+        pin_alloc((void **)&h_spec, sizeof(gss_spec_t) * rows_max) !=
             hipSuccess)
         rc = gss_fail(GSS_E_NOMEM, "carrier-chain buffers (%zu rows)", rows_max);
     int64_t hits = 0, n_rows = 0;
@@ -392,7 +506,7 @@ int chain_upfront_spec(Run &r, double *carr, const gss_chain_t *chain)
     if (trace_on())
         fprintf(stderr, "trace spec upfront rows %lld hits %lld\n", (long long)n_rows,
                 (long long)hits);
-    (void)hipHostFree(h_in); (void)hipHostFree(h_spec);
+    pin_free(h_in); pin_free(h_spec);
     return rc;
 }
 
@@ -459,12 +573,11 @@ int take_nav_sources(Run &r, Slot &sl, int upto)
         upto = n_all;
     const int n = upto > r.nav_planned ? upto - r.nav_planned : 0;
     if (n > sl.nav_cap) {
-        (void)hipHostFree(sl.nav);
+        pin_free(sl.nav);
         sl.nav = nullptr;
         sl.nav_cap = 0;
         const int cap = n * 2 + 16;
-        if (hipHostMalloc((void **)&sl.nav, sizeof(gss_nav_src_t) * (size_t)cap,
-                          hipHostMallocDefault) != hipSuccess)
+        if (pin_alloc((void **)&sl.nav, sizeof(gss_nav_src_t) * (size_t)cap) != hipSuccess)
             return gss_fail(GSS_E_NOMEM, "pinned nav sources");
         sl.nav_cap = cap;
     }
@@ -971,12 +1084,12 @@ int nav_reserve(Run &r, size_t rows, hipStream_t st)
     while (cap < rows)
         cap *= 2;
     uint32_t *p = nullptr;
-    RUN_TRY(hipMalloc((void **)&p, sizeof(uint32_t) * GSS_NAV_WORDS * cap));
+    RUN_TRY(dev_alloc((void **)&p, sizeof(uint32_t) * GSS_NAV_WORDS * cap));
     if (r.d_nav) {
         RUN_TRY(hipStreamSynchronize(st));             /* earlier slots' kernels read it */
         RUN_TRY(hipMemcpy(p, r.d_nav, sizeof(uint32_t) * GSS_NAV_WORDS * r.d_nav_cap,
                           hipMemcpyDeviceToDevice));
-        RUN_TRY(hipFree(r.d_nav));
+        dev_free(r.d_nav);
     }
     r.d_nav = p;
     r.d_nav_cap = cap;
@@ -1031,10 +1144,10 @@ int proof_ahead(Run &r, Slot &sl)
        continue one that an earlier slot brought); the proof only for the slots that take it */
     const size_t need = slot_dev(sl).need;
     if (need > sl.d_in_cap) {                          /* the slot is FREE: nothing reads it */
-        (void)hipFree(sl.d_in);
+        dev_free(sl.d_in);
         sl.d_in = nullptr;
         sl.d_in_cap = 0;
-        RUN_TRY(hipMalloc((void **)&sl.d_in, need));
+        RUN_TRY(dev_alloc((void **)&sl.d_in, need));
         sl.d_in_cap = need;
     }
     const SlotDev v = slot_dev(sl);
@@ -1112,10 +1225,10 @@ int submit(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, in
     const size_t need = slot_dev(sl).need;
     if (need > sl.d_in_cap) {
         RUN_TRY(hipStreamSynchronize(st));
-        (void)hipFree(sl.d_in);
+        dev_free(sl.d_in);
         sl.d_in = nullptr;
         sl.d_in_cap = 0;
-        RUN_TRY(hipMalloc((void **)&sl.d_in, need));
+        RUN_TRY(dev_alloc((void **)&sl.d_in, need));
         sl.d_in_cap = need;
     }
     const double tq0 = trace_on() ? tnow() : 0.0;
@@ -1291,7 +1404,7 @@ hipError_t cu_mask_stream(hipStream_t *st, int n_sel, bool rest)
 bool make_streams(hipStream_t *cp)
 {
     for (int k = 0; k < NCOPY; k++)
-        if (hipStreamCreateWithFlags(&cp[k], hipStreamNonBlocking) != hipSuccess)
+        if (stream_get(&cp[k], false) != hipSuccess)
             return false;
     return true;
 }
@@ -1391,12 +1504,12 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         for (Slot &sl : r.slot)                        /* proofs run ahead, not yet rendered */
             if (sl.pst) (void)hipStreamSynchronize(sl.pst);
         for (Slot &sl : r.slot) {
-            (void)hipHostFree(sl.blk); (void)hipHostFree(sl.nch); (void)hipHostFree(sl.ck);
-            (void)hipHostFree(sl.nav); (void)hipHostFree(sl.h_status);
+            pin_free(sl.blk); pin_free(sl.nch); pin_free(sl.ck);
+            pin_free(sl.nav); pin_free(sl.h_status);
             pool_put(sl.h_out, sl.h_out_bytes, true, ordinal);
             pool_put(sl.d_out, sl.d_out_bytes, false, ordinal);
-            (void)hipHostFree(sl.lin); (void)hipHostFree(sl.fast); (void)hipHostFree(sl.anch);
-            (void)hipFree(sl.d_in); (void)hipFree(sl.d_status);
+            pin_free(sl.lin); pin_free(sl.fast); pin_free(sl.anch);
+            dev_free(sl.d_in); dev_free(sl.d_status);
             if (sl.done) (void)hipEventDestroy(sl.done);
             if (sl.rendered) (void)hipEventDestroy(sl.rendered);
             if (sl.tq) (void)hipEventDestroy(sl.tq);
@@ -1404,37 +1517,37 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             if (sl.tc) (void)hipEventDestroy(sl.tc);
         }
         for (Slot &sl : r.slot) {
-            if (sl.pst) (void)hipStreamDestroy(sl.pst);
+            stream_put(sl.pst);
             if (sl.navd) (void)hipEventDestroy(sl.navd);
             if (sl.proved) (void)hipEventDestroy(sl.proved);
         }
-        if (r.nav_st) (void)hipStreamDestroy(r.nav_st);
-        (void)hipFree(d_ca);
-        (void)hipFree(r.d_nav);
+        stream_put(r.nav_st);
+        dev_free(d_ca);
+        dev_free(r.d_nav);
         if (r.spec_st) (void)hipStreamSynchronize(r.spec_st);
         for (Run::SpecBatch &b : r.sb) {
-            (void)hipHostFree(b.h_in); (void)hipHostFree(b.h_spec); (void)hipHostFree(b.h_rec);
-            (void)hipFree(b.d_in); (void)hipFree(b.d_spec);
+            pin_free(b.h_in); pin_free(b.h_spec); pin_free(b.h_rec);
+            dev_free(b.d_in); dev_free(b.d_spec);
             if (b.walked) (void)hipEventDestroy(b.walked);
             if (b.consumed) (void)hipEventDestroy(b.consumed);
         }
-        (void)hipFree(r.spec_warm);
-        if (r.spec_st) (void)hipStreamDestroy(r.spec_st);
+        dev_free(r.spec_warm);
+        stream_put(r.spec_st);
         if (trace_on() && r.spec_rows)
             fprintf(stderr, "trace spec total rows %lld hits %lld\n", (long long)r.spec_rows,
                     (long long)r.spec_hits);
-        if (st) (void)hipStreamDestroy(st);
+        stream_put(st);
         for (hipStream_t c : cp)
-            if (c) (void)hipStreamDestroy(c);
+            stream_put(c);
         if (r.t_base) (void)hipEventDestroy(r.t_base);
     };
     /* buffers */
     {
         gss_ca_table(r.ca);                            /* the proofs' copy, on the host */
-        if (hipMalloc((void **)&d_ca, sizeof r.ca) != hipSuccess ||
+        if (dev_alloc((void **)&d_ca, sizeof r.ca) != hipSuccess ||
             (spec_cus() > 0 && getenv("GSS_RUN_RENDER_REST")
                  ? cu_mask_stream(&st, spec_cus(), true)
-                 : hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess ||
+                 : stream_get(&st, false)) != hipSuccess ||
             !make_streams(cp) ||
             (trace_on() && (hipEventCreate(&r.t_base) != hipSuccess ||
                             hipEventRecord(r.t_base, st) != hipSuccess)))
@@ -1445,19 +1558,17 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         const size_t nb = (size_t)r.batch;
         for (Slot &sl : r.slot) {
             if (err) break;
-            if (hipHostMalloc((void **)&sl.blk, sizeof(gss_chan_blk_t) * GSS_MAXCH * nb,
-                              hipHostMallocDefault) != hipSuccess ||
-                hipHostMalloc((void **)&sl.nch, sizeof(int32_t) * nb, hipHostMallocDefault) !=
+            if (pin_alloc((void **)&sl.blk, sizeof(gss_chan_blk_t) * GSS_MAXCH * nb) != hipSuccess ||
+                pin_alloc((void **)&sl.nch, sizeof(int32_t) * nb) !=
                     hipSuccess ||
-                hipHostMalloc((void **)&sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * nb,
-                              hipHostMallocDefault) != hipSuccess ||
+                pin_alloc((void **)&sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * nb) != hipSuccess ||
                 pool_get((void **)&sl.h_out, bb * nb, true, ordinal, &sl.h_out_bytes) !=
                     hipSuccess ||
-                hipHostMalloc((void **)&sl.h_status, sizeof(int32_t), hipHostMallocDefault) !=
+                pin_alloc((void **)&sl.h_status, sizeof(int32_t)) !=
                     hipSuccess ||
                 pool_get((void **)&sl.d_out, bb * nb, false, ordinal, &sl.d_out_bytes) !=
                     hipSuccess ||
-                hipMalloc((void **)&sl.d_status, sizeof(int32_t)) != hipSuccess ||
+                dev_alloc((void **)&sl.d_status, sizeof(int32_t)) != hipSuccess ||
                 hipEventCreateWithFlags(&sl.done, trace_on() ? hipEventDefault
                                                              : hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&sl.rendered, trace_on() ? hipEventDefault
@@ -1468,13 +1579,12 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                                 hipEventCreate(&sl.tc) != hipSuccess)))
                 err = gss_fail(GSS_E_NOMEM, "run buffers (%zu B per slot)", bb * nb);
             if (!err && r.use_lin &&
-                (hipHostMalloc((void **)&sl.lin, sizeof(gss_lin_t) * GSS_MAXCH * nb,
-                               hipHostMallocDefault) != hipSuccess ||
-                 hipHostMalloc((void **)&sl.fast, sizeof(int32_t) * 2 * nb,
-                               hipHostMallocDefault) != hipSuccess))
+                (pin_alloc((void **)&sl.lin, sizeof(gss_lin_t) * GSS_MAXCH * nb) != hipSuccess ||
+                 pin_alloc((void **)&sl.fast, sizeof(int32_t) * 2 * nb) != hipSuccess))
                 err = gss_fail(GSS_E_NOMEM, "run lines (%zu B per slot)",
                                sizeof(gss_lin_t) * GSS_MAXCH * nb);
         }
+        const double t_slots = trace_on() ? tnow() : 0.0;
         /* the chain run ahead: fast path, float carrier (per batch, or over the up-front range
            of a hand-off) */
         {
@@ -1489,13 +1599,11 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             const size_t rows = nb * GSS_MAXCH;
             r.dev = d;
             /* high priority: the walks wait for free CUs behind the render kernels otherwise */
-            int lo_pri = 0, hi_pri = 0;
-            (void)hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri);
             if ((spec_cus() > 0
                      ? cu_mask_stream(&r.spec_st, spec_cus(), false)
-                     : hipStreamCreateWithPriority(&r.spec_st, hipStreamNonBlocking, hi_pri)) !=
+                     : stream_get(&r.spec_st, true)) !=
                     hipSuccess ||
-                hipMalloc((void **)&r.spec_warm, 1024) != hipSuccess)
+                dev_alloc((void **)&r.spec_warm, 1024) != hipSuccess)
                 err = gss_fail(GSS_E_HIP, "run carrier-chain stream");
             for (Run::SpecBatch &b : r.sb) {
                 if (err) break;
@@ -1504,16 +1612,13 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                 b.chain.resize(rows);
                 if (hipEventCreateWithFlags(&b.walked, hipEventDisableTiming) != hipSuccess ||
                     hipEventCreateWithFlags(&b.consumed, hipEventDisableTiming) != hipSuccess ||
-                    hipHostMalloc((void **)&b.h_in, sizeof(gss_spec_in_t) * rows,
-                                  hipHostMallocDefault) != hipSuccess ||
-                    (r.rec ? hipMalloc((void **)&b.d_in, sizeof(gss_spec_in_t) * rows) !=
+                    pin_alloc((void **)&b.h_in, sizeof(gss_spec_in_t) * rows) != hipSuccess ||
+                    (r.rec ? dev_alloc((void **)&b.d_in, sizeof(gss_spec_in_t) * rows) !=
                                      hipSuccess ||
-                                 hipMalloc((void **)&b.d_spec, sizeof(gss_spec_t) * rows) !=
+                                 dev_alloc((void **)&b.d_spec, sizeof(gss_spec_t) * rows) !=
                                      hipSuccess ||
-                                 hipHostMalloc((void **)&b.h_rec, sizeof(gss_spec_rec_t) * rows,
-                                               hipHostMallocDefault) != hipSuccess
-                           : hipHostMalloc((void **)&b.h_spec, sizeof(gss_spec_t) * rows,
-                                           hipHostMallocDefault) != hipSuccess))
+                                 pin_alloc((void **)&b.h_rec, sizeof(gss_spec_rec_t) * rows) != hipSuccess
+                           : pin_alloc((void **)&b.h_spec, sizeof(gss_spec_t) * rows) != hipSuccess))
                     err = gss_fail(GSS_E_NOMEM, "run carrier-chain buffers (%zu rows)", rows);
             }
             /* the chain's anchors for the proofs' carrier walks (GSS_RUN_ANCHORS=0: none) */
@@ -1521,8 +1626,7 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             if (r.use_lin && !(opts && opts->carr_in) && !(ea && ea[0] == '0'))
                 for (Slot &sl : r.slot) {
                     if (err) break;
-                    if (hipHostMalloc((void **)&sl.anch, sizeof(gss_carr_anchor_t) * rows,
-                                      hipHostMallocDefault) != hipSuccess)
+                    if (pin_alloc((void **)&sl.anch, sizeof(gss_carr_anchor_t) * rows) != hipSuccess)
                         err = gss_fail(GSS_E_NOMEM, "run anchors (%zu rows)", rows);
                 }
         }
@@ -1567,21 +1671,23 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             }
             err = gss_scn_carrier(s, r.carr);
         }
+        const double t_rows = trace_on() ? tnow() : 0.0;
         if (!err)
             err = gss_dev_reserve(d, r.batch, info.n_per_blk);
+        const double t_reserve = trace_on() ? tnow() : 0.0;
+        if (trace_on())
+            fprintf(stderr, "trace setup_parts slots %.6f spec_rows %.6f reserve %.6f\n",
+                    t_slots - t_enter, t_rows - t_slots, t_reserve - t_rows);
         if (!err && r.gpu_proof) {
             /* proofs run ahead on the slots' own streams (proof_ahead); the device nav table
                reserved for the whole run (nav_rows_bound) */
             r.dev = d;
             r.d_ca = d_ca;
-            int lo_pri = 0, hi_pri = 0;
-            (void)hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri);
-            if (hipStreamCreateWithFlags(&r.nav_st, hipStreamNonBlocking) != hipSuccess)
+            if (stream_get(&r.nav_st, false) != hipSuccess)
                 err = gss_fail(GSS_E_HIP, "run nav stream");
             for (Slot &sl : r.slot) {
                 if (err) break;
-                if (hipStreamCreateWithPriority(&sl.pst, hipStreamNonBlocking, hi_pri) !=
-                        hipSuccess ||
+                if (stream_get(&sl.pst, true) != hipSuccess ||
                     hipEventCreateWithFlags(&sl.navd, hipEventDisableTiming) != hipSuccess ||
                     hipEventCreateWithFlags(&sl.proved, hipEventDisableTiming) != hipSuccess)
                     err = gss_fail(GSS_E_HIP, "run proof streams");

@@ -1,7 +1,7 @@
 """gss_run over one of bench.py's per-config workloads (configs[2..4]) with the run's own trace
 (GSS_RUN_TRACE=1 on stderr, summarised by tools/e2e_trace_summary.py): where the end-to-end time of a
 non-headline config goes.  Usage: python tools/e2e_cfg_probe.py <config index 2-4> [window s]
-[threads].  GPU box only."""
+[threads] [batch blocks].  GPU box only."""
 import os
 import sys
 import time
@@ -17,7 +17,7 @@ window = float(sys.argv[2]) if len(sys.argv) > 2 else c["window"]
 threads = int(sys.argv[3]) if len(sys.argv) > 3 else 16
 dev = G.Device(0)
 bb = G.block_bytes(int(round(c["fs"] / 10)), c["fmt"])
-batch = max(1, B.E2E_SLOT_BYTES // bb)
+batch = int(sys.argv[4]) if len(sys.argv) > 4 else max(1, B.E2E_SLOT_BYTES // bb)
 s = G.Scenario(B.NAV, duration=window, samp_freq=c["fs"], data_format=c["fmt"], **c["kw"])
 got = {"blocks": 0, "bytes": 0}
 
