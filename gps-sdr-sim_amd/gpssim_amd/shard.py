@@ -233,10 +233,14 @@ def chain_speculated(scn_carr, blk, nch, chain, n_per_blk, walker, baton, thread
     spec = _walk_rows(gi.reshape(-1), n_per_blk, walker).reshape(gi.shape)
     first = blk if rank == 0 else blk.copy()
     e0, hits = carr_chain_spec(x0, first, nch, chain, n_per_blk, gi, spec, threads=threads)
-    if rank == 0:                            # the exact chain: on to rank 1 at once
-        baton.isend(e0)
+    if rank == 0:                            # the exact chain
         t["fix_s"] = time.perf_counter() - t0
     maps = baton.all_gather(map_vec(x0 if rank else scn_carr, e0, resets))
+    if rank == 0:
+        # on to rank 1 after the last collective: from here on only the batons move, in rank
+        # order, so that no backend (RCCL orders a rank's operations) can interleave a pending
+        # send with a collective the receiver has not reached
+        baton.isend(e0)
     rewalked = 0
     if rank > 0:
         x1 = compose_start(maps, rank)
