@@ -18,12 +18,16 @@
  * at the same path: the payload carries a fingerprint of everything the carriers depend on (the
  * scenario options, the bytes of the navigation and motion files, the world size and the
  * boundary block), and a reader ignores a file whose fingerprint differs and waits for its own.
+ * With a run id the chain is also speculated across the ranks (gss_run_opts_t.carr_predict): each
+ * rank publishes its map of the slot carriers in two rounds of FILE.gss-map-* files and walks its
+ * range before its carriers arrive (GSS_HANDOFF_SPEC=0: off).
  * Env: GSS_DEVICE (ordinal; default LOCAL_RANK or 0), GSS_BATCH (blocks per launch, default
  *      128), GSS_THREADS (planner threads, default the CPU share: cgroup cpu.max, else the online
  *      CPUs, at most 16), GSS_HANDOFF_TIMEOUT (seconds a rank waits
  *      for its carriers, default 3600).
  */
 #include <fcntl.h>
+#include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -79,13 +83,24 @@ static int default_threads(void)
     return n < 1 ? 1 : n > 16 ? 16 : (int)n;
 }
 
-/* The carrier hand-off between ranks (plan once per node): a 16-double file per boundary. */
+/* The carrier hand-off between ranks (plan once per node): a 16-double file per boundary, and,
+   for the chain speculated across ranks (gss_run_opts_t.carr_predict), each rank's map of the
+   slot carriers per round, FILE.gss-map-<run id>-<round>-<first block>, read by the ranks after
+   it and removed by the last rank once its own carriers have arrived (every rank has read the
+   maps by then: each reads them before it waits for its carriers). */
 typedef struct {
     gss_scn *scn;
     char in_path[600], out_path[600];      /* empty: none (rank 0 / last rank) */
     uint64_t fp_in, fp_out;                /* fingerprints: scenario + boundary block */
     double timeout_s;
+    /* speculation */
+    const char *out_file, *run_id;
+    int rank, world;
+    int64_t n_blocks;
+    uint64_t fp;                           /* the scenario's fingerprint */
 } handoff_ctx;
+
+static int64_t rank_first(const handoff_ctx *h, int r) { return h->n_blocks * r / h->world; }
 
 #define HANDOFF_MAGIC 0x67737364u          /* "gssd": magic, fingerprint, 16 carriers */
 
@@ -96,6 +111,18 @@ static uint64_t fnv(uint64_t h, const void *p, size_t n)
     for (size_t i = 0; i < n; i++)
         h = (h ^ b[i]) * 0x100000001b3ull;
     return h;
+}
+
+static void map_path(const handoff_ctx *h, int round, int r, char *out, size_t n)
+{
+    snprintf(out, n, "%s.gss-map-%s-%d-%lld", h->out_file, h->run_id, round,
+             (long long)rank_first(h, r));
+}
+
+static uint64_t map_fp(const handoff_ctx *h, int round, int r)
+{
+    const int64_t first = rank_first(h, r);
+    return fnv(fnv(h->fp ^ 0x6d6170u, &round, sizeof round), &first, sizeof first);
 }
 
 static uint64_t fnv_file(uint64_t h, const char *path)
@@ -147,6 +174,13 @@ static int handoff_in(void *user, double *carr)
             fclose(f);
             if (ok && magic == HANDOFF_MAGIC && fp == h->fp_in) {
                 unlink(h->in_path);
+                if (h->rank == h->world - 1 && h->run_id)   /* every rank has read the maps */
+                    for (int round = 0; round < 2; round++)
+                        for (int r = 0; r + 1 < h->world; r++) {
+                            char path[640];
+                            map_path(h, round, r, path, sizeof path);
+                            unlink(path);
+                        }
                 return 0;
             }
             /* another run's (or a torn) file: not ours, wait for rank r-1 to replace it */
@@ -156,6 +190,62 @@ static int handoff_in(void *user, double *carr)
         nanosleep(&nap, NULL);
         waited += 1e-3;
     }
+}
+
+#define MAP_MAGIC 0x6773736du              /* "gssm": magic, fingerprint, 48 doubles */
+
+/* publish this rank's map of `round`, then compose the maps of the ranks before it */
+static int handoff_predict(void *user, int round, const double *map, double *start)
+{
+    const handoff_ctx *h = (const handoff_ctx *)user;
+    char path[640], tmp[660];
+    map_path(h, round, h->rank, path, sizeof path);
+    if (h->rank + 1 < h->world) {                       /* the last rank's map has no reader */
+        snprintf(tmp, sizeof tmp, "%s.tmp", path);
+        FILE *f = fopen(tmp, "wb");
+        if (!f)
+            return 1;
+        const uint32_t magic = MAP_MAGIC;
+        const uint64_t fp = map_fp(h, round, h->rank);
+        int ok = fwrite(&magic, sizeof magic, 1, f) == 1 && fwrite(&fp, sizeof fp, 1, f) == 1 &&
+                 fwrite(map, sizeof(double), 3 * GSS_MAXCH, f) == 3 * GSS_MAXCH;
+        ok = (fclose(f) == 0) && ok;
+        if (!ok || rename(tmp, path) != 0)
+            return 1;
+    }
+    double x[GSS_MAXCH];
+    memcpy(x, map, sizeof x);                           /* rank 0: its own start */
+    for (int r = 0; r < h->rank; r++) {
+        double m[3 * GSS_MAXCH];
+        map_path(h, round, r, path, sizeof path);
+        struct timespec nap = {0, 1000000};
+        double waited = 0.0;
+        for (;;) {
+            FILE *f = fopen(path, "rb");
+            if (f) {
+                uint32_t magic = 0;
+                uint64_t fp = 0;
+                const int ok = fread(&magic, sizeof magic, 1, f) == 1 &&
+                               fread(&fp, sizeof fp, 1, f) == 1 &&
+                               fread(m, sizeof(double), 3 * GSS_MAXCH, f) == 3 * GSS_MAXCH;
+                fclose(f);
+                if (ok && magic == MAP_MAGIC && fp == map_fp(h, round, r))
+                    break;
+            }
+            if (waited > h->timeout_s)
+                return 1;
+            nanosleep(&nap, NULL);
+            waited += 1e-3;
+        }
+        if (r == 0)
+            memcpy(x, m, sizeof x);                     /* the run's initial carriers */
+        for (int i = 0; i < GSS_MAXCH; i++) {
+            const double add = m[GSS_MAXCH + i], v = x[i] + add;
+            x[i] = m[2 * GSS_MAXCH + i] != 0.0 ? add : v - floor(v);
+        }
+    }
+    memcpy(start, x, sizeof x);
+    return 0;
 }
 
 static int handoff_out(void *user, const double *carr)
@@ -207,7 +297,16 @@ static int run_rank(const gss_cli_t *cli, gss_scn *scn, const gss_scn_info_t *in
     const uint64_t fp = scenario_fingerprint(cli, world);
     h.fp_in = fnv(fp, &first, sizeof first);
     h.fp_out = fnv(fp, &last, sizeof last);
-    gss_run_opts_t ro = {handoff_in, handoff_out, &h};
+    h.fp = fp;
+    h.out_file = cli->out_file;
+    h.run_id = run_id;
+    h.rank = rank;
+    h.world = world;
+    h.n_blocks = nb;
+    /* GSS_HANDOFF_SPEC=0: the carriers first, then the chain (no speculation; every rank of a
+       run must agree) */
+    gss_run_opts_t ro = {handoff_in, handoff_out, &h,
+                         env_int("GSS_HANDOFF_SPEC", 1) ? handoff_predict : NULL};
     if (run_id && *run_id) {
         if (rank > 0)
             snprintf(h.in_path, sizeof h.in_path, "%s.gss-carr-%s-%lld", cli->out_file, run_id,

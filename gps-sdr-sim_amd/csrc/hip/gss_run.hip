@@ -32,6 +32,7 @@
  * output buffer is rewritten only after its own D2H (event).
  */
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <stdio.h>
@@ -510,12 +511,166 @@ int chain_upfront_spec(Run &r, double *carr, const gss_chain_t *chain)
     return rc;
 }
 
+/* The walks' records of every row of the up-front range, CH blocks per launch, from starts per
+   row (g: [pre_n][GSS_MAXCH]) or, without them, from the lines out of carr (the first pass) */
+int upfront_records(Run &r, const gss_chain_t *chain, const double *carr, const double *g,
+                    std::vector<gss_spec_rec_t> &rec)
+{
+    constexpr int CH = 4096;
+    const size_t rows_max = (size_t)CH * GSS_MAXCH;
+    gss_spec_in_t *h_in = nullptr, *d_in = nullptr;
+    gss_spec_t *d_spec = nullptr;
+    gss_spec_rec_t *h_rec = nullptr;
+    int rc = 0;
+    if (pin_alloc((void **)&h_in, sizeof(gss_spec_in_t) * rows_max) != hipSuccess ||
+        pin_alloc((void **)&h_rec, sizeof(gss_spec_rec_t) * rows_max) != hipSuccess ||
+        dev_alloc((void **)&d_in, sizeof(gss_spec_in_t) * rows_max) != hipSuccess ||
+        dev_alloc((void **)&d_spec, sizeof(gss_spec_t) * rows_max) != hipSuccess)
+        rc = gss_fail(GSS_E_NOMEM, "carrier-chain buffers (%zu rows)", rows_max);
+    rec.resize((size_t)r.pre_n * GSS_MAXCH);
+    double c[GSS_MAXCH];
+    memcpy(c, carr, sizeof c);
+    for (int64_t b0 = 0; !rc && b0 < r.pre_n; b0 += CH) {
+        const int nb = r.pre_n - b0 < CH ? (int)(r.pre_n - b0) : CH;
+        const int nrow = nb * GSS_MAXCH;
+        const gss_chan_blk_t *blk = &r.pre_blk[(size_t)b0 * GSS_MAXCH];
+        const int32_t *nch = &r.pre_nch[(size_t)b0];
+        const gss_chain_t *ch = chain + (size_t)b0 * GSS_MAXCH;
+        rc = gss_carr_chain_starts(c, blk, nch, ch, nb, r.n_per_blk, h_in);   /* k, s, pad */
+        if (rc) break;
+        if (g) {                                       /* the given starts instead of lines */
+            for (int i = 0; i < nrow; i++)
+                if (h_in[i].k == 0)
+                    h_in[i].g = g[(size_t)b0 * GSS_MAXCH + i];
+        } else {
+            (void)gss_carr_line_end(c, blk, nch, ch, nb, r.n_per_blk, c);
+        }
+        if ((rc = gss_spec_records_device(r.dev, h_in, nrow, r.n_per_blk, d_in, d_spec, h_rec,
+                                          r.spec_st)) != 0 ||
+            hipStreamSynchronize(r.spec_st) != hipSuccess) {
+            if (!rc) rc = gss_fail(GSS_E_HIP, "carrier-chain records");
+            break;
+        }
+        memcpy(&rec[(size_t)b0 * GSS_MAXCH], h_rec, sizeof(gss_spec_rec_t) * (size_t)nrow);
+    }
+    pin_free(h_in); pin_free(h_rec); dev_free(d_in); dev_free(d_spec);
+    return rc;
+}
+
+/* The up-front chain speculated across ranks (opts->carr_predict; shard.chain_speculated's
+   steps): the range's map by the lines -> a predicted start -> walks and records from it -> the
+   exact chain from that start and its map -> a second, ~1e-13 prediction -> the rows whose
+   carrier depends on the start walked again from the first chain's carriers moved by the
+   correction -> carr_in -> the records' chain (a compare and two adds per row where the
+   links hold) -> carr_out.  Exact whatever the predictions. */
+int chain_upfront_speculated(Run &r, const gss_chain_t *chain, const double *start0,
+                             double *carr)
+{
+    const int64_t nb = r.pre_n;
+    const size_t rows = (size_t)nb * GSS_MAXCH;
+    const double t0 = tnow();
+    int reset[GSS_MAXCH] = {0};
+    for (int64_t b = 0; b < nb; b++)
+        for (int k = 0; k < r.pre_nch[(size_t)b] && k < GSS_MAXCH; k++) {
+            const gss_chain_t &c = chain[(size_t)b * GSS_MAXCH + k];
+            if (c.reset && c.slot >= 0 && c.slot < GSS_MAXCH)
+                reset[c.slot] = 1;
+        }
+    const bool exact0 = r.first == 0;                   /* the run's own start: no prediction */
+    double zero[GSS_MAXCH] = {0}, end[GSS_MAXCH], map[3 * GSS_MAXCH], x0[GSS_MAXCH],
+        x1[GSS_MAXCH];
+    int rc = gss_carr_line_end(zero, r.pre_blk.data(), r.pre_nch.data(), chain, (int)nb,
+                               r.n_per_blk, end);
+    auto make_map = [&](const double *from, const double *to) {
+        for (int i = 0; i < GSS_MAXCH; i++) {
+            map[i] = exact0 ? start0[i] : 0.0;
+            const double a = to[i] - from[i];
+            map[GSS_MAXCH + i] = reset[i] ? to[i] : a - floor(a);
+            map[2 * GSS_MAXCH + i] = reset[i] ? 1.0 : 0.0;
+        }
+    };
+    make_map(zero, end);
+    if (!rc && r.opts->carr_predict(r.opts->carr_user, 0, map, x0))
+        rc = gss_fail(GSS_E_IO, "carrier prediction (round 0) failed at block %lld",
+                      (long long)r.first);
+    if (rc)
+        return rc;
+    if (exact0)
+        memcpy(x0, start0, sizeof x0);
+    std::vector<gss_spec_rec_t> rec;
+    rc = upfront_records(r, chain, x0, nullptr, rec);
+    if (rc)
+        return rc;
+    std::vector<gss_chan_blk_t> first(r.pre_blk);      /* the chain from the predicted start */
+    double e0[GSS_MAXCH];
+    memcpy(e0, x0, sizeof e0);
+    int hit = 0;
+    rc = gss_carr_chain_records(e0, first.data(), r.pre_nch.data(), chain, (int)nb, r.n_per_blk,
+                                rec.data(), r.threads, &hit);
+    if (rc)
+        return rc;
+    make_map(x0, e0);
+    if (r.opts->carr_predict(r.opts->carr_user, 1, map, x1))
+        return gss_fail(GSS_E_IO, "carrier prediction (round 1) failed at block %lld",
+                        (long long)r.first);
+    if (exact0)
+        memcpy(x1, x0, sizeof x1);
+    double d[GSS_MAXCH];
+    bool moved = false;
+    for (int i = 0; i < GSS_MAXCH; i++) {
+        const double v = x1[i] - x0[i] + 0.5;
+        d[i] = (v - floor(v)) - 0.5;
+        moved = moved || (d[i] != 0.0 && !reset[i]);
+    }
+    int64_t rewalked = 0;
+    if (moved) {                                       /* the start-dependent rows, corrected */
+        std::vector<double> g(rows);
+        int seen_reset[GSS_MAXCH] = {0};
+        for (int64_t b = 0; b < nb; b++)
+            for (int k = 0; k < GSS_MAXCH; k++) {
+                const size_t e = (size_t)b * GSS_MAXCH + k;
+                g[e] = first[e].carr0;
+                if (k >= r.pre_nch[(size_t)b])
+                    continue;
+                const int sl = chain[e].slot;
+                if (sl < 0 || sl >= GSS_MAXCH)
+                    continue;
+                if (chain[e].reset)
+                    seen_reset[sl] = 1;
+                if (!seen_reset[sl]) {
+                    const double v = first[e].carr0 + d[sl];
+                    g[e] = v - floor(v);
+                    rewalked++;
+                }
+            }
+        rc = upfront_records(r, chain, x1, g.data(), rec);
+        if (rc)
+            return rc;
+    }
+    const double t1 = tnow();
+    if (r.opts->carr_in(r.opts->carr_user, carr))
+        return gss_fail(GSS_E_IO, "carrier hand-off (in) failed at block %lld",
+                        (long long)r.first);
+    const double t2 = tnow();
+    rc = gss_carr_chain_records(carr, r.pre_blk.data(), r.pre_nch.data(), chain, (int)nb,
+                                r.n_per_blk, rec.data(), r.threads, &hit);
+    if (trace_on())
+        fprintf(stderr, "trace spec speculated rows %zu hits %d rewalked %lld pre %.6f wait %.6f "
+                "handoff %.6f\n", rows, hit, (long long)rewalked, t1 - t0, t2 - t1, tnow() - t2);
+    return rc;
+}
+
 /* gss_run_ex with a carrier hand-off: seek to the range, produce its rows, take the slot
    carriers at its first block from carr_in, walk the chain, give the end state to carr_out. */
 int plan_range_upfront(Run &r)
 {
     int rc = gss_scn_seek(r.scn, r.first, r.threads);
     if (rc)
+        return rc;
+    /* the speculated chain: with a prediction callback and the walks on the GPU */
+    const bool speculate = r.opts->carr_predict && r.spec && r.rec;
+    double start0[GSS_MAXCH] = {0};
+    if (speculate && r.first == 0 && (rc = gss_scn_carrier(r.scn, start0)) != 0)
         return rc;
     std::vector<gss_chain_t> chain;
     const int step = 4096;
@@ -538,11 +693,20 @@ int plan_range_upfront(Run &r)
             break;                                     /* end of the run */
     }
     double carr[GSS_MAXCH];
+    if (!lazy_ck(r))
+        r.pre_ck.resize((size_t)r.pre_n * GSS_MAXCH * GSS_NCK);
+    if (speculate) {
+        rc = chain_upfront_speculated(r, chain.data(), start0, carr);
+        if (rc)
+            return rc;
+        if (r.opts->carr_out && r.opts->carr_out(r.opts->carr_user, carr))
+            return gss_fail(GSS_E_IO, "carrier hand-off (out) failed after block %lld",
+                            (long long)(r.first + r.pre_n - 1));
+        return 0;
+    }
     if (r.opts->carr_in(r.opts->carr_user, carr))
         return gss_fail(GSS_E_IO, "carrier hand-off (in) failed at block %lld",
                         (long long)r.first);
-    if (!lazy_ck(r))
-        r.pre_ck.resize((size_t)r.pre_n * GSS_MAXCH * GSS_NCK);
     if (r.spec)                                        /* the chain run ahead on the GPU */
         rc = chain_upfront_spec(r, carr, chain.data());
     else
@@ -1591,7 +1755,8 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
             const char *e = getenv("GSS_RUN_SPEC");
             r.spec = lazy_ck(r) && !(e && e[0] == '0');
             const char *er = getenv("GSS_RUN_REC");
-            r.rec = r.spec && !(opts && opts->carr_in) && !(er && er[0] == '0');
+            r.rec = r.spec && !(opts && opts->carr_in && !opts->carr_predict) &&
+                    !(er && er[0] == '0');
             const char *ed = getenv("GSS_RUN_DEV_ANCHORS");
             r.dev_anch = ed && ed[0] == '1';
         }

@@ -499,6 +499,15 @@ typedef struct gss_run_opts {
     int (*carr_in)(void *user, double *carr);             /* [GSS_MAXCH], out                  */
     int (*carr_out)(void *user, const double *carr);      /* [GSS_MAXCH]                       */
     void *carr_user;
+    /* Optional: the chain speculated across ranks.  Called twice (round 0: by the lines, round
+       1: by an exact chain from the first prediction) before carr_in, with this range's map of
+       the slot carriers, map[3 * GSS_MAXCH] = {start (the run's initial carriers when the range
+       starts at block 0, else 0), add, reset}: the range takes x to reset ? add : (x + add) mod
+       1 per slot.  It publishes the map to the ranks after this one and returns in start_out
+       the composition of the maps of the ranks before it (gpssim_amd/shard.py compose_start).
+       The walks then run before carr_in, and from carr_in to carr_out only the records' chain
+       is left.  Exact whatever the predictions.                               */
+    int (*carr_predict)(void *user, int round, const double *map, double *start_out);
 } gss_run_opts_t;
 int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_blocks, int batch,
                int threads, gss_sink_fn sink, void *user, const gss_run_opts_t *opts);

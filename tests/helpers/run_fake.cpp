@@ -17,6 +17,7 @@
  *
  * usage: run_fake NAV_FILE [seconds] [batch] [fmt]
  */
+#include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -156,7 +157,31 @@ struct Baton {
     double carr[GSS_MAXCH];
     int set = 0;
     gss_scn *first = nullptr;     /* rank 0: its carriers are its scenario's own */
+    /* the chain speculated across ranks (carr_predict): the ranks' published maps per round */
+    int rank = 0;
+    double maps[4][2][3 * GSS_MAXCH];
+    int calls = 0;
 };
+/* what the ranks' collective (shard.compose_start, or the CLI's map files) would return: the
+   composition of the maps of the ranks before this one, started from rank 0's initial carriers */
+static int carr_predict(void *u, int round, const double *map, double *out)
+{
+    Baton *b = (Baton *)u;
+    if (round < 0 || round > 1 || b->rank < 0 || b->rank > 3)
+        return 1;
+    memcpy(b->maps[b->rank][round], map, sizeof b->maps[0][0]);
+    b->calls++;
+    double x[GSS_MAXCH];
+    memcpy(x, b->maps[0][round], sizeof x);
+    for (int r = 0; r < b->rank; r++)
+        for (int i = 0; i < GSS_MAXCH; i++) {
+            const double add = b->maps[r][round][GSS_MAXCH + i];
+            const double v = x[i] + add;
+            x[i] = b->maps[r][round][2 * GSS_MAXCH + i] != 0.0 ? add : v - floor(v);
+        }
+    memcpy(out, x, sizeof x);
+    return 0;
+}
 static int carr_out(void *u, const double *c)
 {
     Baton *b = (Baton *)u;
@@ -275,6 +300,35 @@ int main(int argc, char **argv)
         k0.next = k1.next;
         check(*proof ? "hand-off, two ranks, device proofs" : "hand-off, two ranks", rc, k0, 0,
               nblk);
+        unsetenv("GSS_RUN_PROOF");
+    }
+    for (const char *proof : {"", "gpu"}) {   /* three ranks, the chain speculated across them */
+        if (*proof)
+            setenv("GSS_RUN_PROOF", proof, 1);
+        const int64_t b1 = nblk / 3 + 7, b2 = 2 * nblk / 3 - 3;
+        Baton baton;
+        gss_run_opts_t o = {carr_in, carr_out, &baton, carr_predict};
+        Sink all{bb, 0};
+        int rc = 0;
+        const int64_t firsts[3] = {0, b1, b2}, counts[3] = {b1, b2 - b1, -1};
+        for (int r = 0; r < 3 && !rc; r++) {
+            gss_scn *s = open_scn();
+            baton.rank = r;
+            baton.first = r == 0 ? s : nullptr;
+            Sink k{bb, firsts[r]};
+            gss_run_opts_t oo = o;
+            if (r == 2)
+                oo.carr_out = nullptr;
+            rc = gss_run_ex(d, s, firsts[r], counts[r], batch, 4, sink, &k, &oo);
+            gss_scn_close(s);
+            all.blocks += k.blocks;
+            all.bad += k.bad;
+            all.next = k.next;
+        }
+        if (!rc && baton.calls != 6)
+            rc = 1;                                     /* two rounds per rank */
+        check(*proof ? "speculated hand-off, 3 ranks, device proofs" : "speculated hand-off, 3 ranks",
+              rc, all, 0, nblk);
         unsetenv("GSS_RUN_PROOF");
     }
     {   /* the sink stops the run: an error, no hang, no leak */

@@ -338,10 +338,18 @@ def test_streaming_run_rows_ahead_midrun_exact_path(dev, golden, monkeypatch, pr
     (2, True, "static_d65_b8_noiono", ["-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8", "-i"]),
     # three ranks: rank 1 both receives (block 216) and hands on (block 432)
     (3, True, "static_d65_b8_noiono", ["-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8", "-i"]),
+    # the same without the chain speculated across the ranks (GSS_HANDOFF_SPEC=0)
+    (3, "nospec", "static_d65_b8_noiono",
+     ["-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8", "-i"]),
+    # four ranks over 30 s -b 16 (a map composed of three)
+    (4, True, "static_d30_b16", ["-l", ",".join(map(str, LOC)), "-d", "30", "-b", "16"]),
 ])
 def test_cli_two_ranks_one_file(golden, world, handoff, gold, args):
     """The CLI as several ranks (RANK/WORLD_SIZE, all on GPU 0 here): each pwrite()s its block
-    range into the same file, which equals the single-process reference output."""
+    range into the same file, which equals the single-process reference output.  With a run id
+    the ranks hand the slot carriers on through files and, by default, speculate the chain across
+    the ranks first (two rounds of map files, gss_run_opts_t.carr_predict); every file is consumed
+    or removed by the end."""
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "gpssim.bin")
         procs = []
@@ -349,9 +357,12 @@ def test_cli_two_ranks_one_file(golden, world, handoff, gold, args):
             env = dict(os.environ, WORLD_SIZE=str(world), RANK=str(r), LOCAL_RANK="0")
             env.pop("TORCHELASTIC_RUN_ID", None)
             env.pop("GSS_RUN_ID", None)
+            env.pop("GSS_HANDOFF_SPEC", None)
             if handoff:
                 env["GSS_RUN_ID"] = "t%d" % os.getpid()
                 env["GSS_RUN_FORCE_EXACT"] = "9"     # + the hand-off path's lazy checkpoints
+            if handoff == "nospec":
+                env["GSS_HANDOFF_SPEC"] = "0"
             procs.append(subprocess.Popen(
                 [G.CLI_PATH, "-e", NAV] + args + ["-o", out], env=env,
                 stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
@@ -361,13 +372,14 @@ def test_cli_two_ranks_one_file(golden, world, handoff, gold, args):
         h = hashlib.sha256(open(out, "rb").read()).hexdigest()
         left = [f for f in os.listdir(td) if f != "gpssim.bin"]
     assert h == golden[gold]["sha256"]
-    assert left == [], left                      # the hand-off file was consumed
+    assert left == [], left                      # the hand-off and map files are gone
 
 
 def test_cli_handoff_ignores_a_stale_file(golden):
-    """torchrun's default run id is "none" for every launch: a hand-off file an interrupted
-    earlier run left at the same path (here: junk carriers, another scenario's fingerprint) is
-    not consumed; rank 1 waits for rank 0's own file and the output is the reference's."""
+    """torchrun's default run id is "none" for every launch: a hand-off file (and speculation map
+    files) an interrupted earlier run left at the same path (here: junk carriers, another
+    scenario's fingerprint) is not consumed; rank 1 waits for rank 0's own files and the output
+    is the reference's."""
     import struct
     args = ["-l", "-33.8688,151.2093,58", "-d", "65", "-b", "8", "-i"]
     with tempfile.TemporaryDirectory() as td:
@@ -377,6 +389,10 @@ def test_cli_handoff_ignores_a_stale_file(golden):
         with open(stale, "wb") as f:
             f.write(struct.pack("<IQ", 0x67737364, 0x0123456789ABCDEF) +
                     struct.pack("<16d", *([0.25] * 16)))
+        for rnd in (0, 1):                      # and rank 0's speculation maps, both rounds
+            with open(f"{out}.gss-map-none-{rnd}-0", "wb") as f:
+                f.write(struct.pack("<IQ", 0x6773736d, 0x0123456789ABCDEF) +
+                        struct.pack("<48d", *([0.5] * 48)))
         procs = []
         for r in range(2):
             env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK="0",
