@@ -1302,7 +1302,7 @@ GSS_HD double gss_spec_fix(double x, int64_t n, const gss_spec_in_t *in, const g
                            int *hit)
 {
     double d;
-    return gss_spec_fix_d(x, n, in, o, hit, &d, NULL);
+    return gss_spec_fix_d(x, n, in, o, hit, &d, 0);
 }
 
 /* gss_carr_to_wrap with the admissible translations [*dlo, *dhi] of the start (lattice 2^-52
