@@ -48,7 +48,7 @@ def run_fake(tmp_path_factory):
     return exe
 
 
-@pytest.mark.parametrize("args", [("70", "64", "1"), ("40", "16", "8")])
+@pytest.mark.parametrize("args", [("35", "64", "1"), ("25", "16", "8")])
 def test_gss_run_on_fake_device(run_fake, args):
     r = subprocess.run([run_fake, NAV, *args], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]

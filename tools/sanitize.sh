@@ -10,7 +10,7 @@
 #  * the host plane alone (scenario, chains, proofs, worker pools, the CLI parser) in
 #    tests/helpers/run_harness.c's arrangement of the same threads.
 # Logs go to $OUT (default profiles/round5/sanitize).  FAKE_ARGS: the run_fake argument sets
-# (";"-separated "seconds batch fmt"), SECS: run_harness's long run.
+# (";"-separated "seconds batch fmt"), SECS: run_harness's long run, HARNESS_ARGS its second.
 set -o pipefail
 cd "$(dirname "$0")/.."
 OUT=${OUT:-profiles/round5/sanitize}
@@ -21,21 +21,34 @@ CF="-O1 -g -fno-omit-frame-pointer -ffp-contract=off -fno-fast-math -D_FILE_OFFS
 NAV=tests/golden/data/brdc3540.14n
 rc=0
 FK="tests/helpers/fake_hip/fake_hip.cpp tests/helpers/fake_dev.cpp tests/helpers/run_fake.cpp"
+# one object per source, built in parallel (each a background job, every status checked)
+build() {  # san dir
+    local san=$1 d=$2 pids=() f
+    for f in gps-sdr-sim_amd/csrc/host/*.c gps-sdr-sim_amd/csrc/cli/cli_args.c \
+             tests/helpers/run_harness.c; do
+        gcc $CF -fsanitize=$san -c $f -o $d/$(basename ${f%.c}).o & pids+=($!)
+    done
+    g++ -std=c++17 $CF -Itests/helpers -Itests/helpers/fake_hip -fsanitize=$san -x c++ \
+        -c gps-sdr-sim_amd/csrc/hip/gss_run.hip -o $d/gss_run.o & pids+=($!)
+    for f in $FK; do
+        g++ -std=c++17 $CF -Itests/helpers -Itests/helpers/fake_hip -fsanitize=$san -c $f \
+            -o $d/$(basename ${f%.cpp}).o & pids+=($!)
+    done
+    local bad=0
+    for p in "${pids[@]}"; do wait $p || bad=1; done
+    return $bad
+}
 for san in thread address,undefined; do
     tag=${san%%,*}
     # gss_run on the fake device: C host sources by gcc, the C++ ones by g++
     d=/tmp/gss_san/fake_$tag
+    rm -rf $d
     mkdir -p $d
-    for f in gps-sdr-sim_amd/csrc/host/*.c gps-sdr-sim_amd/csrc/cli/cli_args.c; do
-        gcc $CF -fsanitize=$san -c $f -o $d/$(basename ${f%.c}).o || exit 1
-    done
-    g++ -std=c++17 $CF -Itests/helpers -Itests/helpers/fake_hip -fsanitize=$san -x c++ \
-        -c gps-sdr-sim_amd/csrc/hip/gss_run.hip -o $d/gss_run.o || exit 1
-    for f in $FK; do
-        g++ -std=c++17 $CF -Itests/helpers -Itests/helpers/fake_hip -fsanitize=$san -c $f \
-            -o $d/$(basename ${f%.cpp}).o || exit 1
-    done
-    g++ -fsanitize=$san -o $d/run_fake $d/*.o -lm -lpthread || exit 1
+    build $san $d || exit 1
+    host_objs=$(ls $d/*.o | grep -v -e '/gss_run.o$' -e '/fake_hip.o$' -e '/fake_dev.o$' \
+                -e '/run_fake.o$' -e '/run_harness.o$')
+    g++ -fsanitize=$san -o $d/run_fake $host_objs $d/gss_run.o $d/fake_hip.o $d/fake_dev.o \
+        $d/run_fake.o -lm -lpthread || exit 1
     IFS=';' read -ra fargs <<< "${FAKE_ARGS:-70 64 1;40 16 8;300 512 1}"
     for args in "${fargs[@]}"; do
         log=$OUT/gss_run_${tag}_$(echo $args | tr ' ' _).log
@@ -51,8 +64,8 @@ for san in thread address,undefined; do
         [ $r -eq 0 ] || rc=1
     done
     exe=/tmp/gss_san/run_harness_$tag
-    gcc $CF -fsanitize=$san $SRC -o $exe -lm -lpthread || exit 1
-    for args in "$SECS 512 1" "60 64 16"; do
+    gcc -fsanitize=$san -o $exe $host_objs $d/run_harness.o -lm -lpthread || exit 1
+    for args in "$SECS 512 1" "${HARNESS_ARGS:-60 64 16}"; do
         log=$OUT/${tag}_$(echo $args | tr ' ' _).log
         echo "== gcc -fsanitize=$san, run_harness $args" > $log
         TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" \
