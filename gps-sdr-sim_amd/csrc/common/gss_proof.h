@@ -85,7 +85,9 @@ GSS_PF uint64_t first_in(uint64_t s, uint64_t m, uint64_t lo, uint64_t hi, uint6
         }
         if (d == GSS_PF_EUCLID_MAX)
             return GSS_PF_GIVE_UP;
-        const uint64_t lr = lo % s, hr = hi % s;         /* 1 <= lr <= hr < s (no multiple inside) */
+        /* no multiple of s in [lo, hi]: both lie in ((x - 1) s, x s), so their residues are
+           one product away (no further division; 1 <= lr <= hr < s) */
+        const uint64_t base = s * (x - 1), lr = lo - base, hr = hi - base;
         const double yd = (double)lim * (double)s / (double)m + 2.0;
         const uint64_t ylim = yd < 0x1p52 ? (uint64_t)yd : UINT64_MAX;
         fs[d] = s; fm[d] = m; flo[d] = lo; flim[d] = lim;
