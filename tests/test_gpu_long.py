@@ -84,8 +84,10 @@ class BlockDigests:
         self.pool.shutdown()
 
 
-@pytest.mark.parametrize("name", ["static20m", "day_b1"])
-def test_long_config_bit_exact(name):
+@pytest.mark.parametrize("name,batch", [("static20m", 256), ("day_b1", 256),
+                                        # the bench's e2e slots: rows ahead, GPU proofs (auto)
+                                        ("day_b1", 2048)])
+def test_long_config_bit_exact(name, batch):
     g = _fixture(name)
     s = G.Scenario(NAV, llh=LOC, duration=g["duration"], samp_freq=float(g["samp_freq"]),
                    data_format=g["fmt"])
@@ -93,7 +95,7 @@ def test_long_config_bit_exact(name):
     dig = BlockDigests(g["block_bytes"], g["chunk_blocks"])
     dev = G.Device(0)
     try:
-        dev.run(s, dig, batch=256, threads=THREADS)
+        dev.run(s, dig, batch=batch, threads=THREADS)
     finally:
         dev.close()
         dig.finish()
