@@ -160,10 +160,77 @@ GSS_PF i128 to_fix(double x, int k, int *inexact)
     return m < 0 ? -(i128)q : (i128)q;
 }
 
+/* The samples p in [1, n) with (a0 + p st) mod B < w (B a power of two, w < B / 2), ascending,
+   up to cap of them in hit[]; their number, or -1 if there are more or a descent gives up.
+   scan: each hit found by its own descent from the one before (first_below: O(log B) each).
+   Otherwise the descents find the first hit and the two gaps of the window's first returns:
+   by the three-gap theorem (Slater) a point x of [0, w) comes back to it after ga steps (moving
+   by da = ga st mod B) if x + da < w, after gb steps (moving back by db = B - gb st mod B) if
+   x >= db, and after ga + gb steps otherwise, ga and gb the first p >= 1 with p st mod B in
+   [0, w) resp. (B - w, B) -- no two returns come sooner, and the three ranges split [0, w)
+   since da + db >= w.  Every further hit is then O(1).  Gaps past the range are not needed:
+   a return through one lies past it too. */
+GSS_PF int hits_mod(uint64_t n, uint64_t B, uint64_t a0, uint64_t st, uint64_t w, int64_t *hit,
+                    int cap, int scan)
+{
+    const uint64_t M = B - 1;
+    int nh = 0;
+    int64_t p0 = 1;
+    while (p0 < (int64_t)n) {
+        const uint64_t a = (a0 + (uint64_t)p0 * st) & M;            /* mod 2^64, then mod B */
+        const uint64_t m = n - (uint64_t)p0;
+        const uint64_t i = first_below(m, B, a, st, w);
+        if (i == GSS_PF_GIVE_UP)
+            return -1;
+        if (i >= m)
+            break;
+        if (nh == cap)
+            return -1;
+        hit[nh++] = p0 + (int64_t)i;
+        p0 += (int64_t)i + 1;
+        if (scan || nh > 1)
+            continue;
+        /* the gaps, for returns that stay inside the range */
+        const int64_t p = hit[0];
+        const uint64_t lim = n - 1 - (uint64_t)p;
+        if (lim == 0)
+            break;
+        const uint64_t s1 = st & M;
+        const uint64_t ia = first_below(lim, B, s1, s1, w);          /* (1 + i) st mod B < w */
+        const uint64_t ib = s1 ? first_in(s1, B, B - w + 1, B - 1, lim) : UINT64_MAX;
+        if (ia == GSS_PF_GIVE_UP || ib == GSS_PF_GIVE_UP)
+            continue;                                 /* the scan from here on */
+        const int has_a = ia < lim, has_b = ib >= 1 && ib <= lim;
+        const uint64_t ga = ia + 1, gb = ib;
+        const uint64_t da = has_a ? (ga * s1) & M : 0, db = has_b ? B - ((gb * s1) & M) : 0;
+        uint64_t x = (a0 + (uint64_t)p * st) & M, q = (uint64_t)p;
+        for (;;) {
+            if (has_a && x + da < w) {
+                q += ga;
+                x += da;
+            } else if (has_b && x >= db) {
+                q += gb;
+                x -= db;
+            } else if (has_a && has_b) {
+                q += ga + gb;
+                x = x + da - db;
+            } else {
+                break;                                /* the next return lies past the range */
+            }
+            if (q >= n)
+                break;
+            if (nh == cap)
+                return -1;
+            hit[nh++] = (int64_t)q;
+        }
+        return nh;
+    }
+    return nh;
+}
+
 /* Step 2: the samples p in [1, n) where the line L0 + p S comes within delta of a cell boundary
    (a multiple of 2^lgB).  Writes up to cap of them in ascending order to hit[]; returns their
-   number, or -1 if there are more (or delta is not small against B).  Each hit is the next
-   sample whose residue falls below 2 delta (first_below: O(log B) per hit). */
+   number, or -1 if there are more (or delta is not small against B). */
 GSS_PF int ambiguous(i128 L0, i128 S, i128 delta, int lgB, int64_t n, int64_t *hit, int cap)
 {
     const uint64_t B = (uint64_t)1 << lgB;           /* lgB <= 55 */
@@ -176,22 +243,7 @@ GSS_PF int ambiguous(i128 L0, i128 S, i128 delta, int lgB, int64_t n, int64_t *h
     /* r(p) in [0, delta) or [B - delta, B)  <=>  (r(p) + delta) mod B < 2 delta */
     const uint64_t a0 = ((uint64_t)L0 + (uint64_t)delta) & (B - 1);
     const uint64_t w = 2 * (uint64_t)delta;
-    int nh = 0;
-    int64_t p0 = 1;
-    while (p0 < n) {
-        const uint64_t a = (a0 + (uint64_t)p0 * st) & (B - 1);    /* mod 2^64, then mod B */
-        const uint64_t m = (uint64_t)(n - p0);
-        const uint64_t i = first_below(m, B, a, st, w);
-        if (i == GSS_PF_GIVE_UP)
-            return -1;
-        if (i >= m)
-            break;
-        if (nh == cap)
-            return -1;
-        hit[nh++] = p0 + (int64_t)i;
-        p0 += (int64_t)i + 1;
-    }
-    return nh;
+    return hits_mod((uint64_t)n, B, a0, st, w, hit, cap, 0);
 }
 
 /* ---- one block ------------------------------------------------------------------------------ */

@@ -92,6 +92,18 @@ uint64_t gss_first_below(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint64_
     return first_below(n, m, a % m, s % m, w);
 }
 
+/* exported for tests: the proof's hit enumeration (hits_mod), by the three gaps or (scan) one
+   descent per hit */
+int gss_hits_mod(uint64_t n, uint64_t lgB, uint64_t a0, uint64_t st, uint64_t w, int64_t *hit,
+                 int cap, int scan)
+{
+    if (lgB < 1 || lgB > 55 || n == 0 || w == 0 || w >= ((uint64_t)1 << lgB) / 2 || !hit ||
+        cap < 0)
+        return -2;
+    const uint64_t B = (uint64_t)1 << lgB;
+    return hits_mod(n, B, a0 & (B - 1), st & (B - 1), w, hit, cap, scan);
+}
+
 /* (64-bit operands) */
 void gss_minmax_mod(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint64_t *mn, uint64_t *mx)
 {

@@ -137,6 +137,7 @@ _SIGS = {
     "gss_minmax_mod": (None, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
                               C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "gss_first_below": (C.c_uint64, [C.c_uint64] * 5),
+    "gss_hits_mod": (C.c_int, [C.c_uint64] * 5 + [_P, C.c_int, C.c_int]),
     "gss_dev_timing": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_float),
                                  C.POINTER(C.c_float)]),
     "gss_dev_timing_lin": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_float)]),
@@ -289,6 +290,15 @@ def minmax_mod(n, m, a, s):
     mn, mx = C.c_uint64(), C.c_uint64()
     lib().gss_minmax_mod(n, m, a, s, C.byref(mn), C.byref(mx))
     return mn.value, mx.value
+
+
+def hits_mod(n, lgB, a0, st, w, cap=64, scan=False):
+    """the proof's ambiguous samples (gss_hits_mod): list of p, or None if more than cap"""
+    out = np.zeros(max(cap, 1), np.int64)
+    k = lib().gss_hits_mod(n, lgB, a0, st, w, _ptr(out), cap, int(bool(scan)))
+    if k == -2:
+        raise ValueError("invalid hits_mod arguments")
+    return None if k < 0 else [int(v) for v in out[:k]]
 
 
 def first_below(n, m, a, s, w):

@@ -177,6 +177,11 @@ void gss_minmax_mod(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint64_t *mn
 /* tests: the least p in [0, n) with (a + p s) mod m < w (n if none; UINT64_MAX for m = 0 or
    m >= 2^62, w = 0 or w > m) -- the proof's enumeration of ambiguous samples */
 uint64_t gss_first_below(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint64_t w);
+/* the proof's ambiguous samples: p in [1, n) with (a0 + p st) mod 2^lgB < w, ascending, up to
+   cap in hit[]; their number, -1 if more, -2 on bad arguments (scan: one descent per hit, else
+   the three-gap stepping the proofs use; both give the same list; exported for tests)        */
+int gss_hits_mod(uint64_t n, uint64_t lgB, uint64_t a0, uint64_t st, uint64_t w, int64_t *hit,
+                 int cap, int scan);
 
 /* Same, from host buffers: uploads inputs, runs, downloads `out` (and carr_end if non-NULL),
    synchronises.  Convenience for the CLI and tests; the bench uses gss_synth_device().

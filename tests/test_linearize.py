@@ -189,6 +189,48 @@ def test_first_below_pow2_vs_numpy(lgm):
             assert len(got) == len(hits), (n, a, s, w)
 
 
+def test_hits_mod_three_gaps_vs_brute():
+    """The proof's hit enumeration (gss_proof.h hits_mod: first hit by a descent, the rest by the
+    three-gap stepping) equals a scan and the one-descent-per-hit loop, over small moduli where
+    every gap case, caps and empty ranges occur."""
+    rng = np.random.default_rng(77)
+    for _ in range(3000):
+        lgb = int(rng.choice([4, 6, 8, 10, 12]))
+        b = 1 << lgb
+        w = int(rng.integers(1, b // 2)) if rng.random() < 0.5 else int(rng.integers(1, b // 32 + 2))
+        w = min(w, b // 2 - 1)
+        n = int(rng.integers(1, 2000))
+        st = int(rng.integers(0, b)) if rng.random() > 0.05 else int(rng.choice([0, 1, b - 1, b // 2]))
+        a0 = int(rng.integers(0, b))
+        cap = int(rng.choice([1, 3, 8, 64, 400]))
+        v = (a0 + np.arange(1, n, dtype=np.int64) * st) % b
+        want = (np.flatnonzero(v < w) + 1).tolist()
+        want = want if len(want) <= cap else None
+        case = (n, lgb, a0, st, w, cap)
+        assert G.hits_mod(n, lgb, a0, st, w, cap=cap) == want, case
+        assert G.hits_mod(n, lgb, a0, st, w, cap=cap, scan=True) == want, case
+
+
+@pytest.mark.parametrize("lgb", [40, 55])
+def test_hits_mod_pow2_vs_numpy(lgb):
+    """hits_mod at the proof's moduli and window widths over runs of a whole block, vs numpy."""
+    rng = np.random.default_rng(200 + lgb)
+    b = 1 << lgb
+    for _ in range(40):
+        n = int(rng.integers(1, 600000))
+        w = int(rng.integers(1, b >> int(rng.integers(8, 24))))
+        st = int(rng.integers(0, b, dtype=np.uint64))
+        if rng.random() < 0.5:
+            q = int(rng.integers(1, 40))
+            st = (b * int(rng.integers(0, q)) // q + int(rng.integers(-1000, 1000))) % b
+        a0 = int(rng.integers(0, b, dtype=np.uint64))
+        p = np.arange(1, n, dtype=np.uint64)
+        v = (np.uint64(a0) + p * np.uint64(st)) & np.uint64(b - 1)
+        want = (np.flatnonzero(v < np.uint64(w)) + 1).tolist()
+        want = want if len(want) <= 2048 else None
+        assert G.hits_mod(n, lgb, a0, st, w, cap=2048) == want, (n, a0, st, w)
+
+
 # ---------------------------------------------------------------------------------------------
 def synth_params(rng, nblk, nch_list, n_per_blk, ties=False, tiny=False, fs=None):
     """random blocks of n_per_blk samples at sample rate fs (realistic Doppler and code rate);
