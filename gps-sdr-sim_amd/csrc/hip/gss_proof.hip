@@ -11,6 +11,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <mutex>
 #include "gpssim_amd.h"
@@ -53,11 +54,14 @@ __device__ static void lin_row_init(gss_lin_t *l)
         l->ppos[i] = INT32_MAX;
 }
 
-static constexpr int PF_BLOCKS = 16;          /* blocks per workgroup, one lane per channel slot */
-
-/* force_exact > 0 (gss_run's test hook GSS_RUN_FORCE_EXACT): blocks first + b with
-   (first + b) % force_exact == 0 are sent to the exact path as well */
-__global__ __launch_bounds__(PF_BLOCKS * GSS_MAXCH) void gss_proof_kernel(
+/* One block per workgroup; STRIDE threads per channel slot, of which the first proves it.  A
+   lane's proof is a long dependent chain (descents, exact walks: latency, not throughput), and a
+   wave lasts as long as the union of its lanes' paths, so a small launch spreads the channels
+   over waves (STRIDE 64: one channel per wave, 16 waves per block) and lets the SIMDs interleave
+   them; a large one fills the chip anyway and keeps the 16 channels of a block in one wave
+   (proof_stride; profiles/round5/proof/README.md). */
+template <int STRIDE>
+__global__ __launch_bounds__(GSS_MAXCH * STRIDE) void gss_proof_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch, int nblk,
     int n_per_blk, const uint32_t *__restrict__ ca, int n_ca, const uint32_t *__restrict__ nav,
     int n_nav, proof_lut lut, const gss_carr_anchor_t *__restrict__ anch,
@@ -65,19 +69,19 @@ __global__ __launch_bounds__(PF_BLOCKS * GSS_MAXCH) void gss_proof_kernel(
     gss_lin_t *__restrict__ lin, int32_t *__restrict__ fast, int64_t first, int force_exact)
 {
     __shared__ int32_t lcos[512], lsin[512];
-    __shared__ int fail_k[PF_BLOCKS * GSS_MAXCH];
-    __shared__ int gabs[PF_BLOCKS * GSS_MAXCH];
+    __shared__ int fail_k[GSS_MAXCH];
+    __shared__ int gabs[GSS_MAXCH];
     for (int i = threadIdx.x; i < 512; i += blockDim.x) {
         lcos[i] = lut.c[i];
         lsin[i] = lut.s[i];
     }
     __syncthreads();
-    const int t = threadIdx.x, bl = t / GSS_MAXCH, k = t % GSS_MAXCH;
-    const int b = blockIdx.x * PF_BLOCKS + bl;
+    const int k = threadIdx.x / STRIDE, b = blockIdx.x;
+    const bool lead = threadIdx.x % STRIDE == 0;
     int failed = 0, g = 0;
     gss_lin_t *l = lin + (size_t)b * GSS_MAXCH + k;
     int nc = 0;
-    if (b < nblk) {
+    if (lead && b < nblk) {
         lin_row_init(l);
         nc = nch[b];
         if (nc < 0 || nc > GSS_MAXCH) {
@@ -99,18 +103,20 @@ __global__ __launch_bounds__(PF_BLOCKS * GSS_MAXCH) void gss_proof_kernel(
             }
         }
     }
-    fail_k[t] = failed ? k : GSS_MAXCH;
-    gabs[t] = g;
+    if (lead) {
+        fail_k[k] = failed ? k : GSS_MAXCH;
+        gabs[k] = g;
+    }
     __syncthreads();
     /* the block's first failing channel and its gain sum (the host's loop order) */
     int kf = GSS_MAXCH, gsum = 0;
     for (int j = 0; j < GSS_MAXCH; j++) {
-        const int f = fail_k[bl * GSS_MAXCH + j];
+        const int f = fail_k[j];
         kf = f < kf ? f : kf;
     }
     for (int j = 0; j < GSS_MAXCH && j <= kf; j++)
-        gsum += gabs[bl * GSS_MAXCH + j];
-    if (b < nblk) {
+        gsum += gabs[j];
+    if (lead && b < nblk) {
         if (k > kf)
             lin_row_init(l);                            /* the host never reached this channel */
         if (k == 0) {
@@ -120,6 +126,22 @@ __global__ __launch_bounds__(PF_BLOCKS * GSS_MAXCH) void gss_proof_kernel(
             fast[b] = ok;
         }
     }
+}
+
+/* threads per channel slot for a launch of nblk blocks: the widest spread whose waves (nblk
+   STRIDE / 4) the chip still holds about at once (256 CUs x 4 SIMDs x 4-8 waves of this kernel);
+   GSS_PROOF_STRIDE = 1, 16, 32 or 64 forces one (measurements, tests) */
+static int proof_stride(int nblk)
+{
+    const char *e = getenv("GSS_PROOF_STRIDE");        /* (read per launch: tests switch it) */
+    const int forced = e ? atoi(e) : 0;
+    if (forced == 1 || forced == 16 || forced == 32 || forced == 64)
+        return forced;
+    const long waves_cap = 8192;
+    for (int s = 64; s >= 16; s /= 2)
+        if ((long)nblk * s / 4 <= waves_cap)
+            return s;
+    return 1;
 }
 
 /* gss_run's launch (force_exact: its test hook; sin / sspec: the batch's walks on the device,
@@ -132,10 +154,17 @@ int run_proof_launch(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, in
 {
     if (nblk <= 0)
         return 0;
-    hipLaunchKernelGGL(gss_proof_kernel, dim3((unsigned)((nblk + PF_BLOCKS - 1) / PF_BLOCKS)),
-                       dim3(PF_BLOCKS * GSS_MAXCH), 0, st, blk, nch, nblk, n_per_blk, ca_bits,
-                       n_ca, nav, n_nav, host_lut(), anch, sin, sspec, lin, fast, first,
-                       force_exact);
+#define PF_LAUNCH(S)                                                                             \
+    hipLaunchKernelGGL(gss_proof_kernel<S>, dim3((unsigned)nblk), dim3(GSS_MAXCH * (S)), 0, st,  \
+                       blk, nch, nblk, n_per_blk, ca_bits, n_ca, nav, n_nav, host_lut(), anch,  \
+                       sin, sspec, lin, fast, first, force_exact)
+    switch (proof_stride(nblk)) {
+    case 64: PF_LAUNCH(64); break;
+    case 32: PF_LAUNCH(32); break;
+    case 16: PF_LAUNCH(16); break;
+    default: PF_LAUNCH(1); break;
+    }
+#undef PF_LAUNCH
     return hipGetLastError() == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "proof kernel launch");
 }
 

@@ -126,3 +126,33 @@ def test_proof_device_rejects_like_host(dev):
         blk[5, k]["gain"] = 1000                      # sum |gain| > 8000
     fast = check_same(dev, blk, nch, nav, n)
     assert not fast[[0, 1, 2, 3, 5]].any()
+
+
+@pytest.mark.parametrize("stride", ["1", "16", "32", "64"])
+def test_proof_device_every_lane_stride(dev, stride, monkeypatch):
+    """every launch shape of the proof kernel (threads per channel slot, proof_stride; forced
+    here by GSS_PROOF_STRIDE, read per launch) gives the host's rows: rejections, ragged channel
+    counts, boundary rows and 20 MS/s blocks with anchors"""
+    monkeypatch.setenv("GSS_PROOF_STRIDE", stride)
+    rng = np.random.default_rng(3)
+    n = 260000
+    blk, nch, nav = synth_params(rng, 6, [12, 12, 5, 12, 3, 9], n)
+    blk[0, 3]["code_step"] = 0.9
+    blk[1, 0]["gain"] = 1500
+    blk[2, 4]["nav_tbl"] = 10 ** 6
+    blk[3, 11]["ca_tbl"] = -1
+    for k in range(9):
+        blk[5, k]["gain"] = 1000
+    fast = check_same(dev, blk, nch, nav, n)
+    assert not fast[[0, 1, 2, 3, 5]].any()
+    blk, nch, nav, n = boundary_params(24, 260000)
+    check_same(dev, blk, nch, nav, n)
+    s = G.Scenario(NAV, llh=LOC, duration=6.0, samp_freq=2.0e7)
+    n = s.n_per_blk
+    c0 = s.carrier()
+    blk, nch, chain = s.next_deferred(60, threads=8)
+    gi = G.carr_chain_guess(c0, blk, nch, chain, n, starts_only=True)
+    spec = G.spec_host(gi, n, threads=8)
+    _, _, anch = G.carr_chain_anchored(c0, blk, nch, chain, n, gi, spec)
+    fast = check_same(dev, blk, nch, s.nav_table(), n, anch)
+    assert fast.sum() >= len(nch) * 0.95
