@@ -242,6 +242,34 @@ static void stream_put(hipStream_t s)
 }
 
 /* free the pooled buffers of device `dev` (gss_dev_close; -1: every device) */
+/* The streams a run takes (compute, copy and nav at normal priority; the walks' and one proof
+   stream per slot at the highest), made into the pool when the device opens (gss_dev_open):
+   creating a high-priority stream costs ~4 ms in a fresh process, and GPU-proof runs take five
+   more than host-proof runs (23 ms of a 0.7 s configs[3] run, profiles/round5/e2e/README.md) */
+extern "C" void gss_run_pool_prewarm(int dev)
+{
+    int have[2] = {0, 0};
+    {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        for (const PoolStream &p : spool)
+            if (p.dev == dev)
+                have[p.hi ? 1 : 0]++;
+    }
+    int lo_pri = 0, hi_pri = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri) != hipSuccess)
+        return;
+    const int want[2] = {2 + NCOPY, 1 + NSLOT};
+    for (int hi = 0; hi < 2; hi++)
+        for (; have[hi] < want[hi]; have[hi]++) {
+            hipStream_t s = nullptr;
+            if ((hi ? hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi_pri)
+                    : hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess)
+                return;
+            std::lock_guard<std::mutex> lk(pool_mu);
+            spool.push_back({s, dev, hi});
+        }
+}
+
 extern "C" void gss_run_pool_drain(int dev)
 {
     std::vector<PoolBuf> out;
@@ -290,6 +318,8 @@ struct Slot {
     int sb_idx = -1;                 /* records mode: the walk batch it came from (its device
                                         walks are the GPU proofs' anchors)                  */
     int n_fb = 0;
+    int verdicts = 0;                /* GPU proofs: the exact-path blocks went with the render
+                                        (submit_proven), no redo in drain                     */
     int nb = 0, nch_max = 1;
     int64_t first = 0;               /* run index of the slot's first block */
     const uint32_t *lin_nav = nullptr;   /* the nav table its proofs read (prover thread)  */
@@ -322,6 +352,7 @@ struct Run {
                                         planner on each slot's own stream (proof_ahead)        */
     hipStream_t nav_st = nullptr;    /* ... the planner's stream for the slots' nav rows      */
     hipEvent_t t_base = nullptr;     /* GSS_RUN_TRACE: the GPU clock's origin (compute stream) */
+    hipEvent_t ca_ready = nullptr;   /* GPU proofs: the device C/A table is built (compute stream) */
     int upload_dev = 1;              /* uploads by kernel (h2d); GSS_RUN_UPLOAD=dma: copy engine */
     const uint32_t *d_ca = nullptr;  /* the run's device C/A table                            */
     int force_exact;                 /* GSS_RUN_FORCE_EXACT=k: every k-th block to the exact
@@ -1347,6 +1378,10 @@ int proof_ahead(Run &r, Slot &sl)
         RUN_TRY(hipEventRecord(sb->consumed, sl.pst));
         sb->consumed_pending = 1;
     }
+    /* the verdicts to the host at once: when the proof is done by the slot's submission, its
+       rejected blocks take the exact path in the same render (submit_proven) */
+    RUN_TRY(hipMemcpyAsync(sl.fast, v.fast, sizeof(int32_t) * (size_t)sl.nb,
+                           hipMemcpyDeviceToHost, sl.pst));
     RUN_TRY(hipEventRecord(sl.proved, sl.pst));
     return 0;
 }
@@ -1359,8 +1394,36 @@ int submit_proven(gss_dev *d, Run &r, Slot &sl, int n_per_blk, int fmt, size_t b
     const SlotDev v = slot_dev(sl);
     const int n_rows = sl.nav_first + sl.n_nav;
     RUN_TRY(hipStreamWaitEvent(st, sl.proved, 0));
+    /* the proof done (it ran ahead): its verdicts are on the host, and the blocks it rejected
+       (rare) render on the exact path beside the certified ones, as with host proofs; else the
+       verdicts come back with the bytes and drain redoes the rejected blocks */
+    int nf = 0;
+    sl.verdicts = 0;
+    const hipError_t q = hipEventQuery(sl.proved);
+    if (q == hipSuccess) {
+        for (int b = 0; b < sl.nb; b++)
+            if (!sl.fast[b])
+                sl.fast[sl.nb + nf++] = b;
+        sl.n_fb = nf;
+        if (nf > 0) {
+            if (lazy_ck(r))
+                for (int i = 0; i < nf; i++) {
+                    const int b = sl.fast[sl.nb + i];
+                    for (int k = 0; k < sl.nch[b]; k++) {
+                        const size_t e = (size_t)b * GSS_MAXCH + k;
+                        (void)gss_carr_advance_ck(sl.blk[e].carr0, sl.blk[e].carr_step,
+                                                  r.n_per_blk, sl.ck + e * GSS_NCK);
+                    }
+                }
+            RUN_H2D(v.ck, sl.ck, sizeof(double) * GSS_MAXCH * GSS_NCK * (size_t)sl.nb, st);
+            RUN_H2D(v.fast + sl.nb, sl.fast + sl.nb, sizeof(int32_t) * (size_t)nf, st);
+        }
+        sl.verdicts = 1;
+    } else if (q != hipErrorNotReady) {
+        return gss_fail(GSS_E_HIP, "proof event query: %s", hipGetErrorString(q));
+    }
     RUN_TRY(hipMemsetAsync(sl.d_status, 0, sizeof(int32_t), st));
-    int rc = gss_synth_lin_device(d, v.blk, v.nch, sl.nch_max, v.lin, v.fast, v.fast + sl.nb, 0,
+    int rc = gss_synth_lin_device(d, v.blk, v.nch, sl.nch_max, v.lin, v.fast, v.fast + sl.nb, nf,
                                   v.ck, r.d_ca, 32, r.d_nav, n_rows > 0 ? n_rows : 1, sl.nb,
                                   n_per_blk, fmt, sl.d_out, sl.d_status, st);
     if (rc)
@@ -1510,7 +1573,7 @@ int drain(gss_dev *d, Run &r, Slot &sl, const uint32_t *d_ca, int n_per_blk, int
     const double t0 = trace_on() ? tnow() : 0.0;
     RUN_TRY(hipEventSynchronize(sl.done));
     const double t1 = trace_on() ? tnow() : 0.0;
-    if (sl.lin && sl.gpu_proven && !*sl.h_status) {
+    if (sl.lin && sl.gpu_proven && !sl.verdicts && !*sl.h_status) {
         int rc = redo_rejected(d, r, sl, d_ca, sl.nav_first + sl.n_nav, n_per_blk, fmt, bb, st);
         if (rc)
             return rc;
@@ -1704,6 +1767,7 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         for (hipStream_t c : cp)
             stream_put(c);
         if (r.t_base) (void)hipEventDestroy(r.t_base);
+        if (r.ca_ready) (void)hipEventDestroy(r.ca_ready);
     };
     /* buffers */
     {
@@ -1857,11 +1921,21 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                     hipEventCreateWithFlags(&sl.proved, hipEventDisableTiming) != hipSuccess)
                     err = gss_fail(GSS_E_HIP, "run proof streams");
             }
+            const double t_pst = trace_on() ? tnow() : 0.0;
             if (!err)
                 err = nav_reserve(r, nav_rows_bound(s, info), st);
-            /* the C/A table (built on st above) before any proof stream reads it */
-            if (!err && hipStreamSynchronize(st) != hipSuccess)
+            /* the C/A table (built on st above) before any proof stream reads it: an event the
+               proof streams wait for (a host wait here held the start-up for the table's first
+               kernel, ~20 ms in a fresh process) */
+            if (!err && (hipEventCreateWithFlags(&r.ca_ready, hipEventDisableTiming) != hipSuccess ||
+                         hipEventRecord(r.ca_ready, st) != hipSuccess))
                 err = gss_fail(GSS_E_HIP, "run set-up");
+            for (Slot &sl : r.slot)
+                if (!err && hipStreamWaitEvent(sl.pst, r.ca_ready, 0) != hipSuccess)
+                    err = gss_fail(GSS_E_HIP, "run set-up");
+            if (trace_on())
+                fprintf(stderr, "trace setup_proofs streams %.6f nav_ca %.6f\n", t_pst - t_reserve,
+                        tnow() - t_pst);
         }
     }
     if (err) {

@@ -1335,6 +1335,8 @@ extern "C" const char *gss_build_info(void)
 }
 
 
+extern "C" void gss_run_pool_prewarm(int dev);    /* gss_run.hip */
+
 extern "C" int gss_dev_open(gss_dev **out, int ordinal)
 {
     *out = nullptr;
@@ -1367,6 +1369,7 @@ extern "C" int gss_dev_open(gss_dev **out, int ordinal)
     HIP_TRY(hipStreamCreateWithPriority(&d->aux, hipStreamNonBlocking, prio_hi));
     HIP_TRY(hipEventCreateWithFlags(&d->ev_in, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&d->ev_fb, hipEventDisableTiming));
+    gss_run_pool_prewarm(ordinal);                   /* gss_run's streams, made once here */
     *out = d;
     return 0;
 }

@@ -180,6 +180,11 @@ hipError_t hipEventSynchronize(hipEvent_t e)
     e->cv.wait(lk, [&] { return e->done >= g; });
     return hipSuccess;
 }
+hipError_t hipEventQuery(hipEvent_t e)
+{
+    std::lock_guard<std::mutex> lk(e->mu);
+    return e->done >= e->recorded ? hipSuccess : hipErrorNotReady;
+}
 hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned flags)
 {
     (void)flags;
