@@ -1874,9 +1874,11 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                proves on the GPU only the planner-bound runs (rows ahead: slots of >= 1024
                blocks, the -b 1 runs) with the walks' records (no walks on the host): there the
                host's CPUs are the limit and the proofs take them off it (configs[4] e2e 0.85-0.86
-               against 0.80-0.82 of the D2H ceiling, profiles/round5/e2e/b_*_r5q).  Elsewhere one
-               lane per channel-block leaves the proof kernel latency-bound (6.8 ms per 20 MS/s
-               slot, more than its download) and host proofs win */
+               against 0.80-0.82 of the D2H ceiling, profiles/round5/e2e/b_*_r5q).  Elsewhere the
+               two are even since the proof kernel spreads a small slot's channels over waves
+               (configs[3]: 0.695-0.702 s against 0.695-0.705, the headline and configs[2] within
+               noise; profiles/round5/e2e/r6e, e2e_modes_r6i.log), and host proofs keep the
+               GPU's queues to the render and the copies */
             const char *e = getenv("GSS_RUN_PROOF");
             const int gpu_auto = r.rows_ahead && r.rec ? 1 : 0;
             r.proof_mode = !r.use_lin ? 0 : !e || !*e || strcmp(e, "auto") == 0 ? gpu_auto :
