@@ -56,6 +56,14 @@ def timed_avg_ns(durs, steps, warmup=0):
     return sum(w) / len(w) if w else 0.0
 
 
+# GRBM_GUI_ACTIVE counts the whole GPU's busy cycles over the counter window, which for a short
+# dispatch is mostly the profiler's own window around it and for overlapping kernels includes the
+# others' work: the effective clock is reported only for dispatches of >= 200 us and at most the
+# chip's peak shader clock (2.4 GHz), else left out
+CLK_MIN_NS = 200_000
+CLK_MAX_GHZ = 2.4
+
+
 def counters(d):
     """per kernel: each counter averaged over its dispatches, and "_clk": the clock the dispatches
     with GRBM_GUI_ACTIVE ran at, their per-XCD cycles summed over their own durations (the
@@ -69,7 +77,7 @@ def counters(d):
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
             if r["Counter_Name"] == "GRBM_GUI_ACTIVE" and r.get("End_Timestamp"):
                 ns = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-                if ns > 0:
+                if ns >= CLK_MIN_NS:
                     clk[k][0] += float(r["Counter_Value"]) / 8
                     clk[k][1] += ns
             meta[k] = {"vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"]),
@@ -79,7 +87,7 @@ def counters(d):
     for k, cs in acc.items():
         res[k] = {c: sum(v) / len(v) for c, v in cs.items()}
         res[k]["_meta"] = meta[k]
-        if clk[k][1] > 0:
+        if clk[k][1] > 0 and clk[k][0] / clk[k][1] <= CLK_MAX_GHZ:
             res[k]["_clk"] = clk[k][0] / clk[k][1]
     return res
 
