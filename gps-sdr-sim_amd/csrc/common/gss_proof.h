@@ -169,11 +169,20 @@ GSS_PF i128 to_fix(double x, int k, int *inexact)
    x >= db, and after ga + gb steps otherwise, ga and gb the first p >= 1 with p st mod B in
    [0, w) resp. (B - w, B) -- no two returns come sooner, and the three ranges split [0, w)
    since da + db >= w.  Every further hit is then O(1).  Gaps past the range are not needed:
-   a return through one lies past it too. */
+   a return through one lies past it too.  The switch from the scan to the gaps comes after
+   gap_at hits (below). */
+#ifndef GSS_PF_GAPS
+#define GSS_PF_GAPS 0            /* (measurement builds: 1 gaps from the first hit, 2 never)       */
+#endif
 GSS_PF int hits_mod(uint64_t n, uint64_t B, uint64_t a0, uint64_t st, uint64_t w, int64_t *hit,
                     int cap, int scan)
 {
     const uint64_t M = B - 1;
+    /* the two gap descents pay once a few hits follow: from the first hit where the window
+       expects two or more in the range (n w / B), after the third where it expects fewer (most
+       such ranges have none or one, which the scan finds in one or two descents) */
+    const int gap_at = GSS_PF_GAPS == 1 ? 1 : GSS_PF_GAPS == 2 ? -1 :
+                       (double)n * (double)w >= 2.0 * (double)B ? 1 : 3;
     int nh = 0;
     int64_t p0 = 1;
     while (p0 < (int64_t)n) {
@@ -188,10 +197,10 @@ GSS_PF int hits_mod(uint64_t n, uint64_t B, uint64_t a0, uint64_t st, uint64_t w
             return -1;
         hit[nh++] = p0 + (int64_t)i;
         p0 += (int64_t)i + 1;
-        if (scan || nh > 1)
+        if (scan || nh != gap_at)
             continue;
         /* the gaps, for returns that stay inside the range */
-        const int64_t p = hit[0];
+        const int64_t p = hit[nh - 1];
         const uint64_t lim = n - 1 - (uint64_t)p;
         if (lim == 0)
             break;
