@@ -65,8 +65,9 @@ GSS_PF uint64_t first_in(uint64_t s, uint64_t m, uint64_t lo, uint64_t hi, uint6
 {
     /* the descent, level by level (iterative: the GPU proof has no call stack to spare); each
        level that needs the next one's answer keeps (s, m, lo, lim) for the way back up */
-    uint64_t fs[GSS_PF_EUCLID_MAX], fm[GSS_PF_EUCLID_MAX], flo[GSS_PF_EUCLID_MAX],
-        flim[GSS_PF_EUCLID_MAX];
+    /* (a level's modulus is the level above's step: m_{d+1} = s_d, so only m_0 is kept) */
+    uint64_t fs[GSS_PF_EUCLID_MAX], flo[GSS_PF_EUCLID_MAX], flim[GSS_PF_EUCLID_MAX];
+    const uint64_t m0 = m;
     int d = 0;
     uint64_t r;
     for (;;) {
@@ -90,7 +91,7 @@ GSS_PF uint64_t first_in(uint64_t s, uint64_t m, uint64_t lo, uint64_t hi, uint6
         const uint64_t base = s * (x - 1), lr = lo - base, hr = hi - base;
         const double yd = (double)lim * (double)s / (double)m + 2.0;
         const uint64_t ylim = yd < 0x1p52 ? (uint64_t)yd : UINT64_MAX;
-        fs[d] = s; fm[d] = m; flo[d] = lo; flim[d] = lim;
+        fs[d] = s; flo[d] = lo; flim[d] = lim;
         d++;
         const uint64_t ns = m % s;
         m = s;
@@ -103,7 +104,8 @@ GSS_PF uint64_t first_in(uint64_t s, uint64_t m, uint64_t lo, uint64_t hi, uint6
         d--;
         if (r == UINT64_MAX)
             return UINT64_MAX;
-        const u128 num = (u128)flo[d] + (u128)fm[d] * r + fs[d] - 1;
+        const uint64_t md = d ? fs[d - 1] : m0;
+        const u128 num = (u128)flo[d] + (u128)md * r + fs[d] - 1;
         /* v <= lim  <=>  num < (lim + 1) s; only then divide (the quotient fits) */
         r = num < ((u128)flim[d] + 1) * fs[d] ? gss_pf_udiv(num, fs[d]) : UINT64_MAX;
     }
