@@ -156,7 +156,8 @@ int gss_linearize(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, int n
    proof is csrc/common/gss_proof.h on both sides).  Device pointers; asynchronous on `stream`.
    gss_run proves with this call the slots of its planner-bound runs (rows ahead, slots of >= 1024
    blocks: the -b 1 runs) and on the host threads the others; GSS_RUN_PROOF=gpu / host / split
-   (every other slot on the GPU) forces a mode.                                                 */
+   (every other slot on the GPU) forces a mode.  One workgroup per block; a small launch spreads
+   the channels over waves (GSS_PROOF_STRIDE=1 / 16 / 32 / 64 forces the shape, for tests).    */
 int gss_linearize_device(gss_dev *d, const gss_chan_blk_t *blk, const int32_t *nch, int nblk,
                          int n_per_blk, const uint32_t *ca_bits, int n_ca, const uint32_t *nav,
                          int n_nav, gss_lin_t *lin, int32_t *fast, void *stream);
