@@ -98,6 +98,15 @@ def planner_of(first, n_blocks, world):
     return r
 
 
+def _run_p2p(dist, ops):
+    """post a list of dist.P2POp as one group (dist.batch_isend_irecv) and wait for all of them;
+    a rank with nothing to exchange posts nothing (allowed: the group already has collectives
+    behind it, the planners' baton and all_gathers)"""
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+
+
 def exchange_rows(plan, n_blocks, rank, world, dist, blk, nch, nav, device="cpu"):
     """Hand each chunk's rows from the rank that planned it (its window: blk[n, 16], nch[n], its
     nav table) to the rank that renders it (plan from chunk_plan(layout="stripe")).  Returns this
@@ -125,30 +134,36 @@ def exchange_rows(plan, n_blocks, rank, world, dist, blk, nch, nav, device="cpu"
                          .view(np.uint8).reshape(-1))
         return np.concatenate(parts)
 
-    # phase 1: nav-table sizes to every renderer this rank plans for (and from every planner)
+    # With the stripe layout most pairs of ranks exchange in BOTH directions.  Each phase is one
+    # dist.batch_isend_irecv: under NCCL/RCCL the group's sends and receives are posted together
+    # (one ncclGroupStart/End), so two ranks' large sends to each other cannot each wait on a
+    # receive queued behind the other (the ungrouped two-way send/recv deadlock); gloo posts them
+    # one by one, which is already safe.
     sends = [q for q in range(world) if q != rank and (rank, q) in pairs]
     recvs = [p for p in range(world) if p != rank and (p, rank) in pairs]
-    ops, sizes = [], {}
+    # phase 1: nav-table sizes to every renderer this rank plans for (and from every planner)
+    sizes, keep = {}, []
+    ops = []
     for q in sends:
-        ops.append(dist.isend(torch.tensor([len(nav)], dtype=torch.int64, device=device), dst=q))
+        t = torch.tensor([len(nav)], dtype=torch.int64, device=device)
+        keep.append(t)
+        ops.append(dist.P2POp(dist.isend, t, q))
     for p in recvs:
         sizes[p] = torch.empty(1, dtype=torch.int64, device=device)
-        ops.append(dist.irecv(sizes[p], src=p))
-    for w in ops:
-        w.wait()
+        ops.append(dist.P2POp(dist.irecv, sizes[p], p))
+    _run_p2p(dist, ops)
     # phase 2: the tables and rows
-    ops, bufs, keep = [], {}, []
+    ops, bufs = [], {}
     for q in sends:
         t = torch.from_numpy(payload(q)).to(device)
         keep.append(t)
-        ops.append(dist.isend(t, dst=q))
+        ops.append(dist.P2POp(dist.isend, t, q))
     for p in recvs:
         n_nav = int(sizes[p].item())
         nbytes = n_nav * NAV_WORDS * 4 + sum(nb for c, nb in pairs[(p, rank)]) * (row_b + 4)
         bufs[p] = torch.empty(nbytes, dtype=torch.uint8, device=device)
-        ops.append(dist.irecv(bufs[p], src=p))
-    for w in ops:
-        w.wait()
+        ops.append(dist.P2POp(dist.irecv, bufs[p], p))
+    _run_p2p(dist, ops)
     # assemble: the planners' nav tables in rank order, rows re-pointed into them
     tables, rows = {}, {}
     for p in range(world):
@@ -246,26 +261,89 @@ def ordered_gather(plan, rank, dist, get_chunk, make_buf, sink, depth=2, stats=N
 
 
 class FileSink:
-    """Writes device (or host) uint8 tensors to a file descriptor in call order, through a
-    pinned host staging buffer."""
+    """Writes device (or host) uint8 tensors to a file descriptor in call order, overlapped: the
+    reference writes each block as it is made (gpssim.c:2276-2287); here chunk i+1's download
+    runs while chunk i is written.
 
-    def __init__(self, torch, fd, cap):
-        self.torch, self.fd = torch, fd
-        self.host = torch.empty(cap, dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+    `nbuf` pinned staging buffers of `cap` bytes rotate between the caller and one writer thread.
+    A call takes a free buffer (waiting only while all of them are still being written), queues
+    the device-to-host copy on a copy stream of its own behind the caller's stream (the chunk's
+    render or receive), records an event and hands (buffer, length, event) to the writer, which
+    waits for that event and os.write()s the bytes in call order.  The caller's stream then waits
+    for the copy's event, so whatever the caller queues next into the same device memory (the
+    next receive into a reused buffer) runs after the copy has read it -- no host wait.  A host
+    tensor is copied into the staging buffer at once (the caller may reuse it on return).
+    close() drains the queue; a write error is raised there (or by the next call)."""
+
+    def __init__(self, torch, fd, cap, nbuf=3):
+        import queue
+        import threading
+        self.torch, self.fd, self.cap = torch, fd, cap
+        pin = torch.cuda.is_available()
+        self.host = [torch.empty(cap, dtype=torch.uint8, pin_memory=pin) for _ in range(nbuf)]
+        self.free = queue.Queue()
+        for i in range(nbuf):
+            self.free.put(i)
+        self.todo = queue.Queue()
+        self.streams = {}                         # device -> copy stream
         self.bytes = 0
+        self.err = None
+        self.writer = threading.Thread(target=self._write_loop, name="gss-file-sink", daemon=True)
+        self.writer.start()
+
+    def _write_loop(self):
+        while True:
+            item = self.todo.get()
+            if item is None:
+                return
+            i, n, ev = item
+            try:
+                if self.err is None:
+                    if ev is not None:
+                        ev.synchronize()
+                    mv = memoryview(self.host[i][:n].numpy())
+                    while len(mv):
+                        w = os.write(self.fd, mv)
+                        mv = mv[w:]
+            except BaseException as e:             # reported by the next call or close()
+                self.err = e
+            finally:
+                self.free.put(i)
+
+    def _check(self):
+        if self.err is not None:
+            raise self.err
 
     def __call__(self, t):
+        self._check()
         n = t.numel()
+        assert n <= self.cap, "chunk larger than the staging buffers"
+        i = self.free.get()
+        ev = None
         if t.is_cuda:
-            self.host[:n].copy_(t, non_blocking=True)
-            self.torch.cuda.current_stream(t.device).synchronize()
-            mv = memoryview(self.host[:n].numpy())
+            torch = self.torch
+            cur = torch.cuda.current_stream(t.device)
+            cs = self.streams.get(t.device)
+            if cs is None:
+                cs = self.streams[t.device] = torch.cuda.Stream(t.device)
+            cs.wait_stream(cur)                    # the chunk's producer first
+            with torch.cuda.stream(cs):
+                self.host[i][:n].copy_(t.reshape(-1), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(cs)
+            t.record_stream(cs)
+            cur.wait_event(ev)                     # the caller's next use of t after the copy
         else:
-            mv = memoryview(t.numpy())
-        while len(mv):
-            w = os.write(self.fd, mv)
-            mv = mv[w:]
+            self.host[i][:n].copy_(t.reshape(-1))
+        self.todo.put((i, n, ev))
         self.bytes += n
+
+    def close(self):
+        """wait until every queued chunk is written; raises the writer's error if any"""
+        if self.writer.is_alive():
+            self.todo.put(None)
+            self.writer.join()
+        self._check()
 
 
 def run_node(argv, rank, world, local, backend="nccl", chunk_blocks=None, threads=16,
@@ -314,7 +392,10 @@ def run_node(argv, rank, world, local, backend="nccl", chunk_blocks=None, thread
         fd = 1 if out_file == "-" else os.open(out_file, os.O_WRONLY | os.O_CREAT | os.O_TRUNC,
                                                0o644)
         sink = FileSink(torch, fd, chunk_blocks * bb)
-        ordered_gather(plan, rank, dist, get_chunk, make_buf, sink, stats=stats)
+        try:
+            ordered_gather(plan, rank, dist, get_chunk, make_buf, sink, stats=stats)
+        finally:
+            sink.close()
         total = sink.bytes
         if fd != 1:
             os.close(fd)

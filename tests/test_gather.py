@@ -8,7 +8,10 @@ shards to rank 0.
   min(world - 1, 2) or more peers at once (the per-peer receive windows), and with "stripe"
   from every peer;
 * CPU, gloo, world sizes 3 and 4: exchange_rows hands each chunk's rows from its planner to its
-  renderer byte for byte, with the nav rows re-pointed into the merged table;
+  renderer byte for byte, with the nav rows re-pointed into the merged table; and again with
+  every pair exchanging in both directions and each message past 8 MB (the grouped posting,
+  batch_isend_irecv, that keeps the same call safe under RCCL);
+* CPU: FileSink writes in call order from its writer thread while the caller reuses its buffers;
 * GPU (-m gpu), two ranks on the one GPU, backend GSS_TEST_BACKEND (default gloo: RCCL needs a
   GPU per rank, so a whole-node driver run sets nccl and exercises the same test unchanged):
   run_node renders the static -d 3 -b 16 run in both layouts and rank 0 writes the file; its
@@ -166,6 +169,121 @@ def test_exchange_rows_gloo(tmp_path, world, n_blocks, chunk):
                                   wnav[want["nav_tbl"].reshape(-1)])
             o += nb
         assert o == len(ob) == len(on)
+
+
+def _rows_big(b0, b1, planner):
+    """as _rows, vectorised, with a large nav table: a pair's message passes 8 MB"""
+    import numpy as np
+    from gpssim_amd import CHAN_DTYPE, MAXCH, NAV_WORDS
+    n_nav = 20000 + planner * 3
+    nav = (np.arange(n_nav * NAV_WORDS, dtype=np.uint32).reshape(n_nav, NAV_WORDS) *
+           np.uint32(2654435761) + np.uint32(1000 * (planner + 1)))
+    b = np.arange(b0, b1, dtype=np.int64)[:, None]
+    k = np.arange(MAXCH, dtype=np.int64)[None, :]
+    blk = np.zeros((b1 - b0, MAXCH), CHAN_DTYPE)
+    blk["carr0"] = b + k / 64
+    blk["code0"] = b * 1.5 - k
+    blk["gain"] = b * 16 + k
+    blk["ca_tbl"] = (b + k) % 32
+    blk["nav_tbl"] = (b * 7 + k) % n_nav
+    nch = ((np.arange(b0, b1) % 12) + 1).astype(np.int32)
+    return blk, nch, nav
+
+
+def _exchange_big_worker(rank, world, port, n_blocks, chunk, out_path):
+    sys.path.insert(0, os.path.join(REPO, "gps-sdr-sim_amd"))
+    import numpy as np
+    import torch.distributed as dist
+    from gpssim_amd.node import chunk_plan, exchange_rows, planner_of, rank_blocks
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b0, b1 = rank_blocks(n_blocks, rank, world)
+    blk, nch, nav = _rows_big(b0, b1, rank)
+    plan = chunk_plan(n_blocks, world, chunk, "stripe")
+    ob, on, onav, firsts = exchange_rows(plan, n_blocks, rank, world, dist, blk, nch, nav)
+    mine = [(c, nb) for q, c, nb in plan if q == rank]
+    ok = firsts == [c for c, _ in mine]
+    o = 0
+    for c, nb in mine:
+        p = planner_of(c, n_blocks, world)
+        pb0, pb1 = rank_blocks(n_blocks, p, world)
+        wb, wn, wnav = _rows_big(pb0, pb1, p)
+        got, want = ob[o:o + nb], wb[c - pb0:c - pb0 + nb]
+        for f in ("carr0", "code0", "gain", "ca_tbl"):
+            ok &= bool(np.array_equal(got[f], want[f]))
+        ok &= bool(np.array_equal(on[o:o + nb], wn[c - pb0:c - pb0 + nb]))
+        ok &= bool(np.array_equal(onav[got["nav_tbl"].reshape(-1)],
+                                  wnav[want["nav_tbl"].reshape(-1)]))
+        o += nb
+    ok &= o == len(ob)
+    open(f"{out_path}.{rank}", "w").write("ok" if ok else "bad")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [3, 4])
+def test_exchange_rows_large_two_way_gloo(tmp_path, world):
+    """every pair of ranks exchanges rows in both directions (stripe layout), each message past
+    8 MB: the grouped posting (batch_isend_irecv) must deliver every byte whatever the sizes"""
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(REPO, "gps-sdr-sim_amd"))
+    from gpssim_amd import CHAN_DTYPE, MAXCH, NAV_WORDS
+    from gpssim_amd.node import chunk_plan, planner_of
+    n_blocks, chunk = world * 30000, 1000
+    plan = chunk_plan(n_blocks, world, chunk, "stripe")
+    per_pair = {}
+    for r, c, nb in plan:
+        p = planner_of(c, n_blocks, world)
+        if p != r:
+            per_pair[(p, r)] = per_pair.get((p, r), 0) + nb * (CHAN_DTYPE.itemsize * MAXCH + 4)
+    pairs = {(p, r) for p, r in per_pair}
+    assert all((r, p) in pairs for p, r in pairs)              # two-way for every pair
+    assert min(per_pair.values()) + 20000 * NAV_WORDS * 4 > 8 << 20
+    out = tmp_path / "x"
+    mp.spawn(_exchange_big_worker, args=(world, _free_port(), n_blocks, chunk, str(out)),
+             nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"x.{r}").read_text() == "ok"
+
+
+def test_file_sink_overlapped(tmp_path):
+    """FileSink: chunks written in call order by its writer thread, the caller free to reuse a
+    chunk's memory on return, errors raised at close()"""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(REPO, "gps-sdr-sim_amd"))
+    from gpssim_amd.node import FileSink
+    rng = np.random.default_rng(5)
+    path = tmp_path / "o.bin"
+    fd = os.open(str(path), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    sink = FileSink(torch, fd, 1 << 16, nbuf=2)
+    want = []
+    buf = torch.empty(1 << 16, dtype=torch.uint8)
+    for i in range(200):
+        n = int(rng.integers(1, 1 << 16))
+        v = torch.from_numpy(rng.integers(0, 256, n, dtype=np.uint8))
+        buf[:n] = v
+        want.append(v.numpy().tobytes())
+        sink(buf[:n])
+        buf.fill_(i & 255)                      # reused at once, as ordered_gather's buffers
+    sink.close()
+    os.close(fd)
+    assert sink.bytes == sum(len(w) for w in want)
+    assert path.read_bytes() == b"".join(want)
+    # a failing write surfaces
+    r, w = os.pipe()
+    os.close(r)
+    sink = FileSink(torch, w, 64, nbuf=2)
+    import signal
+    old = signal.signal(signal.SIGPIPE, signal.SIG_IGN)
+    try:
+        sink(torch.zeros(8, dtype=torch.uint8))
+        with pytest.raises(OSError):
+            sink.close()
+    finally:
+        signal.signal(signal.SIGPIPE, old)
+        os.close(w)
 
 
 def test_planner_of():
