@@ -554,20 +554,39 @@ def gather_leg(G, torch, td, dev, dev_t, rank, world, coll_t, walker, threads, w
     def make_buf(nb):
         return torch.empty(nb * bb, dtype=torch.uint8, device="cpu" if host_wire else dev_t)
 
-    stats = {}
-    td.barrier()
-    torch.cuda.synchronize(dev_t)
-    t1 = time.perf_counter()
-    _, evs = render_chunks(torch, win, dev_t)
-    get_chunk = chunk_source(torch, win, firsts, evs, dev_t,
-                             host_wire=host_wire and rank != 0)
-    ordered_gather(plan, rank, td, get_chunk, make_buf, sink if rank == 0 else None,
-                   stats=stats)
-    torch.cuda.synchronize(dev_t)
-    el = time.perf_counter() - t1
-    t = torch.tensor([el, plan_s], dtype=torch.float64, device=coll_t)
+    def once(sink0):
+        """render + gather once into rank 0's sink0; wall seconds, max over ranks"""
+        stats = {}
+        td.barrier()
+        torch.cuda.synchronize(dev_t)
+        t1 = time.perf_counter()
+        _, evs = render_chunks(torch, win, dev_t)
+        get_chunk = chunk_source(torch, win, firsts, evs, dev_t,
+                                 host_wire=host_wire and rank != 0)
+        ordered_gather(plan, rank, td, get_chunk, make_buf, sink0 if rank == 0 else None,
+                       stats=stats)
+        if rank == 0 and hasattr(sink0, "close"):
+            sink0.close()                         # the last chunk written
+        torch.cuda.synchronize(dev_t)
+        el = time.perf_counter() - t1
+        t = torch.tensor([el], dtype=torch.float64, device=coll_t)
+        td.all_reduce(t, op=td.ReduceOp.MAX)
+        return t.item(), stats
+
+    el, stats = once(sink)
+    # the same gather into a real file sink: rank 0 downloads each chunk into a ring of pinned
+    # buffers and a writer thread os.write()s it to /dev/null (node.FileSink, as run_node)
+    fsink = None
+    if rank == 0:
+        from gpssim_amd.node import FileSink
+        fd_null = os.open(os.devnull, os.O_WRONLY)
+        fsink = FileSink(torch, fd_null, chunk * bb)
+    el_file, _ = once(fsink)
+    if rank == 0:
+        os.close(fd_null)
+    t = torch.tensor([plan_s], dtype=torch.float64, device=coll_t)
     td.all_reduce(t, op=td.ReduceOp.MAX)
-    el, plan_s = t.tolist()
+    plan_s = t.item()
     total = nb_all * bb
     win.free()
     return {"workload": f"static -s 20000000 -b 16, {window_s * world:g} s over {world} ranks "
@@ -581,7 +600,13 @@ def gather_leg(G, torch, td, dev, dev_t, rank, world, coll_t, walker, threads, w
             "MSps": round(nb_all * npb / el / 1e6, 1), "host_plan_s_max": round(plan_s, 3),
             "recv_outstanding_max": stats.get("max_outstanding") if rank == 0 else None,
             "peers_outstanding_max": stats.get("max_peers_outstanding") if rank == 0 else None,
-            "spec_rows_translated_rank": pt.get("spec_hits")}
+            "spec_rows_translated_rank": pt.get("spec_hits"),
+            "file_sink": {"workload": "the same render + gather into node.FileSink (pinned "
+                                      "ring, copy stream, writer thread) writing /dev/null",
+                          "wall_s": round(el_file, 3),
+                          "GBps_at_rank0": round(total / el_file / 1e9, 2),
+                          "bytes_written": fsink.bytes if rank == 0 else None,
+                          "vs_discarding": round(el / el_file, 3)}}
 
 
 def main():

@@ -193,26 +193,41 @@ static int handoff_in(void *user, double *carr)
 }
 
 #define MAP_MAGIC 0x6773736du              /* "gssm": magic, fingerprint, 48 doubles */
+#define NOSPEC_MAGIC 0x6773736eu           /* "gssn": the rank does not speculate      */
 
-/* publish this rank's map of `round`, then compose the maps of the ranks before it */
+static int write_map(const handoff_ctx *h, int round, uint32_t magic, const double *map)
+{
+    char path[640], tmp[660];
+    static const double zero[3 * GSS_MAXCH];
+    map_path(h, round, h->rank, path, sizeof path);
+    snprintf(tmp, sizeof tmp, "%s.tmp", path);
+    FILE *f = fopen(tmp, "wb");
+    if (!f)
+        return 1;
+    const uint64_t fp = map_fp(h, round, h->rank);
+    int ok = fwrite(&magic, sizeof magic, 1, f) == 1 && fwrite(&fp, sizeof fp, 1, f) == 1 &&
+             fwrite(map ? map : zero, sizeof(double), 3 * GSS_MAXCH, f) == 3 * GSS_MAXCH;
+    ok = (fclose(f) == 0) && ok;
+    return (ok && rename(tmp, path) == 0) ? 0 : 1;
+}
+
+/* publish this rank's map of `round`, then compose the maps of the ranks before it; round -1:
+   this rank does not speculate -- markers in place of both rounds' maps, so a rank after it
+   that does fails at once (gss_run_opts_t.carr_predict) */
 static int handoff_predict(void *user, int round, const double *map, double *start)
 {
     const handoff_ctx *h = (const handoff_ctx *)user;
-    char path[640], tmp[660];
-    map_path(h, round, h->rank, path, sizeof path);
-    if (h->rank + 1 < h->world) {                       /* the last rank's map has no reader */
-        snprintf(tmp, sizeof tmp, "%s.tmp", path);
-        FILE *f = fopen(tmp, "wb");
-        if (!f)
-            return 1;
-        const uint32_t magic = MAP_MAGIC;
-        const uint64_t fp = map_fp(h, round, h->rank);
-        int ok = fwrite(&magic, sizeof magic, 1, f) == 1 && fwrite(&fp, sizeof fp, 1, f) == 1 &&
-                 fwrite(map, sizeof(double), 3 * GSS_MAXCH, f) == 3 * GSS_MAXCH;
-        ok = (fclose(f) == 0) && ok;
-        if (!ok || rename(tmp, path) != 0)
-            return 1;
+    char path[640];
+    if (round < 0) {
+        if (h->rank + 1 < h->world)
+            for (int q = 0; q < 2; q++)
+                if (write_map(h, q, NOSPEC_MAGIC, NULL))
+                    return 1;
+        return 0;
     }
+    /* the last rank's map has no reader */
+    if (h->rank + 1 < h->world && write_map(h, round, MAP_MAGIC, map))
+        return 1;
     double x[GSS_MAXCH];
     memcpy(x, map, sizeof x);                           /* rank 0: its own start */
     for (int r = 0; r < h->rank; r++) {
@@ -229,6 +244,12 @@ static int handoff_predict(void *user, int round, const double *map, double *sta
                                fread(&fp, sizeof fp, 1, f) == 1 &&
                                fread(m, sizeof(double), 3 * GSS_MAXCH, f) == 3 * GSS_MAXCH;
                 fclose(f);
+                if (ok && magic == NOSPEC_MAGIC && fp == map_fp(h, round, r)) {
+                    fprintf(stderr, "ERROR: rank %d does not speculate the carrier chain but "
+                            "rank %d does: give every rank the same GSS_HANDOFF_SPEC, "
+                            "GSS_RUN_SPEC, GSS_RUN_REC and GSS_PATH.\n", r, h->rank);
+                    return 1;
+                }
                 if (ok && magic == MAP_MAGIC && fp == map_fp(h, round, r))
                     break;
             }
@@ -305,8 +326,8 @@ static int run_rank(const gss_cli_t *cli, gss_scn *scn, const gss_scn_info_t *in
     h.n_blocks = nb;
     /* GSS_HANDOFF_SPEC=0: the carriers first, then the chain (no speculation; every rank of a
        run must agree) */
-    gss_run_opts_t ro = {handoff_in, handoff_out, &h,
-                         env_int("GSS_HANDOFF_SPEC", 1) ? handoff_predict : NULL};
+    const int spec = env_int("GSS_HANDOFF_SPEC", 1);
+    gss_run_opts_t ro = {handoff_in, handoff_out, &h, spec ? handoff_predict : NULL};
     if (run_id && *run_id) {
         if (rank > 0)
             snprintf(h.in_path, sizeof h.in_path, "%s.gss-carr-%s-%lld", cli->out_file, run_id,
@@ -314,6 +335,12 @@ static int run_rank(const gss_cli_t *cli, gss_scn *scn, const gss_scn_info_t *in
         if (rank + 1 < world)
             snprintf(h.out_path, sizeof h.out_path, "%s.gss-carr-%s-%lld", cli->out_file,
                      run_id, (long long)last);
+        /* not speculating here: the markers tell a rank after this one that does (the library
+           writes them through the callback when its own settings rule speculation out) */
+        if (!spec && handoff_predict(&h, -1, NULL, NULL)) {
+            fprintf(stderr, "ERROR: rank %d: carrier hand-off files.\n", rank);
+            return 1;
+        }
     }
     if (gss_run_ex(dev, scn, first, last - first, env_int("GSS_BATCH", 128),
                    env_int("GSS_THREADS", default_threads()), pwrite_sink, &c,

@@ -169,6 +169,8 @@ __global__ __launch_bounds__(REC_ROWS) void gss_spec_rec_kernel(
         const bool ok = p >= 0 && p < i;
         gss_spec_record(&in[i], &spec[i], ok ? &in[p] : nullptr, ok ? &spec[p] : nullptr, n,
                         &s_rec[lane]);
+        if (s_rec[lane].ok & 2)
+            s_rec[lane].ok |= (i - p) << 2;         /* the row the link was built against */
     }
     __syncthreads();
     constexpr int W = sizeof(gss_spec_rec_t) * REC_ROWS / 16;

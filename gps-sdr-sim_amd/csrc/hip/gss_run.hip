@@ -357,6 +357,9 @@ struct Run {
     const uint32_t *d_ca = nullptr;  /* the run's device C/A table                            */
     int force_exact;                 /* GSS_RUN_FORCE_EXACT=k: every k-th block to the exact
                                         path (tests of the mixed batch), 0 = off */
+    int late_verdicts = 0;           /* GSS_RUN_LATE_VERDICTS=1 (tests): submit_proven treats every
+                                        GPU proof as still running, so rejected blocks always take
+                                        the redo path in drain (redo_rejected)            */
     int64_t first, last;             /* [first, last) block range of the run */
     int64_t start = 0;               /* the handle's next block when the run began (an earlier
                                         run, a seek): the planner's and rows thread's cursor   */
@@ -700,6 +703,11 @@ int plan_range_upfront(Run &r)
         return rc;
     /* the speculated chain: with a prediction callback and the walks on the GPU */
     const bool speculate = r.opts->carr_predict && r.spec && r.rec;
+    /* a prediction callback this rank will not use (GSS_RUN_SPEC=0, GSS_RUN_REC=0, the exact
+       path): round -1 tells the ranks after it not to wait for its maps */
+    if (r.opts->carr_predict && !speculate &&
+        r.opts->carr_predict(r.opts->carr_user, -1, nullptr, nullptr))
+        return gss_fail(GSS_E_IO, "carrier hand-off: publishing the no-speculation marker");
     double start0[GSS_MAXCH] = {0};
     if (speculate && r.first == 0 && (rc = gss_scn_carrier(r.scn, start0)) != 0)
         return rc;
@@ -1111,9 +1119,10 @@ int plan_into(Run &r, Slot &sl, int64_t *cursor)
             Run::SpecBatch &b = r.sb[r.sb_cur];
             if (!b.launched && ask > 0)
                 rc = spec_launch(r, b, ask);
-            if (!rc && b.launched)                     /* else the range is done: nb stays 0 */
+            if (!rc && b.launched) {                   /* else the range is done: nb stays 0 */
                 rc = spec_finish(r, b, sl.blk, sl.nch, &nb, sl.anch);
-                sl.sb_idx = r.sb_cur;
+                sl.sb_idx = r.sb_cur;                  /* the walks this slot's anchors are in */
+            }
             if (!rc && nb > 0) {                       /* the next batch's walks, on the GPU now */
                 const int ask2 = next_ask(r, *cursor + nb);
                 r.sb_cur ^= 1;
@@ -1399,7 +1408,7 @@ int submit_proven(gss_dev *d, Run &r, Slot &sl, int n_per_blk, int fmt, size_t b
        verdicts come back with the bytes and drain redoes the rejected blocks */
     int nf = 0;
     sl.verdicts = 0;
-    const hipError_t q = hipEventQuery(sl.proved);
+    const hipError_t q = r.late_verdicts ? hipErrorNotReady : hipEventQuery(sl.proved);
     if (q == hipSuccess) {
         for (int b = 0; b < sl.nb; b++)
             if (!sl.fast[b])
@@ -1703,6 +1712,8 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
         r.use_lin = !(path && strcmp(path, "walk") == 0);
         const char *fe = getenv("GSS_RUN_FORCE_EXACT");
         r.force_exact = fe && *fe ? atoi(fe) : 0;
+        const char *lv = getenv("GSS_RUN_LATE_VERDICTS");
+        r.late_verdicts = lv && *lv == '1';
         const char *up = getenv("GSS_RUN_UPLOAD");
         r.upload_dev = !(up && strcmp(up, "dma") == 0);
     }

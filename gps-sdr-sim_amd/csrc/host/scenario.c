@@ -903,6 +903,8 @@ static void rec_part(void *arg, int part)
         const int ok = p >= 0 && p < i;
         gss_spec_record(&j->in[i], &j->spec[i], ok ? &j->in[p] : NULL, ok ? &j->spec[p] : NULL,
                         j->n_per_blk, &j->rec[i]);
+        if (j->rec[i].ok & 2)
+            j->rec[i].ok |= (i - p) << 2;            /* the row the link was built against */
     }
 }
 
@@ -932,6 +934,7 @@ static void rec_slot_part(void *arg, int slot)
     const int64_t n = j->n_per_blk;
     double x = j->carr[slot], d = 0.0;
     int hits = 0, held = 0;
+    size_t e_prev = 0;                               /* the slot's previous row (held: valid) */
     for (int b = 0; b < j->nblk; b++)
         for (int k = 0; k < j->nch[b]; k++) {
             const size_t e = (size_t)b * GSS_MAXCH + k;
@@ -943,7 +946,12 @@ static void rec_slot_part(void *arg, int slot)
             }
             j->blk[e].carr0 = x;
             const gss_spec_rec_t *R = &j->rec[e];
-            if (held && (R->ok & 2) && d >= R->llo && d <= R->lhi) {
+            /* a link record holds only if it was built against this slot's previous row
+               (ok bits 2.., the row distance; rows from elsewhere, e.g. zero-filled pads, fail
+               the check and walk) */
+            const int linked = held && (R->ok & 2) && (size_t)(R->ok >> 2) == e - e_prev;
+            e_prev = e;
+            if (linked && d >= R->llo && d <= R->lhi) {
                 d += R->ldd;                         /* the link: no walk at all */
                 x = R->end + d;
                 hits++;

@@ -367,7 +367,9 @@ typedef struct gss_spec_rec {
     double llo, lhi, ldd;              /* link: the previous row of the slot translated by d in
                                           [llo, lhi] -> this one's last translation is d + ldd    */
     int32_t p1;                        /* samples to the guess's first wrap                        */
-    int32_t ok;                        /* bit 0: self record, bit 1: link record                   */
+    int32_t ok;                        /* bit 0: self record, bit 1: link record, bits 2..: the
+                                          link's row distance (this row - in[].pad), which the
+                                          chain checks against the slot's actual previous row  */
 } gss_spec_rec_t;                      /* 72 bytes */
 #endif
 int gss_spec_records(const gss_spec_in_t *in, const gss_spec_t *spec, int nrow, int n_per_blk,
@@ -512,7 +514,10 @@ typedef struct gss_run_opts {
        1 per slot.  It publishes the map to the ranks after this one and returns in start_out
        the composition of the maps of the ranks before it (gpssim_amd/shard.py compose_start).
        The walks then run before carr_in, and from carr_in to carr_out only the records' chain
-       is left.  Exact whatever the predictions.                               */
+       is left.  Exact whatever the predictions.  A rank that is given the
+       callback but does not speculate (GSS_RUN_SPEC=0 or GSS_RUN_REC=0 in its environment, or
+       no fast path) calls it once with round -1 and map == start_out == NULL, so that the
+       ranks after it can fail at once instead of waiting for maps that never come.          */
     int (*carr_predict)(void *user, int round, const double *map, double *start_out);
 } gss_run_opts_t;
 int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n_blocks, int batch,

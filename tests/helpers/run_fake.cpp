@@ -129,7 +129,7 @@ struct Mode {
 static const char *ENV_KEYS[] = {"GSS_RUN_SPEC", "GSS_RUN_ROWS_AHEAD", "GSS_RUN_PROVER",
                                  "GSS_RUN_PROOF", "GSS_RUN_FORCE_EXACT", "GSS_RUN_UPLOAD",
                                  "GSS_RUN_ROWS_POOL", "GSS_RUN_REC", "GSS_RUN_ANCHORS",
-                                 "GSS_RUN_DEV_ANCHORS"};
+                                 "GSS_RUN_DEV_ANCHORS", "GSS_RUN_LATE_VERDICTS"};
 
 static void set_env(const Mode &m)
 {
@@ -240,6 +240,8 @@ int main(int argc, char **argv)
         {"split proofs", {{"GSS_RUN_PROOF", "split"}, {"GSS_RUN_ROWS_AHEAD", "1"}}},
         {"every 7th block exact", {{"GSS_RUN_FORCE_EXACT", "7"}}},
         {"every 5th exact, device proofs", {{"GSS_RUN_FORCE_EXACT", "5"}, {"GSS_RUN_PROOF", "gpu"}}},
+        {"every 5th exact, device proofs, late verdicts (redo in drain)",
+         {{"GSS_RUN_FORCE_EXACT", "5"}, {"GSS_RUN_PROOF", "gpu"}, {"GSS_RUN_LATE_VERDICTS", "1"}}},
         {"every 3rd exact, rows ahead", {{"GSS_RUN_FORCE_EXACT", "3"}, {"GSS_RUN_ROWS_AHEAD", "1"}}},
         {"every 3rd exact, rows ahead, host proofs",
          {{"GSS_RUN_FORCE_EXACT", "3"}, {"GSS_RUN_ROWS_AHEAD", "1"}, {"GSS_RUN_PROOF", "host"}}},

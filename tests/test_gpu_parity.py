@@ -278,15 +278,19 @@ def test_streaming_run_bit_exact(dev, golden):
     assert [x for _, x in blocks] == g["block_sha16"][123:184]
 
 
-@pytest.mark.parametrize("proof", ["gpu", "host", "split"])
+@pytest.mark.parametrize("proof", ["gpu", "host", "split", "gpu_late"])
 @pytest.mark.parametrize("fmt,every", [(16, 5), (8, 7)])
 def test_streaming_run_mixed_exact(dev, golden, monkeypatch, fmt, every, proof):
     """gss_run with every k-th block sent to the exact path (GSS_RUN_FORCE_EXACT, a test hook):
     the planner walks the chain without checkpoints and computes them afterwards for those
-    blocks only (fill_fb_ck; with the proofs on the GPU, drain renders the slot again with
-    them: redo_rejected); whole run and a mid-run range against the golden hashes."""
+    blocks only (fill_fb_ck); with the proofs on the GPU a rejected block renders on the exact
+    path in the same launch when its slot's proof is done at submission, else drain renders
+    them again (redo_rejected).  The proofs usually finish first, so "gpu_late"
+    (GSS_RUN_LATE_VERDICTS=1) forces the redo path on every slot.  Whole run and a mid-run
+    range against the golden hashes."""
     monkeypatch.setenv("GSS_RUN_FORCE_EXACT", str(every))
-    monkeypatch.setenv("GSS_RUN_PROOF", proof)
+    monkeypatch.setenv("GSS_RUN_PROOF", "gpu" if proof == "gpu_late" else proof)
+    monkeypatch.setenv("GSS_RUN_LATE_VERDICTS", "1" if proof == "gpu_late" else "0")
     g = golden[f"static_d30_b{fmt}"]
     s = G.Scenario(NAV, llh=LOC, duration=30.0, data_format=fmt)
     bb = G.block_bytes(s.n_per_blk, fmt)
@@ -408,6 +412,37 @@ def test_cli_handoff_ignores_a_stale_file(golden):
         left = [f for f in os.listdir(td) if f != "gpssim.bin"]
     assert h == golden["static_d65_b8_noiono"]["sha256"]
     assert left == [], left
+
+
+def test_cli_handoff_speculation_mismatch_fails_fast():
+    """Ranks that disagree on speculating the carrier chain: rank 0 runs with GSS_RUN_SPEC=0
+    (so the library rules speculation out and publishes no maps), rank 1 with the default.  Rank
+    0 writes no-speculation markers in place of its maps (carr_predict round -1) and rank 1 stops
+    at once with a message naming the settings, instead of polling for maps until the hand-off
+    timeout."""
+    import time
+    args = ["-l", "-33.8688,151.2093,58", "-d", "20", "-b", "8", "-i"]
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "gpssim.bin")
+        procs = []
+        t0 = time.perf_counter()
+        for r in range(2):
+            env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK="0",
+                       GSS_RUN_ID="m%d" % os.getpid(), GSS_HANDOFF_TIMEOUT="600")
+            env.pop("TORCHELASTIC_RUN_ID", None)
+            env.pop("GSS_HANDOFF_SPEC", None)
+            env.pop("GSS_RUN_SPEC", None)
+            if r == 0:
+                env["GSS_RUN_SPEC"] = "0"
+            procs.append(subprocess.Popen(
+                [G.CLI_PATH, "-e", NAV] + args + ["-o", out], env=env,
+                stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
+        errs = [p.communicate(timeout=300)[1].decode(errors="replace") for p in procs]
+        dt = time.perf_counter() - t0
+    assert procs[0].returncode == 0, errs[0][-2000:]
+    assert procs[1].returncode != 0
+    assert "does not speculate" in errs[1], errs[1][-2000:]
+    assert dt < 120
 
 
 def test_streaming_run_walk_path(dev, golden, monkeypatch):

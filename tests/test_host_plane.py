@@ -288,6 +288,50 @@ def test_records_chain_equals_exact_chain(kind, pert):
         assert hit2 >= 0.97 * rows
 
 
+@pytest.mark.parametrize("bad", ["zero", "shift", "distance"])
+def test_records_chain_exact_with_wrong_links(bad):
+    """Records whose link does not belong to the slot's previous row: rows with wrong in[].pad
+    (zero-filled, or every pad one slot row too far back), and correct records whose stored row
+    distance (ok bits 2..) is altered.  The chain applies a link only when its distance names
+    the slot's actual previous row, so it stays exact; with the distances altered no link
+    holds and the rows fall back to their own records and walks."""
+    s = G.Scenario(NAV, llh=LOC, duration=120.0)
+    n = s.n_per_blk
+    b0, n0, c0 = s.next_deferred(60, threads=8)
+    carr, _ = G.carr_chain(s.carrier(), b0, n0, c0, n, with_ck=False)
+    blk, nch, chain = s.next_deferred(600, threads=8)
+    ref = blk.copy()
+    end_ref, _ = G.carr_chain(carr, ref, nch, chain, n, with_ck=False)
+    gi = G.carr_chain_guess(carr, blk, nch, chain, n, starts_only=True)
+    flat = gi.reshape(-1)
+    if bad == "zero":
+        flat["pad"] = 0
+    elif bad == "shift":
+        pads = flat["pad"].copy()
+        flat["pad"] = np.where(pads >= 0, pads[np.maximum(pads, 0)], -1)   # the row before last
+    spec = G.spec_host(gi, n, threads=8).reshape(gi.shape)
+    rec = G.spec_records(gi, spec, n)
+    if bad == "distance":
+        # poisoned links: any translation passes their interval and they move the carrier by a
+        # quarter cycle; with their true row distance the chain takes them (control), with an
+        # altered one it must refuse them
+        linked = (rec["ok"] & 2) != 0
+        assert linked.sum() >= 0.9 * int(nch.sum())
+        d = rec["ok"] >> 2
+        assert (d[linked] >= 1).all()
+        rec["llo"] = np.where(linked, -1.0, rec["llo"])
+        rec["lhi"] = np.where(linked, 1.0, rec["lhi"])
+        rec["ldd"] = np.where(linked, rec["ldd"] + 0.25, rec["ldd"])
+        b1 = blk.copy()
+        G.carr_chain_records(carr, b1, nch, chain, n, rec)
+        assert b1["carr0"].tobytes() != ref["carr0"].tobytes()       # the links are in use
+        rec["ok"] = np.where(linked, (rec["ok"] & 3) | ((d + G.MAXCH) << 2), rec["ok"])
+    b2 = blk.copy()
+    end2, _ = G.carr_chain_records(carr, b2, nch, chain, n, rec)
+    assert b2["carr0"].tobytes() == ref["carr0"].tobytes()
+    assert end2.tobytes() == end_ref.tobytes()
+
+
 def test_worker_pool_after_fork():
     """The host plane's persistent worker threads do not survive fork(): a child that plans
     (gss_pool_run on 8 threads) after the parent has grown its pools must still finish, with the
