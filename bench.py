@@ -43,7 +43,12 @@ Extra JSON fields besides the driver contract:
   window        the fast path including its proofs on the device, per step: gss_linearize_device
                 over the window's resident rows (the proof kernel) and then the render
                 (gss_synth_lin_device: window tables, segment rows, gss_lin_kernel) -- the cost of
-                a window that is proven once and rendered once, beside the kernel-only headline.
+                a window that is proven once and rendered once, beside the kernel-only headline;
+                window.device_window adds the carrier chain's speculative walks and records
+                (gss_spec_records_device) in front: the whole per-window GPU pipeline;
+  step_issue_efficiency  the fast kernel against the issue-bound peak of its own step (was
+                roofline_compute), with bound_frac / floor_bound_frac: the HBM-write fraction that
+                step, and the LUT formulation's floor, allow.
 """
 import argparse
 import json
@@ -77,18 +82,46 @@ VALU_PEAK_CHS = SIMDS * 64 * CLOCK_MAX_HZ / VALU_CYC_PER_CHSTEP
 LDS_PEAK_CHS = CUS * CLOCK_MAX_HZ * 64 / 2.0
 
 
-def compute_roofline(ch_samples, kern_ms):
-    """achieved channel-samples/s of one fast-kernel launch against the VALU issue bound (the
-    binding pipe) and the LDS bound"""
+# The LUT formulation's floor in hardware terms ("Where the plateau ends"): per
+# channel-sample a phase advance, a chip-sign extraction, a LUT address and a LUT read cannot be
+# fewer than one VOP2 op each for the first three (2.75 SIMD cycles apiece at 4 waves per SIMD,
+# profiles/round2/issue_ubench2.log) plus the accumulate's share of the MFMA (2 cycles: a
+# 16x16x32 f16 MFMA holds vector issue 8 cycles, MI355X_MICROARCH.md, per 4 channel-steps).
+FLOOR_CYC_PER_CHSTEP = 3 * 2.75 + 2.0
+FLOOR_PEAK_CHS = SIMDS * 64 * CLOCK_MAX_HZ / FLOOR_CYC_PER_CHSTEP
+
+
+def compute_roofline(ch_samples, kern_ms, bytes_per_sample=None, ch_per_sample=None):
+    """The fast kernel's issue efficiency: achieved channel-samples/s of one launch against the
+    issue-bound peak of ITS OWN step (4 VALU + a quarter MFMA at the top clock) -- how well the
+    chosen step issues, not whether it is the cheapest step -- and the LDS bound.  bound_frac:
+    the HBM-write roofline fraction that this step allows at 100 % issue and 2.4 GHz
+    (bytes_per_sample, ch_per_sample of the launch); floor_bound_frac: the same for the LUT
+    formulation's floor (FLOOR_CYC_PER_CHSTEP)."""
     if kern_ms <= 0:
         return None
     a = ch_samples / (kern_ms * 1e-3)
-    return {"bound": "valu", "achieved": round(a / 1e12, 4), "peak": round(VALU_PEAK_CHS / 1e12, 4),
-            "unit": "T channel-samples/s", "frac": round(a / VALU_PEAK_CHS, 4),
-            "lds_peak": round(LDS_PEAK_CHS / 1e12, 4), "lds_frac": round(a / LDS_PEAK_CHS, 4),
-            "channel_samples_per_launch": int(ch_samples),
-            "model": f"{VALU_CYC_PER_CHSTEP:.2f} SIMD cycles per wave channel-step, "
-                     f"{SIMDS} SIMDs at {CLOCK_MAX_HZ / 1e9:.1f} GHz"}
+    out = {"what": "issue efficiency of the 4-VALU + 1/4-MFMA step (not an HBM roofline)",
+           "bound": "valu issue of this step", "achieved": round(a / 1e12, 4),
+           "peak": round(VALU_PEAK_CHS / 1e12, 4),
+           "unit": "T channel-samples/s", "frac": round(a / VALU_PEAK_CHS, 4),
+           "lds_peak": round(LDS_PEAK_CHS / 1e12, 4), "lds_frac": round(a / LDS_PEAK_CHS, 4),
+           "channel_samples_per_launch": int(ch_samples),
+           "model": f"{VALU_CYC_PER_CHSTEP:.2f} SIMD cycles per wave channel-step, "
+                    f"{SIMDS} SIMDs at {CLOCK_MAX_HZ / 1e9:.1f} GHz"}
+    if bytes_per_sample and ch_per_sample:
+        def hbm_frac(peak_chs):
+            return round(peak_chs / ch_per_sample * bytes_per_sample / (HBM_PEAK_GBS * 1e9), 4)
+        out.update({"bound_frac": hbm_frac(VALU_PEAK_CHS),
+                    "floor_bound_frac": hbm_frac(FLOOR_PEAK_CHS),
+                    "lds_bound_frac": hbm_frac(LDS_PEAK_CHS),
+                    "channels_per_sample": round(ch_per_sample, 3),
+                    "bound_model": f"HBM-write fraction at 100 % issue: this step "
+                                   f"{VALU_CYC_PER_CHSTEP:.2f}, the formulation's floor "
+                                   f"{FLOOR_CYC_PER_CHSTEP:.2f} SIMD cycles per wave "
+                                   f"channel-step; one conflict-free ds_read_b32 per wave "
+                                   f"channel-step for the LDS"})
+    return out
 
 # BASELINE.json configs[2..4] (per_config); configs[1] is the headline, configs[0] the CPU case
 CONFIGS = [
@@ -344,12 +377,20 @@ def time_steps(torch, dev, dev_t, res, steps, warmup, stream):
     return el, n_lin, lin_ms
 
 
-def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None, anch=None):
+def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None, anch=None,
+               heads=None):
     """proof + render of the resident window per step (see the module docstring): the proof kernel
     rewrites the window's rows and fast flags in place (byte-identical rows: tests/
     test_gpu_proof.py), then the window renders from them; HIP events on the launch stream time
     the proof apart.  anch: the planner's chain anchors (resident like the rows), where the
-    proofs' carrier walks start (gss_linearize_device_ex)"""
+    proofs' carrier walks start (gss_linearize_device_ex).
+    heads (the window's walk inputs, SPEC_IN_DTYPE [nblk, 16]): a second pass, device_window,
+    adds the planner's device work per step -- the carrier chain's speculative walks and their
+    records (gss_spec_records_device: gss_spec_kernel + gss_spec_rec_kernel, resident in and out)
+    -- so that spec + proof + render, the whole per-window GPU pipeline gss_run runs, is timed
+    on the device (the host's chain between them excluded)."""
+    import numpy as np
+    import gpssim_amd as G
     st = torch.cuda.current_stream(dev_t)
     d_anch = None
     if anch is not None:
@@ -360,30 +401,71 @@ def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None, anch=N
                              res.d_ca.data_ptr(), res.n_ca, res.d_nav.data_ptr(), res.n_nav,
                              res.d_lin.data_ptr(), res.d_fast.data_ptr(), stream,
                              anch_ptr=d_anch.data_ptr() if d_anch is not None else None)
-    for _ in range(warmup):
-        prove()
-        res.step(stream)
-    torch.cuda.synchronize(dev_t)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
-    t0 = time.perf_counter()
-    for i in range(steps):
-        ev[i][0].record(st)
-        prove()
-        ev[i][1].record(st)
-        res.step(stream)
-    torch.cuda.synchronize(dev_t)
-    el = time.perf_counter() - t0
-    proof_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+
+    spec = None
+    if heads is not None:
+        nrow = heads.size
+        d_heads = torch.from_numpy(np.ascontiguousarray(heads).reshape(-1).view(np.uint8)
+                                   .copy()).to(dev_t)
+        d_in = torch.empty(nrow * G.SPEC_IN_DTYPE.itemsize, dtype=torch.uint8, device=dev_t)
+        d_spec = torch.empty(nrow * G.SPEC_DTYPE.itemsize, dtype=torch.uint8, device=dev_t)
+        d_rec = torch.empty(nrow * G.SPEC_REC_DTYPE.itemsize, dtype=torch.uint8, device=dev_t)
+
+        def spec():
+            dev.spec_records_device(d_heads.data_ptr(), nrow, res.npb, d_in.data_ptr(),
+                                    d_spec.data_ptr(), d_rec.data_ptr(), stream)
+
+    def run(with_spec):
+        for _ in range(warmup):
+            if with_spec:
+                spec()
+            prove()
+            res.step(stream)
+        torch.cuda.synchronize(dev_t)
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+        t0 = time.perf_counter()
+        for i in range(steps):
+            ev[i][0].record(st)
+            if with_spec:
+                spec()
+            ev[i][1].record(st)
+            prove()
+            ev[i][2].record(st)
+            res.step(stream)
+            ev[i][3].record(st)
+        torch.cuda.synchronize(dev_t)
+        el = time.perf_counter() - t0
+        part = [sum(e[j].elapsed_time(e[j + 1]) for e in ev) / steps for j in range(3)]
+        return el, part
+
     samples = res.nblk * res.npb
+    el, (_, proof_ms, render_ms) = run(False)
     out = {"value": round(samples * steps / el / 1e6, 2), "unit": "MS/s",
            "ms_per_step": round(el / steps * 1e3, 3), "proof_ms": round(proof_ms, 3),
-           "steps": steps, "warmup": warmup,
+           "render_ms": round(render_ms, 3), "steps": steps, "warmup": warmup,
            "workload": "the headline window: proof kernel (gss_linearize_device) + render "
                        "(gss_synth_lin_device) per step on resident rows",
            "anchors": d_anch is not None}
     if exact:
         out["vs_exact_path"] = round(out["value"] / exact["value"], 3)
+    if spec is not None:
+        el2, (spec_ms, proof2_ms, render2_ms) = run(True)
+        dev_ms = spec_ms + proof2_ms + render2_ms
+        bytes_step = res.n_fast * res.bb
+        out["device_window"] = {
+            "workload": "the headline window's whole GPU pipeline per step on resident rows: "
+                        "the chain's speculative walks + records (gss_spec_records_device), "
+                        "the proofs (gss_linearize_device_ex, anchors), the render",
+            "value": round(samples * steps / el2 / 1e6, 2), "unit": "MS/s",
+            "ms_per_step": round(el2 / steps * 1e3, 3),
+            "spec_ms": round(spec_ms, 3), "proof_ms": round(proof2_ms, 3),
+            "render_ms": round(render2_ms, 3), "device_ms": round(dev_ms, 3),
+            "rows_walked": int(heads.size),
+            "roofline": {"bound": "hbm", "achieved": round(bytes_step / (dev_ms * 1e-3) / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(bytes_step / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "note": "the window's output bytes over the three kernels' summed "
+                                 "event time"}}
     return out
 
 
@@ -406,7 +488,8 @@ def per_config(G, torch, dev, dev_t, stream, steps, warmup, threads, e2e=True):
         msps = samples * steps / el / 1e6
         per_launch = (res.n_fast * res.bb) / len(res.batches)
         achieved = per_launch / (lin_ms * 1e-3) / 1e9 if lin_ms > 0 else 0.0
-        comp = compute_roofline(res.ch_samples_fast / len(res.batches), lin_ms)
+        comp = compute_roofline(res.ch_samples_fast / len(res.batches), lin_ms, res.bb / res.npb,
+                                res.ch_samples_fast / max(1, res.n_fast * res.npb))
         out.append({
             "config": c["name"], "workload": c["desc"], "fmt": c["fmt"],
             "value": round(msps, 2), "unit": "MS/s", "x_realtime": round(msps / (c["fs"] / 1e6), 1),
@@ -782,7 +865,7 @@ def main():
     window = None
     if single and not args.no_window and res.proof == "gpu":
         window = window_leg(torch, dev, dev_t, res, args.steps, args.warmup, stream, exact,
-                            anch=plan_t.get("anch"))
+                            anch=plan_t.get("anch"), heads=plan_t.get("spec_heads"))
         progress(f"window (proof + render): {window['value']} MS/s, proof {window['proof_ms']} ms")
     ms_per_step = elapsed / args.steps * 1e3
     progress(f"timed {args.steps} steps: {ms_per_step:.3f} ms/step, kernel {lin_ms:.3f} ms")
@@ -790,7 +873,8 @@ def main():
     # the dominant kernel is gss_lin_kernel; its algorithmic bytes are the certified blocks'
     bytes_launch = res.n_fast * res.bb
     achieved = bytes_launch / (lin_ms * 1e-3) / 1e9 if lin_ms > 0 else 0.0
-    comp_head = compute_roofline(res.ch_samples_fast, lin_ms)
+    comp_head = compute_roofline(res.ch_samples_fast, lin_ms, res.bb / npb,
+                                 res.ch_samples_fast / max(1, res.n_fast * npb))
     workload = (f"static -l {LOC[0]},{LOC[1]},{LOC[2]:g} -s 2600000 -b {args.fmt}, "
                 f"{args.window:g} s per GPU ({nblk} blocks x {npb} samples)")
     version = G.lib().gss_version().decode()
@@ -860,7 +944,7 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "profile": prof},
-        "roofline_compute": comp_head,
+        "step_issue_efficiency": comp_head,
         "cpu_baseline": cpu,
         "per_config": configs,
         "gather": gather,

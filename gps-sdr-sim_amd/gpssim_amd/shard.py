@@ -70,16 +70,21 @@ def device_walker(dev, torch):
 
 
 def chain_run_ahead(carr, blk, nch, chain, n_per_blk, walker, threads=8, chunk=SPEC_CHUNK,
-                    anch=None):
+                    anch=None, heads=None):
     """gss_carr_chain's result (blk["carr0"] filled in place, the carriers after the last block)
     from speculative walks: returns (end carriers, rows whose translation held).  anch
-    (ANCHOR_DTYPE [nb, 16], optional): filled with the chain's anchors (the proofs' walk starts)."""
+    (ANCHOR_DTYPE [nb, 16], optional): filled with the chain's anchors (the proofs' walk starts).
+    heads (SPEC_IN_DTYPE [nb, 16], optional): filled with the rows' walk inputs as the walkers
+    got them (start guesses, steps, previous rows; segment starts left to the walkers), e.g. to
+    replay the window's walks on the device (bench.py device_window)."""
     c = np.array(carr, np.float64, copy=True)
     hits = 0
     for b0 in range(0, len(nch), chunk):
         b1 = min(len(nch), b0 + chunk)
         gi = carr_chain_guess(c, blk[b0:b1], nch[b0:b1], chain[b0:b1], n_per_blk,
                               starts_only=True)
+        if heads is not None:
+            heads[b0:b1] = gi
         spec = walker(gi, n_per_blk).reshape(gi.shape)
         if anch is None:
             c, h = carr_chain_spec(c, blk[b0:b1], nch[b0:b1], chain[b0:b1], n_per_blk, gi, spec,
@@ -342,10 +347,12 @@ def plan_window(scn, first, count, baton=None, threads=8, batch=2000, with_ck=Tr
     ct = chain_threads or threads
     if walker is not None and len(nch):
         anch = np.zeros((len(nch), MAXCH), ANCHOR_DTYPE) if anchors else None
+        heads = np.zeros((len(nch), MAXCH), SPEC_IN_DTYPE) if anchors else None
         end, t["spec_hits"] = chain_run_ahead(carr, blk, nch, chain, scn.n_per_blk, walker,
-                                              threads=ct, anch=anch)
+                                              threads=ct, anch=anch, heads=heads)
         if anchors:
             t["anch"] = anch
+            t["spec_heads"] = heads
         ck = None
     else:
         end, ck = carr_chain(carr, blk, nch, chain, scn.n_per_blk, carrier_int=scn.carrier_int,
