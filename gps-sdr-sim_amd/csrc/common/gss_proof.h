@@ -59,7 +59,16 @@ GSS_PF uint64_t gss_pf_udiv(u128 a, uint64_t b)
     return q;
 }
 
-#define GSS_PF_EUCLID_MAX 64       /* descent levels kept (a deeper one gives up: uncertified) */
+#ifndef GSS_PF_EUCLID_MAX
+#define GSS_PF_EUCLID_MAX 32       /* descent levels kept (a deeper one gives up: uncertified).
+                                      The deepest descent of every test scenario (static and
+                                      circle 2.6 MS/s, 20 MS/s, -b 1; ~2.5 M descents) is 21
+                                      levels (GSS_PF_STATS builds); 32 keeps a
+                                      margin at 768 B of stack per lane instead of 1.5 KB */
+#endif
+#ifdef GSS_PF_STATS
+void gss_pf_depth_note(int d);     /* linearize.c: a histogram of descent depths */
+#endif
 #define GSS_PF_GIVE_UP (UINT64_MAX - 1)
 GSS_PF uint64_t first_in(uint64_t s, uint64_t m, uint64_t lo, uint64_t hi, uint64_t lim)
 {
@@ -86,6 +95,9 @@ GSS_PF uint64_t first_in(uint64_t s, uint64_t m, uint64_t lo, uint64_t hi, uint6
         }
         if (d == GSS_PF_EUCLID_MAX)
             return GSS_PF_GIVE_UP;
+#ifdef GSS_PF_STATS                                  /* (host measurement builds only) */
+        gss_pf_depth_note(d + 1);
+#endif
         /* no multiple of s in [lo, hi]: both lie in ((x - 1) s, x s), so their residues are
            one product away (no further division; 1 <= lr <= hr < s) */
         const uint64_t base = s * (x - 1), lr = lo - base, hr = hi - base;
@@ -176,7 +188,7 @@ GSS_PF i128 to_fix(double x, int k, int *inexact)
 #ifndef GSS_PF_GAPS
 #define GSS_PF_GAPS 0            /* (measurement builds: 1 gaps from the first hit, 2 never)       */
 #endif
-GSS_PF int hits_mod(uint64_t n, uint64_t B, uint64_t a0, uint64_t st, uint64_t w, int64_t *hit,
+GSS_PF int hits_mod(uint64_t n, uint64_t B, uint64_t a0, uint64_t st, uint64_t w, int32_t *hit,
                     int cap, int scan)
 {
     const uint64_t M = B - 1;
@@ -197,7 +209,7 @@ GSS_PF int hits_mod(uint64_t n, uint64_t B, uint64_t a0, uint64_t st, uint64_t w
             break;
         if (nh == cap)
             return -1;
-        hit[nh++] = p0 + (int64_t)i;
+        hit[nh++] = (int32_t)(p0 + (int64_t)i);
         p0 += (int64_t)i + 1;
         if (scan || nh != gap_at)
             continue;
@@ -232,7 +244,7 @@ GSS_PF int hits_mod(uint64_t n, uint64_t B, uint64_t a0, uint64_t st, uint64_t w
                 break;
             if (nh == cap)
                 return -1;
-            hit[nh++] = (int64_t)q;
+            hit[nh++] = (int32_t)q;
         }
         return nh;
     }
@@ -242,7 +254,7 @@ GSS_PF int hits_mod(uint64_t n, uint64_t B, uint64_t a0, uint64_t st, uint64_t w
 /* Step 2: the samples p in [1, n) where the line L0 + p S comes within delta of a cell boundary
    (a multiple of 2^lgB).  Writes up to cap of them in ascending order to hit[]; returns their
    number, or -1 if there are more (or delta is not small against B). */
-GSS_PF int ambiguous(i128 L0, i128 S, i128 delta, int lgB, int64_t n, int64_t *hit, int cap)
+GSS_PF int ambiguous(i128 L0, i128 S, i128 delta, int lgB, int64_t n, int32_t *hit, int cap)
 {
     const uint64_t B = (uint64_t)1 << lgB;           /* lgB <= 55 */
     if (delta >= (i128)(B / 4))
@@ -269,7 +281,7 @@ GSS_PF int signed_gain(int gain, const uint32_t *nav, int iword, int ibit)
     return ((nav[iword] >> (29 - ibit)) & 1u) ? gain : -gain;
 }
 
-GSS_PF int find_hit(const int64_t *hit, int nh, int64_t q)
+GSS_PF int find_hit(const int32_t *hit, int nh, int64_t q)
 {
     for (int i = 0; i < nh; i++)
         if (hit[i] == q)
@@ -283,6 +295,12 @@ GSS_PF int64_t wraps_of(const gss_code_state *c, const gss_chan_blk_t *p)
     return ((int64_t)(c->iword - p->iword) * 30 + (c->ibit - p->ibit)) * 20 +
            (c->icode - p->icode);
 }
+
+/* what the proof keeps of the exact code state at an ambiguous code sample: its chip and its
+   wraps since the block start (8 B instead of a 24-B gss_code_state per sample) */
+typedef struct gss_pf_code {
+    int32_t chip, wraps;
+} gss_pf_code;
 
 /* cos + 2^22 sin of LUT cell c (the kernel's packed I/Q term, gpssim.c:15-83), from the tables of
    gss_lut */
@@ -303,19 +321,6 @@ GSS_PF int near_boundary(i128 v, i128 d, int lgB)
     return (i128)(((uint64_t)v + (uint64_t)d) & (B - 1)) < 2 * d;
 }
 
-/* merge two ascending sample lists and {0}: ascending, no duplicates */
-GSS_PF int merge_hits(const int64_t *a, int na, const int64_t *b, int nb, int64_t *out)
-{
-    int i = 0, j = 0, n = 0;
-    out[n++] = 0;
-    while (i < na || j < nb) {
-        int64_t v = (j >= nb || (i < na && a[i] <= b[j])) ? a[i++] : b[j++];
-        if (v != out[n - 1])
-            out[n++] = v;
-    }
-    return n;
-}
-
 /* 1 if certified (lin filled), 0 if this channel needs the exact path.  an (NULL: none): the
    chain's exact carrier values inside the block (gss_carr_anchor_t), where the carrier walks to
    the ambiguous samples start instead of at the block start; or, without them, sin / sspec (NULL:
@@ -328,12 +333,12 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
 {
     gss_carr_anchor_t la;
     int inexact = 0;
-    int64_t hx[LIN_MAXHIT], hz[LIN_MAXHIT], hq[2 * LIN_MAXHIT + 1];
-    gss_code_state at_hz[LIN_MAXHIT];
+    int32_t hx[LIN_MAXHIT], hz[LIN_MAXHIT];
+    gss_pf_code at_hz[LIN_MAXHIT];
 
     /* ---- the two lines and the samples where they decide nothing (gpssim.c:2212-2250) ---- */
     const double x0 = p->carr0, s = p->carr_step;
-    if (!(x0 >= 0.0 && x0 < 1.0) || !(s > -0.5 && s < 0.5))
+    if (!(x0 >= 0.0 && x0 < 1.0) || !(s > -0.5 && s < 0.5) || n <= 0 || n > INT32_MAX / 2)
         return 0;
     const i128 X0 = to_fix(x0, 64, &inexact), XS = to_fix(s, 64, &inexact);
     const i128 DX1 = 2 + (i128)n * (LIN_CARR_ERR + 1);           /* line vs reference */
@@ -386,14 +391,13 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
         if (near_boundary(zq, DZ1, LIN_CODE_LGB)) {
             gss_code_walk_cc(&st, cs, hz[i] - at);
             at = hz[i];
-            at_hz[i] = st;
+            at_hz[i].chip = (int32_t)floor(st.ph);
+            at_hz[i].wraps = (int32_t)wraps_of(&st, p);
         } else {
-            const int64_t chips = (int64_t)(zq >> LIN_CODE_LGB);   /* from chip 0 of the block */
-            const int64_t tot = p->icode + chips / GSS_CA_LEN, bits = p->ibit + tot / 20;
-            at_hz[i].ph = (double)(chips % GSS_CA_LEN) + 0.5;      /* (only its floor is read) */
-            at_hz[i].icode = (int)(tot % 20);
-            at_hz[i].ibit = (int)(bits % 30);
-            at_hz[i].iword = p->iword + (int)(bits / 30);
+            /* the line's chip and wraps (from chip 0 of the block) */
+            const int64_t chips = (int64_t)(zq >> LIN_CODE_LGB);
+            at_hz[i].chip = (int32_t)(chips % GSS_CA_LEN);
+            at_hz[i].wraps = (int32_t)(chips / GSS_CA_LEN);
         }
     }
 
@@ -414,9 +418,9 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
         if (q - 1 >= n)
             break;
         int j = find_hit(hz, nhz, q - 1);
-        if (j >= 0 && wraps_of(&at_hz[j], p) >= k)
+        if (j >= 0 && at_hz[j].wraps >= k)
             q--;                                 /* the exact value wrapped one sample earlier */
-        else if ((j = find_hit(hz, nhz, q)) >= 0 && wraps_of(&at_hz[j], p) < k)
+        else if ((j = find_hit(hz, nhz, q)) >= 0 && at_hz[j].wraps < k)
             q++;                                 /* ... or one sample later */
         if (q >= n)
             break;
@@ -440,13 +444,13 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
         lin->gval[i] = g;
     }
 
-    /* ---- patches: the exact term where the kernel's differs ---- */
-    const int nq = merge_hits(hx, nhx, hz, nhz, hq);
+    /* ---- patches: the exact term where the kernel's differs, at sample 0 and every ambiguous
+       sample of either line, in ascending order (the two lists merged as they are read) ---- */
     double x = x0;
     int64_t xat = 0;
     int np = 0, gi = 0;
-    for (int i = 0; i < nq; i++) {
-        const int64_t q = hq[i];
+    int hxi = 0, hzi = 0;
+    for (int64_t q = 0; q >= 0;) {
         int cell, chip;
         if (q == 0) {
             cell = (int)floor(x0 * 512.0);
@@ -471,11 +475,10 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
         } else {                                 /* proven: exact = line */
             cell = (int)((uint64_t)(X0 + (i128)q * XS) >> LIN_CARR_LGB);
         }
-        int j;
         if (q == 0)
             chip = (int)floor(c0);
-        else if ((j = find_hit(hz, nhz, q)) >= 0)
-            chip = (int)floor(at_hz[j].ph);
+        else if (hzi < nhz && hz[hzi] == q)            /* (hzi: the first code hit not below q) */
+            chip = at_hz[hzi].chip;
         else
             chip = (int)((uint64_t)((Z0 + (i128)q * ZS) >> LIN_CODE_LGB) % GSS_CA_LEN);
         const gss_lin_kc kk = gss_lin_kernel_at((uint64_t)X0, (uint64_t)XS, (uint64_t)Z0,
@@ -483,14 +486,20 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
         const int kcell = kk.cell, kchip = kk.chip;
         const int64_t te = ca_sign(ca, chip) * lut_packed(lcos, lsin, cell);
         const int64_t tk = ca_sign(ca, kchip) * lut_packed(lcos, lsin, kcell);
-        if (te == tk)
-            continue;
-        while (gi + 1 < GSS_NGC && lin->gpos[gi + 1] <= q)
-            gi++;
-        if (np == GSS_NPATCH)
-            return 0;
-        lin->ppos[np] = (int32_t)q;
-        lin->pdelta[np++] = (int64_t)lin->gval[gi] * (te - tk);
+        if (te != tk) {
+            while (gi + 1 < GSS_NGC && lin->gpos[gi + 1] <= q)
+                gi++;
+            if (np == GSS_NPATCH)
+                return 0;
+            lin->ppos[np] = (int32_t)q;
+            lin->pdelta[np++] = (int64_t)lin->gval[gi] * (te - tk);
+        }
+        /* the next sample of the merged lists past q (-1: none) */
+        while (hxi < nhx && hx[hxi] <= q)
+            hxi++;
+        while (hzi < nhz && hz[hzi] <= q)
+            hzi++;
+        q = hxi < nhx ? (hzi < nhz && hz[hzi] < hx[hxi] ? hz[hzi] : hx[hxi]) : hzi < nhz ? hz[hzi] : -1;
     }
     (void)inexact;
     return 1;

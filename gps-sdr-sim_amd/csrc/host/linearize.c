@@ -84,6 +84,17 @@ u128 gss_maxmod(u128 n, u128 m, u128 a, u128 s)
     return m - 1 - gss_minmod(n, m, m - 1 - a, (m - s) % m);
 }
 
+#ifdef GSS_PF_STATS
+/* measurement builds: how deep the proofs' descents go (gss_pf_stats reads and clears) */
+static long pf_depth_hist[GSS_PF_EUCLID_MAX + 2];
+void gss_pf_depth_note(int d) { __atomic_add_fetch(&pf_depth_hist[d], 1, __ATOMIC_RELAXED); }
+void gss_pf_stats(long *out)
+{
+    for (int i = 0; i < GSS_PF_EUCLID_MAX + 2; i++)
+        out[i] = __atomic_exchange_n(&pf_depth_hist[i], 0, __ATOMIC_RELAXED);
+}
+#endif
+
 /* exported for tests: first_below, and min and max of (a + p s) mod m over [0, n) */
 uint64_t gss_first_below(uint64_t n, uint64_t m, uint64_t a, uint64_t s, uint64_t w)
 {
@@ -101,7 +112,16 @@ int gss_hits_mod(uint64_t n, uint64_t lgB, uint64_t a0, uint64_t st, uint64_t w,
         cap < 0)
         return -2;
     const uint64_t B = (uint64_t)1 << lgB;
-    return hits_mod(n, B, a0 & (B - 1), st & (B - 1), w, hit, cap, scan);
+    if (n > INT32_MAX)
+        return -2;
+    int32_t *h32 = malloc(sizeof(int32_t) * (size_t)(cap > 0 ? cap : 1));
+    if (!h32)
+        return -2;
+    const int nh = hits_mod(n, B, a0 & (B - 1), st & (B - 1), w, h32, cap, scan);
+    for (int i = 0; i < nh; i++)
+        hit[i] = h32[i];
+    free(h32);
+    return nh;
 }
 
 /* (64-bit operands) */
