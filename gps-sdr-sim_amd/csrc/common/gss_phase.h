@@ -1133,9 +1133,14 @@ GSS_HD double gss_walk_margins(double x, double s, int64_t n, double *dlo, doubl
    so the chain's fix-up stays exact).  A miss walks the cycle with margins and caches it.
    Descending: the head down to T is cached the same way; the few real steps below T keep their
    per-step margins.  Cuts a segment's walk from ~13 binade jumps per carrier cycle to one cache
-   probe for most cycles. */
+   probe for most cycles: 2.3x faster on one host core, but 12 % SLOWER on the GPU (gss_spec_kernel
+   1.36-1.42 against 1.21-1.23 ms per headline window, profiles/round6/spec_cache/): each lane
+   misses its cold cache at its own cycles, so nearly every cycle some lane of the wave walks it
+   in full while the others wait, and the probes go through scratch.  Off by default, so that the
+   host and the GPU walks stay the same bytes (tests/test_gpu_parity.py
+   test_spec_records_on_device); -DGSS_SPEC_CC=1 builds it (test_phase_walk.py checks it). */
 #ifndef GSS_SPEC_CC
-#define GSS_SPEC_CC 1
+#define GSS_SPEC_CC 0
 #endif
 GSS_HD double gss_walk_margins_cc(double x, double s, int64_t n, double *dlo, double *dhi,
                                   int *wrap_end, gss_cyc_cache *cc)

@@ -100,6 +100,8 @@ def walk_lib():
                                      C.c_void_p, C.c_void_p]
         L.wc_carr_walk_ck.restype = D
         L.wc_carr_walk_ck.argtypes = [D, D, C.c_int, C.c_void_p]
+        L.wc_margins.restype = D
+        L.wc_margins.argtypes = [D, D, I64, C.c_int, C.POINTER(D), C.POINTER(D), P]
         L.wc_carr_anchors.restype = C.c_int
         L.wc_carr_anchors.argtypes = [D, D, I64, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         _walk = L

@@ -147,3 +147,16 @@ double wc_carr_trip(double x, double s, int64_t n)
         gss_trip(kind, &x, s, rs, &left, &J, &Ds);
     return x;
 }
+
+/* the speculative segment walk's margins, plain (gss_walk_margins) or from the cycle cache
+   (gss_walk_margins_cc, GSS_SPEC_CC builds): end value, admissible start translations, wrap */
+double wc_margins(double x, double s, int64_t n, int use_cc, double *dlo, double *dhi, int *we)
+{
+    *dlo = -GSS_BIG;
+    *dhi = GSS_BIG;
+    if (use_cc) {
+        gss_cyc_cache cc;
+        return gss_walk_margins_cc(x, s, n, dlo, dhi, we, &cc);
+    }
+    return gss_walk_margins(x, s, n, dlo, dhi, we);
+}

@@ -288,3 +288,34 @@ def test_block_chains_successor_fast_path(seed):
             assert W.wc_carr_walk_ck(x, s, n, ck.ctypes.data) == want, (seed, i, b, x, s)
             assert np.array_equal(ck, oracle.carr_brute_trace(x, s, at)), (seed, i, b, x, s)
             x, s = want, s * (1.0 + rng.uniform(-2e-7, 2e-7))
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_margin_walk_cycle_cache(seed):
+    """The speculative walks' cycle-cached margins (gss_walk_margins_cc, -DGSS_SPEC_CC=1 builds:
+    2.3x faster on the host, slower on the GPU, so off by default): from a post-wrap start the
+    same end and wrap as the plain margin walk, an interval inside the plain one, and every
+    lattice translation d inside it moves the brute-force end by exactly d."""
+    W = walk_lib()
+    rng = random.Random(seed)
+    D = C.c_double
+    checked = 0
+    for x, s, n in cases(seed, 60):
+        if s == 0.0 or abs(s) > 0.01:
+            continue
+        unit = 2.0 ** -52 if s > 0 else 2.0 ** -53
+        w = math.floor(rng.random() * abs(s) / unit) * unit      # a post-wrap lattice value
+        n = min(n, 200000)
+        lo0, hi0, lo1, hi1 = D(), D(), D(), D()
+        we0, we1 = C.c_int32(0), C.c_int32(0)
+        e0 = W.wc_margins(w, s, n, 0, C.byref(lo0), C.byref(hi0), C.byref(we0))
+        e1 = W.wc_margins(w, s, n, 1, C.byref(lo1), C.byref(hi1), C.byref(we1))
+        assert e0 == e1 == oracle.carr_brute(w, s, n), (w, s, n)
+        assert we0.value == we1.value
+        assert lo0.value <= lo1.value <= 0.0 <= hi1.value <= hi0.value, (w, s, n)
+        for k in (math.ceil(lo1.value / unit), math.floor(hi1.value / unit), 1, -1):
+            d = k * unit
+            if lo1.value <= d <= hi1.value and 0.0 <= w + d < 1.0:
+                assert oracle.carr_brute(w + d, s, n) == e1 + d, (w, s, n, d)
+                checked += 1
+    assert checked > 20
