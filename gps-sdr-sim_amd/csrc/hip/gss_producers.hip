@@ -98,6 +98,167 @@ __device__ inline int spec_row_of(int u, int nrow)
     return nrow % GSS_MAXCH ? u : (u % nb) * GSS_MAXCH + u / nb;
 }
 
+/* ---- a cycle cache shared by the GSS_SPEC_K lanes of one row, in LDS ----------------------------
+ * The 8 segments of a row walk with the same step s, so every cycle map one lane walks (its
+ * start interval [lo, hi], length L, end v0 of start w0: gss_cc_put's entry) serves the other
+ * seven too.  Each lane writes its own 4 entries (a ring), every lane reads all 32; all of a
+ * row's lanes are in one wave, so a lane's LDS writes are seen by the wave's later reads (program
+ * order), no barrier.  A per-lane cache (GSS_SPEC_CC) missed at each lane's own cycles, so the
+ * wave walked nearly every cycle in full (12 % slower than no cache); shared, a row's cache holds
+ * its ~10-16 cycle types after each lane's first few cycles and the wave then mostly takes the
+ * O(1) path.  The intervals are the cached walks' (shrunk by `safe`), so a segment's [dlo, dhi]
+ * can be narrower than the host's plain walk (gss_walk_margins) gives: still conservative, the
+ * same ends and wraps, and the chain exact (tests/test_gpu_parity.py test_spec_records_on_device). */
+constexpr int SCC_PER_LANE = 4;
+constexpr int SCC_N = GSS_SPEC_K * SCC_PER_LANE;         /* entries per row */
+struct spec_cc {
+    double lo[SCC_N], hi[SCC_N], w0[SCC_N], v0[SCC_N];
+    int32_t L[SCC_N];                                    /* 0: empty */
+    int32_t succ[SCC_N];                                 /* the entry the next cycle used */
+};
+
+/* an entry holding start w with at most nmax steps, the hint (the successor of the previous
+   cycle's entry) first; -1 if none */
+__device__ inline int scc_find(const spec_cc *c, double w, int64_t nmax, int prev)
+{
+    if (prev >= 0) {
+        const int p = c->succ[prev];
+        if (p >= 0 && c->L[p] > 0 && w >= c->lo[p] && w <= c->hi[p] && c->L[p] <= nmax)
+            return p;
+    }
+    for (int i = 0; i < SCC_N; i++)
+        if (c->L[i] > 0 && w >= c->lo[i] && w <= c->hi[i] && c->L[i] <= nmax)
+            return i;
+    return -1;
+}
+
+__device__ inline int scc_put(spec_cc *c, int j, int &ring, double w, double dlo, double dhi,
+                              double safe, double v_end, int64_t L)
+{
+    if (!(dlo <= 0.0 && dhi >= 0.0) || L <= 0 || L > INT32_MAX)
+        return -1;
+    const int i = j * SCC_PER_LANE + (ring++ & (SCC_PER_LANE - 1));
+    double lo = w + dlo + safe, hi = w + dhi - safe;
+    if (lo > w) lo = w;                                  /* the walked start is always valid */
+    if (hi < w) hi = w;
+    c->L[i] = 0;                                         /* (invalid while rewritten) */
+    c->lo[i] = lo;
+    c->hi[i] = hi;
+    c->w0[i] = w;
+    c->v0[i] = v_end;
+    c->succ[i] = -1;
+    c->L[i] = (int32_t)L;
+    return i;
+}
+
+/* gss_walk_margins from a post-wrap value x, whole cycles from the row's shared cache */
+__device__ double spec_walk_margins_shared(double x, double s, int64_t n, double *dlo,
+                                           double *dhi, int *wrap_end, spec_cc *c, int j)
+{
+    int64_t left = n;
+    int last = 0, prev = -1, ring = 0;
+    const double safe = 4.0 * gss_pow2(-52);
+    const double T = s > 0.0 ? 0.0 : gss_pow2(gss_exp2i(-s) + 2);
+    const double dunit = gss_pow2(-53);
+    while (left > 0) {
+        const double w = x;
+        const int e = scc_find(c, w, left, prev);
+        if (prev >= 0 && e >= 0)
+            c->succ[prev] = e;
+        if (e >= 0) {
+            const double lo = c->lo[e] - w, hi = c->hi[e] - w;
+            if (lo > *dlo) *dlo = lo;
+            if (hi < *dhi) *dhi = hi;
+            x = c->v0[e] + (w - c->w0[e]);
+            left -= c->L[e];
+            prev = e;
+            if (s > 0.0) {
+                last = 1;
+                continue;
+            }
+        } else {
+            double clo = -GSS_BIG, chi = GSS_BIG;
+            int st = 0;
+            int64_t taken;
+            if (s > 0.0) {
+                taken = gss_asc_to_wrap(&x, s, 1.0, left, &st, &clo, &chi);
+                last = st;
+            } else {
+                last = 0;
+                taken = gss_desc_head(&x, s, T, left, &st, &clo, &chi);
+            }
+            left -= taken;
+            if (clo > *dlo) *dlo = clo;
+            if (chi < *dhi) *dhi = chi;
+            const int put = st ? scc_put(c, j, ring, w, clo, chi, safe, x, taken) : -1;
+            if (prev >= 0 && put >= 0)
+                c->succ[prev] = put;
+            prev = put;
+            if (s > 0.0)
+                continue;
+            if (!st || left <= 0)
+                break;
+        }
+        last = 0;
+        while (left > 0) {                      /* descending, below T: real steps to the wrap */
+            gss_margin_step(x, s, dunit, dlo, dhi);
+            const double r = x + s;
+            left--;
+            if (r < 0.0) {
+                const double lim = -r - 2.0 * dunit;
+                if (lim < *dhi) *dhi = lim;
+                gss_margin_step(r, 1.0, dunit, dlo, dhi);
+                x = r + 1.0;
+                last = 1;
+                break;
+            }
+            if (-r > *dlo) *dlo = -r;
+            x = r;
+        }
+    }
+    *wrap_end = last;
+    return x;
+}
+
+/* gss_spec_seg_walk (gss_phase.h) with the segment's margins walk from the row's shared cache */
+__device__ void spec_seg_walk_shared(const gss_spec_in_t *in, int j, int64_t n, gss_spec_t *o,
+                                     spec_cc *c)
+{
+    const double s = in->s;
+    const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
+    gss_spec_seg_t *sg = &o->seg[j];
+    const int64_t stop = j + 1 < k ? in->P[j + 1] : n;
+    double x;
+    int64_t pos;
+    sg->dlo = 1.0;
+    sg->dhi = 0.0;
+    sg->wrap_end = 0;
+    if (j == 0) {
+        x = in->g;
+        int wr = 0;
+        const int64_t t = s != 0.0 ? gss_carr_to_wrap(&x, s, stop, &wr) : stop;
+        o->p1 = wr ? t : n;
+        o->w1 = x;
+        sg->end = x;
+        if (!wr || t >= stop)
+            return;
+        pos = t;
+    } else {
+        x = in->W[j];
+        pos = in->P[j];
+        sg->end = x;
+        if (s == 0.0 || pos >= stop)
+            return;
+    }
+    double dlo = -GSS_BIG, dhi = GSS_BIG;
+    int we = 0;
+    x = spec_walk_margins_shared(x, s, stop - pos, &dlo, &dhi, &we, c, j);
+    sg->end = x;
+    sg->dlo = dlo;
+    sg->dhi = dhi;
+    sg->wrap_end = we;
+}
+
 /* in: the rows (read); back: where the rows go back with the walkers' guesses (in itself for
    gss_spec_device, only the rows guessed here; the device copy for gss_spec_records_device, every
    row).  heads: read only each row's start, step, k and pad (the walkers guess the rest) */
@@ -108,6 +269,7 @@ __global__ __launch_bounds__(64) void gss_spec_kernel(const gss_spec_in_t *in,
     __shared__ gss_spec_in_t s_in[SPEC_ROWS];
     __shared__ gss_spec_t s_out[SPEC_ROWS];
     __shared__ int s_guessed[SPEC_ROWS];
+    __shared__ spec_cc s_cc[SPEC_ROWS];                  /* a cycle cache per row */
     constexpr int WI = sizeof(gss_spec_in_t) / 8, WO = sizeof(gss_spec_t) / 16;
     const int lane = threadIdx.x, r = lane / GSS_SPEC_K, j = lane % GSS_SPEC_K;
     const int u0 = blockIdx.x * SPEC_ROWS;
@@ -120,6 +282,8 @@ __global__ __launch_bounds__(64) void gss_spec_kernel(const gss_spec_in_t *in,
     }
     for (int q = lane; q < SPEC_ROWS * WO; q += 64)      /* the walks zeroed */
         ((uint4 *)s_out)[q] = make_uint4(0, 0, 0, 0);
+    for (int q = lane; q < SPEC_ROWS * SCC_N; q += 64)   /* the caches empty */
+        s_cc[q / SCC_N].L[q % SCC_N] = 0;
     __syncthreads();
     const bool live = u0 + r < nrow;
     gss_spec_in_t row = s_in[r];
@@ -136,7 +300,7 @@ __global__ __launch_bounds__(64) void gss_spec_kernel(const gss_spec_in_t *in,
             s_in[r] = row;
     }
     if (live && j < row.k)
-        gss_spec_seg_walk(&row, j, n, &s_out[r]);
+        spec_seg_walk_shared(&row, j, n, &s_out[r], &s_cc[r]);
     __syncthreads();
     for (int q = lane; q < SPEC_ROWS * WO; q += 64) {    /* the walks out, 16 bytes a lane */
         const int rr = q / WO, w = q % WO;
