@@ -118,16 +118,31 @@ struct spec_cc {
 };
 
 /* an entry holding start w with at most nmax steps, the hint (the successor of the previous
-   cycle's entry) first; -1 if none */
-__device__ inline int scc_find(const spec_cc *c, double w, int64_t nmax, int prev)
+   cycle's entry) first; -1 if none.  The entry is copied out in the same reads that test it: a
+   lane on the other side of a divergent branch may overwrite the slot (its ring) before this
+   lane uses it */
+struct scc_entry {
+    double lo, hi, w0, v0;
+    int32_t L;
+};
+__device__ inline bool scc_take(const spec_cc *c, int i, double w, int64_t nmax, scc_entry *h)
+{
+    const int32_t L = c->L[i];
+    const double lo = c->lo[i], hi = c->hi[i], w0 = c->w0[i], v0 = c->v0[i];
+    if (!(L > 0 && w >= lo && w <= hi && L <= nmax))
+        return false;
+    *h = scc_entry{lo, hi, w0, v0, L};
+    return true;
+}
+__device__ inline int scc_find(const spec_cc *c, double w, int64_t nmax, int prev, scc_entry *h)
 {
     if (prev >= 0) {
         const int p = c->succ[prev];
-        if (p >= 0 && c->L[p] > 0 && w >= c->lo[p] && w <= c->hi[p] && c->L[p] <= nmax)
+        if (p >= 0 && scc_take(c, p, w, nmax, h))
             return p;
     }
     for (int i = 0; i < SCC_N; i++)
-        if (c->L[i] > 0 && w >= c->lo[i] && w <= c->hi[i] && c->L[i] <= nmax)
+        if (scc_take(c, i, w, nmax, h))
             return i;
     return -1;
 }
@@ -162,15 +177,16 @@ __device__ double spec_walk_margins_shared(double x, double s, int64_t n, double
     const double dunit = gss_pow2(-53);
     while (left > 0) {
         const double w = x;
-        const int e = scc_find(c, w, left, prev);
+        scc_entry h;
+        const int e = scc_find(c, w, left, prev, &h);
         if (prev >= 0 && e >= 0)
             c->succ[prev] = e;
         if (e >= 0) {
-            const double lo = c->lo[e] - w, hi = c->hi[e] - w;
+            const double lo = h.lo - w, hi = h.hi - w;
             if (lo > *dlo) *dlo = lo;
             if (hi < *dhi) *dhi = hi;
-            x = c->v0[e] + (w - c->w0[e]);
-            left -= c->L[e];
+            x = h.v0 + (w - h.w0);
+            left -= h.L;
             prev = e;
             if (s > 0.0) {
                 last = 1;
