@@ -321,31 +321,52 @@ GSS_PF int near_boundary(i128 v, i128 d, int lgB)
     return (i128)(((uint64_t)v + (uint64_t)d) & (B - 1)) < 2 * d;
 }
 
-/* 1 if certified (lin filled), 0 if this channel needs the exact path.  an (NULL: none): the
-   chain's exact carrier values inside the block (gss_carr_anchor_t), where the carrier walks to
-   the ambiguous samples start instead of at the block start; or, without them, sin / sspec (NULL:
+/* ---- one channel's proof in three parts ----------------------------------------------------
+ * lin_carrier  the carrier line, its ambiguous samples and the exact LUT cell at each of them
+ *              (exact walks from the chain's anchors where the reference may differ from it);
+ * lin_code     the code line, its ambiguous samples and the exact chip at each, the code wraps'
+ *              data bits and the signed-gain schedule;
+ * lin_patches  sample 0 and every ambiguous sample of either line in ascending order: the exact
+ *              term against the kernel's, a patch where they differ.
+ * The first two are independent: the GPU proves them on two lanes at once (gss_proof.hip), the
+ * host in order (lin_channel).  A failing channel's row is reset to its initial state
+ * (lin_row_reset) on both, so the rows match byte for byte whichever part failed first. */
+typedef struct gss_pf_side {          /* one line's ambiguous samples and the exact values there */
+    int32_t n;                        /* their number                                         */
+    int32_t q[LIN_MAXHIT];            /* samples, ascending                                  */
+    int32_t v[LIN_MAXHIT];            /* the exact LUT cell (carrier) or chip (code) there    */
+} gss_pf_side;
+
+GSS_PF void lin_row_reset(gss_lin_t *l)
+{
+    memset(l, 0, sizeof *l);
+    for (int i = 0; i < GSS_NGC; i++)
+        l->gpos[i] = INT32_MAX;
+    for (int i = 0; i < GSS_NPATCH; i++)
+        l->ppos[i] = INT32_MAX;
+}
+
+/* the carrier part (1: done, 0: the channel needs the exact path).  an (NULL: none): the chain's
+   exact carrier values inside the block (gss_carr_anchor_t), where the carrier walks to the
+   ambiguous samples start instead of at the block start; or, without them, sin / sspec (NULL:
    none): the row's speculative walk, from which the anchors are made the first time a walk is
    needed (gss_spec_anchors; gss_run's GPU proofs over the walks it keeps on the device).  The
    rows are the same either way. */
-GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, const uint32_t *ca,
-                       const int32_t *lcos, const int32_t *lsin, const gss_carr_anchor_t *an,
-                       const gss_spec_in_t *sin, const gss_spec_t *sspec, gss_lin_t *lin)
+GSS_PF int lin_carrier(const gss_chan_blk_t *p, int n, const gss_carr_anchor_t *an,
+                       const gss_spec_in_t *sin, const gss_spec_t *sspec, gss_pf_side *cx,
+                       gss_lin_t *lin)
 {
     gss_carr_anchor_t la;
     int inexact = 0;
-    int32_t hx[LIN_MAXHIT], hz[LIN_MAXHIT];
-    gss_pf_code at_hz[LIN_MAXHIT];
-
-    /* ---- the two lines and the samples where they decide nothing (gpssim.c:2212-2250) ---- */
-    const double x0 = p->carr0, s = p->carr_step;
-    if (!(x0 >= 0.0 && x0 < 1.0) || !(s > -0.5 && s < 0.5) || n <= 0 || n > INT32_MAX / 2)
+    cx->n = 0;
+    /* ---- the line and the samples where it decides nothing (gpssim.c:2245-2250) ---- */
+    const double x0 = p->carr0, s = p->carr_step, cs = p->code_step;
+    if (!(x0 >= 0.0 && x0 < 1.0) || !(s > -0.5 && s < 0.5) || n <= 0 || n > INT32_MAX / 2 ||
+        !(cs > 0.0 && cs < 1.0))
         return 0;
     const i128 X0 = to_fix(x0, 64, &inexact), XS = to_fix(s, 64, &inexact);
     const i128 DX1 = 2 + (i128)n * (LIN_CARR_ERR + 1);           /* line vs reference */
-    const double c0 = p->code0, cs = p->code_step;
-    if (!(c0 >= 0.0 && c0 < GSS_CA_SEQ_LEN_D) || !(cs > 0.0 && cs < 1.0))
-        return 0;
-    const int64_t ZS = (int64_t)to_fix(cs, 50, &inexact);
+    const int64_t ZS = (int64_t)to_fix(cs, 50, &inexact);       /* (the kernel's deviation) */
     /* An exact chain: the integer-carrier variant's rows (--carrier=int, gpssim.c:2252) are
        multiples of 2^-25 cycle, so every IEEE step and wrap of the reference is exact and the
        line IS the reference.  The kernel then rounds nothing either (xs is a multiple of 2^39,
@@ -356,9 +377,60 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
     (void)to_fix(s, 25, &ix);
     const int exact_carr = !ix && GSS_LIN_KDEV_CARR((uint64_t)ZS) < ((uint64_t)1 << 39);
     const int nhx = exact_carr ? 0 : ambiguous(X0, XS, DX1 + GSS_LIN_KDEV_CARR((uint64_t)ZS),
-                                               LIN_CARR_LGB, n, hx, LIN_MAXHIT);
+                                               LIN_CARR_LGB, n, cx->q, LIN_MAXHIT);
     if (nhx < 0)
         return 0;
+    lin->x0 = (uint64_t)X0;
+    lin->xs = (uint64_t)XS;
+    /* ---- the exact cell at each: the line's where it is farther than DX1 from a cell boundary
+       (the reference lies within DX1 of it), else an exact walk from the last anchor or the
+       last walk before it ---- */
+    double x = x0;
+    int64_t xat = 0;
+    for (int i = 0; i < nhx; i++) {
+        const int64_t q = cx->q[i];
+        int cell;
+        if (near_boundary(X0 + (i128)q * XS, DX1, LIN_CARR_LGB)) {
+            if (!an && sin && sspec && sin->s == s) {  /* the anchors, once, from the walk */
+                gss_spec_anchors(x0, n, sin, sspec, la.pos, la.val);
+                an = &la;
+            }
+            if (an)                                  /* from the last anchor past the walk */
+                for (int a = GSS_SPEC_K - 1; a >= 1; a--)
+                    if (an->pos[a] > xat && an->pos[a] <= q) {
+                        x = an->val[a];
+                        xat = an->pos[a];
+                        break;
+                    }
+            x = gss_carr_walk_cc(x, s, q - xat);     /* the reference may differ from the line */
+            xat = q;
+            cell = (int)floor(x * 512.0);
+            if (cell > 511)      /* carr += 1.0 rounded to 1.0: the reference reads cosTable512[512]
+                                    (SURVEY A.7); the exact path renders it (DESIGN 4.2) */
+                return 0;
+        } else {                                 /* proven: exact = line */
+            cell = (int)((uint64_t)(X0 + (i128)q * XS) >> LIN_CARR_LGB);
+        }
+        cx->v[i] = cell;
+    }
+    cx->n = nhx;
+    (void)inexact;
+    return 1;
+}
+
+/* the code part (1: done, 0: the exact path) */
+GSS_PF int lin_code(const gss_chan_blk_t *p, int n, const uint32_t *nav, gss_pf_side *cz,
+                    gss_lin_t *lin)
+{
+    int inexact = 0;
+    int32_t wr_hz[LIN_MAXHIT];                       /* code wraps at each ambiguous sample */
+    const int32_t *hz = cz->q;
+    cz->n = 0;
+    const double c0 = p->code0, cs = p->code_step;
+    if (n <= 0 || n > INT32_MAX / 2 || !(c0 >= 0.0 && c0 < GSS_CA_SEQ_LEN_D) ||
+        !(cs > 0.0 && cs < 1.0))
+        return 0;
+    const int64_t ZS = (int64_t)to_fix(cs, 50, &inexact);
     if (p->iword < 0 || p->iword >= GSS_NAV_WORDS || p->ibit < 0 || p->ibit >= 30 ||
         p->icode < 0 || p->icode >= 20)
         return 0;
@@ -371,11 +443,10 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
         !gss_lin_win16_ok((uint64_t)ZS, n))
         return 0;
     const i128 DZ1 = 2 + (i128)n * (LIN_CODE_ERR + 1);            /* line vs reference */
-    const int nhz = ambiguous(Z0, ZS, DZ1 + GSS_LIN_KDEV_CODE, LIN_CODE_LGB, n, hz, LIN_MAXHIT);
+    const int nhz = ambiguous(Z0, ZS, DZ1 + GSS_LIN_KDEV_CODE, LIN_CODE_LGB, n, cz->q,
+                              LIN_MAXHIT);
     if (nhz < 0)
         return 0;
-    lin->x0 = (uint64_t)X0;
-    lin->xs = (uint64_t)XS;
     lin->z0 = (uint64_t)Z0;
     lin->zs = (uint64_t)ZS;
 
@@ -391,13 +462,13 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
         if (near_boundary(zq, DZ1, LIN_CODE_LGB)) {
             gss_code_walk_cc(&st, cs, hz[i] - at);
             at = hz[i];
-            at_hz[i].chip = (int32_t)floor(st.ph);
-            at_hz[i].wraps = (int32_t)wraps_of(&st, p);
+            cz->v[i] = (int32_t)floor(st.ph);
+            wr_hz[i] = (int32_t)wraps_of(&st, p);
         } else {
             /* the line's chip and wraps (from chip 0 of the block) */
             const int64_t chips = (int64_t)(zq >> LIN_CODE_LGB);
-            at_hz[i].chip = (int32_t)(chips % GSS_CA_LEN);
-            at_hz[i].wraps = (int32_t)(chips / GSS_CA_LEN);
+            cz->v[i] = (int32_t)(chips % GSS_CA_LEN);
+            wr_hz[i] = (int32_t)(chips / GSS_CA_LEN);
         }
     }
 
@@ -418,9 +489,9 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
         if (q - 1 >= n)
             break;
         int j = find_hit(hz, nhz, q - 1);
-        if (j >= 0 && at_hz[j].wraps >= k)
+        if (j >= 0 && wr_hz[j] >= k)
             q--;                                 /* the exact value wrapped one sample earlier */
-        else if ((j = find_hit(hz, nhz, q)) >= 0 && at_hz[j].wraps < k)
+        else if ((j = find_hit(hz, nhz, q)) >= 0 && wr_hz[j] < k)
             q++;                                 /* ... or one sample later */
         if (q >= n)
             break;
@@ -443,42 +514,38 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
         lin->gpos[i] = INT32_MAX;
         lin->gval[i] = g;
     }
+    cz->n = nhz;
+    (void)inexact;
+    return 1;
+}
 
-    /* ---- patches: the exact term where the kernel's differs, at sample 0 and every ambiguous
-       sample of either line, in ascending order (the two lists merged as they are read) ---- */
-    double x = x0;
-    int64_t xat = 0;
+/* the patches, after both parts: the exact term where the kernel's differs, at sample 0 and
+   every ambiguous sample of either line in ascending order (the two lists merged as read) */
+GSS_PF int lin_patches(const gss_chan_blk_t *p, int n, const uint32_t *ca, const int32_t *lcos,
+                       const int32_t *lsin, const gss_pf_side *cx, const gss_pf_side *cz,
+                       gss_lin_t *lin)
+{
+    int inexact = 0;
+    const double x0 = p->carr0, c0 = p->code0;
+    const i128 X0 = to_fix(x0, 64, &inexact), XS = to_fix(p->carr_step, 64, &inexact);
+    const int64_t Z0 = (int64_t)to_fix(c0, 50, &inexact);
+    const int64_t ZS = (int64_t)to_fix(p->code_step, 50, &inexact);
+    const int nhx = cx->n, nhz = cz->n;
     int np = 0, gi = 0;
     int hxi = 0, hzi = 0;
+    (void)n;
     for (int64_t q = 0; q >= 0;) {
         int cell, chip;
-        if (q == 0) {
+        if (q == 0)
             cell = (int)floor(x0 * 512.0);
-        } else if (near_boundary(X0 + (i128)q * XS, DX1, LIN_CARR_LGB)) {
-            if (!an && sin && sspec && sin->s == s) {  /* the anchors, once, from the walk */
-                gss_spec_anchors(x0, n, sin, sspec, la.pos, la.val);
-                an = &la;
-            }
-            if (an)                                  /* from the last anchor past the walk */
-                for (int a = GSS_SPEC_K - 1; a >= 1; a--)
-                    if (an->pos[a] > xat && an->pos[a] <= q) {
-                        x = an->val[a];
-                        xat = an->pos[a];
-                        break;
-                    }
-            x = gss_carr_walk_cc(x, s, q - xat);     /* the reference may differ from the line */
-            xat = q;
-            cell = (int)floor(x * 512.0);
-            if (cell > 511)      /* carr += 1.0 rounded to 1.0: the reference reads cosTable512[512]
-                                    (SURVEY A.7); the exact path renders it (DESIGN 4.2) */
-                return 0;
-        } else {                                 /* proven: exact = line */
+        else if (hxi < nhx && cx->q[hxi] == q)       /* (hxi: the first carrier hit not below q) */
+            cell = cx->v[hxi];
+        else
             cell = (int)((uint64_t)(X0 + (i128)q * XS) >> LIN_CARR_LGB);
-        }
         if (q == 0)
             chip = (int)floor(c0);
-        else if (hzi < nhz && hz[hzi] == q)            /* (hzi: the first code hit not below q) */
-            chip = at_hz[hzi].chip;
+        else if (hzi < nhz && cz->q[hzi] == q)
+            chip = cz->v[hzi];
         else
             chip = (int)((uint64_t)((Z0 + (i128)q * ZS) >> LIN_CODE_LGB) % GSS_CA_LEN);
         const gss_lin_kc kk = gss_lin_kernel_at((uint64_t)X0, (uint64_t)XS, (uint64_t)Z0,
@@ -495,14 +562,29 @@ GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, cons
             lin->pdelta[np++] = (int64_t)lin->gval[gi] * (te - tk);
         }
         /* the next sample of the merged lists past q (-1: none) */
-        while (hxi < nhx && hx[hxi] <= q)
+        while (hxi < nhx && cx->q[hxi] <= q)
             hxi++;
-        while (hzi < nhz && hz[hzi] <= q)
+        while (hzi < nhz && cz->q[hzi] <= q)
             hzi++;
-        q = hxi < nhx ? (hzi < nhz && hz[hzi] < hx[hxi] ? hz[hzi] : hx[hxi]) : hzi < nhz ? hz[hzi] : -1;
+        q = hxi < nhx ? (hzi < nhz && cz->q[hzi] < cx->q[hxi] ? cz->q[hzi] : cx->q[hxi])
+                      : hzi < nhz ? cz->q[hzi] : -1;
     }
     (void)inexact;
     return 1;
+}
+
+/* 1 if certified (lin filled), 0 if this channel needs the exact path (lin reset): the three
+   parts in order (lin_carrier's anchors: as there) */
+GSS_PF int lin_channel(const gss_chan_blk_t *p, int n, const uint32_t *nav, const uint32_t *ca,
+                       const int32_t *lcos, const int32_t *lsin, const gss_carr_anchor_t *an,
+                       const gss_spec_in_t *sin, const gss_spec_t *sspec, gss_lin_t *lin)
+{
+    gss_pf_side cx, cz;
+    const int ok = lin_carrier(p, n, an, sin, sspec, &cx, lin) && lin_code(p, n, nav, &cz, lin) &&
+                   lin_patches(p, n, ca, lcos, lsin, &cx, &cz, lin);
+    if (!ok)
+        lin_row_reset(lin);
+    return ok;
 }
 
 

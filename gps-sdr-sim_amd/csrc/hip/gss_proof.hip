@@ -47,19 +47,18 @@ const proof_lut &host_lut()
    "(anonymous namespace)::..." for the others) */
 __device__ static void lin_row_init(gss_lin_t *l)
 {
-    memset(l, 0, sizeof *l);
-    for (int i = 0; i < GSS_NGC; i++)
-        l->gpos[i] = INT32_MAX;
-    for (int i = 0; i < GSS_NPATCH; i++)
-        l->ppos[i] = INT32_MAX;
+    lin_row_reset(l);
 }
 
-/* One block per workgroup; STRIDE threads per channel slot, of which the first proves it.  A
-   lane's proof is a long dependent chain (descents, exact walks: latency, not throughput), and a
-   wave lasts as long as the union of its lanes' paths, so a small launch spreads the channels
-   over waves (STRIDE 64: one channel per wave, 16 waves per block) and lets the SIMDs interleave
-   them; a large one fills the chip anyway and keeps the 16 channels of a block in one wave
-   (proof_stride; profiles/round5/proof/README.md). */
+/* One block per workgroup; STRIDE (>= 2) threads per channel slot.  A lane's proof is a long
+   dependent chain (descents, exact walks: latency, not throughput), so a channel's two
+   independent parts run on two threads of its slot (gss_proof.h): thread 0 the carrier line
+   (lin_carrier: its descents and the exact walks from the anchors), thread 1 the code line and
+   the gain schedule (lin_code); after a barrier thread 0 merges them into the patches
+   (lin_patches).  A wave lasts as long as the union of its lanes' paths, so a small launch
+   spreads the channels over waves (STRIDE 64: one channel per wave, 16 waves per block) and lets
+   the SIMDs interleave them; a large one fills the chip anyway and keeps the 16 channels of a
+   block in one wave (proof_stride; profiles/round5/proof/README.md). */
 template <int STRIDE>
 __global__ __launch_bounds__(GSS_MAXCH * STRIDE) void gss_proof_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch, int nblk,
@@ -68,39 +67,57 @@ __global__ __launch_bounds__(GSS_MAXCH * STRIDE) void gss_proof_kernel(
     const gss_spec_in_t *__restrict__ sin, const gss_spec_t *__restrict__ sspec,
     gss_lin_t *__restrict__ lin, int32_t *__restrict__ fast, int64_t first, int force_exact)
 {
+    static_assert(STRIDE >= 2, "two threads per channel slot");
     __shared__ int32_t lcos[512], lsin[512];
     __shared__ int fail_k[GSS_MAXCH];
     __shared__ int gabs[GSS_MAXCH];
+    __shared__ int part_ok[GSS_MAXCH][2];
+    __shared__ gss_pf_side s_cz[GSS_MAXCH];              /* the code parts, for thread 0 */
+    gss_pf_side cx;                                      /* thread 0's carrier part */
     for (int i = threadIdx.x; i < 512; i += blockDim.x) {
         lcos[i] = lut.c[i];
         lsin[i] = lut.s[i];
     }
-    __syncthreads();
-    const int k = threadIdx.x / STRIDE, b = blockIdx.x;
-    const bool lead = threadIdx.x % STRIDE == 0;
-    int failed = 0, g = 0;
+    const int k = threadIdx.x / STRIDE, role = threadIdx.x % STRIDE, b = blockIdx.x;
+    const bool lead = role == 0;
     gss_lin_t *l = lin + (size_t)b * GSS_MAXCH + k;
-    int nc = 0;
-    if (lead && b < nblk) {
+    const int nc = b < nblk ? nch[b] : 0;
+    const bool live = b < nblk && nc >= 0 && nc <= GSS_MAXCH && k < nc;
+    const gss_chan_blk_t *p = blk + (size_t)b * GSS_MAXCH + k;
+    const bool tables_ok = live && p->nav_tbl >= 0 && p->nav_tbl < n_nav && p->ca_tbl >= 0 &&
+                           p->ca_tbl < n_ca;
+    if (lead && b < nblk)
         lin_row_init(l);
-        nc = nch[b];
+    __syncthreads();                                      /* (the row reset before both parts) */
+    if (role < 2) {
+        int ok = 0;
+        if (tables_ok) {
+            if (role == 0)
+                ok = lin_carrier(p, n_per_blk, anch ? anch + (size_t)b * GSS_MAXCH + k : nullptr,
+                                 sin ? sin + (size_t)b * GSS_MAXCH + k : nullptr,
+                                 sspec ? sspec + (size_t)b * GSS_MAXCH + k : nullptr,
+                                 &cx, l);
+            else
+                ok = lin_code(p, n_per_blk, nav + (size_t)p->nav_tbl * GSS_NAV_WORDS,
+                              &s_cz[k], l);
+        }
+        part_ok[k][role] = ok;
+    }
+    __syncthreads();                                      /* both parts' sides and row fields */
+    int failed = 0, g = 0;
+    if (lead && b < nblk) {
         if (nc < 0 || nc > GSS_MAXCH) {
             failed = k == 0;                            /* the block fails before any channel */
         } else if (k < nc) {
-            const gss_chan_blk_t *p = blk + (size_t)b * GSS_MAXCH + k;
             g = p->gain < 0 ? -p->gain : p->gain;
-            if (p->nav_tbl < 0 || p->nav_tbl >= n_nav || p->ca_tbl < 0 || p->ca_tbl >= n_ca) {
-                failed = 1;
-            } else {
-                int ok = lin_channel(p, n_per_blk, nav + (size_t)p->nav_tbl * GSS_NAV_WORDS,
-                                     ca + (size_t)p->ca_tbl * GSS_CA_WORDS, lcos, lsin,
-                                     anch ? anch + (size_t)b * GSS_MAXCH + k : nullptr,
-                                     sin ? sin + (size_t)b * GSS_MAXCH + k : nullptr,
-                                     sspec ? sspec + (size_t)b * GSS_MAXCH + k : nullptr, l);
-                if (p->gain > 1024 || p->gain < -1024)
-                    ok = 0;
-                failed = !ok;
-            }
+            int ok = tables_ok && part_ok[k][0] && part_ok[k][1] &&
+                     lin_patches(p, n_per_blk, ca + (size_t)p->ca_tbl * GSS_CA_WORDS, lcos, lsin,
+                                 &cx, &s_cz[k], l);
+            if (!ok)
+                lin_row_reset(l);                       /* as lin_channel on the host */
+            if (p->gain > 1024 || p->gain < -1024)
+                ok = 0;
+            failed = !ok;
         }
     }
     if (lead) {
@@ -110,12 +127,12 @@ __global__ __launch_bounds__(GSS_MAXCH * STRIDE) void gss_proof_kernel(
     __syncthreads();
     /* the block's first failing channel and its gain sum (the host's loop order) */
     int kf = GSS_MAXCH, gsum = 0;
-    for (int j = 0; j < GSS_MAXCH; j++) {
-        const int f = fail_k[j];
+    for (int jj = 0; jj < GSS_MAXCH; jj++) {
+        const int f = fail_k[jj];
         kf = f < kf ? f : kf;
     }
-    for (int j = 0; j < GSS_MAXCH && j <= kf; j++)
-        gsum += gabs[j];
+    for (int jj = 0; jj < GSS_MAXCH && jj <= kf; jj++)
+        gsum += gabs[jj];
     if (lead && b < nblk) {
         if (k > kf)
             lin_row_init(l);                            /* the host never reached this channel */
@@ -130,18 +147,18 @@ __global__ __launch_bounds__(GSS_MAXCH * STRIDE) void gss_proof_kernel(
 
 /* threads per channel slot for a launch of nblk blocks: the widest spread whose waves (nblk
    STRIDE / 4) the chip still holds about at once (256 CUs x 4 SIMDs x 4-8 waves of this kernel);
-   GSS_PROOF_STRIDE = 1, 16, 32 or 64 forces one (measurements, tests) */
+   GSS_PROOF_STRIDE = 2, 16, 32 or 64 forces one (measurements, tests) */
 static int proof_stride(int nblk)
 {
     const char *e = getenv("GSS_PROOF_STRIDE");        /* (read per launch: tests switch it) */
     const int forced = e ? atoi(e) : 0;
-    if (forced == 1 || forced == 16 || forced == 32 || forced == 64)
+    if (forced == 2 || forced == 16 || forced == 32 || forced == 64)
         return forced;
     const long waves_cap = 8192;
     for (int s = 64; s >= 16; s /= 2)
         if ((long)nblk * s / 4 <= waves_cap)
             return s;
-    return 1;
+    return 2;
 }
 
 /* gss_run's launch (force_exact: its test hook; sin / sspec: the batch's walks on the device,
@@ -162,7 +179,7 @@ int run_proof_launch(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, in
     case 64: PF_LAUNCH(64); break;
     case 32: PF_LAUNCH(32); break;
     case 16: PF_LAUNCH(16); break;
-    default: PF_LAUNCH(1); break;
+    default: PF_LAUNCH(2); break;
     }
 #undef PF_LAUNCH
     return hipGetLastError() == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "proof kernel launch");
