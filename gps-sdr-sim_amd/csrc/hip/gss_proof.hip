@@ -50,36 +50,39 @@ __device__ static void lin_row_init(gss_lin_t *l)
     lin_row_reset(l);
 }
 
-/* One block per workgroup; STRIDE (>= 2) threads per channel slot.  A lane's proof is a long
-   dependent chain (descents, exact walks: latency, not throughput), so a channel's two
-   independent parts run on two threads of its slot (gss_proof.h): thread 0 the carrier line
-   (lin_carrier: its descents and the exact walks from the anchors), thread 1 the code line and
-   the gain schedule (lin_code); after a barrier thread 0 merges them into the patches
-   (lin_patches).  A wave lasts as long as the union of its lanes' paths, so a small launch
-   spreads the channels over waves (STRIDE 64: one channel per wave, 16 waves per block) and lets
-   the SIMDs interleave them; a large one fills the chip anyway and keeps the 16 channels of a
-   block in one wave (proof_stride; profiles/round5/proof/README.md). */
+/* One block per workgroup, as two halves of 16 * STRIDE threads: the first half proves the
+   channels' carrier lines (lin_carrier: its descents and the exact walks from the anchors), the
+   second their code lines and gain schedules (lin_code), thread STRIDE k of a half for channel
+   k; after a barrier the first half merges the two into the patches (lin_patches).  A lane's
+   proof is a long dependent chain (descents, exact walks: latency, not throughput: VALU issue
+   0.22), so the two independent parts run on different waves at the same time (on one wave
+   they would diverge and run one after the other).  A small launch spreads a half over more
+   waves (STRIDE 16 / 32: 4 / 8 waves of a few live lanes) so that the SIMDs interleave them; a
+   large one (STRIDE 4) still gives each half one wave per block (proof_stride). */
 template <int STRIDE>
-__global__ __launch_bounds__(GSS_MAXCH * STRIDE) void gss_proof_kernel(
+__global__ __launch_bounds__(2 * GSS_MAXCH * STRIDE) void gss_proof_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch, int nblk,
     int n_per_blk, const uint32_t *__restrict__ ca, int n_ca, const uint32_t *__restrict__ nav,
     int n_nav, proof_lut lut, const gss_carr_anchor_t *__restrict__ anch,
     const gss_spec_in_t *__restrict__ sin, const gss_spec_t *__restrict__ sspec,
     gss_lin_t *__restrict__ lin, int32_t *__restrict__ fast, int64_t first, int force_exact)
 {
-    static_assert(STRIDE >= 2, "two threads per channel slot");
+    static_assert(GSS_MAXCH * STRIDE % 64 == 0, "each half whole waves");
+    constexpr int HALF = GSS_MAXCH * STRIDE;
     __shared__ int32_t lcos[512], lsin[512];
     __shared__ int fail_k[GSS_MAXCH];
     __shared__ int gabs[GSS_MAXCH];
     __shared__ int part_ok[GSS_MAXCH][2];
-    __shared__ gss_pf_side s_cz[GSS_MAXCH];              /* the code parts, for thread 0 */
-    gss_pf_side cx;                                      /* thread 0's carrier part */
+    __shared__ gss_pf_side s_cz[GSS_MAXCH];              /* the code parts, for the first half */
+    gss_pf_side cx;                                      /* a first-half thread's carrier part */
     for (int i = threadIdx.x; i < 512; i += blockDim.x) {
         lcos[i] = lut.c[i];
         lsin[i] = lut.s[i];
     }
-    const int k = threadIdx.x / STRIDE, role = threadIdx.x % STRIDE, b = blockIdx.x;
-    const bool lead = role == 0;
+    const int role = threadIdx.x / HALF, t = threadIdx.x % HALF, b = blockIdx.x;
+    const int k = t / STRIDE;
+    const bool slot = t % STRIDE == 0;                   /* the thread of channel slot k */
+    const bool lead = role == 0 && slot;
     gss_lin_t *l = lin + (size_t)b * GSS_MAXCH + k;
     const int nc = b < nblk ? nch[b] : 0;
     const bool live = b < nblk && nc >= 0 && nc <= GSS_MAXCH && k < nc;
@@ -89,17 +92,16 @@ __global__ __launch_bounds__(GSS_MAXCH * STRIDE) void gss_proof_kernel(
     if (lead && b < nblk)
         lin_row_init(l);
     __syncthreads();                                      /* (the row reset before both parts) */
-    if (role < 2) {
+    if (slot) {
         int ok = 0;
         if (tables_ok) {
             if (role == 0)
                 ok = lin_carrier(p, n_per_blk, anch ? anch + (size_t)b * GSS_MAXCH + k : nullptr,
                                  sin ? sin + (size_t)b * GSS_MAXCH + k : nullptr,
-                                 sspec ? sspec + (size_t)b * GSS_MAXCH + k : nullptr,
-                                 &cx, l);
+                                 sspec ? sspec + (size_t)b * GSS_MAXCH + k : nullptr, &cx, l);
             else
-                ok = lin_code(p, n_per_blk, nav + (size_t)p->nav_tbl * GSS_NAV_WORDS,
-                              &s_cz[k], l);
+                ok = lin_code(p, n_per_blk, nav + (size_t)p->nav_tbl * GSS_NAV_WORDS, &s_cz[k],
+                              l);
         }
         part_ok[k][role] = ok;
     }
@@ -145,20 +147,20 @@ __global__ __launch_bounds__(GSS_MAXCH * STRIDE) void gss_proof_kernel(
     }
 }
 
-/* threads per channel slot for a launch of nblk blocks: the widest spread whose waves (nblk
-   STRIDE / 4) the chip still holds about at once (256 CUs x 4 SIMDs x 4-8 waves of this kernel);
-   GSS_PROOF_STRIDE = 2, 16, 32 or 64 forces one (measurements, tests) */
+/* threads per channel slot and half (waves: nblk STRIDE / 2) for a launch of nblk blocks: the
+   widest spread the chip still holds about at once (256 CUs x 4 SIMDs x 4-8 waves of this
+   kernel); GSS_PROOF_STRIDE = 4, 16 or 32 forces one (measurements, tests) */
 static int proof_stride(int nblk)
 {
     const char *e = getenv("GSS_PROOF_STRIDE");        /* (read per launch: tests switch it) */
     const int forced = e ? atoi(e) : 0;
-    if (forced == 2 || forced == 16 || forced == 32 || forced == 64)
+    if (forced == 4 || forced == 16 || forced == 32)
         return forced;
     const long waves_cap = 8192;
-    for (int s = 64; s >= 16; s /= 2)
-        if ((long)nblk * s / 4 <= waves_cap)
+    for (int s = 32; s >= 16; s /= 2)
+        if ((long)nblk * s / 2 <= waves_cap)
             return s;
-    return 2;
+    return 4;
 }
 
 /* gss_run's launch (force_exact: its test hook; sin / sspec: the batch's walks on the device,
@@ -172,14 +174,14 @@ int run_proof_launch(const gss_chan_blk_t *blk, const int32_t *nch, int nblk, in
     if (nblk <= 0)
         return 0;
 #define PF_LAUNCH(S)                                                                             \
-    hipLaunchKernelGGL(gss_proof_kernel<S>, dim3((unsigned)nblk), dim3(GSS_MAXCH * (S)), 0, st,  \
+    hipLaunchKernelGGL(gss_proof_kernel<S>, dim3((unsigned)nblk), dim3(2 * GSS_MAXCH * (S)), 0, \
+                       st,                                                                      \
                        blk, nch, nblk, n_per_blk, ca_bits, n_ca, nav, n_nav, host_lut(), anch,  \
                        sin, sspec, lin, fast, first, force_exact)
     switch (proof_stride(nblk)) {
-    case 64: PF_LAUNCH(64); break;
     case 32: PF_LAUNCH(32); break;
     case 16: PF_LAUNCH(16); break;
-    default: PF_LAUNCH(2); break;
+    default: PF_LAUNCH(4); break;
     }
 #undef PF_LAUNCH
     return hipGetLastError() == hipSuccess ? 0 : gss_fail(GSS_E_HIP, "proof kernel launch");

@@ -506,47 +506,12 @@ def test_producers_on_device(dev, golden):
         assert np.array_equal(rows.cpu().numpy().view(np.uint32), want), kw
 
 
-def _seg_nested(got, want, where):
-    """a GPU segment walk against the host's: the same end and wrap (exact values), and the
-    admissible start translations [dlo, dhi] inside the host's (the GPU's row-shared cycle cache
-    keeps its entries' shrunk intervals: gss_producers.hip spec_walk_margins_shared)"""
-    assert got["end"] == want["end"] and got["wrap_end"] == want["wrap_end"], where
-    if want["dlo"] <= want["dhi"]:
-        assert want["dlo"] <= got["dlo"] <= 0.0 <= got["dhi"] <= want["dhi"], where
-    else:                                                # not walked: the same empty interval
-        assert got["dlo"] == want["dlo"] and got["dhi"] == want["dhi"], where
-
-
-def _seg_translations_brute(gi, spec, n, rows):
-    """every lattice translation at the ends of a segment's interval moves the brute-force end of
-    the segment by exactly that much (the intervals are sound, not only nested)"""
-    import oracle
-    checked = 0
-    for r in rows:
-        row = gi[r]
-        k = int(row["k"])
-        for j in range(1, k):
-            sg = spec[r]["seg"][j]
-            if not sg["dlo"] <= sg["dhi"]:
-                continue
-            unit = 2.0 ** -52 if row["s"] > 0 else 2.0 ** -53
-            stop = int(row["P"][j + 1]) if j + 1 < k else n
-            for d in (np.ceil(sg["dlo"] / unit) * unit, np.floor(sg["dhi"] / unit) * unit):
-                x = row["W"][j] + d
-                if 0.0 <= x < 1.0:
-                    assert oracle.carr_brute(x, row["s"], stop - int(row["P"][j])) == \
-                        sg["end"] + d, (r, j, d)
-                    checked += 1
-    return checked
-
-
 def test_spec_walks_on_device(dev):
     """The carrier chain run ahead: the GPU's speculative block walks
-    (gss_spec_device, a lane per segment, rows channel-major, a cycle cache shared by a row's
-    lanes) against the host's (gss_spec_host): the same first wraps, segment ends and wraps,
-    intervals nested in the host's and sound at their ends (brute force), and the chain from
-    them equals the exact chain (gss_carr_chain), for a static run across 30 s updates and the
-    circle.csv run; nearly every block takes the translation."""
+    (gss_spec_device, a lane per segment, rows channel-major) equal the host's (gss_spec_host)
+    field for field, and
+    the chain from them equals the exact chain (gss_carr_chain), for a static run across 30 s
+    updates and the circle.csv run; nearly every block takes the translation."""
     import torch
     for kw in (dict(llh=LOC, duration=400.0), dict(motion_file=CIRCLE, data_format=8)):
         s = G.Scenario(NAV, **kw)
@@ -565,10 +530,7 @@ def test_spec_walks_on_device(dev):
         assert np.array_equal(got["w1"][live], want["w1"][live]), kw
         for r in np.flatnonzero(live):
             k = gi.reshape(-1)["k"][r]
-            for j in range(k):
-                _seg_nested(got["seg"][r][j], want["seg"][r][j], (kw, r, j))
-        assert _seg_translations_brute(gi.reshape(-1), got, n,
-                                       np.flatnonzero(live)[::97]) > 10, kw
+            assert got["seg"][r][:k].tobytes() == want["seg"][r][:k].tobytes(), (kw, r)
         ref = blk.copy()
         end_ref, _ = G.carr_chain(carr, ref, nch, chain, n, with_ck=False)
         end, hit = G.carr_chain_spec(carr, blk, nch, chain, n, gi, got)
@@ -597,11 +559,9 @@ def test_spec_walks_on_device(dev):
 
 def test_spec_records_on_device(dev):
     """gss_spec_records_device (gss_run's default): the walks stay on the device and only each
-    row's 72-byte record comes back; against the host's (gss_spec_records over gss_spec_host's
-    walks) the same first wraps, ends and translation offsets, intervals nested in the host's
-    (the GPU walks' row-shared cycle cache), no record the host lacks, and the chain from them
-    (gss_carr_chain_records) equals the exact chain, for a static run across 30 s updates and
-    the circle.csv run."""
+    row's 72-byte record comes back; the records equal the host's (gss_spec_records over
+    gss_spec_host's walks) byte for byte, and the chain from them (gss_carr_chain_records) equals
+    the exact chain, for a static run across 30 s updates and the circle.csv run."""
     import torch
     for kw in (dict(llh=LOC, duration=400.0), dict(motion_file=CIRCLE, data_format=8)):
         s = G.Scenario(NAV, **kw)
@@ -623,18 +583,7 @@ def test_spec_records_on_device(dev):
         torch.cuda.synchronize()
         got = h_rec.numpy().view(G.SPEC_REC_DTYPE).reshape(g0.shape)
         live = g0["s"] != 0
-        g, w = got[live], want[live]
-        for f in ("w1", "p1"):
-            assert np.array_equal(g[f], w[f]), (kw, f)
-        assert ((g["ok"] & 3) & ~(w["ok"] & 3)).sum() == 0, kw          # no record the host lacks
-        for bit, lo, hi, dd in ((1, "slo", "shi", "sdd"), (2, "llo", "lhi", "ldd")):
-            both = ((g["ok"] & bit) != 0)
-            assert np.array_equal(g[dd][both], w[dd][both]), (kw, dd)
-            assert (g[lo][both] >= w[lo][both]).all() and (g[hi][both] <= w[hi][both]).all(), kw
-        sb = (g["ok"] & 1) != 0
-        assert np.array_equal(g["end"][sb], w["end"][sb]), kw
-        lk = (g["ok"] & 2) != 0
-        assert np.array_equal(g["ok"][lk] >> 2, w["ok"][lk] >> 2), kw     # link row distances
+        assert got[live].tobytes() == want[live].tobytes(), kw
         assert (got["ok"][live] & 2).sum() >= 0.9 * 2 * live.sum(), kw     # linked rows
         ref = blk.copy()
         end_ref, _ = G.carr_chain(carr, ref, nch, chain, n, with_ck=False)

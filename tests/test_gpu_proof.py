@@ -128,7 +128,7 @@ def test_proof_device_rejects_like_host(dev):
     assert not fast[[0, 1, 2, 3, 5]].any()
 
 
-@pytest.mark.parametrize("stride", ["2", "16", "32", "64"])
+@pytest.mark.parametrize("stride", ["4", "16", "32"])
 def test_proof_device_every_lane_stride(dev, stride, monkeypatch):
     """every launch shape of the proof kernel (threads per channel slot, proof_stride; forced
     here by GSS_PROOF_STRIDE, read per launch) gives the host's rows: rejections, ragged channel

@@ -1,7 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/s6d; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_proof.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread -k "spec or proof or streaming_run_mixed or cli" > $O/pytest.log 2>&1 || exit 1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_proof.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread -k "spec or proof or streaming_run_mixed or cli or linearize" > $O/pytest.log 2>&1 || exit 1
 BA="--steps 10 --warmup 3 --no-configs --no-e2e --no-pmc --no-cpu-baseline --no-exact --no-sustained"
 for v in cur nocc cur nocc; do
   lib=gps-sdr-sim_amd/lib/libgpssim_amd.so; [ $v = nocc ] && lib=_var/nocc/libgpssim_amd.so
