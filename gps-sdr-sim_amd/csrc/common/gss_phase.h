@@ -124,11 +124,25 @@ GSS_HD int64_t gss_jump(double v, double s, double W, double *D)
     if (lim < 0) return 0;
     *D = (s > 0.0 ? (double)K : -(double)K) * u;
 #if defined(__HIP_DEVICE_COMPILE__)
-    /* no 64-bit integer divider on the GPU: f64 quotient (lim, K < 2^53) then exact fix-up */
-    int64_t q = (int64_t)((double)lim / (double)K);
-    if (q * K > lim) q--;
-    else if ((q + 1) * K <= lim) q++;
-    return q + 1;
+    /* no 64-bit integer divider on the GPU: floor(lim / K) from the hardware reciprocal refined
+       by one Newton step (relative error ~2^-50: the estimate is off by at most a few), then
+       fixed up exactly in f64 -- lim, K < 2^53 and the residual lim - q K is an integer of
+       magnitude below 2^53, so one fma gives it exactly (no IEEE division sequence and no
+       64-bit integer multiplies on this hot path of every exact walk) */
+    const double Kd = (double)K, ld = (double)lim;
+    double r = __builtin_amdgcn_rcp(Kd);
+    r = __builtin_fma(__builtin_fma(-Kd, r, 1.0), r, r);
+    double q = __builtin_floor(ld * r);
+    double res = __builtin_fma(-q, Kd, ld);
+    while (res < 0.0) {
+        q -= 1.0;
+        res += Kd;
+    }
+    while (res >= Kd) {
+        q += 1.0;
+        res -= Kd;
+    }
+    return (int64_t)q + 1;
 #else
     return lim / K + 1;
 #endif
