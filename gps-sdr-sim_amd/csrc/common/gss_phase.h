@@ -1047,7 +1047,9 @@ GSS_HD double gss_carr_walk_cc(double x, double s, int64_t n)
  * and the serial chain. */
 #ifndef GSS_SPEC_T_DEFINED             /* = include/gpssim_amd.h */
 #define GSS_SPEC_T_DEFINED
+#ifndef GSS_SPEC_K
 #define GSS_SPEC_K 8                   /* segments per block */
+#endif
 typedef struct gss_spec_in {           /* a row's guesses (host, gss_carr_chain_guess)          */
     double g, s;                       /* start guess, carr_step (0: padding row)               */
     int32_t k, pad;                    /* segments (1..GSS_SPEC_K)                              */

@@ -434,8 +434,11 @@ struct Run {
 };
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
-static_assert(sizeof(gss_spec_in_t) <= 256 && 256 + sizeof(gss_spec_t) <= 1024,
-              "one row in and out fit the walks' 1024-byte warm-up scratch");
+/* the walks' warm-up scratch (one row): in, its device copy, the walk, the record */
+constexpr size_t WARM_IN = (sizeof(gss_spec_in_t) + 255) & ~(size_t)255;
+constexpr size_t WARM_SPEC = (sizeof(gss_spec_t) + 255) & ~(size_t)255;
+constexpr size_t WARM_BYTES = 2 * WARM_IN + WARM_SPEC + 128;
+static_assert(sizeof(gss_spec_rec_t) <= 128, "the record fits its warm-up slot");
 
 /* The carrier checkpoints feed only the exact path's Stage A, i.e. the blocks the proofs do not
    certify (none of the 2,999 of the bench run).  With the fast path the chain is therefore
@@ -1843,7 +1846,7 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
                      ? cu_mask_stream(&r.spec_st, spec_cus(), false)
                      : stream_get(&r.spec_st, true)) !=
                     hipSuccess ||
-                dev_alloc((void **)&r.spec_warm, 1024) != hipSuccess)
+                dev_alloc((void **)&r.spec_warm, WARM_BYTES) != hipSuccess)
                 err = gss_fail(GSS_E_HIP, "run carrier-chain stream");
             for (Run::SpecBatch &b : r.sb) {
                 if (err) break;
@@ -1969,15 +1972,17 @@ extern "C" int gss_run_ex(gss_dev *d, gss_scn *s, int64_t first_block, int64_t n
     if (r.spec) {
         /* the walks' first launch costs ~1 ms (the kernel's first use): here, on one zero row,
            while the planner produces its first rows, instead of inside its first batch */
-        (void)hipMemsetAsync(r.spec_warm, 0, 1024, r.spec_st);
-        (void)gss_spec_device(d, (gss_spec_in_t *)r.spec_warm, 1, info.n_per_blk,
-                              (gss_spec_t *)((uint8_t *)r.spec_warm + 256), r.spec_st);
+        uint8_t *w = (uint8_t *)r.spec_warm;
+        (void)hipMemsetAsync(r.spec_warm, 0, WARM_BYTES, r.spec_st);
+        (void)gss_spec_device(d, (gss_spec_in_t *)w, 1, info.n_per_blk,
+                              (gss_spec_t *)(w + 2 * WARM_IN), r.spec_st);
         if (r.rec) {
-            uint8_t *w = (uint8_t *)r.spec_warm;
-            (void)hipMemsetAsync(r.spec_warm, 0, 1024, r.spec_st);
+            (void)hipMemsetAsync(r.spec_warm, 0, WARM_BYTES, r.spec_st);
             (void)gss_spec_records_device(d, (gss_spec_in_t *)w, 1, info.n_per_blk,
-                                          (gss_spec_in_t *)(w + 256), (gss_spec_t *)(w + 512),
-                                          (gss_spec_rec_t *)(w + 800), r.spec_st);
+                                          (gss_spec_in_t *)(w + WARM_IN),
+                                          (gss_spec_t *)(w + 2 * WARM_IN),
+                                          (gss_spec_rec_t *)(w + 2 * WARM_IN + WARM_SPEC),
+                                          r.spec_st);
         }
     }
     err = run_main(d, r, info.n_per_blk, info.data_format, bb, sink, user, st, cp, d_ca);

@@ -1331,7 +1331,8 @@ extern "C" int gss_dev_ordinal(const gss_dev *d) { return d->ordinal; }
 
 extern "C" const char *gss_build_info(void)
 {
-    return "lin_mfma=2 lin_ch=" GSS_STR(LIN_CH) " lin_swin=3 arch=gfx950";
+    return "lin_mfma=2 lin_ch=" GSS_STR(LIN_CH) " lin_swin=3 spec_k=" GSS_STR(GSS_SPEC_K)
+           " arch=gfx950";
 }
 
 

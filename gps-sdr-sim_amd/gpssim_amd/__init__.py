@@ -52,13 +52,25 @@ assert LIN_DTYPE.itemsize == 192
 CHAIN_DTYPE = np.dtype([("slot", "i1"), ("reset", "u1"), ("pad", "u1", (6,)), ("init", "<f8")])
 assert CHAIN_DTYPE.itemsize == 16
 # the carrier chain run ahead (gss_carr_chain_guess / gss_spec_* / gss_carr_chain_spec)
-SPEC_K = 8
+def _lib_spec_k():
+    """GSS_SPEC_K of the library to be loaded (its gss_build_info; 8 when it cannot be read:
+    the sizes below must match the library's, tests/test_abi.py checks them)"""
+    try:
+        L = C.CDLL(LIB_PATH)
+        L.gss_build_info.restype = C.c_char_p
+        kv = dict(x.split("=", 1) for x in L.gss_build_info().decode().split())
+        return int(kv.get("spec_k", "8"))
+    except (OSError, AttributeError, ValueError):
+        return 8
+
+
+SPEC_K = _lib_spec_k()              # speculative segments per block (GSS_SPEC_K, default 8)
 SPEC_IN_DTYPE = np.dtype([("g", "<f8"), ("s", "<f8"), ("k", "<i4"), ("pad", "<i4"),
                           ("P", "<i8", (SPEC_K,)), ("W", "<f8", (SPEC_K,))])
-assert SPEC_IN_DTYPE.itemsize == 152
+assert SPEC_IN_DTYPE.itemsize == 24 + 16 * SPEC_K
 SPEC_SEG_DTYPE = np.dtype([("end", "<f8"), ("dlo", "<f8"), ("dhi", "<f8"), ("wrap_end", "<i8")])
 SPEC_DTYPE = np.dtype([("p1", "<i8"), ("w1", "<f8"), ("seg", SPEC_SEG_DTYPE, (SPEC_K,))])
-assert SPEC_DTYPE.itemsize == 272
+assert SPEC_DTYPE.itemsize == 16 + 32 * SPEC_K
 SPEC_LINK_DTYPE = np.dtype([("lo", "<f8"), ("hi", "<f8"), ("dd", "<f8"), ("end", "<f8")])
 assert SPEC_LINK_DTYPE.itemsize == 32
 # gss_spec_rec_t: a row's speculative walk folded into one record (gss_spec_records*)
@@ -68,7 +80,7 @@ SPEC_REC_DTYPE = np.dtype([("w1", "<f8"), ("slo", "<f8"), ("shi", "<f8"), ("sdd"
 assert SPEC_REC_DTYPE.itemsize == 72
 # gss_carr_anchor_t: the chain's exact carrier values inside a block (the proofs' walk starts)
 ANCHOR_DTYPE = np.dtype([("pos", "<i4", (SPEC_K,)), ("val", "<f8", (SPEC_K,))])
-assert ANCHOR_DTYPE.itemsize == 96
+assert ANCHOR_DTYPE.itemsize == 12 * SPEC_K
 # gss_nav_src_t: one nav-table row's source for the GPU producer (include/gpssim_amd.h)
 NAV_SRC_DTYPE = np.dtype([("sbf", "<u4", (5, 10)), ("tow", "<u4"), ("wn", "<u4"), ("prev", "<i4"),
                           ("next", "<i4"), ("head", "<u4", (10,))])

@@ -313,7 +313,9 @@ int gss_carr_chain(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
                            translation applies); *n_hit counts the blocks where it did.        */
 #ifndef GSS_SPEC_T_DEFINED
 #define GSS_SPEC_T_DEFINED
+#ifndef GSS_SPEC_K
 #define GSS_SPEC_K 8                   /* segments per block */
+#endif
 typedef struct gss_spec_in {           /* a row's guesses (host, gss_carr_chain_guess)          */
     double g, s;                       /* start guess, carr_step (0: padding row)               */
     int32_t k, pad;                    /* segments (1..GSS_SPEC_K; 0: not guessed yet)          */
