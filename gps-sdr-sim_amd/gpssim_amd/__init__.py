@@ -52,19 +52,10 @@ assert LIN_DTYPE.itemsize == 192
 CHAIN_DTYPE = np.dtype([("slot", "i1"), ("reset", "u1"), ("pad", "u1", (6,)), ("init", "<f8")])
 assert CHAIN_DTYPE.itemsize == 16
 # the carrier chain run ahead (gss_carr_chain_guess / gss_spec_* / gss_carr_chain_spec)
-def _lib_spec_k():
-    """GSS_SPEC_K of the library to be loaded (its gss_build_info; 8 when it cannot be read:
-    the sizes below must match the library's, tests/test_abi.py checks them)"""
-    try:
-        L = C.CDLL(LIB_PATH)
-        L.gss_build_info.restype = C.c_char_p
-        kv = dict(x.split("=", 1) for x in L.gss_build_info().decode().split())
-        return int(kv.get("spec_k", "8"))
-    except (OSError, AttributeError, ValueError):
-        return 8
-
-
-SPEC_K = _lib_spec_k()              # speculative segments per block (GSS_SPEC_K, default 8)
+# speculative segments per block (GSS_SPEC_K: 8 in the product build; a measurement build of
+# another value is loaded with GSS_SPEC_K set to it as well -- lib() checks that the library
+# agrees, without loading it at import: torch must load its HIP runtime first)
+SPEC_K = int(os.environ.get("GSS_SPEC_K", "8"))
 SPEC_IN_DTYPE = np.dtype([("g", "<f8"), ("s", "<f8"), ("k", "<i4"), ("pad", "<i4"),
                           ("P", "<i8", (SPEC_K,)), ("W", "<f8", (SPEC_K,))])
 assert SPEC_IN_DTYPE.itemsize == 24 + 16 * SPEC_K
@@ -223,6 +214,10 @@ def lib():
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
+        kv = dict(x.split("=", 1) for x in L.gss_build_info().decode().split())
+        if int(kv.get("spec_k", "8")) != SPEC_K:
+            raise ImportError(f"{LIB_PATH} was built with GSS_SPEC_K={kv.get('spec_k')}: set "
+                              f"GSS_SPEC_K to match (Python's walk dtypes use {SPEC_K})")
         _lib = L
     return _lib
 
