@@ -59,3 +59,20 @@ def test_dtype_label_follows_the_build():
     assert info["lin_mfma"] in ("0", "1", "2")
     assert G.lib_mfma() == (info["lin_mfma"] != "0")
     assert info["lin_mfma"] == "2"                 # the shipped build: channel pairs on MFMA
+
+
+def test_step_issue_efficiency_bounds():
+    """the fast kernel's issue-efficiency line (was roofline_compute) says what it is and carries
+    the HBM fraction its step and the formulation's floor allow: 19.6 SIMD
+    cycles per wave channel-step at 11.3 channels and 4 B per sample bound the headline at
+    ~0.355 of 8 TB/s; the floor and the LDS bound sit above it"""
+    r = bench.compute_roofline(8.8e9, 1.466, 4.0, 11.3)
+    assert "issue efficiency" in r["what"] and "not an HBM roofline" in r["what"]
+    assert abs(r["bound_frac"] - 0.355) < 0.002
+    assert r["bound_frac"] < r["floor_bound_frac"] < 1.0
+    assert r["bound_frac"] < r["lds_bound_frac"] < 1.0
+    # the kernel's HBM fraction over the step's bound = its issue efficiency
+    hbm = 8.8e9 / 11.3 * 4.0 / 1.466e-3 / 8e12
+    assert abs(hbm / r["bound_frac"] - r["frac"]) < 0.01
+    assert "bound_frac" not in bench.compute_roofline(8.8e9, 1.466)    # without the shape
+    assert bench.compute_roofline(8.8e9, 0.0) is None
