@@ -55,7 +55,7 @@ assert CHAIN_DTYPE.itemsize == 16
 # speculative segments per block (GSS_SPEC_K: 8 in the product build; a measurement build of
 # another value is loaded with GSS_SPEC_K set to it as well -- lib() checks that the library
 # agrees, without loading it at import: torch must load its HIP runtime first)
-SPEC_K = int(os.environ.get("GSS_SPEC_K", "8"))
+SPEC_K = int(os.environ.get("GSS_SPEC_K", "16"))
 SPEC_IN_DTYPE = np.dtype([("g", "<f8"), ("s", "<f8"), ("k", "<i4"), ("pad", "<i4"),
                           ("P", "<i8", (SPEC_K,)), ("W", "<f8", (SPEC_K,))])
 assert SPEC_IN_DTYPE.itemsize == 24 + 16 * SPEC_K
