@@ -52,7 +52,7 @@ assert LIN_DTYPE.itemsize == 192
 CHAIN_DTYPE = np.dtype([("slot", "i1"), ("reset", "u1"), ("pad", "u1", (6,)), ("init", "<f8")])
 assert CHAIN_DTYPE.itemsize == 16
 # the carrier chain run ahead (gss_carr_chain_guess / gss_spec_* / gss_carr_chain_spec)
-# speculative segments per block (GSS_SPEC_K: 8 in the product build; a measurement build of
+# speculative segments per block (GSS_SPEC_K: 16 in the product build; a measurement build of
 # another value is loaded with GSS_SPEC_K set to it as well -- lib() checks that the library
 # agrees, without loading it at import: torch must load its HIP runtime first)
 SPEC_K = int(os.environ.get("GSS_SPEC_K", "16"))
@@ -215,7 +215,7 @@ def lib():
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
         kv = dict(x.split("=", 1) for x in L.gss_build_info().decode().split())
-        if int(kv.get("spec_k", "8")) != SPEC_K:
+        if int(kv.get("spec_k", "8")) != SPEC_K:          # (builds before round 6: 8)
             raise ImportError(f"{LIB_PATH} was built with GSS_SPEC_K={kv.get('spec_k')}: set "
                               f"GSS_SPEC_K to match (Python's walk dtypes use {SPEC_K})")
         _lib = L

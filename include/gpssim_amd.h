@@ -314,7 +314,8 @@ int gss_carr_chain(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
 #ifndef GSS_SPEC_T_DEFINED
 #define GSS_SPEC_T_DEFINED
 #ifndef GSS_SPEC_K
-#define GSS_SPEC_K 16                   /* segments per block */
+#define GSS_SPEC_K 16                   /* segments per block (8 before round 6: the GPU walks
+                                          then took 1.19 ms per headline window, 0.88 with 16) */
 #endif
 typedef struct gss_spec_in {           /* a row's guesses (host, gss_carr_chain_guess)          */
     double g, s;                       /* start guess, carr_step (0: padding row)               */
