@@ -1090,7 +1090,7 @@ typedef struct gss_spec_in {           /* a row's guesses (host, gss_carr_chain_
     int32_t k, pad;                    /* segments (1..GSS_SPEC_K)                              */
     int64_t P[GSS_SPEC_K];             /* segment j >= 1 starts at sample P[j], a predicted wrap */
     double W[GSS_SPEC_K];              /* ... with post-wrap value W[j]                         */
-} gss_spec_in_t;                       /* 152 bytes */
+} gss_spec_in_t;                       /* 24 + 16 GSS_SPEC_K bytes */
 typedef struct gss_spec_seg {
     double end, dlo, dhi;              /* end value, admissible translations of the start       */
     int64_t wrap_end;                  /* 1: the segment's last step wrapped                    */
@@ -1099,7 +1099,7 @@ typedef struct gss_spec {              /* a row's speculative walk (GPU or host)
     int64_t p1;                        /* samples to the guess's first wrap (n: none)           */
     double w1;                         /* its post-wrap value                                   */
     gss_spec_seg_t seg[GSS_SPEC_K];
-} gss_spec_t;                          /* 272 bytes */
+} gss_spec_t;                          /* 16 + 32 GSS_SPEC_K bytes */
 #endif
 
 /* Exactly to the first wrap or n steps (the reference's order: ">= 1" before "< 0"). */

@@ -322,7 +322,7 @@ typedef struct gss_spec_in {           /* a row's guesses (host, gss_carr_chain_
     int32_t k, pad;                    /* segments (1..GSS_SPEC_K; 0: not guessed yet)          */
     int64_t P[GSS_SPEC_K];             /* segment j >= 1 starts at sample P[j], a predicted wrap */
     double W[GSS_SPEC_K];              /* ... with post-wrap value W[j]                         */
-} gss_spec_in_t;                       /* 152 bytes */
+} gss_spec_in_t;                       /* 24 + 16 GSS_SPEC_K bytes (280) */
 typedef struct gss_spec_seg {
     double end, dlo, dhi;              /* end value, admissible translations of the start       */
     int64_t wrap_end;                  /* 1: the segment's last step wrapped                    */
@@ -331,7 +331,7 @@ typedef struct gss_spec {              /* a row's speculative walk (GPU or host)
     int64_t p1;                        /* samples to the guess's first wrap (n: none)           */
     double w1;                         /* its post-wrap value                                   */
     gss_spec_seg_t seg[GSS_SPEC_K];
-} gss_spec_t;                          /* 272 bytes */
+} gss_spec_t;                          /* 16 + 32 GSS_SPEC_K bytes (528) */
 #endif
 int gss_carr_chain_guess(const double *carr, const gss_chan_blk_t *blk, const int32_t *nch,
                          const gss_chain_t *chain, int nblk, int n_per_blk, gss_spec_in_t *in);
@@ -352,7 +352,7 @@ int gss_carr_chain_spec(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
 /* Records: each row's speculative walk folded into 72 bytes (gss_spec_rec_t: the interval of
    translations of its first post-wrap value that carry it through every segment, and of its
    predecessor's last translation that carry it from the predecessor's end), so that the chain
-   needs neither the walks (272 B) nor the segment guesses (152 B) on the host (gss_run: the
+   needs neither the walks (528 B) nor the segment guesses (280 B) on the host (gss_run: the
    walks stay on the device and only the records cross the link).  The previous row of a row's
    slot chain in the batch is in[].pad (gss_carr_chain_starts / _guess set it; -1: none).
      gss_spec_records         the records from walks on the host
@@ -392,7 +392,7 @@ int gss_carr_chain_records(double *carr, gss_chan_blk_t *blk, const int32_t *nch
 typedef struct gss_carr_anchor {
     int32_t pos[GSS_SPEC_K];           /* sample positions within the block (-1: none); pos[0] 0 */
     double val[GSS_SPEC_K];            /* the reference's carr_phase at sample pos (val[0] carr0) */
-} gss_carr_anchor_t;                   /* 96 bytes */
+} gss_carr_anchor_t;                   /* 12 GSS_SPEC_K bytes (192) */
 int gss_carr_chain_anchored(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
                             const gss_chain_t *chain, int nblk, int n_per_blk,
                             const gss_spec_in_t *in, const gss_spec_t *spec, int threads,
