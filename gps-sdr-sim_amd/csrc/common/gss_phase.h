@@ -82,62 +82,6 @@ GSS_HD void gss_code_step1(gss_code_state *c, double cs)
  */
 GSS_HD int64_t gss_jump(double v, double s, double W, double *D)
 {
-#if defined(__HIP_DEVICE_COMPILE__)
-    /* The same arithmetic in f64 on the GPU: every quantity below is an integer under 2^54 held
-       exactly in a double (m = v / u is the significand, power-of-two scaling), so the run is
-       the host's bit for bit without 64-bit integer arithmetic (emulated on the VALU); the
-       quotient floor(lim / K) from the reciprocal with an exact fma fix-up, no IEEE division */
-    {
-        const uint32_t hi = (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32);
-        if (hi >> 31) return 0;                   /* negative or -0 */
-        const int E = (int)((hi >> 20) & 0x7FF);
-        if (E < 64 || E == 0x7FF) return 0;      /* zero / tiny / non-finite: real steps */
-        const double u = gss_pow2(E - 1075), inv_u = gss_pow2(1075 - E);
-        const double md = v * inv_u;              /* the significand m, exact */
-        const double as = s < 0.0 ? -s : s;
-        const double sig = as * inv_u;            /* |s|/u, exact */
-        if (!(sig < 4503599627370496.0)) return 0;
-        const double k = __builtin_floor(sig);
-        const double frac = sig - k;              /* exact */
-        double K;
-        if (frac < 0.5)
-            K = k;
-        else if (frac > 0.5)
-            K = k + 1.0;
-        else {                                    /* tie: stable only from an even lattice point */
-            if ((uint32_t)__builtin_bit_cast(uint64_t, v) & 1u) return 0;
-            K = (__builtin_fmod(k, 2.0) != 0.0) ? k + 1.0 : k;
-        }
-        if (K == 0.0) { *D = 0.0; return INT64_MAX; }
-        double lim;
-        if (s > 0.0) {
-            lim = ((0x1p53 - md) - k) - 1.0;      /* tau - k - 1 */
-            if (W <= gss_pow2(E - 1022)) {        /* wrap threshold inside this binade */
-                const double omega = __builtin_trunc((W - v) * inv_u);
-                const double lim2 = (omega - K) - 1.0;
-                if (lim2 < lim) lim = lim2;
-            }
-        } else {
-            const double kc = frac > 0.0 ? k + 1.0 : k;
-            lim = (md - 0x1p52) - kc;             /* beta - ceil(|s|/u) */
-        }
-        if (lim < 0.0) return 0;
-        *D = (s > 0.0 ? K : -K) * u;
-        double r = __builtin_amdgcn_rcp(K);
-        r = __builtin_fma(__builtin_fma(-K, r, 1.0), r, r);
-        double q = __builtin_floor(lim * r);
-        double res = __builtin_fma(-q, K, lim);   /* exact: an integer below 2^53 */
-        while (res < 0.0) {
-            q -= 1.0;
-            res += K;
-        }
-        while (res >= K) {
-            q += 1.0;
-            res -= K;
-        }
-        return (int64_t)q + 1;
-    }
-#endif
     gss_bits64 b;
     b.d = v;
     if (b.u >> 63) return 0;                      /* negative or -0 */
@@ -179,7 +123,29 @@ GSS_HD int64_t gss_jump(double v, double s, double W, double *D)
     }
     if (lim < 0) return 0;
     *D = (s > 0.0 ? (double)K : -(double)K) * u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    /* no 64-bit integer divider on the GPU: floor(lim / K) from the hardware reciprocal refined
+       by one Newton step (relative error ~2^-50: the estimate is off by at most a few), then
+       fixed up exactly in f64 -- lim, K < 2^53 and the residual lim - q K is an integer of
+       magnitude below 2^53, so one fma gives it exactly (no IEEE division sequence and no
+       64-bit integer multiplies on this hot path of every exact walk) */
+    const double Kd = (double)K, ld = (double)lim;
+    double r = __builtin_amdgcn_rcp(Kd);
+    r = __builtin_fma(__builtin_fma(-Kd, r, 1.0), r, r);
+    double q = __builtin_floor(ld * r);
+    double res = __builtin_fma(-q, Kd, ld);
+    while (res < 0.0) {
+        q -= 1.0;
+        res += Kd;
+    }
+    while (res >= Kd) {
+        q += 1.0;
+        res -= Kd;
+    }
+    return (int64_t)q + 1;
+#else
     return lim / K + 1;
+#endif
 }
 
 /* ---- the same jump in f64 only (GPU form: no 64-bit integer multiply/divide) ------------------
