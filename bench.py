@@ -396,10 +396,12 @@ def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None, anch=N
     if anch is not None:
         d_anch = torch.from_numpy(anch.view("u1").reshape(-1).copy()).to(dev_t)
 
-    def prove():
+    def prove(lin=None, fast=None, on=None):
+        lin = res.d_lin if lin is None else lin
+        fast = res.d_fast if fast is None else fast
         dev.linearize_device(res.d_blk.data_ptr(), res.d_nch.data_ptr(), res.nblk, res.npb,
                              res.d_ca.data_ptr(), res.n_ca, res.d_nav.data_ptr(), res.n_nav,
-                             res.d_lin.data_ptr(), res.d_fast.data_ptr(), stream,
+                             lin.data_ptr(), fast.data_ptr(), stream if on is None else on,
                              anch_ptr=d_anch.data_ptr() if d_anch is not None else None)
 
     spec = None
@@ -411,9 +413,46 @@ def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None, anch=N
         d_spec = torch.empty(nrow * G.SPEC_DTYPE.itemsize, dtype=torch.uint8, device=dev_t)
         d_rec = torch.empty(nrow * G.SPEC_REC_DTYPE.itemsize, dtype=torch.uint8, device=dev_t)
 
-        def spec():
+        def spec(on=None):
             dev.spec_records_device(d_heads.data_ptr(), nrow, res.npb, d_in.data_ptr(),
-                                    d_spec.data_ptr(), d_rec.data_ptr(), stream)
+                                    d_spec.data_ptr(), d_rec.data_ptr(),
+                                    stream if on is None else on)
+
+    def pipelined():
+        """device_pipeline: gss_run's stream structure on resident windows -- window i + 1's
+        walks and proofs on a highest-priority planning stream (gss_run's spec and proof streams)
+        while window i renders on the launch stream.  The proofs alternate between two sets of
+        lines and fast flags, so a proof never rewrites the set a render reads; render i waits for
+        proof i, proof i + 2 for render i (events only, no host synchronisation).  Returns the ms
+        per window over the timed steps (events on the render stream) and the sets' agreement."""
+        plan = torch.cuda.Stream(device=dev_t,
+                                 priority=int(os.environ.get("GSS_BENCH_PIPE_PRIO", "-1")))
+        sets = [(res.d_lin, res.d_fast), (res.d_lin.clone(), res.d_fast.clone())]
+        proved = [torch.cuda.Event() for _ in range(2)]
+        rendered = [torch.cuda.Event() for _ in range(2)]
+        rs = torch.cuda.ExternalStream(stream, device=dev_t) if stream else st
+        n = warmup + steps
+        t = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        torch.cuda.synchronize(dev_t)
+        for i in range(n + 1):
+            if i < n:                                       # plan window i
+                k = i % 2
+                if i >= 2:
+                    plan.wait_event(rendered[k])
+                spec(plan.cuda_stream)
+                prove(*sets[k], on=plan.cuda_stream)
+                proved[k].record(plan)
+            if i >= 1:                                      # render window i - 1
+                k = (i - 1) % 2
+                if i - 1 == warmup:
+                    t[0].record(rs)
+                rs.wait_event(proved[k])
+                res.step(stream, *sets[k])
+                rendered[k].record(rs)
+        t[1].record(rs)
+        torch.cuda.synchronize(dev_t)
+        same = bool(torch.equal(sets[0][0], sets[1][0]) and torch.equal(sets[0][1], sets[1][1]))
+        return t[0].elapsed_time(t[1]) / steps, same
 
     def run(with_spec):
         for _ in range(warmup):
@@ -466,6 +505,23 @@ def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None, anch=N
                          "frac": round(bytes_step / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "note": "the window's output bytes over the three kernels' summed "
                                  "event time"}}
+        want = res.out[:res.nblk * res.bb].clone()       # the serial pass's output
+        pipe_ms, same = pipelined()
+        same_out = bool(torch.equal(want, res.out[:res.nblk * res.bb]))
+        del want
+        out["device_pipeline"] = {
+            "workload": "the same three stages in gss_run's stream structure: window i + 1's "
+                        "walks + records and proofs on a highest-priority stream while window "
+                        "i renders (two sets of lines, events only)",
+            "ms_per_window": round(pipe_ms, 3),
+            "value": round(samples / (pipe_ms * 1e-3) / 1e6, 2), "unit": "MS/s",
+            "vs_device_window": round(dev_ms / pipe_ms, 3),
+            "lines_identical": same, "output_identical": same_out,
+            "roofline": {"bound": "hbm", "achieved": round(bytes_step / (pipe_ms * 1e-3) / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(bytes_step / (pipe_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "note": "the window's output bytes per window of the pipelined steady "
+                                 "state (events on the render stream)"}}
     return out
 
 

@@ -92,18 +92,22 @@ class DeviceWindow:
         if self.nblk:
             dev.reserve(max(sizes), n_per_blk)
 
-    def step(self, stream=0):
-        """Render every block of the window into self.out (stream-ordered)."""
+    def step(self, stream=0, lin=None, fast=None):
+        """Render every block of the window into self.out (stream-ordered).  lin, fast: device
+        tensors holding the window's certified lines and fast flags in place of d_lin, d_fast
+        (a second set proven while this one renders: bench.py's device_pipeline)."""
         for i in range(len(self.batches)):
-            self.step_batch(i, stream)
+            self.step_batch(i, stream, lin, fast)
 
-    def step_batch(self, i, stream=0):
+    def step_batch(self, i, stream=0, lin=None, fast=None):
         """Render batch i (blocks batches[i][0] .. batches[i][1]) into its part of self.out."""
         cs, ls, ks = CHAN_DTYPE.itemsize * MAXCH, LIN_DTYPE.itemsize * MAXCH, 8 * MAXCH * NCK
+        d_lin = self.d_lin if lin is None else lin
+        d_fast = self.d_fast if fast is None else fast
         for b0, b1, d_fb, n_fb in self.batches[i:i + 1]:
             self.dev.synth_lin_device(
                 self.d_blk.data_ptr() + b0 * cs, self.d_nch.data_ptr() + b0 * 4, self.nch_max,
-                self.d_lin.data_ptr() + b0 * ls, self.d_fast.data_ptr() + b0 * 4,
+                d_lin.data_ptr() + b0 * ls, d_fast.data_ptr() + b0 * 4,
                 d_fb.data_ptr(), n_fb, self.d_ca.data_ptr(), self.n_ca, self.d_nav.data_ptr(),
                 self.n_nav, b1 - b0, self.npb, self.fmt, self.out.data_ptr() + b0 * self.bb,
                 stream=stream,
