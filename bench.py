@@ -46,6 +46,8 @@ Extra JSON fields besides the driver contract:
                 a window that is proven once and rendered once, beside the kernel-only headline;
                 window.device_window adds the carrier chain's speculative walks and records
                 (gss_spec_records_device) in front: the whole per-window GPU pipeline;
+                window.device_pipeline runs those three stages as gss_run's streams do (the next
+                window's walks and proofs on a highest-priority stream beside the render);
   step_issue_efficiency  the fast kernel against the issue-bound peak of its own step (was
                 roofline_compute), with bound_frac / floor_bound_frac: the HBM-write fraction that
                 step, and the LUT formulation's floor, allow.
