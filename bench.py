@@ -421,40 +421,64 @@ def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None, anch=N
                                     stream if on is None else on)
 
     def pipelined():
-        """device_pipeline: gss_run's stream structure on resident windows -- window i + 1's
-        walks and proofs on a highest-priority planning stream (gss_run's spec and proof streams)
-        while window i renders on the launch stream.  The proofs alternate between two sets of
-        lines and fast flags, so a proof never rewrites the set a render reads; render i waits for
-        proof i, proof i + 2 for render i (events only, no host synchronisation).  Returns the ms
-        per window over the timed steps (events on the render stream) and the sets' agreement."""
-        plan = torch.cuda.Stream(device=dev_t,
-                                 priority=int(os.environ.get("GSS_BENCH_PIPE_PRIO", "-1")))
+        """device_pipeline: gss_run's stream structure on resident windows: the walks + records
+        and the proofs on a highest-priority stream (gss_run's spec and proof streams), the render
+        on the launch stream (its compute stream); window i's proof follows its walks (in gss_run
+        through the host's chain) and its render follows its proof, so in the steady state window
+        i + 1 is walked and proven while window i renders.  GSS_BENCH_PIPE_STAGES=3 gives the
+        proofs a stream of their own (window i + 2 walked, i + 1 proven, i rendered at once):
+        measured slower, 2.19-2.27 against 2.13-2.15 ms per window (profiles/round6/pipeline/:
+        the three stages share one chip's issue, and the proofs run 0.9 ms beside two kernels
+        against 0.6 beside one).  The proofs alternate
+        between two sets of lines and fast flags, so a proof never rewrites the set a render reads
+        (proof i + 2 waits for render i; the walks of window i + 3 for it too: at most three
+        windows in flight).  Events only, no host synchronisation.  Returns the ms per window over
+        the timed steps (events on the render stream), the walks' and proofs' own ms per window
+        under the render (events on their streams) and the two sets' agreement."""
+        prio = int(os.environ.get("GSS_BENCH_PIPE_PRIO", "-1"))
+        three = os.environ.get("GSS_BENCH_PIPE_STAGES", "2") == "3"
+        sp = torch.cuda.Stream(device=dev_t, priority=prio)
+        pp = torch.cuda.Stream(device=dev_t, priority=prio) if three else sp
         sets = [(res.d_lin, res.d_fast), (res.d_lin.clone(), res.d_fast.clone())]
+        walked = [torch.cuda.Event() for _ in range(3)]
         proved = [torch.cuda.Event() for _ in range(2)]
-        rendered = [torch.cuda.Event() for _ in range(2)]
+        rendered = [torch.cuda.Event() for _ in range(3)]
         rs = torch.cuda.ExternalStream(stream, device=dev_t) if stream else st
         n = warmup + steps
         t = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ts = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(n)]
         torch.cuda.synchronize(dev_t)
-        for i in range(n + 1):
-            if i < n:                                       # plan window i
-                k = i % 2
+        for it in range(n + 2):
+            i = it                                          # walk window i
+            if i < n:
+                if i >= 3:
+                    sp.wait_event(rendered[(i - 3) % 3])
+                ts[i][0].record(sp)
+                spec(sp.cuda_stream)
+                ts[i][1].record(sp)
+                walked[i % 3].record(sp)
+            i = it - 1                                      # prove window i
+            if 0 <= i < n:
+                pp.wait_event(walked[i % 3])
                 if i >= 2:
-                    plan.wait_event(rendered[k])
-                spec(plan.cuda_stream)
-                prove(*sets[k], on=plan.cuda_stream)
-                proved[k].record(plan)
-            if i >= 1:                                      # render window i - 1
-                k = (i - 1) % 2
-                if i - 1 == warmup:
+                    pp.wait_event(rendered[(i - 2) % 3])
+                ts[i][2].record(pp)
+                prove(*sets[i % 2], on=pp.cuda_stream)
+                ts[i][3].record(pp)
+                proved[i % 2].record(pp)
+            i = it - 2                                      # render window i
+            if 0 <= i < n:
+                if i == warmup:
                     t[0].record(rs)
-                rs.wait_event(proved[k])
-                res.step(stream, *sets[k])
-                rendered[k].record(rs)
+                rs.wait_event(proved[i % 2])
+                res.step(stream, *sets[i % 2])
+                rendered[i % 3].record(rs)
         t[1].record(rs)
         torch.cuda.synchronize(dev_t)
         same = bool(torch.equal(sets[0][0], sets[1][0]) and torch.equal(sets[0][1], sets[1][1]))
-        return t[0].elapsed_time(t[1]) / steps, same
+        spec_ms = sum(e[0].elapsed_time(e[1]) for e in ts[warmup:]) / steps
+        proof_ms = sum(e[2].elapsed_time(e[3]) for e in ts[warmup:]) / steps
+        return t[0].elapsed_time(t[1]) / steps, spec_ms, proof_ms, three, same
 
     def run(with_spec):
         for _ in range(warmup):
@@ -508,14 +532,21 @@ def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None, anch=N
                          "note": "the window's output bytes over the three kernels' summed "
                                  "event time"}}
         want = res.out[:res.nblk * res.bb].clone()       # the serial pass's output
-        pipe_ms, same = pipelined()
+        pipe_ms, spec_ms_p, proof_ms_p, three, same = pipelined()
         same_out = bool(torch.equal(want, res.out[:res.nblk * res.bb]))
         del want
         out["device_pipeline"] = {
-            "workload": "the same three stages in gss_run's stream structure: window i + 1's "
-                        "walks + records and proofs on a highest-priority stream while window "
-                        "i renders (two sets of lines, events only)",
+            "workload": ("the same three stages in gss_run's stream structure: window i + 2's "
+                         "walks + records and window i + 1's proofs on two highest-priority "
+                         "streams while window i renders (two sets of lines, events only)"
+                         if three else
+                         "the same three stages, window i + 1's walks + records and proofs on "
+                         "one highest-priority stream while window i renders (two sets of "
+                         "lines, events only)"),
+            "stages": 3 if three else 2,
             "ms_per_window": round(pipe_ms, 3),
+            "spec_ms_beside_render": round(spec_ms_p, 3),
+            "proof_ms_beside_render": round(proof_ms_p, 3),
             "value": round(samples / (pipe_ms * 1e-3) / 1e6, 2), "unit": "MS/s",
             "vs_device_window": round(dev_ms / pipe_ms, 3),
             "lines_identical": same, "output_identical": same_out,
