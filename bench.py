@@ -448,7 +448,8 @@ def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None, anch=N
         t = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ts = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(n)]
         torch.cuda.synchronize(dev_t)
-        for it in range(n + 2):
+        po = 1 if three else 0                              # the proofs' and renders' lag
+        for it in range(n + po + 1):
             i = it                                          # walk window i
             if i < n:
                 if i >= 3:
@@ -457,7 +458,7 @@ def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None, anch=N
                 spec(sp.cuda_stream)
                 ts[i][1].record(sp)
                 walked[i % 3].record(sp)
-            i = it - 1                                      # prove window i
+            i = it - po                                     # prove window i
             if 0 <= i < n:
                 pp.wait_event(walked[i % 3])
                 if i >= 2:
@@ -466,7 +467,7 @@ def window_leg(torch, dev, dev_t, res, steps, warmup, stream, exact=None, anch=N
                 prove(*sets[i % 2], on=pp.cuda_stream)
                 ts[i][3].record(pp)
                 proved[i % 2].record(pp)
-            i = it - 2                                      # render window i
+            i = it - po - 1                                 # render window i
             if 0 <= i < n:
                 if i == warmup:
                     t[0].record(rs)
