@@ -98,6 +98,212 @@ __device__ inline int spec_row_of(int u, int nrow)
     return nrow % GSS_MAXCH ? u : (u % nb) * GSS_MAXCH + u / nb;
 }
 
+/* ---- the walks from a cycle cache shared by a row's lanes, misses walked in rounds ------------
+ * A row's GSS_SPEC_K lanes walk the same carrier step s, so a cycle one lane walks (from post-wrap
+ * w, with the interval [w + clo, w + chi] of starts it translates exactly: gss_walk_margins_cc's
+ * argument) serves every lane of the row whose cycle starts inside it: end = w' + (v0 - w0), the
+ * segment's interval narrowed to the entry's (conservative, so the chain's fix-up stays exact).
+ * On SIMT lanes a miss must not stall the wave once per lane (the per-lane caches of round 6 ran
+ * 12 % slower for that reason), so a lane whose cycle is not in the cache waits, the others go on
+ * from the cache, and the waiting lanes walk their cycles together, one round for all of them,
+ * once half the active lanes wait (or none can go on); their cycles then enter the cache.
+ * Descending cycles are cached whole (head, the real steps below T and the wrap), not only their
+ * heads: every step's rounding is a translation inside the intersection of the steps' margins.
+ * The cache: SC_N entries per row in LDS (start interval [lo, hi], end offset dv = v0 - w0, steps
+ * L) and SC_NB buckets over the row's post-wrap range (|s| wide) of the last two entries that
+ * cover each; a lookup reads one bucket and tests at most two entries.  A stale bucket slot only
+ * misses (an entry is used only when its own interval holds the start).  Host model of the
+ * schedule (miss rounds 4-5 per wave against 11-12 cycle walks, headline rows): DESIGN.md §7.1.
+ * The intervals differ from the host walk's (gss_spec_seg_walk) by the cache's `safe` shrink and
+ * the entries' own margins: the tests compare ends, wraps and p1/w1 bit for bit and require the
+ * device intervals inside the host's; GSS_SPEC_SHARED=0 builds the plain per-lane walk. */
+#ifndef GSS_SPEC_SHARED
+#define GSS_SPEC_SHARED 1
+#endif
+#ifndef SC_N
+#define SC_N 64                                       /* cache entries per row */
+#endif
+#define SC_NB 64                                      /* buckets per row */
+#ifndef SC_TH4
+#define SC_TH4 2                                      /* a miss round once SC_TH4/4 wait */
+#endif
+#define SC_GUARD (1 << 20)                            /* rounds; never reached (then: no interval) */
+
+/* one whole cycle from post-wrap value *x (at most left steps), its start margins in [*clo, *chi];
+   *wr: it ended on a wrap (a whole cycle, cacheable) */
+__device__ inline int64_t sc_cycle(double *x, double s, int64_t left, double *clo, double *chi,
+                                   int *wr)
+{
+    if (s > 0.0)
+        return gss_asc_to_wrap(x, s, 1.0, left, wr, clo, chi);
+    const double T = gss_pow2(gss_exp2i(-s) + 2);
+    const double dunit = gss_pow2(-53);
+    int st = 0;
+    double v = *x;
+    int64_t t = gss_desc_head(&v, s, T, left, &st, clo, chi);
+    *wr = 0;
+    if (st) {
+        while (t < left) {                            /* below T: real steps to the wrap */
+            gss_margin_step(v, s, dunit, clo, chi);
+            const double r = v + s;
+            t++;
+            if (r < 0.0) {
+                const double lim = -r - 2.0 * dunit;
+                if (lim < *chi) *chi = lim;
+                gss_margin_step(r, 1.0, dunit, clo, chi);
+                v = r + 1.0;
+                *wr = 1;
+                break;
+            }
+            if (-r > *clo) *clo = -r;
+            v = r;
+        }
+    }
+    *x = v;
+    return t;
+}
+
+struct spec_cc {                                      /* one row's cache (LDS) */
+    double lo[SC_N], hi[SC_N], dv[SC_N];
+    int32_t L[SC_N];
+    uint16_t bk[SC_NB];                               /* two entry indices + 1 (0: empty) */
+    int32_t next;
+};
+
+__device__ inline int sc_bucket(double w, double base, double scale)
+{
+    const double f = (w - base) * scale;
+    return f <= 0.0 ? 0 : f >= (double)(SC_NB - 1) ? SC_NB - 1 : (int)f;
+}
+
+/* a lane's results, written to the row's walk after the cache is done with (the two share LDS) */
+struct sc_res {
+    gss_spec_seg_t sg;
+    int64_t p1;
+    double w1;
+};
+
+/* the segment walk of gss_spec_seg_walk, its cycles through the row's cache; every lane of the
+   wave calls it (walk: this lane has a segment to walk, whose fields it returns in *res) */
+__device__ void sc_seg_walk(const gss_spec_in_t *in, int j, int64_t n, sc_res *res, bool walk,
+                            spec_cc *cc)
+{
+    const double s = in->s;
+    const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
+    gss_spec_seg_t *sg = &res->sg;
+    bool act = false;
+    double x = 0.0;
+    int64_t left = 0;
+    if (walk) {
+        const int64_t stop = j + 1 < k ? in->P[j + 1] : n;
+        int64_t pos = 0;
+        sg->dlo = 1.0;                                /* an empty interval until walked */
+        sg->dhi = 0.0;
+        sg->wrap_end = 0;
+        if (j == 0) {
+            x = in->g;
+            int wr = 0;
+            const int64_t t = s != 0.0 ? gss_carr_to_wrap(&x, s, stop, &wr) : stop;
+            res->p1 = wr ? t : n;
+            res->w1 = x;
+            sg->end = x;
+            act = wr && t < stop;
+            pos = t;
+        } else {
+            x = in->W[j];
+            pos = in->P[j];
+            sg->end = x;
+            act = s != 0.0 && pos < stop;
+        }
+        left = stop - pos;
+#ifdef SC_SKIP
+        act = false;                                  /* measurement: the kernel without walks */
+#endif
+    }
+    const bool walked = act;                          /* the segment's interval is walked */
+    const double as = s < 0.0 ? -s : s;
+    const double base = s > 0.0 ? 0.0 : 1.0 - as;
+    const double scale = as > 0.0 ? (double)SC_NB / as : 0.0;
+    const double safe = 4.0 * gss_pow2(-52);
+    double dlo = -GSS_BIG, dhi = GSS_BIG;
+    int last = 0;
+    bool blocked = false;
+    for (int round = 0;; round++) {
+        const uint64_t am = __builtin_amdgcn_ballot_w64(act);
+        if (!am)
+            break;
+        if (round >= SC_GUARD) {                      /* (never) no interval: the host walks it */
+            if (act) {
+                dlo = 1.0;
+                dhi = 0.0;
+            }
+            break;
+        }
+        bool hit = false;
+        if (act && !blocked) {
+            /* both slots' entries read at once (one LDS round trip after the bucket's) */
+            const uint32_t wd = cc->bk[sc_bucket(x, base, scale)];
+            const int i0 = (int)(wd & 0xFFu) - 1, i1 = (int)((wd >> 8) & 0xFFu) - 1;
+            const int a0 = i0 < 0 ? 0 : i0, a1 = i1 < 0 ? 0 : i1;
+            const double lo0 = cc->lo[a0], hi0 = cc->hi[a0], dv0 = cc->dv[a0];
+            const double lo1 = cc->lo[a1], hi1 = cc->hi[a1], dv1 = cc->dv[a1];
+            const int32_t L0 = cc->L[a0], L1 = cc->L[a1];
+            const bool ok0 = i0 >= 0 && x >= lo0 && x <= hi0 && L0 <= left;
+            const bool ok1 = i1 >= 0 && x >= lo1 && x <= hi1 && L1 <= left;
+            if (ok0 || ok1) {
+                const double lo = (ok0 ? lo0 : lo1) - x, hi = (ok0 ? hi0 : hi1) - x;
+                if (lo > dlo) dlo = lo;
+                if (hi < dhi) dhi = hi;
+                x = x + (ok0 ? dv0 : dv1);
+                left -= ok0 ? L0 : L1;
+                last = 1;
+                hit = true;
+            }
+            blocked = !hit;
+            if (left <= 0)
+                act = false;
+        }
+        const uint64_t bm = __builtin_amdgcn_ballot_w64(act && blocked);
+        const uint64_t hm = __builtin_amdgcn_ballot_w64(hit);
+        if (!bm || (hm && 4 * __builtin_popcountll(bm) < SC_TH4 * __builtin_popcountll(am)))
+            continue;
+        /* a miss round: every waiting lane walks its cycle and enters it */
+        if (act && blocked) {
+            const double w = x;
+            double clo = -GSS_BIG, chi = GSS_BIG;
+            int wr = 0;
+            const int64_t t = sc_cycle(&x, s, left, &clo, &chi, &wr);
+            left -= t;
+            if (clo > dlo) dlo = clo;
+            if (chi < dhi) dhi = chi;
+            last = wr;
+            blocked = false;
+            if (left <= 0)
+                act = false;
+            if (wr && clo <= 0.0 && chi >= 0.0 && t <= INT32_MAX) {
+                const int i = atomicAdd(&cc->next, 1) % SC_N;
+                double lo = w + clo + safe, hi = w + chi - safe;
+                if (lo > w) lo = w;                   /* the walked start itself is valid */
+                if (hi < w) hi = w;
+                cc->lo[i] = lo;
+                cc->hi[i] = hi;
+                cc->dv[i] = x - w;
+                cc->L[i] = (int32_t)t;
+                const int b1 = sc_bucket(lo, base, scale), b2 = sc_bucket(hi, base, scale);
+                for (int b = b1; b <= b2; b++)        /* (racing lanes may drop a slot: a miss) */
+                    cc->bk[b] = (uint16_t)((cc->bk[b] << 8) | (uint32_t)(i + 1));
+            }
+        }
+        __syncthreads();                              /* one wave: the entries before the lookups */
+    }
+    if (walked) {
+        sg->end = x;
+        sg->dlo = dlo;
+        sg->dhi = dhi;
+        sg->wrap_end = last;
+    }
+}
+
 /* in: the rows (read); back: where the rows go back with the walkers' guesses (in itself for
    gss_spec_device, only the rows guessed here; the device copy for gss_spec_records_device, every
    row).  heads: read only each row's start, step, k and pad (the walkers guess the rest) */
@@ -106,7 +312,15 @@ __global__ __launch_bounds__(64) void gss_spec_kernel(const gss_spec_in_t *in,
                                                       gss_spec_t *__restrict__ spec, int heads)
 {
     __shared__ gss_spec_in_t s_in[SPEC_ROWS];
+#if GSS_SPEC_SHARED
+    __shared__ union {                                  /* the caches, then the walks */
+        spec_cc cc[SPEC_ROWS];
+        gss_spec_t out[SPEC_ROWS];
+    } s_u;
+    gss_spec_t *s_out = s_u.out;
+#else
     __shared__ gss_spec_t s_out[SPEC_ROWS];
+#endif
     __shared__ int s_guessed[SPEC_ROWS];
     constexpr int WI = sizeof(gss_spec_in_t) / 8, WO = sizeof(gss_spec_t) / 16;
     const int lane = threadIdx.x, r = lane / GSS_SPEC_K, j = lane % GSS_SPEC_K;
@@ -118,8 +332,10 @@ __global__ __launch_bounds__(64) void gss_spec_kernel(const gss_spec_in_t *in,
             ((uint64_t *)&s_in[rr])[w] =
                 w < wr ? ((const uint64_t *)&in[spec_row_of(u0 + rr, nrow)])[w] : 0;
     }
+#if !GSS_SPEC_SHARED
     for (int q = lane; q < SPEC_ROWS * WO; q += 64)      /* the walks zeroed */
         ((uint4 *)s_out)[q] = make_uint4(0, 0, 0, 0);
+#endif
     __syncthreads();
     const bool live = u0 + r < nrow;
     gss_spec_in_t row = s_in[r];
@@ -135,8 +351,30 @@ __global__ __launch_bounds__(64) void gss_spec_kernel(const gss_spec_in_t *in,
         if (guess)
             s_in[r] = row;
     }
+#if GSS_SPEC_SHARED
+    for (int q = lane; q < SPEC_ROWS * SC_NB; q += 64)
+        s_u.cc[q / SC_NB].bk[q % SC_NB] = 0;
+    if (lane < SPEC_ROWS)
+        s_u.cc[lane].next = 0;
+    __syncthreads();
+    const bool walk = live && j < row.k;
+    sc_res res;
+    sc_seg_walk(&row, j, n, &res, walk, &s_u.cc[r]);
+    __syncthreads();                                     /* the caches are done with */
+    for (int q = lane; q < SPEC_ROWS * WO; q += 64)      /* the walks zeroed */
+        ((uint4 *)s_out)[q] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    if (walk) {
+        s_out[r].seg[j] = res.sg;
+        if (j == 0) {
+            s_out[r].p1 = res.p1;
+            s_out[r].w1 = res.w1;
+        }
+    }
+#else
     if (live && j < row.k)
         gss_spec_seg_walk(&row, j, n, &s_out[r]);
+#endif
     __syncthreads();
     for (int q = lane; q < SPEC_ROWS * WO; q += 64) {    /* the walks out, 16 bytes a lane */
         const int rr = q / WO, w = q % WO;

@@ -506,10 +506,33 @@ def test_producers_on_device(dev, golden):
         assert np.array_equal(rows.cpu().numpy().view(np.uint32), want), kw
 
 
+def _spec_walks_agree(got, want, gi, kw):
+    """The device's walks against the host's (gss_spec_host): the same ends, wraps and first wraps
+    bit for bit, and each segment's interval of exact start translations inside the host's (the
+    device walks cycles from a cache its row's lanes share, whose entries' intervals are narrower:
+    gss_producers.hip, sc_seg_walk); padding rows are not walked."""
+    live = gi.reshape(-1)["s"] != 0
+    assert np.array_equal(got["p1"][live], want["p1"][live]), kw
+    assert np.array_equal(got["w1"][live], want["w1"][live]), kw
+    narrower = 0
+    for r in np.flatnonzero(live):
+        k = gi.reshape(-1)["k"][r]
+        g, w = got["seg"][r][:k], want["seg"][r][:k]
+        assert g["end"].tobytes() == w["end"].tobytes(), (kw, r)
+        assert np.array_equal(g["wrap_end"], w["wrap_end"]), (kw, r)
+        empty = w["dlo"] > w["dhi"]                      # not walked: the same empty interval
+        assert g[empty].tobytes() == w[empty].tobytes(), (kw, r)
+        assert np.all(g["dlo"][~empty] >= w["dlo"][~empty]), (kw, r)
+        assert np.all(g["dhi"][~empty] <= w["dhi"][~empty]), (kw, r)
+        assert np.all(g["dlo"][~empty] <= 0) and np.all(g["dhi"][~empty] >= 0), (kw, r)
+        narrower += int(np.sum((g["dlo"] != w["dlo"]) | (g["dhi"] != w["dhi"])))
+    return narrower
+
+
 def test_spec_walks_on_device(dev):
     """The carrier chain run ahead: the GPU's speculative block walks
-    (gss_spec_device, a lane per segment, rows channel-major) equal the host's (gss_spec_host)
-    field for field, and
+    (gss_spec_device, a lane per segment, rows channel-major) agree with the host's
+    (gss_spec_host: _spec_walks_agree), and
     the chain from them equals the exact chain (gss_carr_chain), for a static run across 30 s
     updates and the circle.csv run; nearly every block takes the translation."""
     import torch
@@ -526,11 +549,7 @@ def test_spec_walks_on_device(dev):
         torch.cuda.synchronize()
         got = d_spec.cpu().numpy().view(G.SPEC_DTYPE)
         live = gi.reshape(-1)["s"] != 0                   # padding rows are not walked
-        assert np.array_equal(got["p1"][live], want["p1"][live]), kw
-        assert np.array_equal(got["w1"][live], want["w1"][live]), kw
-        for r in np.flatnonzero(live):
-            k = gi.reshape(-1)["k"][r]
-            assert got["seg"][r][:k].tobytes() == want["seg"][r][:k].tobytes(), (kw, r)
+        _spec_walks_agree(got, want, gi, kw)
         ref = blk.copy()
         end_ref, _ = G.carr_chain(carr, ref, nch, chain, n, with_ck=False)
         end, hit = G.carr_chain_spec(carr, blk, nch, chain, n, gi, got)
@@ -559,9 +578,10 @@ def test_spec_walks_on_device(dev):
 
 def test_spec_records_on_device(dev):
     """gss_spec_records_device (gss_run's default): the walks stay on the device and only each
-    row's 72-byte record comes back; the records equal the host's (gss_spec_records over
-    gss_spec_host's walks) byte for byte, and the chain from them (gss_carr_chain_records) equals
-    the exact chain, for a static run across 30 s updates and the circle.csv run."""
+    row's 72-byte record comes back; the walks agree with the host's (_spec_walks_agree), the
+    records equal the host's over the device's walks (gss_spec_records) byte for byte, and the
+    chain from them (gss_carr_chain_records) equals the exact chain, for a static run across 30 s
+    updates and the circle.csv run."""
     import torch
     for kw in (dict(llh=LOC, duration=400.0), dict(motion_file=CIRCLE, data_format=8)):
         s = G.Scenario(NAV, **kw)
@@ -572,7 +592,7 @@ def test_spec_records_on_device(dev):
         blk, nch, chain = s.next_deferred(400, threads=8)
         g0 = G.carr_chain_guess(carr, blk, nch, chain, n, starts_only=True)
         gi = g0.copy()
-        want = G.spec_records(gi, G.spec_host(gi, n, threads=8).reshape(gi.shape), n)
+        host = G.spec_host(gi, n, threads=8)
         nrow = g0.size
         h_in = torch.from_numpy(g0.reshape(-1).view(np.uint8).copy()).pin_memory()
         d_in = torch.zeros(nrow * G.SPEC_IN_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
@@ -582,6 +602,10 @@ def test_spec_records_on_device(dev):
                                 h_rec.data_ptr())
         torch.cuda.synchronize()
         got = h_rec.numpy().view(G.SPEC_REC_DTYPE).reshape(g0.shape)
+        walks = d_spec.cpu().numpy().view(G.SPEC_DTYPE)
+        gi = d_in.cpu().numpy().view(G.SPEC_IN_DTYPE).reshape(g0.shape)    # with the guesses
+        _spec_walks_agree(walks, host, gi, kw)
+        want = G.spec_records(gi, walks.reshape(gi.shape), n)
         live = g0["s"] != 0
         assert got[live].tobytes() == want[live].tobytes(), kw
         assert (got["ok"][live] & 2).sum() >= 0.9 * 2 * live.sum(), kw     # linked rows
