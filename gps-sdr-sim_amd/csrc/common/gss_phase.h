@@ -1153,9 +1153,10 @@ GSS_HD double gss_walk_margins(double x, double s, int64_t n, double *dlo, doubl
    probe for most cycles: 2.3x faster on one host core, but 12 % SLOWER on the GPU (gss_spec_kernel
    1.36-1.42 against 1.21-1.23 ms per headline window, profiles/round6/spec_cache/): each lane
    misses its cold cache at its own cycles, so nearly every cycle some lane of the wave walks it
-   in full while the others wait, and the probes go through scratch.  Off by default, so that the
-   host and the GPU walks stay the same bytes (tests/test_gpu_parity.py
-   test_spec_records_on_device); -DGSS_SPEC_CC=1 builds it (test_phase_walk.py checks it). */
+   in full while the others wait, and the probes go through scratch.  Off by default (the host
+   walk, gss_spec_host); -DGSS_SPEC_CC=1 builds it (test_phase_walk.py checks it).  The GPU walks
+   instead share one cache per row in LDS and walk their misses in rounds (gss_producers.hip,
+   sc_seg_walk). */
 #ifndef GSS_SPEC_CC
 #define GSS_SPEC_CC 0
 #endif
