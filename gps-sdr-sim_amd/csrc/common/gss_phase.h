@@ -1244,6 +1244,35 @@ GSS_HD double gss_walk_margins_cc(double x, double s, int64_t n, double *dlo, do
    over the block's wraps after its first (gss_carr_chain_guess on the host, or the walkers
    themselves for rows left with k = 0).  Doubles suffice (errors ~1e-13 against translation
    intervals ~1e-8; guesses only: any mismatch is caught by the fix-up). */
+/* the wraps m in the block the line predicts and the guesses kk to make (0: none, k = 1) */
+GSS_HD int64_t gss_spec_guess_kk(double g0, double s, int64_t n, int64_t *m)
+{
+    if (s == 0.0)
+        return 0;
+    const double e = g0 + (double)n * s;                 /* the line at the block end */
+    const double mw = s > 0.0 ? floor(e) : floor(1.0 - e);   /* wraps in the block */
+    if (!(mw >= 2.0))
+        return 0;
+    *m = mw > 1e9 ? (int64_t)1e9 : (int64_t)mw;
+    return *m < GSS_SPEC_K ? *m : GSS_SPEC_K;
+}
+
+/* guess j (1 <= j < kk): the predicted wrap's position *p and post-wrap value *w; 0 if the value
+   is off the unit interval (the guesses end before it).  The caller also ends them where p is
+   not past the guess before it or not inside the block. */
+GSS_HD int gss_spec_guess_one(double g0, double s, int64_t m, int64_t kk, int64_t j, int64_t *p,
+                              double *w)
+{
+    const double as = s > 0.0 ? s : -s;
+    const double unit = s > 0.0 ? 0x1p-52 : 0x1p-53;
+    const int64_t q = 1 + (j * (m - 1) + kk - 1) / kk;          /* wrap index, >= 2 */
+    *p = s > 0.0 ? (int64_t)ceil(((double)q - g0) / as)
+                 : (int64_t)floor((g0 + (double)q - 1.0) / as) + 1;
+    const double v = (g0 + (double)*p * s) + (s > 0.0 ? -(double)q : (double)q);
+    *w = rint(v / unit) * unit;
+    return *w >= 0.0 && *w < 1.0;
+}
+
 GSS_HD void gss_spec_guess_row(double g, double s, int64_t n, gss_spec_in_t *in)
 {
     const double g0 = g;
@@ -1251,27 +1280,15 @@ GSS_HD void gss_spec_guess_row(double g, double s, int64_t n, gss_spec_in_t *in)
     in->s = s;
     in->k = 1;
     /* in->pad: the caller's (the previous row of the slot, gss_carr_chain_starts) */
-    if (s == 0.0)
-        return;
-    const double as = s > 0.0 ? s : -s;
-    const double e = g0 + (double)n * s;                 /* the line at the block end */
-    const double mw = s > 0.0 ? floor(e) : floor(1.0 - e);   /* wraps in the block */
-    if (!(mw >= 2.0))
-        return;
-    const int64_t m = mw > 1e9 ? (int64_t)1e9 : (int64_t)mw;
-    const int64_t kk = m < GSS_SPEC_K ? m : GSS_SPEC_K;
-    const double unit = s > 0.0 ? 0x1p-52 : 0x1p-53;
+    int64_t m = 0;
+    const int64_t kk = gss_spec_guess_kk(g0, s, n, &m);
     int k = 1;
     int64_t prev = 0;
     for (int64_t j = 1; j < kk; j++) {
-        const int64_t q = 1 + (j * (m - 1) + kk - 1) / kk;          /* wrap index, >= 2 */
-        const int64_t p = s > 0.0 ? (int64_t)ceil(((double)q - g0) / as)
-                                  : (int64_t)floor((g0 + (double)q - 1.0) / as) + 1;
-        if (p <= prev || p >= n)
-            break;
-        const double v = (g0 + (double)p * s) + (s > 0.0 ? -(double)q : (double)q);
-        const double w = rint(v / unit) * unit;
-        if (!(w >= 0.0 && w < 1.0))
+        int64_t p;
+        double w;
+        const int ok = gss_spec_guess_one(g0, s, m, kk, j, &p, &w);
+        if (p <= prev || p >= n || !ok)
             break;
         in->P[k] = p;
         in->W[k] = w;

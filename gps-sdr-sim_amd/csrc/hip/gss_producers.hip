@@ -184,24 +184,22 @@ struct sc_res {
 };
 
 /* the segment walk of gss_spec_seg_walk, its cycles through the row's cache; every lane of the
-   wave calls it (walk: this lane has a segment to walk, whose fields it returns in *res) */
-__device__ void sc_seg_walk(const gss_spec_in_t *in, int j, int64_t n, sc_res *res, bool walk,
-                            spec_cc *cc)
+   wave calls it (walk: this lane has segment j to walk, from the row's start guess g (j = 0) or
+   its guessed start Pj, Wj, to stop; its fields come back in *res) */
+__device__ void sc_seg_walk(double g, double s, int64_t Pj, double Wj, int64_t stop, int j,
+                            int64_t n, sc_res *res, bool walk, spec_cc *cc)
 {
-    const double s = in->s;
-    const int k = in->k < 1 ? 1 : (in->k > GSS_SPEC_K ? GSS_SPEC_K : in->k);
     gss_spec_seg_t *sg = &res->sg;
     bool act = false;
     double x = 0.0;
     int64_t left = 0;
     if (walk) {
-        const int64_t stop = j + 1 < k ? in->P[j + 1] : n;
         int64_t pos = 0;
         sg->dlo = 1.0;                                /* an empty interval until walked */
         sg->dhi = 0.0;
         sg->wrap_end = 0;
         if (j == 0) {
-            x = in->g;
+            x = g;
             int wr = 0;
             const int64_t t = s != 0.0 ? gss_carr_to_wrap(&x, s, stop, &wr) : stop;
             res->p1 = wr ? t : n;
@@ -210,8 +208,8 @@ __device__ void sc_seg_walk(const gss_spec_in_t *in, int j, int64_t n, sc_res *r
             act = wr && t < stop;
             pos = t;
         } else {
-            x = in->W[j];
-            pos = in->P[j];
+            x = Wj;
+            pos = Pj;
             sg->end = x;
             act = s != 0.0 && pos < stop;
         }
@@ -338,6 +336,56 @@ __global__ __launch_bounds__(64) void gss_spec_kernel(const gss_spec_in_t *in,
 #endif
     __syncthreads();
     const bool live = u0 + r < nrow;
+#if GSS_SPEC_SHARED
+    /* the row's guesses (gss_spec_guess_row) made in parallel, lane j the j-th, and its walk
+       fields read from LDS: no lane holds a copy of the row (which went to scratch) */
+    const double g = s_in[r].g, s = s_in[r].s;
+    const bool guess = live && s_in[r].k == 0;
+    __syncthreads();                                     /* every lane has read k */
+    if (guess) {
+        int64_t m = 0, p = 0;
+        double w = 0.0;
+        const int64_t kk = gss_spec_guess_kk(g, s, n, &m);
+        int ok = 0;
+        if (j >= 1 && j < kk)
+            ok = gss_spec_guess_one(g, s, m, kk, j, &p, &w);
+        const int64_t pp = __shfl_up(p, 1, GSS_SPEC_K);  /* guess j - 1's position */
+        const int64_t prev = j == 1 ? 0 : pp;
+        const bool bad = j >= 1 && (j >= kk || !ok || p <= prev || p >= n);
+        const uint64_t rm = GSS_SPEC_K == 64 ? ~0ull : ((1ull << GSS_SPEC_K) - 1);
+        const uint64_t rb = (__builtin_amdgcn_ballot_w64(bad) >> (r * GSS_SPEC_K)) & rm;
+        const int k = rb ? __builtin_ctzll(rb) : GSS_SPEC_K;    /* the first guess that fails */
+        if (j >= 1 && j < k) {
+            s_in[r].P[j] = p;
+            s_in[r].W[j] = w;
+        }
+        if (j == 0)
+            s_in[r].k = k;
+    }
+    if (j == 0)
+        s_guessed[r] = guess;
+    for (int q = lane; q < SPEC_ROWS * SC_NB; q += 64)
+        s_u.cc[q / SC_NB].bk[q % SC_NB] = 0;
+    if (lane < SPEC_ROWS)
+        s_u.cc[lane].next = 0;
+    __syncthreads();
+    const int kr = s_in[r].k, k = kr < 1 ? 1 : (kr > GSS_SPEC_K ? GSS_SPEC_K : kr);
+    const bool walk = live && j < kr;
+    sc_res res;
+    sc_seg_walk(g, s, s_in[r].P[j], s_in[r].W[j], j + 1 < k ? s_in[r].P[j + 1] : (int64_t)n, j,
+                n, &res, walk, &s_u.cc[r]);
+    __syncthreads();                                     /* the caches are done with */
+    for (int q = lane; q < SPEC_ROWS * WO; q += 64)      /* the walks zeroed */
+        ((uint4 *)s_out)[q] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    if (walk) {
+        s_out[r].seg[j] = res.sg;
+        if (j == 0) {
+            s_out[r].p1 = res.p1;
+            s_out[r].w1 = res.w1;
+        }
+    }
+#else
     gss_spec_in_t row = s_in[r];
     const bool guess = live && row.k == 0;
     if (guess) {
@@ -351,27 +399,6 @@ __global__ __launch_bounds__(64) void gss_spec_kernel(const gss_spec_in_t *in,
         if (guess)
             s_in[r] = row;
     }
-#if GSS_SPEC_SHARED
-    for (int q = lane; q < SPEC_ROWS * SC_NB; q += 64)
-        s_u.cc[q / SC_NB].bk[q % SC_NB] = 0;
-    if (lane < SPEC_ROWS)
-        s_u.cc[lane].next = 0;
-    __syncthreads();
-    const bool walk = live && j < row.k;
-    sc_res res;
-    sc_seg_walk(&row, j, n, &res, walk, &s_u.cc[r]);
-    __syncthreads();                                     /* the caches are done with */
-    for (int q = lane; q < SPEC_ROWS * WO; q += 64)      /* the walks zeroed */
-        ((uint4 *)s_out)[q] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-    if (walk) {
-        s_out[r].seg[j] = res.sg;
-        if (j == 0) {
-            s_out[r].p1 = res.p1;
-            s_out[r].w1 = res.w1;
-        }
-    }
-#else
     if (live && j < row.k)
         gss_spec_seg_walk(&row, j, n, &s_out[r]);
 #endif
