@@ -59,8 +59,20 @@ __device__ static void lin_row_init(gss_lin_t *l)
    they would diverge and run one after the other).  A small launch spreads a half over more
    waves (STRIDE 16 / 32: 4 / 8 waves of a few live lanes) so that the SIMDs interleave them; a
    large one (STRIDE 4) still gives each half one wave per block (proof_stride). */
+/* waves per SIMD the register budget aims at: the compiler's own (131 VGPRs: 3 waves) left the
+   headline window's 2,999 workgroups in two rounds; 5 (96 VGPRs, 96 B more scratch) proves it in
+   0.45 ms against 0.48, 4 and 6 in between (profiles/round6/proof/ab_pw_s6v.txt); 0: the
+   compiler's budget */
+#ifndef PF_WAVES_PER_EU
+#define PF_WAVES_PER_EU 5
+#endif
+#if PF_WAVES_PER_EU
+#define PF_OCC __attribute__((amdgpu_waves_per_eu(PF_WAVES_PER_EU)))
+#else
+#define PF_OCC
+#endif
 template <int STRIDE>
-__global__ __launch_bounds__(2 * GSS_MAXCH * STRIDE) void gss_proof_kernel(
+__global__ __launch_bounds__(2 * GSS_MAXCH * STRIDE) PF_OCC void gss_proof_kernel(
     const gss_chan_blk_t *__restrict__ blk, const int32_t *__restrict__ nch, int nblk,
     int n_per_blk, const uint32_t *__restrict__ ca, int n_ca, const uint32_t *__restrict__ nav,
     int n_nav, proof_lut lut, const gss_carr_anchor_t *__restrict__ anch,
