@@ -1048,8 +1048,10 @@ GSS_HD double gss_carr_walk_cc(double x, double s, int64_t n)
 #ifndef GSS_SPEC_T_DEFINED             /* = include/gpssim_amd.h */
 #define GSS_SPEC_T_DEFINED
 #ifndef GSS_SPEC_K
-#define GSS_SPEC_K 16                   /* segments per block (8 before round 6: the GPU walks
-                                          then took 1.19 ms per headline window, 0.88 with 16) */
+#define GSS_SPEC_K 32                   /* segments per block (8 before round 6: the GPU walks
+                                          then took 1.19 ms per headline window, 0.88 with 16;
+                                          with the row-shared cycle cache 0.65 with 16, 0.55
+                                          with 32, 0.61 with 64: profiles/round6/spec_k/s6z) */
 #endif
 typedef struct gss_spec_in {           /* a row's guesses (host, gss_carr_chain_guess)          */
     double g, s;                       /* start guess, carr_step (0: padding row)               */

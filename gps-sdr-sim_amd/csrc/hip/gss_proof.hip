@@ -106,6 +106,11 @@ __global__ __launch_bounds__(2 * GSS_MAXCH * STRIDE) PF_OCC void gss_proof_kerne
     __syncthreads();                                      /* (the row reset before both parts) */
     if (slot) {
         int ok = 0;
+#ifdef PF_SKIP                                           /* measurement builds: one half only */
+        if (role == PF_SKIP - 1) {
+            part_ok[k][role] = 0;
+        } else
+#endif
         if (tables_ok) {
             if (role == 0)
                 ok = lin_carrier(p, n_per_blk, anch ? anch + (size_t)b * GSS_MAXCH + k : nullptr,

@@ -52,10 +52,10 @@ assert LIN_DTYPE.itemsize == 192
 CHAIN_DTYPE = np.dtype([("slot", "i1"), ("reset", "u1"), ("pad", "u1", (6,)), ("init", "<f8")])
 assert CHAIN_DTYPE.itemsize == 16
 # the carrier chain run ahead (gss_carr_chain_guess / gss_spec_* / gss_carr_chain_spec)
-# speculative segments per block (GSS_SPEC_K: 16 in the product build; a measurement build of
+# speculative segments per block (GSS_SPEC_K: 32 in the product build; a measurement build of
 # another value is loaded with GSS_SPEC_K set to it as well -- lib() checks that the library
 # agrees, without loading it at import: torch must load its HIP runtime first)
-SPEC_K = int(os.environ.get("GSS_SPEC_K", "16"))
+SPEC_K = int(os.environ.get("GSS_SPEC_K", "32"))
 SPEC_IN_DTYPE = np.dtype([("g", "<f8"), ("s", "<f8"), ("k", "<i4"), ("pad", "<i4"),
                           ("P", "<i8", (SPEC_K,)), ("W", "<f8", (SPEC_K,))])
 assert SPEC_IN_DTYPE.itemsize == 24 + 16 * SPEC_K

@@ -314,15 +314,17 @@ int gss_carr_chain(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
 #ifndef GSS_SPEC_T_DEFINED
 #define GSS_SPEC_T_DEFINED
 #ifndef GSS_SPEC_K
-#define GSS_SPEC_K 16                   /* segments per block (8 before round 6: the GPU walks
-                                          then took 1.19 ms per headline window, 0.88 with 16) */
+#define GSS_SPEC_K 32                   /* segments per block (8 before round 6: the GPU walks
+                                          then took 1.19 ms per headline window, 0.88 with 16;
+                                          with the row-shared cycle cache 0.65 with 16, 0.55
+                                          with 32, 0.61 with 64: profiles/round6/spec_k/s6z) */
 #endif
 typedef struct gss_spec_in {           /* a row's guesses (host, gss_carr_chain_guess)          */
     double g, s;                       /* start guess, carr_step (0: padding row)               */
     int32_t k, pad;                    /* segments (1..GSS_SPEC_K; 0: not guessed yet)          */
     int64_t P[GSS_SPEC_K];             /* segment j >= 1 starts at sample P[j], a predicted wrap */
     double W[GSS_SPEC_K];              /* ... with post-wrap value W[j]                         */
-} gss_spec_in_t;                       /* 24 + 16 GSS_SPEC_K bytes (280) */
+} gss_spec_in_t;                       /* 24 + 16 GSS_SPEC_K bytes (536) */
 typedef struct gss_spec_seg {
     double end, dlo, dhi;              /* end value, admissible translations of the start       */
     int64_t wrap_end;                  /* 1: the segment's last step wrapped                    */
@@ -331,7 +333,7 @@ typedef struct gss_spec {              /* a row's speculative walk (GPU or host)
     int64_t p1;                        /* samples to the guess's first wrap (n: none)           */
     double w1;                         /* its post-wrap value                                   */
     gss_spec_seg_t seg[GSS_SPEC_K];
-} gss_spec_t;                          /* 16 + 32 GSS_SPEC_K bytes (528) */
+} gss_spec_t;                          /* 16 + 32 GSS_SPEC_K bytes (1040) */
 #endif
 int gss_carr_chain_guess(const double *carr, const gss_chan_blk_t *blk, const int32_t *nch,
                          const gss_chain_t *chain, int nblk, int n_per_blk, gss_spec_in_t *in);
@@ -392,7 +394,7 @@ int gss_carr_chain_records(double *carr, gss_chan_blk_t *blk, const int32_t *nch
 typedef struct gss_carr_anchor {
     int32_t pos[GSS_SPEC_K];           /* sample positions within the block (-1: none); pos[0] 0 */
     double val[GSS_SPEC_K];            /* the reference's carr_phase at sample pos (val[0] carr0) */
-} gss_carr_anchor_t;                   /* 12 GSS_SPEC_K bytes (192) */
+} gss_carr_anchor_t;                   /* 12 GSS_SPEC_K bytes (384) */
 int gss_carr_chain_anchored(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
                             const gss_chain_t *chain, int nblk, int n_per_blk,
                             const gss_spec_in_t *in, const gss_spec_t *spec, int threads,
