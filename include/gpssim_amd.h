@@ -354,7 +354,7 @@ int gss_carr_chain_spec(double *carr, gss_chan_blk_t *blk, const int32_t *nch,
 /* Records: each row's speculative walk folded into 72 bytes (gss_spec_rec_t: the interval of
    translations of its first post-wrap value that carry it through every segment, and of its
    predecessor's last translation that carry it from the predecessor's end), so that the chain
-   needs neither the walks (528 B) nor the segment guesses (280 B) on the host (gss_run: the
+   needs neither the walks (1,040 B) nor the segment guesses (536 B) on the host (gss_run: the
    walks stay on the device and only the records cross the link).  The previous row of a row's
    slot chain in the batch is in[].pad (gss_carr_chain_starts / _guess set it; -1: none).
      gss_spec_records         the records from walks on the host
