@@ -27,9 +27,14 @@ def sink(mv, first, nb):
     got["bytes"] += len(mv)
 
 
-t0 = time.perf_counter()
-dev.run(s, sink, batch=batch, threads=threads)
-wall = time.perf_counter() - t0
-print(f"{c['name']} window {window:g} s batch {batch} threads {threads}: {got['blocks']} blocks "
-      f"in {wall:.3f} s = {got['blocks'] / wall:.0f} blocks/s, {got['bytes'] / wall / 1e9:.2f} GB/s, "
-      f"{wall / got['blocks'] * 1e6:.1f} us/block", flush=True)
+for rep in range(int(os.environ.get("E2E_REPEAT", "1"))):   # later runs: warm (pooled buffers)
+    if rep:
+        s = G.Scenario(B.NAV, duration=window, samp_freq=c["fs"], data_format=c["fmt"], **c["kw"])
+        got = {"blocks": 0, "bytes": 0}
+    t0 = time.perf_counter()
+    dev.run(s, sink, batch=batch, threads=threads)
+    wall = time.perf_counter() - t0
+    print(f"{c['name']} run {rep} window {window:g} s batch {batch} threads {threads}: "
+          f"{got['blocks']} blocks in {wall:.3f} s = {got['blocks'] / wall:.0f} blocks/s, "
+          f"{got['bytes'] / wall / 1e9:.2f} GB/s, {wall / got['blocks'] * 1e6:.1f} us/block",
+          flush=True)
