@@ -909,11 +909,41 @@ GSS_HD void gss_cc_put(gss_cyc_cache *cc, double w, double dlo, double dhi, doub
     if (cc->n < GSS_CC_N) cc->n++;
 }
 
+/* The entry the last cycle used, copied out of the cache (on the GPU the cache lives in scratch,
+   a probe is two or three dependent loads): a code walk's cycles take the same entry as the
+   cycle before 85 % of the time, so the walks test this copy first (any entry that holds the
+   start gives the exact end, so which one a walk takes changes nothing but its speed). */
+typedef struct gss_cyc_mru {
+    double lo, hi, w0, v0;
+    int64_t L;             /* 0: none */
+} gss_cyc_mru;
+
+GSS_HD void gss_mru_set(gss_cyc_mru *m, const gss_cyc *e)
+{
+    m->lo = e->lo;
+    m->hi = e->hi;
+    m->w0 = e->w0;
+    m->v0 = e->v0;
+    m->L = e->L;
+}
+
+/* the cycle from w by the copy, if it holds w (1) */
+GSS_HD int gss_mru_take(const gss_cyc_mru *m, double *w, int64_t nmax, int64_t *L)
+{
+    if (m->L > 0 && *w >= m->lo && *w <= m->hi && m->L <= nmax) {
+        *w = m->v0 + (*w - m->w0);
+        *L = m->L;
+        return 1;
+    }
+    return 0;
+}
+
 /* ---- carrier iterator: exact, cycle by cycle ---------------------------------------------- */
 typedef struct gss_carr_it {
     double x, s, T;
     int64_t pos, left;     /* samples done / remaining */
     int mid;               /* x is not a post-wrap value (block start) */
+    gss_cyc_mru mru;
     gss_cyc_cache cc;
 } gss_carr_it;
 
@@ -928,6 +958,7 @@ GSS_HD void gss_carr_it_init(gss_carr_it *it, double x, double s, int64_t n)
     it->cc.next = 0;
     it->cc.last = -1;
     it->cc.enabled = (s != 0.0);
+    it->mru.L = 0;
     double as = s < 0.0 ? -s : s;
     it->T = as > 0.0 ? gss_pow2(gss_exp2i(as) + 2) : 0.0;
 }
@@ -975,9 +1006,16 @@ GSS_HD int gss_carr_next_wrap(gss_carr_it *it)
         return gss_carr_plain_to_wrap(it);
     }
     const double safe = 4.0 * gss_pow2(-52);
+    int64_t L = 0;
     if (it->s > 0.0) {
+        if (gss_mru_take(&it->mru, &it->x, it->left, &L)) {
+            it->pos += L;
+            it->left -= L;
+            return 1;
+        }
         const gss_cyc *e = gss_cc_find(&it->cc, it->x, it->left);
         if (e) {
+            gss_mru_set(&it->mru, e);
             it->x = e->v0 + (it->x - e->w0);
             it->pos += e->L;
             it->left -= e->L;
@@ -988,23 +1026,35 @@ GSS_HD int gss_carr_next_wrap(gss_carr_it *it)
         int64_t taken = gss_asc_to_wrap(&it->x, it->s, 1.0, it->left, &wr, &dlo, &dhi);
         it->pos += taken;
         it->left -= taken;
-        if (wr) gss_cc_put(&it->cc, w, dlo, dhi, safe, it->x, taken);
+        if (wr && dlo <= 0.0 && dhi >= 0.0) {
+            gss_cc_put(&it->cc, w, dlo, dhi, safe, it->x, taken);
+            gss_mru_set(&it->mru, &it->cc.e[it->cc.last]);
+        }
         return wr;
     }
     /* descending: cached head down to T, then real steps to the wrap */
-    const gss_cyc *e = gss_cc_find(&it->cc, it->x, it->left);
-    if (e) {
-        it->x = e->v0 + (it->x - e->w0);
-        it->pos += e->L;
-        it->left -= e->L;
+    if (gss_mru_take(&it->mru, &it->x, it->left, &L)) {
+        it->pos += L;
+        it->left -= L;
     } else {
-        double w = it->x, dlo = -GSS_BIG, dhi = GSS_BIG;
-        int st = 0;
-        int64_t taken = gss_desc_head(&it->x, it->s, it->T, it->left, &st, &dlo, &dhi);
-        it->pos += taken;
-        it->left -= taken;
-        if (!st) return 0;
-        gss_cc_put(&it->cc, w, dlo, dhi, safe, it->x, taken);
+        const gss_cyc *e = gss_cc_find(&it->cc, it->x, it->left);
+        if (e) {
+            gss_mru_set(&it->mru, e);
+            it->x = e->v0 + (it->x - e->w0);
+            it->pos += e->L;
+            it->left -= e->L;
+        } else {
+            double w = it->x, dlo = -GSS_BIG, dhi = GSS_BIG;
+            int st = 0;
+            int64_t taken = gss_desc_head(&it->x, it->s, it->T, it->left, &st, &dlo, &dhi);
+            it->pos += taken;
+            it->left -= taken;
+            if (!st) return 0;
+            if (dlo <= 0.0 && dhi >= 0.0) {
+                gss_cc_put(&it->cc, w, dlo, dhi, safe, it->x, taken);
+                gss_mru_set(&it->mru, &it->cc.e[it->cc.last]);
+            }
+        }
     }
     while (it->left > 0) {
         double r = it->x + it->s;
@@ -1565,6 +1615,7 @@ typedef struct gss_code_it {
     double cs;
     int64_t pos, left;
     int mid;
+    gss_cyc_mru mru;
     gss_cyc_cache cc;
 } gss_code_it;
 
@@ -1579,6 +1630,7 @@ GSS_HD void gss_code_it_init(gss_code_it *it, gss_code_state c, double cs, int64
     it->cc.next = 0;
     it->cc.last = -1;
     it->cc.enabled = (cs > 0.0);
+    it->mru.L = 0;
 }
 
 GSS_HD void gss_code_count_wrap(gss_code_state *c)
@@ -1607,8 +1659,16 @@ GSS_HD int gss_code_next_wrap(gss_code_it *it)
         if (wr) gss_code_count_wrap(&it->c);
         return wr;
     }
+    int64_t L = 0;
+    if (gss_mru_take(&it->mru, &it->c.ph, it->left, &L)) {
+        it->pos += L;
+        it->left -= L;
+        gss_code_count_wrap(&it->c);
+        return 1;
+    }
     const gss_cyc *e = gss_cc_find(&it->cc, it->c.ph, it->left);
     if (e) {
+        gss_mru_set(&it->mru, e);
         it->c.ph = e->v0 + (it->c.ph - e->w0);
         it->pos += e->L;
         it->left -= e->L;
@@ -1620,7 +1680,10 @@ GSS_HD int gss_code_next_wrap(gss_code_it *it)
     it->pos += taken;
     it->left -= taken;
     if (wr) {
-        gss_cc_put(&it->cc, w, dlo, dhi, 4.0 * gss_pow2(-43), it->c.ph, taken);
+        if (dlo <= 0.0 && dhi >= 0.0) {
+            gss_cc_put(&it->cc, w, dlo, dhi, 4.0 * gss_pow2(-43), it->c.ph, taken);
+            gss_mru_set(&it->mru, &it->cc.e[it->cc.last]);
+        }
         gss_code_count_wrap(&it->c);
     }
     return wr;

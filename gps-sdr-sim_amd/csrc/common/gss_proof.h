@@ -402,7 +402,9 @@ GSS_PF int lin_carrier(const gss_chan_blk_t *p, int n, const gss_carr_anchor_t *
                         xat = an->pos[a];
                         break;
                     }
+#ifndef GSS_PF_NOWALK                                /* (measurement builds: no walks) */
             x = gss_carr_walk_cc(x, s, q - xat);     /* the reference may differ from the line */
+#endif
             xat = q;
             cell = (int)floor(x * 512.0);
             if (cell > 511)      /* carr += 1.0 rounded to 1.0: the reference reads cosTable512[512]
@@ -460,7 +462,9 @@ GSS_PF int lin_code(const gss_chan_blk_t *p, int n, const uint32_t *nav, gss_pf_
     for (int i = 0; i < nhz; i++) {
         const i128 zq = (i128)Z0 + (i128)hz[i] * ZS;
         if (near_boundary(zq, DZ1, LIN_CODE_LGB)) {
+#ifndef GSS_PF_NOWALK
             gss_code_walk_cc(&st, cs, hz[i] - at);
+#endif
             at = hz[i];
             cz->v[i] = (int32_t)floor(st.ph);
             wr_hz[i] = (int32_t)wraps_of(&st, p);
