@@ -606,20 +606,24 @@ def per_config(G, torch, dev, dev_t, stream, steps, warmup, threads, e2e=True):
     return out
 
 
-def d2h_ceiling(nbytes, reps=8):
-    """device -> pinned host copy rate of one gss_run slot (the PCIe ceiling of e2e_run)"""
+def d2h_ceiling(nbytes, reps=8, trials=3):
+    """device -> pinned host copy rate of one gss_run slot (the PCIe ceiling of e2e_run): the best
+    of `trials` timings of `reps` back-to-back copies (one trial right after a long run has read
+    as low as 0.78 of the link, which put that run above its "ceiling": round 6, s6ak)"""
     import torch
     src = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     dst = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
     dst.copy_(src, non_blocking=True)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        dst.copy_(src, non_blocking=True)
-    torch.cuda.synchronize()
-    rate = nbytes * reps / (time.perf_counter() - t0) / 1e9
+    best = 0.0
+    for _ in range(trials):
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        best = max(best, nbytes * reps / (time.perf_counter() - t0) / 1e9)
     del src, dst
-    return round(rate, 2)
+    return round(best, 2)
 
 
 E2E_SLOT_BYTES = 128 * 1040000  # gss_run slot size: 128 blocks at 2.6 MS/s -b 16 (133 MB)
