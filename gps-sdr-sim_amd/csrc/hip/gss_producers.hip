@@ -84,11 +84,12 @@ extern "C" int gss_nav_rows_device(gss_dev *d, const gss_nav_src_t *src, int fir
    channel-major, so that a wave's lanes walk the segments of consecutive blocks of one channel:
    close steps, nearly the same cycles and binades (uniform control flow) instead of 16 different
    Dopplers per wave.
-   The rows and walks live in pinned host memory (gss_run), so the workgroup (8 rows x 8
-   segments) stages them in LDS: each row read once across the link in 8-byte words instead of
-   by each of its 8 lanes, and the walks written back whole (16-byte stores, 272 B per row)
-   instead of field by field -- the walks' link traffic had slowed the slot downloads beside
-   them by a tenth (tools/d2h_overlap.py).  Segments past a row's k are written as zeros. */
+   The rows and walks may live in pinned host memory (gss_spec_device from gss_run's host-walk
+   modes), so the workgroup (64 / GSS_SPEC_K rows x GSS_SPEC_K segments: 2 x 32) stages them in
+   LDS: each row read once across the link in 8-byte words instead of by each of its lanes, and
+   the walks written back whole (16-byte stores) instead of field by field -- the walks' link
+   traffic had slowed the slot downloads beside them by a tenth (tools/d2h_overlap.py).
+   Segments past a row's k are written as zeros. */
 constexpr int SPEC_ROWS = 64 / GSS_SPEC_K;               /* rows per workgroup */
 static_assert(sizeof(gss_spec_in_t) % 8 == 0 && sizeof(gss_spec_t) % 16 == 0, "row sizes");
 
